@@ -1,0 +1,193 @@
+"""ctypes binding of the CPU oracle (oracle/_build/liboracle.so) -- TEST INFRASTRUCTURE.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_ROOT = os.path.dirname(_HERE)
+_LIB = os.path.join(_HERE, "_build", "liboracle.so")
+_lib = None
+
+P, I, LL = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong
+
+
+def build() -> None:
+    subprocess.check_call(["make", "-s", "-f", "oracle/Makefile"], cwd=_ROOT)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB):
+            build()
+        L = ctypes.CDLL(_LIB)
+        L.orc_codebook.argtypes = [I, I, P, P, P, I]
+        L.orc_codebook.restype = I
+        L.orc_codebook_serialize.argtypes = [I, I, P, P, I, P, LL]
+        L.orc_codebook_serialize.restype = LL
+        L.orc_histogram.argtypes = [P, I, LL, I, I, I, P]
+        L.orc_encode.argtypes = [P, I, LL, I, I, I, P, P, I, P, LL]
+        L.orc_encode.restype = LL
+        L.orc_decode.argtypes = [P, LL, LL, I, I, I, P, P, I, P, I]
+        L.orc_decode.restype = I
+        L.orc_sort_rows.argtypes = [P, LL, I]
+        L.orc_pq_assign.argtypes = [P, LL, I, I, I, P, P, I, P, I]
+        L.orc_compute_error.argtypes = [P, LL, I, I, I, P, P, I]
+        L.orc_compute_error.restype = ctypes.c_double
+        L.orc_estimate_size.argtypes = [P, P, LL]
+        L.orc_estimate_size.restype = ctypes.c_double
+        L.orc_stats_json.argtypes = [LL, I, I, I, P, ctypes.c_char_p, I]
+        L.orc_stats_json.restype = I
+        L.orc_bitstream_write.argtypes = [P, P, I, P, LL]
+        L.orc_bitstream_write.restype = LL
+        _lib = L
+    return _lib
+
+
+def bitstream_write(data: np.ndarray, lens: np.ndarray) -> bytes:
+    data = np.ascontiguousarray(data, np.uint8)
+    lens = np.ascontiguousarray(lens, np.int64)
+    cap = int(lens.sum()) // 8 + 8
+    out = np.zeros(cap, np.uint8)
+    n = lib().orc_bitstream_write(_p(data), _p(lens), len(lens), _p(out), cap)
+    assert n >= 0
+    return out[:n].tobytes()
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class Codebooks:
+    """m codebooks: lens [m][items] int32, codes [m][items][stride] uint8."""
+
+    def __init__(self, k: int, context: bool, lens, codes, stride: int):
+        self.k, self.context, self.lens, self.codes, self.stride = k, context, lens, codes, stride
+
+    @property
+    def items(self):
+        return self.k * self.k if self.context else self.k
+
+
+def codebook(alphabet: int, counts: np.ndarray, context: bool = False, stride: int | None = None):
+    rows = alphabet if context else 1
+    stride = stride or max(8, (alphabet + 7) // 8 + 1)
+    counts = np.ascontiguousarray(counts, np.float64)
+    lens = np.zeros(rows * alphabet, np.int32)
+    codes = np.zeros((rows * alphabet, stride), np.uint8)
+    rc = lib().orc_codebook(alphabet, rows, _p(counts), _p(lens), _p(codes), stride)
+    if rc < 0:
+        raise ValueError("code longer than stride")
+    return lens, codes
+
+
+def serialize(alphabet: int, context: bool, lens, codes) -> bytes:
+    items = alphabet * alphabet if context else alphabet
+    cap = 5 + items * 4 + int(lens.sum()) // 8 + 16
+    out = np.zeros(cap, np.uint8)
+    n = lib().orc_codebook_serialize(alphabet, int(context), _p(lens), _p(codes),
+                                     codes.shape[1], _p(out), cap)
+    assert n >= 0
+    return out[:n].tobytes()
+
+
+def histogram(codes: np.ndarray, k: int, context: bool) -> np.ndarray:
+    codes = np.ascontiguousarray(codes)
+    n, m = codes.shape
+    per = k * k if context else k
+    out = np.zeros(m * per, np.float64)
+    lib().orc_histogram(_p(codes), codes.itemsize, n, m, k, int(context), _p(out))
+    return out.reshape(m, per)
+
+
+def build_codebooks(codes: np.ndarray, k: int, context: bool, stride: int = 8) -> Codebooks:
+    counts = histogram(codes, k, context)
+    m = codes.shape[1]
+    items = k * k if context else k
+    lens = np.zeros((m, items), np.int32)
+    cds = np.zeros((m, items, stride), np.uint8)
+    for i in range(m):
+        lens[i], cds[i] = codebook(k, counts[i], context, stride)
+    return Codebooks(k, context, lens, cds, stride)
+
+
+def codebooks_file(cbs: Codebooks) -> bytes:
+    m = cbs.lens.shape[0]
+    parts = [np.uint32(m).tobytes()]
+    for i in range(m):
+        parts.append(serialize(cbs.k, cbs.context, cbs.lens[i], cbs.codes[i]))
+    return b"".join(parts)
+
+
+def encode(codes: np.ndarray, cbs: Codebooks) -> tuple[bytes, int]:
+    codes = np.ascontiguousarray(codes)
+    n, m = codes.shape
+    cap = int(cbs.lens.max(initial=8) + 8) * n * m // 8 + 64
+    out = np.zeros(cap, np.uint8)
+    bits = lib().orc_encode(_p(codes), codes.itemsize, n, m, cbs.k, int(cbs.context),
+                            _p(cbs.lens), _p(cbs.codes), cbs.stride, _p(out), cap)
+    assert bits >= 0
+    return out[:(bits + 7) // 8].tobytes(), bits
+
+
+def indices_file(codes: np.ndarray, cbs: Codebooks) -> bytes:
+    stream, _ = encode(codes, cbs)
+    return np.uint64(codes.shape[0]).tobytes() + stream
+
+
+def decode(stream: bytes, n: int, m: int, cbs: Codebooks) -> np.ndarray:
+    buf = np.frombuffer(stream, np.uint8).copy() if len(stream) else np.zeros(1, np.uint8)
+    dt = np.uint8 if cbs.k <= 256 else np.uint16
+    out = np.zeros((n, m), dt)
+    rc = lib().orc_decode(_p(buf), len(stream), n, m, cbs.k, int(cbs.context), _p(cbs.lens),
+                          _p(cbs.codes), cbs.stride, _p(out), out.itemsize)
+    if rc != 0:
+        raise ValueError(f"oracle decode failed rc={rc}")
+    return out
+
+
+def sort_rows(codes: np.ndarray) -> np.ndarray:
+    out = np.ascontiguousarray(codes, np.uint8).copy()
+    lib().orc_sort_rows(_p(out), out.shape[0], out.shape[1])
+    return out
+
+
+def pq_assign(x: np.ndarray, centroids: np.ndarray, threads: int = 1):
+    x = np.ascontiguousarray(x, np.float32)
+    centroids = np.ascontiguousarray(centroids, np.float32)
+    m, k, ds = centroids.shape
+    n, d = x.shape
+    codes = np.zeros((n, m), np.uint8 if k <= 256 else np.uint16)
+    dists = np.zeros((n, m), np.float32)
+    lib().orc_pq_assign(_p(x), n, d, m, k, _p(centroids), _p(codes), codes.itemsize,
+                        _p(dists), threads)
+    return codes, dists
+
+
+def compute_error(x, centroids, codes) -> float:
+    x = np.ascontiguousarray(x, np.float32)
+    centroids = np.ascontiguousarray(centroids, np.float32)
+    codes = np.ascontiguousarray(codes)
+    m, k, _ = centroids.shape
+    return lib().orc_compute_error(_p(x), x.shape[0], x.shape[1], m, k, _p(centroids),
+                                   _p(codes), codes.itemsize)
+
+
+def stats_json(n: int, m: int, k: int, num_roots: int, partial) -> str:
+    partial = np.ascontiguousarray(partial, np.float64)
+    buf = ctypes.create_string_buffer(8192 + 256 * m)
+    lib().orc_stats_json(n, m, k, num_roots, _p(partial), buf, len(buf))
+    return buf.value.decode()
+
+
+def estimate_parts(cbs: Codebooks, counts: np.ndarray) -> np.ndarray:
+    return np.array([lib().orc_estimate_size(_p(np.ascontiguousarray(cbs.lens[i])),
+                                             _p(np.ascontiguousarray(counts[i])), cbs.items)
+                     for i in range(cbs.lens.shape[0])])

@@ -1,0 +1,57 @@
+# oracle/ref.mk -- TEST INFRASTRUCTURE: build the reference's Huffman/bitstream half from its
+# own sources where they lie (/root/reference/src), outputs only into oracle/_ref/.
+#
+#   make -f oracle/ref.mk            (from the repo root)
+#
+# Nothing is copied out of the reference; no stand-in headers are written.  The PQ half
+# (pq_encoder.c) is NOT buildable here: it needs yael v438 (yael/kmeans.h, .profile:9-11),
+# which is not vendored and not in this image -- see DESIGN.md "Oracle".
+# Reference build flags are `-std=c99 -g` (src/Makefile:9, no -O); we build both that
+# (as-shipped, *_O0) and -O2 (calibration of the CPU baseline).
+
+REF ?= /root/reference/src
+OUT := oracle/_ref
+CC  := gcc
+CFLAGS_O0 := -std=c99 -g -w -I$(REF)
+CFLAGS_O2 := -std=c99 -O2 -w -I$(REF)
+
+LIBSRC := $(REF)/huffman_encode.c $(REF)/huffman_decode.c $(REF)/huffman_codebook.c \
+          $(REF)/bitstream.c $(REF)/stats.c $(REF)/misc.c $(REF)/vecs_io.c
+TREESRC := $(REF)/mst.c $(REF)/dsu.c
+
+BINS := $(OUT)/huffman_encoder $(OUT)/huffman_decoder \
+        $(OUT)/huffman_encoder_O0 $(OUT)/huffman_decoder_O0 \
+        $(OUT)/bitstream_test $(OUT)/huffman_encode_test $(OUT)/huffman_decode_test \
+        $(OUT)/huffman_codebook_test $(OUT)/libref.so
+
+.PHONY: all clean
+all: $(BINS)
+
+$(OUT):
+	mkdir -p $(OUT)
+
+$(OUT)/huffman_encoder: $(REF)/huffman_encoder.c $(LIBSRC) $(TREESRC) | $(OUT)
+	$(CC) $(CFLAGS_O2) -o $@ $^ -lm
+$(OUT)/huffman_decoder: $(REF)/huffman_decoder.c $(LIBSRC) $(TREESRC) | $(OUT)
+	$(CC) $(CFLAGS_O2) -o $@ $^ -lm
+$(OUT)/huffman_encoder_O0: $(REF)/huffman_encoder.c $(LIBSRC) $(TREESRC) | $(OUT)
+	$(CC) $(CFLAGS_O0) -o $@ $^ -lm
+$(OUT)/huffman_decoder_O0: $(REF)/huffman_decoder.c $(LIBSRC) $(TREESRC) | $(OUT)
+	$(CC) $(CFLAGS_O0) -o $@ $^ -lm
+
+# embedded `#ifdef _X_TEST` mains (src/bitstream.c:196, huffman_encode.c:280,
+# huffman_decode.c:193, huffman_codebook.c:145); not built by the reference Makefile
+$(OUT)/bitstream_test: $(REF)/bitstream.c $(REF)/misc.c | $(OUT)
+	$(CC) $(CFLAGS_O2) -D_BITSTREAM_TEST -o $@ $^ -lm
+$(OUT)/huffman_encode_test: $(LIBSRC) | $(OUT)
+	$(CC) $(CFLAGS_O2) -D_HUFFMAN_ENCODE_TEST -o $@ $^ -lm
+$(OUT)/huffman_decode_test: $(LIBSRC) | $(OUT)
+	$(CC) $(CFLAGS_O2) -D_HUFFMAN_DECODE_TEST -o $@ $^ -lm
+$(OUT)/huffman_codebook_test: $(LIBSRC) | $(OUT)
+	$(CC) $(CFLAGS_O2) -D_HUFFMAN_CODEBOOK_TEST -o $@ $^ -lm
+
+$(OUT)/libref.so: oracle/ref_harness.c $(LIBSRC) | $(OUT)
+	$(CC) $(CFLAGS_O2) -fPIC -shared -o $@ $^ -lm
+
+clean:
+	rm -rf $(OUT)
