@@ -1,0 +1,285 @@
+#!/usr/bin/env python3
+"""Benchmark: encode+decode round trip of the PQ+Huffman hot path on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--mode ctx|noctx]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Workload (BASELINE.json configs[1], SIFT1M-shaped): per GPU 1,000,000 synthetic SIFT-like
+128-d fp32 vectors resident in HBM, M=8 sub-spaces, K=256 centroids (weak scaling: every
+rank owns its own 1M-vector shard).  One step = the reference pipeline
+pq_encoder (assignment) -> huffman_encoder -> huffman_decoder on device-resident data:
+
+    pq_assign (MFMA screen + exact re-rank) -> symbol histogram [-> RCCL all-reduce]
+    -> GPU codebooks (reference heap tie-breaks) + decode tables -> encode size
+    [-> all-gather of shard bit totals and halo rows] -> encode write -> chunked decode
+
+value = vectors round-tripped by all ranks / wall time (Mvec/s).  `roofline` is for the
+dominant kernel, pq_assign: algorithmic bytes = 512 B read per vector (+8 B codes) over
+its HIP-event-timed duration against 8 TB/s HBM.  `cpu_baseline` times the CPU oracle
+(a byte-exact restatement of the reference, tests/test_oracle_golden.py) on a bounded
+sample on this host, rank 0 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Mvec/s encode+decode round-trip, 128-d fp32 M=8 K=256; % HBM-read roofline"
+HBM_PEAK_GBS = 8000.0
+BYTES_PER_VEC_READ = 512          # 128 fp32
+BYTES_PER_VEC_WRITE = 8           # M=8 uint8 codes
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--vectors", type=int, default=1_000_000, help="vectors per GPU")
+    ap.add_argument("--mode", choices=["ctx", "noctx"], default="ctx")
+    ap.add_argument("--chunk", type=int, default=16)
+    ap.add_argument("--cpu-sample", type=int, default=200_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def make_data(torch, n, d, seed, rank, device):
+    """SIFT-like synthetic shard generated on the device: integer-valued floats in [0,255]
+    from a Gaussian mixture with Zipf(1.1) weights.  Mixture centres
+    come from `seed` (shared by all ranks), rows from (seed, rank)."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    centers = 1024
+    mu = torch.distributions.Gamma(torch.tensor(1.2), torch.tensor(1 / 30.0)).sample((centers, d))
+    mu = mu.to(device)
+    w = 1.0 / torch.arange(1, centers + 1, dtype=torch.float64) ** 1.1
+    w = (w / w.sum()).to(device)
+    g.manual_seed(seed * 1000003 + rank)
+    lab = torch.multinomial(w, n, replacement=True, generator=g)
+    x = mu[lab] + 12.0 * torch.randn((n, d), generator=g, device=device)
+    return torch.clamp(torch.round(x), 0, 255).contiguous()
+
+
+def train_centroids(torch, x, m, k, iters=4, sample=50_000, seed=7):
+    """Setup only (not timed): Lloyd iterations on a device sample, float64 accumulation."""
+    n, d = x.shape
+    ds = d // m
+    g = torch.Generator(device=x.device)
+    g.manual_seed(seed)
+    xs = x[torch.randperm(n, generator=g, device=x.device)[:sample]].double()
+    out = torch.empty((m, k, ds), dtype=torch.float32)
+    for j in range(m):
+        sub = xs[:, j * ds:(j + 1) * ds]
+        c = sub[torch.randperm(sub.shape[0], generator=g, device=x.device)[:k]].clone()
+        for _ in range(iters):
+            a = torch.cdist(sub, c).argmin(1)
+            s = torch.zeros_like(c).index_add_(0, a, sub)
+            cnt = torch.bincount(a, minlength=k).double()
+            nz = cnt > 0
+            c[nz] = s[nz] / cnt[nz, None]
+        out[j] = c.float().cpu()
+    return out.numpy()
+
+
+def cpu_baseline(x_host, cent, ctxm, sample):
+    """The reference CPU path (oracle restatement, single thread) on a bounded sample."""
+    from oracle import oracle_ctypes as orc
+    xs = np.ascontiguousarray(x_host[:sample])
+    t0 = time.perf_counter()
+    codes, _ = orc.pq_assign(xs, cent, threads=1)
+    t1 = time.perf_counter()
+    cbs = orc.build_codebooks(codes, 256, ctxm)
+    stream, bits = orc.encode(codes, cbs)
+    t2 = time.perf_counter()
+    dec = orc.decode(stream, len(codes), codes.shape[1], cbs)
+    t3 = time.perf_counter()
+    assert np.array_equal(dec, codes)
+    return {"value": round(sample / (t3 - t0) / 1e6, 4), "unit": "Mvec/s", "cores": 1,
+            "kind": "port",
+            "sample": f"{sample} vectors of the rank-0 shard, M=8 K=256 "
+                      f"{'context' if ctxm else 'non-context'}: oracle assign + histogram + "
+                      f"codebooks + bit-serial encode + trie decode, single thread -O2",
+            "stages_s": {"assign": round(t1 - t0, 3), "encode": round(t2 - t1, 3),
+                         "decode": round(t3 - t2, 3)}}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    from pq_huffman_amd import codec
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    ctxm = args.mode == "ctx"
+    n, d, m, k = args.vectors, 128, 8, 256
+
+    x = make_data(torch, n, d, 0x5EED, rank, dev)
+    cent = train_centroids(torch, make_data(torch, 200_000, d, 0x5EED, 0, dev), m, k)
+    ctx = codec.Context(local)
+    pq = codec.PQ(ctx, cent)
+    items = k * k if ctxm else k
+    codes = torch.empty((n, m), dtype=torch.uint8, device=dev)
+    counts = torch.zeros((m, items), dtype=torch.int32, device=dev)
+    dec = torch.empty_like(codes)
+    chunks = (n + args.chunk - 1) // args.chunk
+    coff = torch.empty(chunks, dtype=torch.int64, device=dev)
+    cprev = torch.empty((chunks, m), dtype=torch.uint8, device=dev) if ctxm else None
+    out = torch.zeros(n * m * 56 // 8 + 64, dtype=torch.uint8, device=dev)  # worst case
+    halo_all = torch.zeros((world, m), dtype=torch.uint8, device=dev)
+    tot_all = torch.zeros(world, dtype=torch.int64, device=dev)
+
+    ev = {s: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for s in ("assign", "hist", "codebook", "encode", "decode")}
+    acc = {s: 0.0 for s in list(ev) + ["collectives"]}
+    tabs = codec.Tables(ctx, m, k, ctxm)
+    state = {}
+
+    def step(timed):
+        def rec(name, i):
+            if timed:
+                ev[name][i].record()
+        rec("assign", 0)
+        pq.assign(x, codes)
+        rec("assign", 1)
+        prev_row = None
+        tc = time.perf_counter()
+        if world > 1 and ctxm:
+            dist.all_gather_into_tensor(halo_all, codes[-1].contiguous())
+            prev_row = halo_all[rank - 1] if rank > 0 else None
+        acc_coll = time.perf_counter() - tc
+        rec("hist", 0)
+        counts.zero_()
+        codec.histogram(ctx, codes, k, ctxm, prev_row=prev_row, counts=counts)
+        rec("hist", 1)
+        tc = time.perf_counter()
+        if world > 1:
+            dist.all_reduce(counts)
+        acc_coll += time.perf_counter() - tc
+        rec("codebook", 0)
+        tabs.build(counts)                        # GPU trees + lookup tables, no host trip
+        rec("codebook", 1)
+        raw_first = 1 if rank == 0 else 0
+        rec("encode", 0)
+        total = codec.encode_size(ctx, tabs, codes, raw_first, prev_row)
+        tc = time.perf_counter()
+        if world > 1:
+            dist.all_gather_into_tensor(tot_all, total)
+            offs = torch.cumsum(tot_all, 0) - tot_all
+            bit_off = int(offs[rank].item()) % 32     # word-aligned with the global stream
+        else:
+            bit_off = 0
+        acc_coll += time.perf_counter() - tc
+        out.zero_()
+        codec.encode_write(ctx, tabs, codes, out, bit_off, raw_first, prev_row, args.chunk,
+                           coff, cprev)
+        rec("encode", 1)
+        enc = codec.Encoded(out, -1, args.chunk, coff, cprev, n, raw_first)
+        rec("decode", 0)
+        codec.decode(ctx, tabs, enc, out=dec)
+        rec("decode", 1)
+        if timed:
+            acc["collectives"] += acc_coll
+        state["enc"], state["total"] = enc, total
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step(False)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+        torch.cuda.synchronize()
+        for s in ev:
+            acc[s] += ev[s][0].elapsed_time(ev[s][1]) / 1e3
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # correctness after timing (not timed): exact round trip + oracle parity spot checks
+    codec.decode_status(ctx)
+    codec.encode_status(ctx)
+    assert torch.equal(dec, codes), "round trip mismatch"
+    rerank = pq.rerank_count()
+    tabs.status()
+    bits_per_vec = int(state["total"].item()) / n
+
+    if rank == 0:
+        t_assign = acc["assign"] / args.steps
+        achieved = (BYTES_PER_VEC_READ + BYTES_PER_VEC_WRITE) * n / t_assign / 1e9
+        res = {
+            "metric": METRIC,
+            "value": round(world * n * args.steps / elapsed / 1e6, 2),
+            "unit": "Mvec/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic SIFT-like (integer-valued fp32 in [0,255], Gaussian mixture, "
+                    "Zipf(1.1) weights), generated on device; centroids from 4 Lloyd "
+                    "iterations on a 50k sample (setup, untimed)",
+            "config": {"workload": "SIFT1M-shaped: 1,000,000 x 128-d fp32 per GPU, M=8, K=256, "
+                                   + ("order-1 context Huffman (reference default coding), "
+                                      "no sort" if ctxm else "non-context Huffman, no sort"),
+                       "vectors_per_gpu": n, "m": m, "k": k, "mode": args.mode,
+                       "chunk_vectors": args.chunk, "parallelism": f"dp{world} row shards"},
+            "roofline": {"kernel": "pq_assign_mfma", "bound": "hbm",
+                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "bytes_per_vector": BYTES_PER_VEC_READ + BYTES_PER_VEC_WRITE,
+                         "avg_ms": round(t_assign * 1e3, 4)},
+            "stages_ms": {s: round(v / args.steps * 1e3, 4) for s, v in acc.items()},
+            "bits_per_vector": round(bits_per_vec, 3),
+            "rerank_fraction": round(rerank / (n * m), 6),
+        }
+        if not args.no_cpu_baseline and world == 1:
+            xh = x[:args.cpu_sample].cpu().numpy()
+            res["cpu_baseline"] = cpu_baseline(xh, cent, ctxm, args.cpu_sample)
+            res["cpu_baseline"]["host_cpu"] = _cpu_name()
+            res["cpu_baseline"]["nproc"] = os.cpu_count()
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _cpu_name():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,55 @@
+/*
+ * pq.h -- the reference ships this header EMPTY (src/pq.h, 0 bytes; the PQ helpers are
+ * `static` in pq_encoder.c:34-255 with "TODO: Move to library part" at :226).  This is
+ * the library surface the build defines for it:
+ *   - centroids_codebook_t with the layout of pq_encoder.c:34-40 and its init/destroy/
+ *     save (pq_encoder.c:227-255) plus load;
+ *   - .fvecs reading in ONE pass (the reference re-reads the file once per subspace,
+ *     pq_encoder.c:58-80,265-269);
+ *   - pq_encode: nearest-centroid assignment, which the reference does inside yael
+ *     kmeans() (pq_encoder.c:270-272), run on the GPU by pqh_pq_assign (pqh.h);
+ *   - pq_compute_error (pq_encoder.c:82-119) on the GPU.
+ * Host-pointer convenience wrappers: they stage through device memory on the default
+ * pqh context.  Return 0 on success, a negative pqh_status_t otherwise (never assert).
+ */
+#ifndef _PQ_H
+#define _PQ_H
+
+#include "misc.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct _centroids_codebook {
+    int num_clusters;      /* K */
+    int num_dimensions;    /* dsub = D / M */
+    int num_parts;         /* M */
+    float* centroids_pool; /* [M][K][dsub] */
+    float** centroids;     /* per-part pointers into the pool */
+} centroids_codebook_t;
+
+void centroids_codebook_init(centroids_codebook_t* codebook, int num_parts, int num_clusters,
+                             int num_dimensions);
+void centroids_codebook_destroy(centroids_codebook_t* codebook);
+/* pq_centroids.fvecsl: u32 M*K, u32 dsub, float[M][K][dsub] (pq_encoder.c:248-255) */
+int centroids_codebook_save(const centroids_codebook_t* codebook, const char* filename);
+int centroids_codebook_load(centroids_codebook_t* codebook, const char* filename, int num_parts,
+                            int num_clusters);
+
+/* .fvecs: per row i32 D + float[D] (pq_encoder.c:46-80).  N = file size / (4 + 4D). */
+int fvecs_load_meta(const char* filename, long long* num_vectors, int* num_dimensions);
+float* fvecs_load(const char* filename, long long* num_vectors, int* num_dimensions);
+
+/* codes: n x M, uint8 when K <= 256 else uint16 (row-major, pq_indices.bvecsl order). */
+int pq_encode(const centroids_codebook_t* codebook, const float* x, long long n, int d,
+              void* codes);
+/* mean over vectors of the summed squared reconstruction error (double). */
+int pq_compute_error(const centroids_codebook_t* codebook, const float* x, long long n, int d,
+                     const void* codes, double* error_out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* _PQ_H */

@@ -1,0 +1,185 @@
+/*
+ * pqh.h -- the GPU batch boundary of pq_huffman_amd (C ABI, plain pointers and sizes).
+ *
+ * The reference has no FFI layer: its boundary is its C headers + CLI + file formats
+ * (SURVEY.md 8b).  Its hot loops become the calls below; each names the reference code
+ * it replaces.  All d_* pointers are DEVICE pointers owned by the caller; every call is
+ * asynchronous on the context's HIP stream unless it says otherwise.  Calls return 0
+ * (PQH_OK) or a negative pqh_status_t -- never assert or exit.  There is no CPU fallback:
+ * without a usable GPU the calls return PQH_ERR_NO_DEVICE.
+ *
+ * Device data formats (shared with the CLI tools and the Python layer):
+ *   codes        n x m row-major, uint8 (K <= 256) or uint16 (K <= 65536)
+ *   counts       uint32 [m][K] (non-context) or [m][K*K] (context, index prev*K + cur)
+ *   stream       byte stream exactly as huffman_indices.bin after its 8-byte header:
+ *                vector-major, part-minor, MSB-first, zero padded at the end
+ *   chunk index  (sidecar for parallel decode; not part of huffman_indices.bin)
+ *                u64 bit offset of vector j*C for every chunk j, and in context mode
+ *                the m codes of vector j*C-1 (row of chunk_prev) for j > 0
+ */
+#ifndef _PQH_H
+#define _PQH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "huffman.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    PQH_OK = 0,
+    PQH_ERR_ARG = -1,
+    PQH_ERR_NO_DEVICE = -2,
+    PQH_ERR_HIP = -3,
+    PQH_ERR_UNSUPPORTED = -4,
+    PQH_ERR_CODE_TOO_LONG = -5,  /* a Huffman code longer than 56 bits (needs N >= F(58)) */
+    PQH_ERR_CORRUPT = -6,        /* invalid code in a stream */
+    PQH_ERR_NOMEM = -7,
+    PQH_ERR_CAPACITY = -8        /* output buffer too small */
+} pqh_status_t;
+
+typedef struct pqh_ctx pqh_ctx_t;
+
+/* ---- context: one per device, one host thread per context ----------------------- */
+/* creates the context with a private non-blocking stream */
+int pqh_ctx_create(pqh_ctx_t** ctx, int device);
+int pqh_ctx_destroy(pqh_ctx_t* ctx);
+/* run all later calls on hip_stream, taken literally: NULL is the device's default
+ * (legacy, synchronising) stream -- what torch's current stream usually is. */
+int pqh_ctx_set_stream(pqh_ctx_t* ctx, void* hip_stream);
+int pqh_ctx_sync(pqh_ctx_t* ctx);
+const char* pqh_status_string(int status);
+const char* pqh_ctx_last_error(const pqh_ctx_t* ctx);
+int pqh_device_count(int* count);
+
+/* ---- PQ assignment (replaces yael kmeans' assignment, pq_encoder.c:270-273, and
+ *      copy_cluster_indices :192-205) ----------------------------------------------- */
+typedef struct pqh_pq pqh_pq_t;
+
+/* centroids: host [m][k][dsub] fp32 (pq_centroids.fvecsl order). */
+int pqh_pq_create(pqh_ctx_t* ctx, const float* centroids, int m, int k, int dsub, pqh_pq_t** pq);
+int pqh_pq_destroy(pqh_pq_t* pq);
+
+/* codes[v][i] = argmin_k sum_j (x[v][i*dsub+j] - c[i][k][j])^2, fp32 direct form, j
+ * order, first minimum wins (oracle definition).  x rows are ld_x floats apart.
+ * d_counts (optional, may be NULL): uint32 [m][k] non-context histogram accumulated
+ * (+=) from the produced codes (huffman_encoder.c:139-164) -- fused in the kernel.
+ * mode: 0 = MFMA screening + exact re-rank (default), 1 = exact VALU kernel only. */
+int pqh_pq_assign(pqh_ctx_t* ctx, const pqh_pq_t* pq, const float* d_x, long long n,
+                  long long ld_x, void* d_codes, uint32_t* d_counts, int mode);
+/* diagnostics of the last pqh_pq_assign (synchronises): vectors x parts re-ranked
+ * exactly because the screening could not separate the best two centroids. */
+int pqh_pq_last_rerank_count(pqh_ctx_t* ctx, unsigned long long* count);
+
+/* mean squared reconstruction error (pq_encoder.c:82-119); synchronises. */
+int pqh_pq_error(pqh_ctx_t* ctx, const pqh_pq_t* pq, const float* d_x, long long n,
+                 long long ld_x, const void* d_codes, double* error_out);
+/* x_hat[v] = concat_i c[i][codes[v][i]] (decode codes -> floats). */
+int pqh_pq_reconstruct(pqh_ctx_t* ctx, const pqh_pq_t* pq, const void* d_codes, long long n,
+                       float* d_out, long long ld_out);
+
+/* ---- symbol histograms (huffman_encoder.c:139-205) ------------------------------- */
+/* counts += histogram of codes.  context: pairs (codes[v-1][i], codes[v][i]) for v >= 1,
+ * plus (d_prev_row[i], codes[0][i]) when d_prev_row != NULL (the one-vector halo of a
+ * shard boundary).  d_counts must be zeroed by the caller before the first call. */
+int pqh_histogram(pqh_ctx_t* ctx, const void* d_codes, long long n, int m, int k, int context,
+                  const void* d_prev_row, uint32_t* d_counts);
+
+/* ---- code tables ------------------------------------------------------------------ */
+/* Device-resident Huffman code tables of m parts: encode entries + decode lookup tables. */
+typedef struct pqh_tables pqh_tables_t;
+
+/* allocate tables for m parts of alphabet k (context: k must be 256) */
+int pqh_tables_alloc(pqh_ctx_t* ctx, int m, int k, int context, pqh_tables_t** tables);
+int pqh_tables_destroy(pqh_tables_t* tables);
+/* Build every code on the GPU from device counts (pqh_histogram layout) -- the reference
+ * codebook construction (huffman_codebook_[context_]encode_init, huffman_encode.c:141-269)
+ * with its exact heap tie-breaks, one lane per alphabet; asynchronous, no host round trip.
+ * Codes longer than 56 bits set an error reported by pqh_tables_status. */
+int pqh_tables_build(pqh_ctx_t* ctx, pqh_tables_t* tables, const uint32_t* d_counts);
+/* Load codes from m host codebooks (e.g. huffman_codebooks.bin read by huffman_codebook_load). */
+int pqh_tables_upload(pqh_ctx_t* ctx, pqh_tables_t* tables, const huffman_codebook_t* codebooks);
+/* alloc + upload */
+int pqh_tables_create(pqh_ctx_t* ctx, const huffman_codebook_t* codebooks, int m,
+                      pqh_tables_t** tables);
+/* Synchronises; PQH_ERR_CODE_TOO_LONG if the last build produced a code > 56 bits. */
+int pqh_tables_status(pqh_ctx_t* ctx, const pqh_tables_t* tables);
+/* Synchronises; fills m caller-provided structs with malloc'd host codebooks equal to the
+ * tables (free with huffman_codebook_destroy) -- for huffman_codebook_save and stats. */
+int pqh_tables_codebooks(pqh_ctx_t* ctx, const pqh_tables_t* tables, huffman_codebook_t* codebooks);
+
+/* counts (host, double [m][items], huffman_encoder.c layout) -> host codebooks, built with
+ * the reference's exact heap tie-breaks (huffman_encode.c:141-269).  Threads over parts
+ * and context rows; codebooks must hold m uninitialised structs. */
+int pqh_codebooks_build(const double* counts, int m, int k, int context,
+                        huffman_codebook_t* codebooks, int num_threads);
+
+/* ---- encode (huffman_encoder.c:207-238 + bitstream.c:71-150) --------------------- */
+/* Phase 1: bits of every vector block; total bits (device, u64) written to d_total_bits.
+ * raw_first: context mode writes row 0 raw (8 bits per part, huffman_encoder.c:234) --
+ * set for the shard holding global row 0; other shards pass d_prev_row instead. */
+int pqh_encode_size(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes, long long n,
+                    int raw_first, const void* d_prev_row, unsigned long long* d_total_bits);
+/* Phase 2: write the stream at bit offset `bit_offset` of d_out (bytes, caller-zeroed
+ * over [bit_offset/8, end)).  Words are OR-ed at the two ends so shards written at
+ * adjacent offsets into one buffer compose.  chunk_vectors > 0 also emits the chunk
+ * index: d_chunk_offsets[ceil(n/C)] (bit offsets relative to d_out bit 0) and, in context
+ * mode, d_chunk_prev[ceil(n/C)][m] codes.  Must follow pqh_encode_size on the same data. */
+int pqh_encode_write(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes, long long n,
+                     int raw_first, const void* d_prev_row, unsigned long long bit_offset,
+                     unsigned char* d_out, unsigned long long out_bytes, int chunk_vectors,
+                     unsigned long long* d_chunk_offsets, void* d_chunk_prev);
+
+/* Synchronises; PQH_ERR_CAPACITY if a pqh_encode_write since the last call had to drop
+ * words because out_bytes was too small (nothing is written out of bounds). */
+int pqh_encode_status(pqh_ctx_t* ctx);
+
+/* ---- decode (huffman_decoder.c:211-255, huffman_decode.c:137-191) ---------------- */
+/* Decodes n vectors from d_stream using the chunk index (C = chunk_vectors).  Context
+ * mode: chunk 0 starts raw when raw_first, else from d_chunk_prev row 0.
+ * Returns PQH_ERR_CORRUPT (after synchronising) if an invalid code was met. */
+int pqh_decode(pqh_ctx_t* ctx, const pqh_tables_t* t, const unsigned char* d_stream,
+               unsigned long long stream_bytes, long long n, int raw_first, int chunk_vectors,
+               const unsigned long long* d_chunk_offsets, const void* d_chunk_prev,
+               void* d_codes);
+/* Synchronises; PQH_ERR_CORRUPT if the last pqh_decode met an invalid code. */
+int pqh_decode_status(pqh_ctx_t* ctx);
+/* Build the chunk index of an existing stream (one produced without a sidecar, e.g. by
+ * the reference encoder) with a sequential table walk on the HOST copy of the stream
+ * (index building only; the symbols themselves are decoded on the GPU). */
+int pqh_chunk_index_host(const pqh_tables_t* t, const unsigned char* stream,
+                         unsigned long long stream_bytes, long long n, int raw_first,
+                         int chunk_vectors, unsigned long long* chunk_offsets,
+                         void* chunk_prev);
+
+/* ---- sort mode (huffman_encoder.c:301-317: qsort + strncmp) ---------------------- */
+/* Stable sort of the n rows by key(row) = row with every byte after its first 0 zeroed
+ * (strncmp order), uint8 codes only.  d_tmp: n*m bytes scratch. */
+int pqh_sort_rows(pqh_ctx_t* ctx, void* d_codes, long long n, int m, void* d_tmp);
+
+/* ---- whole-file host helpers used by the CLI tools ------------------------------- */
+typedef struct {
+    int context;           /* order-1 context coding (default 1) */
+    int sort;              /* 0 none, 1 strncmp sort (default 1) */
+    int chunk_vectors;     /* decode chunk size for the sidecar (default 64) */
+    int only_estimate;     /* stats only (huffman_encoder --only-estimate) */
+} pqh_encode_options_t;
+
+/* Runs histogram -> GPU codebooks -> encode on host codes (n x m, K=256).  Produces the
+ * reference files under out_prefix: huffman_codebooks.bin, huffman_indices.bin,
+ * huffman_stats.txt (appended), and the decode sidecar huffman_chunks.bin. */
+int pqh_encode_files(const unsigned char* codes, long long n, int m,
+                     const pqh_encode_options_t* options, const char* out_prefix);
+/* Decodes huffman_indices.bin (+ sidecar when present) under in_prefix into codes
+ * (n x m host buffer, n from the file header). */
+int pqh_decode_files(const char* in_prefix, unsigned char** codes_out, long long* n_out,
+                     int* m_out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* _PQH_H */

@@ -1,0 +1,366 @@
+"""Python mirror of the reference's encode/decode flow over the pqh C ABI.
+
+The reference pipeline is pq_encoder -> huffman_encoder ->
+huffman_decoder, gluing CLI programs through files.  Here the same stages run as C-ABI
+calls on device-resident data:
+
+    PQ.assign            pq_encoder.c:270-272 (yael kmeans assignment) + :192-205
+    histogram            huffman_encoder.c:139-205
+    build_codebooks      huffman_encoder.c:377-388 (huffman_codebook_[context_]encode_init)
+    encode               huffman_encoder.c:413-428 (+ sidecar chunk index)
+    decode               huffman_decoder.c:206-255
+
+torch is used only for device memory and the stream (data_ptr / cuda_stream); every
+computation is a libpqh kernel.  Device buffers are torch tensors owned by the caller.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import tempfile
+from dataclasses import dataclass
+
+import numpy as np
+
+from .capi import (EncodeOptions, HuffmanCodebook, PqhError, check, lib)
+
+_libc = ctypes.CDLL(None)
+_libc.fopen.restype = ctypes.c_void_p
+_libc.fopen.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+_libc.fclose.argtypes = [ctypes.c_void_p]
+_libc.fwrite.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p]
+_libc.fseek.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_int]
+
+
+def _ptr(t):
+    """device/host pointer of a torch tensor or numpy array (None -> NULL)."""
+    if t is None:
+        return None
+    if isinstance(t, np.ndarray):
+        return t.ctypes.data_as(ctypes.c_void_p)
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    lib().pqh_device_count(ctypes.byref(n))
+    return n.value
+
+
+class Context:
+    """pqh_ctx_t bound to a torch device and its current stream (pqh.h)."""
+
+    def __init__(self, device: int = 0, stream=None):
+        torch = _torch()
+        self.device = device
+        torch.cuda.set_device(device)
+        self.stream = stream or torch.cuda.current_stream(device)
+        self.ptr = ctypes.c_void_p()
+        check(lib().pqh_ctx_create(ctypes.byref(self.ptr), device), "pqh_ctx_create")
+        # bind to torch's stream (often the NULL/default stream) so torch's allocations,
+        # fills and copies are ordered with the pqh kernels
+        check(lib().pqh_ctx_set_stream(self.ptr, ctypes.c_void_p(self.stream.cuda_stream)),
+              "pqh_ctx_set_stream")
+
+    def set_stream(self, stream) -> None:
+        self.stream = stream
+        check(lib().pqh_ctx_set_stream(self.ptr, ctypes.c_void_p(stream.cuda_stream)))
+
+    def sync(self) -> None:
+        check(lib().pqh_ctx_sync(self.ptr), "pqh_ctx_sync")
+
+    def last_error(self) -> str:
+        return (lib().pqh_ctx_last_error(self.ptr) or b"").decode()
+
+    def close(self) -> None:
+        if self.ptr:
+            lib().pqh_ctx_destroy(self.ptr)
+            self.ptr = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class PQ:
+    """Prepared sub-codebooks on the device (pq.h centroids_codebook_t + MFMA fragments)."""
+
+    def __init__(self, ctx: Context, centroids: np.ndarray):
+        c = np.ascontiguousarray(centroids, np.float32)
+        self.m, self.k, self.dsub = c.shape
+        self.ctx = ctx
+        self.ptr = ctypes.c_void_p()
+        check(lib().pqh_pq_create(ctx.ptr, _ptr(c), self.m, self.k, self.dsub,
+                                  ctypes.byref(self.ptr)), "pqh_pq_create")
+
+    @property
+    def code_dtype(self):
+        torch = _torch()
+        return torch.uint8 if self.k <= 256 else torch.int16
+
+    def assign(self, x, codes=None, counts=None, mode: int = 0):
+        torch = _torch()
+        n = x.shape[0]
+        if codes is None:
+            codes = torch.empty((n, self.m), dtype=self.code_dtype, device=x.device)
+        check(lib().pqh_pq_assign(self.ctx.ptr, self.ptr, _ptr(x), n, x.stride(0), _ptr(codes),
+                                  _ptr(counts), mode), "pqh_pq_assign")
+        return codes
+
+    def rerank_count(self) -> int:
+        v = ctypes.c_ulonglong(0)
+        check(lib().pqh_pq_last_rerank_count(self.ctx.ptr, ctypes.byref(v)))
+        return v.value
+
+    def error(self, x, codes) -> float:
+        v = ctypes.c_double(0)
+        check(lib().pqh_pq_error(self.ctx.ptr, self.ptr, _ptr(x), x.shape[0], x.stride(0),
+                                 _ptr(codes), ctypes.byref(v)), "pqh_pq_error")
+        return v.value
+
+    def reconstruct(self, codes):
+        torch = _torch()
+        out = torch.empty((codes.shape[0], self.m * self.dsub), dtype=torch.float32,
+                          device=codes.device)
+        check(lib().pqh_pq_reconstruct(self.ctx.ptr, self.ptr, _ptr(codes), codes.shape[0],
+                                       _ptr(out), out.stride(0)), "pqh_pq_reconstruct")
+        return out
+
+    def close(self):
+        if self.ptr:
+            lib().pqh_pq_destroy(self.ptr)
+            self.ptr = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Codebooks:
+    """m host codebooks (huffman.h huffman_codebook_t) built by the library."""
+
+    def __init__(self, counts: np.ndarray, k: int, context: bool, threads: int = 0):
+        counts = np.ascontiguousarray(counts, np.float64)
+        self.m = counts.shape[0]
+        self.k, self.context = k, bool(context)
+        self.arr = (HuffmanCodebook * self.m)()
+        check(lib().pqh_codebooks_build(_ptr(counts), self.m, k, int(context),
+                                        ctypes.cast(self.arr, ctypes.c_void_p),
+                                        threads or min(self.m, os.cpu_count() or 1)),
+              "pqh_codebooks_build")
+        self.counts = counts
+
+    @classmethod
+    def _empty(cls, m):
+        obj = cls.__new__(cls)
+        obj.m = m
+        obj.arr = (HuffmanCodebook * m)()
+        return obj
+
+    @property
+    def items(self):
+        return self.k * self.k if self.context else self.k
+
+    def lengths(self) -> np.ndarray:
+        out = np.zeros((self.m, self.items), np.int32)
+        for i in range(self.m):
+            cb = self.arr[i]
+            for j in range(cb.num_items):
+                out[i, j] = cb.items[j].bit_length
+        return out
+
+    def estimate(self) -> np.ndarray:
+        return np.array([lib().huffman_estimate_size(ctypes.byref(self.arr[i]),
+                                                     _ptr(np.ascontiguousarray(self.counts[i])))
+                         for i in range(self.m)])
+
+    def file_bytes(self) -> bytes:
+        """huffman_codebooks.bin content (huffman_encoder.c:398-409)."""
+        with tempfile.TemporaryDirectory() as d:
+            path = os.path.join(d, "cb.bin").encode()
+            f = _libc.fopen(path, b"wb")
+            _libc.fwrite(ctypes.byref(ctypes.c_uint32(self.m)), 4, 1, ctypes.c_void_p(f))
+            for i in range(self.m):
+                lib().huffman_codebook_save(ctypes.byref(self.arr[i]), ctypes.c_void_p(f))
+            _libc.fclose(ctypes.c_void_p(f))
+            with open(path, "rb") as fh:
+                return fh.read()
+
+    @classmethod
+    def load_file(cls, path: str) -> "Codebooks":
+        with open(path, "rb") as fh:
+            m = int(np.frombuffer(fh.read(4), np.uint32)[0])
+        obj = cls._empty(m)
+        f = _libc.fopen(path.encode(), b"rb")
+        _libc.fseek(ctypes.c_void_p(f), ctypes.c_long(4), 0)
+        for i in range(m):
+            lib().huffman_codebook_load(ctypes.byref(obj.arr[i]), ctypes.c_void_p(f))
+        _libc.fclose(ctypes.c_void_p(f))
+        obj.k = obj.arr[0].alphabet_size
+        obj.context = bool(obj.arr[0].is_context)
+        obj.counts = None
+        return obj
+
+    def close(self):
+        if getattr(self, "arr", None) is not None:
+            for i in range(self.m):
+                if self.arr[i].items:
+                    lib().huffman_codebook_destroy(ctypes.byref(self.arr[i]))
+            self.arr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Tables:
+    """Device code tables (pqh_tables_t): encode entries + decode lookup tables."""
+
+    def __init__(self, ctx: Context, m: int, k: int, context: bool):
+        self.ctx, self.m, self.k, self.context = ctx, m, k, bool(context)
+        self.ptr = ctypes.c_void_p()
+        st = lib().pqh_tables_alloc(ctx.ptr, m, k, int(context), ctypes.byref(self.ptr))
+        if st:
+            raise PqhError(st, "pqh_tables_alloc: " + ctx.last_error())
+
+    @classmethod
+    def from_codebooks(cls, ctx: Context, cbs: "Codebooks") -> "Tables":
+        t = cls(ctx, cbs.m, cbs.k, cbs.context)
+        st = lib().pqh_tables_upload(ctx.ptr, t.ptr, ctypes.cast(cbs.arr, ctypes.c_void_p))
+        if st:
+            raise PqhError(st, "pqh_tables_upload: " + ctx.last_error())
+        return t
+
+    def build(self, counts) -> "Tables":
+        """GPU codebook construction from device counts (async)."""
+        check(lib().pqh_tables_build(self.ctx.ptr, self.ptr, _ptr(counts)), "pqh_tables_build")
+        return self
+
+    def status(self) -> None:
+        st = lib().pqh_tables_status(self.ctx.ptr, self.ptr)
+        if st:
+            raise PqhError(st, "pqh_tables: " + self.ctx.last_error())
+
+    def codebooks(self, counts_host=None) -> "Codebooks":
+        cbs = Codebooks._empty(self.m)
+        st = lib().pqh_tables_codebooks(self.ctx.ptr, self.ptr, ctypes.cast(cbs.arr, ctypes.c_void_p))
+        if st:
+            raise PqhError(st, "pqh_tables_codebooks: " + self.ctx.last_error())
+        cbs.k, cbs.context, cbs.counts = self.k, self.context, counts_host
+        return cbs
+
+    def close(self):
+        if self.ptr:
+            lib().pqh_tables_destroy(self.ptr)
+            self.ptr = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def histogram(ctx: Context, codes, k: int, context: bool, prev_row=None, counts=None):
+    torch = _torch()
+    n, m = codes.shape
+    items = k * k if context else k
+    if counts is None:
+        counts = torch.zeros((m, items), dtype=torch.int32, device=codes.device)
+    check(lib().pqh_histogram(ctx.ptr, _ptr(codes), n, m, k, int(context), _ptr(prev_row),
+                              _ptr(counts)), "pqh_histogram")
+    return counts
+
+
+def counts_to_host(counts) -> np.ndarray:
+    """uint32 device counts -> float64 host counts (the reference keeps counts in double)."""
+    return counts.cpu().numpy().view(np.uint32).astype(np.float64)
+
+
+@dataclass
+class Encoded:
+    stream: object            # device uint8, length padded to a multiple of 4
+    bits: int
+    chunk_vectors: int
+    chunk_offsets: object     # device int64 [chunks]
+    chunk_prev: object        # device codes [chunks, m] (context) or None
+    n: int
+    raw_first: int
+
+    @property
+    def nbytes(self) -> int:
+        return (self.bits + 7) // 8
+
+
+def encode_size(ctx: Context, tables: Tables, codes, raw_first: int = 1, prev_row=None):
+    """device int64[1] total bits (async)."""
+    torch = _torch()
+    total = torch.zeros(1, dtype=torch.int64, device=codes.device)
+    check(lib().pqh_encode_size(ctx.ptr, tables.ptr, _ptr(codes), codes.shape[0], raw_first,
+                                _ptr(prev_row), _ptr(total)), "pqh_encode_size")
+    return total
+
+
+def encode_write(ctx: Context, tables: Tables, codes, out, bit_offset: int = 0, raw_first: int = 1,
+                 prev_row=None, chunk_vectors: int = 64, chunk_offsets=None, chunk_prev=None):
+    check(lib().pqh_encode_write(ctx.ptr, tables.ptr, _ptr(codes), codes.shape[0], raw_first,
+                                 _ptr(prev_row), bit_offset, _ptr(out), out.numel(),
+                                 chunk_vectors, _ptr(chunk_offsets), _ptr(chunk_prev)),
+          "pqh_encode_write: " + ctx.last_error())
+
+
+def encode(ctx: Context, tables: Tables, codes, chunk_vectors: int = 64, raw_first: int = 1,
+           prev_row=None) -> Encoded:
+    torch = _torch()
+    n, m = codes.shape
+    total = encode_size(ctx, tables, codes, raw_first, prev_row)
+    bits = int(total.item())
+    words = (bits + 31) // 32 + 1
+    out = torch.zeros(words * 4, dtype=torch.uint8, device=codes.device)
+    chunks = (n + chunk_vectors - 1) // chunk_vectors
+    coff = torch.empty(max(chunks, 1), dtype=torch.int64, device=codes.device)
+    cprev = torch.empty((max(chunks, 1), m), dtype=codes.dtype, device=codes.device) \
+        if tables.context else None
+    encode_write(ctx, tables, codes, out, 0, raw_first, prev_row, chunk_vectors, coff, cprev)
+    encode_status(ctx)
+    return Encoded(out, bits, chunk_vectors, coff, cprev, n, raw_first)
+
+
+def decode(ctx: Context, tables: Tables, enc: Encoded, out=None):
+    torch = _torch()
+    dt = torch.uint8 if tables.k <= 256 else torch.int16
+    if out is None:
+        out = torch.empty((enc.n, tables.m), dtype=dt, device=enc.stream.device)
+    check(lib().pqh_decode(ctx.ptr, tables.ptr, _ptr(enc.stream), enc.stream.numel(), enc.n,
+                           enc.raw_first, enc.chunk_vectors, _ptr(enc.chunk_offsets),
+                           _ptr(enc.chunk_prev), _ptr(out)), "pqh_decode")
+    return out
+
+
+def encode_status(ctx: Context) -> None:
+    st = lib().pqh_encode_status(ctx.ptr)
+    if st:
+        raise PqhError(st, "pqh_encode_write")
+
+
+def decode_status(ctx: Context) -> None:
+    st = lib().pqh_decode_status(ctx.ptr)
+    if st:
+        raise PqhError(st, "pqh_decode")
+
+
+def indices_file_bytes(enc: Encoded) -> bytes:
+    """huffman_indices.bin content: u64 N + stream bytes."""
+    body = enc.stream[:enc.nbytes].cpu().numpy().tobytes()
+    return np.uint64(enc.n).tobytes() + body

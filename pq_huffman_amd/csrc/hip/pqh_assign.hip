@@ -1,0 +1,615 @@
+// pqh_assign.hip -- PQ nearest-centroid assignment on gfx950.
+//
+// Replaces the assignment half of yael kmeans() called at pq_encoder.c:270-272 plus
+// copy_cluster_indices (pq_encoder.c:192-205); fuses the non-context symbol histogram
+// (huffman_encoder.c:139-164).
+//
+// Result definition (= the oracle, oracle/pqh_oracle.c): for every vector v and part i,
+//   D_k = sum_j (x_j - c_kj)^2 in fp32, j ascending, product and sum rounded separately,
+//   code = the first k reaching min_k D_k.
+//
+// Kernel design (DESIGN.md "pq_assign"):
+//  * One wave per subspace, its centroid sub-codebook resident in VGPRs as MFMA A
+//    fragments; a workgroup = up to 8 subspace waves over the same 32-vector block, so
+//    every input row is read from HBM once per workgroup (512 B per SIFT vector).
+//  * Screening score S_k = ||c_k||^2 - 2 x.c_k + b_v computed exactly-as-bounded by
+//    v_mfma_f32_32x32x16_bf16 over an augmented K dimension:
+//       [xh . ch | xh . cl | 1,1,1,b_v . n1,n2,n3,1]  (+ xl . ch only if the block has
+//    any x that is not bf16-exact -- SIFT-like integer data skips that pass);
+//    x = xh + xl + r, c = ch + cl + r', ||c||^2 = n1 + n2 + n3 (bf16 splits).
+//  * Scores become packed uint keys (float bits, low 4 bits = accumulator register) and
+//    each lane keeps the smallest and second smallest key over its 128 centroids; the
+//    two half-waves merge.  If the runner-up is further than a rigorous error bound tau
+//    from the winner the winner IS the fp32 direct-form argmin; otherwise (and for any
+//    non-finite input) the wave re-ranks all K centroids of that vector with the exact
+//    fp32 direct form and first-index tie break.
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "pqh_internal.h"
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+namespace {
+
+constexpr int kTiles = 8;        // K = 256 centroids = 8 tiles of 32 rows
+constexpr int kWavesPerWG = 8;   // subspace waves per workgroup
+
+template <int D>
+struct Plan {
+    static constexpr int MAIN = 2 * D + 4;            // xh.ch | xh.cl | aux
+    static constexpr int PM = (MAIN + 15) / 16;       // main MFMA passes
+    static constexpr int PL = (D + 15) / 16;          // lo passes (xl . ch)
+    static constexpr bool REUSE = (D == 16);          // lo pass A == main pass 0 A
+    static constexpr int PA = PM + (REUSE ? 0 : PL);  // distinct A fragments per tile
+};
+
+__device__ __forceinline__ unsigned med3u(unsigned a, unsigned b, unsigned c) {
+    unsigned r;
+    asm volatile("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+__device__ __forceinline__ float bf16_up(float x) {
+    // smallest bf16 >= x for finite x >= 0
+    unsigned u = __float_as_uint(x);
+    if (u & 0xFFFFu) u = (u & 0xFFFF0000u) + 0x10000u;
+    return __uint_as_float(u);
+}
+
+// main-layout B slot value for vector-side quantities
+template <int D>
+__device__ __forceinline__ float main_slot(int s, const float* xh, float bv) {
+    if (s < D) return xh[s];
+    if (s < 2 * D) return xh[s - D];
+    if (s < 2 * D + 3) return 1.0f;
+    if (s == 2 * D + 3) return bv;
+    return 0.0f;
+}
+
+// Exact fp32 direct-form distance (no contraction: __fadd_rn/__fmul_rn).
+template <int D>
+__device__ __forceinline__ float exact_dist(const float* x, const float* c) {
+#pragma clang fp contract(off)
+    float acc = 0.0f;
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        float d = __fsub_rn(x[j], c[j]);
+        acc = __fadd_rn(acc, __fmul_rn(d, d));
+    }
+    return acc;
+}
+
+template <int D, typename CodeT>
+__global__ void __launch_bounds__(64 * kWavesPerWG)
+pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_total,
+               const bf16x8* __restrict__ afrag, const float* __restrict__ cent,
+               const float* __restrict__ cmax, const float* __restrict__ sqrt_cmax,
+               CodeT* __restrict__ codes, uint32_t* __restrict__ counts,
+               unsigned long long* __restrict__ rerank) {
+    using P = Plan<D>;
+    constexpr int K = kTiles * 32;
+    __shared__ uint32_t hist[kWavesPerWG][K];
+
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int m = blockIdx.y * kWavesPerWG + wave;
+    if (m >= m_total) return;  // whole wave leaves; no workgroup barriers below
+    const int r = lane & 31;
+    const int h = lane >> 5;
+
+    if (counts) {
+        for (int i = lane; i < K; i += 64) hist[wave][i] = 0;
+    }
+
+    // resident A fragments of this subspace: PA passes x 8 tiles x 4 VGPRs
+    bf16x8 A[P::PA][kTiles];
+#pragma unroll
+    for (int p = 0; p < P::PA; ++p)
+#pragma unroll
+        for (int t = 0; t < kTiles; ++t)
+            A[p][t] = afrag[(((long long)m * P::PA + p) * kTiles + t) * 64 + lane];
+
+    const float cm = cmax[m];
+    const float sc = sqrt_cmax[m];
+    const float* cbase = cent + (long long)m * K * D;
+    const long long nblk = (n + 31) / 32;
+    unsigned long long slow_count = 0;
+
+    for (long long blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        const long long v = blk * 32 + r;
+        const bool valid = v < n;
+        float xs[D];
+        const float* xp = x + (valid ? v : 0) * ldx + (long long)m * D;
+        if constexpr (D % 4 == 0) {
+#pragma unroll
+            for (int j = 0; j < D; j += 4) {
+                float4 q = valid ? *reinterpret_cast<const float4*>(xp + j) : make_float4(0, 0, 0, 0);
+                xs[j] = q.x; xs[j + 1] = q.y; xs[j + 2] = q.z; xs[j + 3] = q.w;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < D; ++j) xs[j] = valid ? xp[j] : 0.0f;
+        }
+
+        float X = 0.0f;
+        bool lo = false;
+        float xh[D], xl[D];
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            X = fmaf(xs[j], xs[j], X);
+            __bf16 hb = (__bf16)xs[j];
+            xh[j] = (float)hb;
+            float rem = xs[j] - xh[j];
+            xl[j] = (float)(__bf16)rem;
+            lo |= rem != 0.0f;
+        }
+        const bool any_lo = __any(lo);
+        const bool finite_x = isfinite(X);
+
+        // error bound of the screening score (DESIGN.md "pq_assign error bound")
+        const float Pm = sqrtf(X) * sc * 1.00001f;
+        const float E0 = 0x1p-13f * Pm + 0x1p-22f * cm +
+                         0x1p-17f * (2.02f * Pm + 1.01f * cm + 1.05f * X);
+        const float bv = finite_x ? bf16_up(X + 3.0f * E0 + 1e-30f) : 0.0f;
+        const float tau = 2.2f * E0 + 1e-30f;
+
+        // B fragments
+        bf16x8 Bm[P::PM];
+#pragma unroll
+        for (int p = 0; p < P::PM; ++p)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                float v0 = main_slot<D>(16 * p + j, xh, bv);
+                float v1 = main_slot<D>(16 * p + 8 + j, xh, bv);
+                Bm[p][j] = (__bf16)(h ? v1 : v0);
+            }
+        bf16x8 Bl[P::PL];
+#pragma unroll
+        for (int p = 0; p < P::PL; ++p)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                int s0 = 16 * p + j, s1 = 16 * p + 8 + j;
+                float v0 = s0 < D ? xl[s0 < D ? s0 : 0] : 0.0f;
+                float v1 = s1 < D ? xl[s1 < D ? s1 : 0] : 0.0f;
+                Bl[p][j] = (__bf16)(h ? v1 : v0);
+            }
+
+        unsigned m1 = 0xFFFFFFFFu, m2 = 0xFFFFFFFFu, mt = 0;
+#pragma unroll
+        for (int t = 0; t < kTiles; ++t) {
+            f32x16 acc = {0};
+#pragma unroll
+            for (int p = 0; p < P::PM; ++p)
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[p][t], Bm[p], acc, 0, 0, 0);
+            if (any_lo) {
+#pragma unroll
+                for (int p = 0; p < P::PL; ++p) {
+                    const bf16x8 a = P::REUSE ? A[0][t] : A[P::PM + (P::REUSE ? 0 : p)][t];
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, Bl[p], acc, 0, 0, 0);
+                }
+            }
+            unsigned k0 = (__float_as_uint(acc[0]) & ~15u);
+            unsigned k1 = (__float_as_uint(acc[1]) & ~15u) | 1u;
+            unsigned t1 = min(k0, k1), t2 = max(k0, k1);
+#pragma unroll
+            for (int i = 2; i < 16; ++i) {
+                unsigned key = (__float_as_uint(acc[i]) & ~15u) | (unsigned)i;
+                t2 = med3u(t1, t2, key);
+                t1 = min(t1, key);
+            }
+            unsigned nm2 = min(min(m2, t2), max(m1, t1));
+            mt = t1 < m1 ? (unsigned)t : mt;
+            m1 = min(m1, t1);
+            m2 = nm2;
+        }
+        // merge the two half-waves (lanes l and l^32 hold the same vector)
+        unsigned o1 = __shfl_xor(m1, 32), o2 = __shfl_xor(m2, 32), ot = __shfl_xor(mt, 32);
+        const bool other = o1 < m1;
+        const unsigned w_h = other ? (unsigned)(1 - h) : (unsigned)h;
+        const unsigned w_t = other ? ot : mt;
+        const unsigned b2 = min(min(m2, o2), max(m1, o1));
+        const unsigned b1 = min(m1, o1);
+        const unsigned reg = b1 & 15u;
+        int code = (int)(32u * w_t + (reg & 3u) + 8u * (reg >> 2) + 4u * w_h);
+        const float K1 = __uint_as_float(b1 & ~15u), K2 = __uint_as_float(b2 & ~15u);
+        const float gap = K2 - K1;
+        const bool slow = !(gap > tau + 0x1p-15f * K2) || !finite_x;
+
+        unsigned long long need = __ballot(slow && valid && h == 0);
+        if (need) {
+            slow_count += __popcll(need);
+            unsigned long long todo = need;
+            while (todo) {
+                const int rs = __ffsll((long long)todo) - 1;
+                todo &= todo - 1;
+                float xv[D];
+#pragma unroll
+                for (int j = 0; j < D; ++j)
+                    xv[j] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xs[j]), rs));
+                float best = INFINITY;
+                int bidx = 0x7FFFFFFF;
+#pragma unroll
+                for (int q = 0; q < K / 64; ++q) {
+                    const int c = lane + 64 * q;
+                    float cv[D];
+#pragma unroll
+                    for (int j = 0; j < D; ++j) cv[j] = cbase[(long long)c * D + j];
+                    const float dd = exact_dist<D>(xv, cv);
+                    if (dd < best) { best = dd; bidx = c; }
+                }
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) {
+                    const float ob = __shfl_xor(best, off);
+                    const int oi = __shfl_xor(bidx, off);
+                    if (ob < best || (ob == best && oi < bidx)) { best = ob; bidx = oi; }
+                }
+                if (lane == rs) code = bidx == 0x7FFFFFFF ? 0 : bidx;
+            }
+        }
+        if (valid && h == 0) {
+            codes[v * m_total + m] = (CodeT)code;
+            if (counts) atomicAdd(&hist[wave][code], 1u);
+        }
+    }
+    if (counts) {
+        __builtin_amdgcn_wave_barrier();
+        for (int i = lane; i < K; i += 64) {
+            uint32_t c = hist[wave][i];
+            if (c) atomicAdd(&counts[(long long)m * K + i], c);
+        }
+    }
+    if (lane == 0 && slow_count) atomicAdd(rerank, slow_count);
+}
+
+// Exact VALU kernel: one thread per (vector, part); any K, any dsub.  Used for shapes the
+// MFMA kernel is not instantiated for, for inputs with non-finite centroids, and as the
+// independent cross-check of the MFMA kernel in the GPU tests.
+template <typename CodeT>
+__global__ void pq_assign_exact(const float* __restrict__ x, long long n, long long ldx, int m_total,
+                                int k, int dsub, const float* __restrict__ cent,
+                                CodeT* __restrict__ codes, uint32_t* __restrict__ counts) {
+#pragma clang fp contract(off)
+    const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= n * m_total) return;
+    const long long v = gid / m_total;
+    const int m = (int)(gid % m_total);
+    const float* xp = x + v * ldx + (long long)m * dsub;
+    const float* cb = cent + (long long)m * k * dsub;
+    float best = INFINITY;
+    int code = 0;
+    for (int c = 0; c < k; ++c) {
+        float acc = 0.0f;
+        for (int j = 0; j < dsub; ++j) {
+            float d = __fsub_rn(xp[j], cb[(long long)c * dsub + j]);
+            acc = __fadd_rn(acc, __fmul_rn(d, d));
+        }
+        if (acc < best) { best = acc; code = c; }
+    }
+    codes[gid] = (CodeT)code;
+    if (counts) atomicAdd(&counts[(long long)m * k + code], 1u);
+}
+
+// Reconstruction error partial sums (pq_encoder.c:82-119): per (vector) double sums,
+// reduced per block; host adds the block sums in order.
+template <typename CodeT>
+__global__ void pq_error_kernel(const float* __restrict__ x, long long n, long long ldx, int m_total,
+                                int k, int dsub, const float* __restrict__ cent,
+                                const CodeT* __restrict__ codes, double* __restrict__ partial) {
+#pragma clang fp contract(off)
+    __shared__ double red[256];
+    const long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    double s = 0.0;
+    if (v < n) {
+        for (int i = 0; i < m_total; ++i) {
+            const float* c = cent + ((long long)i * k + codes[v * m_total + i]) * dsub;
+            for (int j = 0; j < dsub; ++j) {
+                float delta = __fsub_rn(x[v * ldx + (long long)i * dsub + j], c[j]);
+                s += (double)delta * (double)delta;
+            }
+        }
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+template <typename CodeT>
+__global__ void pq_reconstruct_kernel(const CodeT* __restrict__ codes, long long n, int m_total,
+                                      int k, int dsub, const float* __restrict__ cent,
+                                      float* __restrict__ out, long long ldo) {
+    const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long d = (long long)m_total * dsub;
+    if (gid >= n * d) return;
+    const long long v = gid / d;
+    const int col = (int)(gid % d);
+    const int i = col / dsub, j = col % dsub;
+    out[v * ldo + col] = cent[((long long)i * k + codes[v * m_total + i]) * dsub + j];
+}
+
+uint16_t bf16_rne(float f) {
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    if ((u & 0x7F800000u) == 0x7F800000u) return (uint16_t)(u >> 16);  // inf/nan
+    u += 0x7FFFu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+
+float bf16_to_f(uint16_t b) {
+    uint32_t u = (uint32_t)b << 16;
+    float f;
+    memcpy(&f, &u, 4);
+    return f;
+}
+
+}  // namespace
+
+struct pqh_pq {
+    pqh_ctx* ctx = nullptr;
+    int m = 0, k = 0, dsub = 0;
+    bool mfma_ok = false;
+    float* d_cent = nullptr;
+    bf16x8* d_afrag = nullptr;
+    float* d_cmax = nullptr;
+    float* d_sqc = nullptr;
+};
+
+namespace {
+
+// A_aug[row][slot] of one subspace for the pass layouts of Plan<D>
+template <int D>
+void build_afrag(const float* c, int k, std::vector<uint16_t>& out, int m, float& cmax_out) {
+    using P = Plan<D>;
+    const int slots_main = 16 * P::PM;
+    std::vector<uint16_t> main((size_t)k * slots_main, 0), lo((size_t)k * 16 * P::PL, 0);
+    double cmax = 0.0;
+    for (int row = 0; row < k; ++row) {
+        const float* cr = c + (size_t)row * D;
+        double q = 0.0;
+        for (int j = 0; j < D; ++j) {
+            q += (double)cr[j] * (double)cr[j];
+            uint16_t hi = bf16_rne(cr[j]);
+            uint16_t lw = bf16_rne(cr[j] - bf16_to_f(hi));
+            uint16_t m2hi = bf16_rne(-2.0f * bf16_to_f(hi));   // exact
+            uint16_t m2lo = bf16_rne(-2.0f * bf16_to_f(lw));   // exact
+            main[(size_t)row * slots_main + j] = m2hi;
+            main[(size_t)row * slots_main + D + j] = m2lo;
+            lo[(size_t)row * 16 * P::PL + j] = m2hi;
+        }
+        cmax = q > cmax ? q : cmax;
+        uint16_t n1 = bf16_rne((float)q);
+        double r1 = q - bf16_to_f(n1);
+        uint16_t n2 = bf16_rne((float)r1);
+        double r2 = r1 - bf16_to_f(n2);
+        uint16_t n3 = bf16_rne((float)r2);
+        main[(size_t)row * slots_main + 2 * D] = n1;
+        main[(size_t)row * slots_main + 2 * D + 1] = n2;
+        main[(size_t)row * slots_main + 2 * D + 2] = n3;
+        main[(size_t)row * slots_main + 2 * D + 3] = bf16_rne(1.0f);
+    }
+    cmax_out = (float)(cmax * (1.0 + 1e-6)) + 1e-30f;
+    // fragment order [m][PA][tile][lane][8]
+    const size_t base = (size_t)m * P::PA * kTiles * 64 * 8;
+    for (int p = 0; p < P::PA; ++p) {
+        const bool is_main = p < P::PM;
+        const std::vector<uint16_t>& src = is_main ? main : lo;
+        const int width = is_main ? slots_main : 16 * P::PL;
+        const int pp = is_main ? p : p - P::PM;
+        for (int t = 0; t < kTiles; ++t)
+            for (int lane = 0; lane < 64; ++lane)
+                for (int j = 0; j < 8; ++j) {
+                    int row = 32 * t + (lane & 31);
+                    int slot = 16 * pp + 8 * (lane >> 5) + j;
+                    out[base + (((size_t)p * kTiles + t) * 64 + lane) * 8 + j] =
+                        src[(size_t)row * width + slot];
+                }
+    }
+}
+
+template <int D>
+int pa_of() { return Plan<D>::PA; }
+
+int plan_pa(int dsub) {
+    switch (dsub) {
+        case 4: return pa_of<4>();
+        case 6: return pa_of<6>();
+        case 8: return pa_of<8>();
+        case 12: return pa_of<12>();
+        case 16: return pa_of<16>();
+        default: return 0;
+    }
+}
+
+template <typename CodeT>
+int launch_mfma(pqh_pq* pq, const float* x, long long n, long long ldx, CodeT* codes,
+                uint32_t* counts) {
+    pqh_ctx* ctx = pq->ctx;
+    const long long nblk = (n + 31) / 32;
+    const int groups = (pq->m + kWavesPerWG - 1) / kWavesPerWG;
+    long long gx = (long long)ctx->num_cus * 2 / groups;
+    if (gx < 1) gx = 1;
+    if (gx > nblk) gx = nblk;
+    dim3 grid((unsigned)gx, (unsigned)groups), block(64 * kWavesPerWG);
+    unsigned long long* rr = ctx->d_diag;
+#define PQH_CASE(DD)                                                                        \
+    case DD:                                                                                \
+        hipLaunchKernelGGL((pq_assign_mfma<DD, CodeT>), grid, block, 0, ctx->stream, x, n, \
+                           ldx, pq->m, pq->d_afrag, pq->d_cent, pq->d_cmax, pq->d_sqc,      \
+                           codes, counts, rr);                                              \
+        break;
+    switch (pq->dsub) {
+        PQH_CASE(4)
+        PQH_CASE(6)
+        PQH_CASE(8)
+        PQH_CASE(12)
+        PQH_CASE(16)
+        default: return PQH_ERR_UNSUPPORTED;
+    }
+#undef PQH_CASE
+    PQH_LAUNCH_CHECK(ctx);
+    return PQH_OK;
+}
+
+template <typename CodeT>
+int launch_exact(pqh_pq* pq, const float* x, long long n, long long ldx, CodeT* codes,
+                 uint32_t* counts) {
+    pqh_ctx* ctx = pq->ctx;
+    const long long total = n * pq->m;
+    if (total == 0) return PQH_OK;
+    hipLaunchKernelGGL((pq_assign_exact<CodeT>), dim3((unsigned)((total + 255) / 256)), dim3(256),
+                       0, ctx->stream, x, n, ldx, pq->m, pq->k, pq->dsub, pq->d_cent, codes,
+                       counts);
+    PQH_LAUNCH_CHECK(ctx);
+    return PQH_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pqh_pq_create(pqh_ctx_t* ctx, const float* centroids, int m, int k, int dsub, pqh_pq_t** out) {
+    if (!ctx || !centroids || !out || m <= 0 || k <= 0 || dsub <= 0 || k > 65536)
+        return PQH_ERR_ARG;
+    int rc = pqh_use_device(ctx);
+    if (rc) return rc;
+    pqh_pq* pq = new pqh_pq();
+    pq->ctx = ctx;
+    pq->m = m;
+    pq->k = k;
+    pq->dsub = dsub;
+    const size_t nc = (size_t)m * k * dsub;
+    bool finite = true;
+    for (size_t i = 0; i < nc; ++i) finite &= std::isfinite(centroids[i]);
+    const int pa = plan_pa(dsub);
+    pq->mfma_ok = finite && k == 256 && pa > 0;
+    if (hipMalloc(&pq->d_cent, nc * sizeof(float)) != hipSuccess) {
+        delete pq;
+        return pqh_set_error(ctx, PQH_ERR_NOMEM, "hipMalloc centroids");
+    }
+    (void)hipMemcpy(pq->d_cent, centroids, nc * sizeof(float), hipMemcpyHostToDevice);
+    if (pq->mfma_ok) {
+        std::vector<uint16_t> frag((size_t)m * pa * kTiles * 64 * 8);
+        std::vector<float> cmax(m), sqc(m);
+        for (int i = 0; i < m; ++i) {
+            const float* c = centroids + (size_t)i * k * dsub;
+            switch (dsub) {
+                case 4: build_afrag<4>(c, k, frag, i, cmax[i]); break;
+                case 6: build_afrag<6>(c, k, frag, i, cmax[i]); break;
+                case 8: build_afrag<8>(c, k, frag, i, cmax[i]); break;
+                case 12: build_afrag<12>(c, k, frag, i, cmax[i]); break;
+                case 16: build_afrag<16>(c, k, frag, i, cmax[i]); break;
+            }
+            sqc[i] = (float)(std::sqrt((double)cmax[i]) * (1.0 + 1e-6)) + 1e-30f;
+        }
+        if (hipMalloc(&pq->d_afrag, frag.size() * 2) != hipSuccess ||
+            hipMalloc(&pq->d_cmax, m * sizeof(float)) != hipSuccess ||
+            hipMalloc(&pq->d_sqc, m * sizeof(float)) != hipSuccess) {
+            pqh_pq_destroy(pq);
+            return pqh_set_error(ctx, PQH_ERR_NOMEM, "hipMalloc fragments");
+        }
+        (void)hipMemcpy(pq->d_afrag, frag.data(), frag.size() * 2, hipMemcpyHostToDevice);
+        (void)hipMemcpy(pq->d_cmax, cmax.data(), m * sizeof(float), hipMemcpyHostToDevice);
+        (void)hipMemcpy(pq->d_sqc, sqc.data(), m * sizeof(float), hipMemcpyHostToDevice);
+    }
+    *out = pq;
+    return PQH_OK;
+}
+
+int pqh_pq_destroy(pqh_pq_t* pq) {
+    if (!pq) return PQH_OK;
+    (void)hipSetDevice(pq->ctx->device);
+    (void)hipStreamSynchronize(pq->ctx->stream);
+    (void)hipFree(pq->d_cent);
+    (void)hipFree(pq->d_afrag);
+    (void)hipFree(pq->d_cmax);
+    (void)hipFree(pq->d_sqc);
+    delete pq;
+    return PQH_OK;
+}
+
+int pqh_pq_assign(pqh_ctx_t* ctx, const pqh_pq_t* cpq, const float* d_x, long long n,
+                  long long ld_x, void* d_codes, uint32_t* d_counts, int mode) {
+    pqh_pq* pq = const_cast<pqh_pq*>(cpq);
+    if (!ctx || !pq || pq->ctx != ctx || (n > 0 && (!d_x || !d_codes)) || n < 0 ||
+        ld_x < (long long)pq->m * pq->dsub)
+        return PQH_ERR_ARG;
+    int rc = pqh_use_device(ctx);
+    if (rc) return rc;
+    PQH_HIP(ctx, hipMemsetAsync(ctx->d_diag, 0, sizeof(unsigned long long), ctx->stream));
+    if (n == 0) return PQH_OK;
+    bool mfma = mode == 0 && pq->mfma_ok;
+    if (mfma && pq->dsub % 4 == 0 &&
+        ((ld_x % 4) != 0 || (reinterpret_cast<uintptr_t>(d_x) & 15u) != 0))
+        mfma = false;  // vector loads need 16-byte aligned subspace slices
+    if (pq->k <= 256) {
+        uint8_t* c = static_cast<uint8_t*>(d_codes);
+        return mfma ? launch_mfma(pq, d_x, n, ld_x, c, d_counts)
+                    : launch_exact(pq, d_x, n, ld_x, c, d_counts);
+    }
+    return launch_exact(pq, d_x, n, ld_x, static_cast<uint16_t*>(d_codes), d_counts);
+}
+
+int pqh_pq_last_rerank_count(pqh_ctx_t* ctx, unsigned long long* count) {
+    if (!ctx || !count) return PQH_ERR_ARG;
+    PQH_HIP(ctx, hipMemcpyAsync(count, ctx->d_diag, sizeof(unsigned long long),
+                                hipMemcpyDeviceToHost, ctx->stream));
+    PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return PQH_OK;
+}
+
+int pqh_pq_error(pqh_ctx_t* ctx, const pqh_pq_t* pq, const float* d_x, long long n,
+                 long long ld_x, const void* d_codes, double* error_out) {
+    if (!ctx || !pq || !error_out || n <= 0) return PQH_ERR_ARG;
+    int rc = pqh_use_device(ctx);
+    if (rc) return rc;
+    const long long blocks = (n + 255) / 256;
+    rc = pqh_ensure_ws(ctx, blocks * sizeof(double));
+    if (rc) return rc;
+    double* part = static_cast<double*>(ctx->ws);
+    if (pq->k <= 256)
+        hipLaunchKernelGGL(pq_error_kernel<uint8_t>, dim3((unsigned)blocks), dim3(256), 0, ctx->stream,
+                           d_x, n, ld_x, pq->m, pq->k, pq->dsub, pq->d_cent,
+                           static_cast<const uint8_t*>(d_codes), part);
+    else
+        hipLaunchKernelGGL(pq_error_kernel<uint16_t>, dim3((unsigned)blocks), dim3(256), 0, ctx->stream,
+                           d_x, n, ld_x, pq->m, pq->k, pq->dsub, pq->d_cent,
+                           static_cast<const uint16_t*>(d_codes), part);
+    PQH_LAUNCH_CHECK(ctx);
+    std::vector<double> h(blocks);
+    PQH_HIP(ctx, hipMemcpyAsync(h.data(), part, blocks * sizeof(double), hipMemcpyDeviceToHost,
+                                ctx->stream));
+    PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    double s = 0.0;
+    for (double v : h) s += v;
+    *error_out = s / (double)n;
+    return PQH_OK;
+}
+
+int pqh_pq_reconstruct(pqh_ctx_t* ctx, const pqh_pq_t* pq, const void* d_codes, long long n,
+                       float* d_out, long long ld_out) {
+    if (!ctx || !pq || n < 0 || ld_out < (long long)pq->m * pq->dsub) return PQH_ERR_ARG;
+    int rc = pqh_use_device(ctx);
+    if (rc) return rc;
+    const long long total = n * pq->m * pq->dsub;
+    if (!total) return PQH_OK;
+    const unsigned blocks = (unsigned)((total + 255) / 256);
+    if (pq->k <= 256)
+        hipLaunchKernelGGL(pq_reconstruct_kernel<uint8_t>, dim3(blocks), dim3(256), 0, ctx->stream,
+                           static_cast<const uint8_t*>(d_codes), n, pq->m, pq->k, pq->dsub,
+                           pq->d_cent, d_out, ld_out);
+    else
+        hipLaunchKernelGGL(pq_reconstruct_kernel<uint16_t>, dim3(blocks), dim3(256), 0, ctx->stream,
+                           static_cast<const uint16_t*>(d_codes), n, pq->m, pq->k, pq->dsub,
+                           pq->d_cent, d_out, ld_out);
+    PQH_LAUNCH_CHECK(ctx);
+    return PQH_OK;
+}
+
+}  // extern "C"

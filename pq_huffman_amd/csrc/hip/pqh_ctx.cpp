@@ -1,0 +1,118 @@
+// pqh_ctx.cpp -- context, error and scratch management for the pqh C ABI (pqh.h).
+#include <cstdlib>
+#include <cstring>
+
+#include "pqh_internal.h"
+
+int pqh_set_error(pqh_ctx* ctx, int code, const char* fmt, ...) {
+    if (ctx) {
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(ctx->err, sizeof(ctx->err), fmt, ap);
+        va_end(ap);
+    }
+    return code;
+}
+
+int pqh_use_device(pqh_ctx* ctx) {
+    PQH_HIP(ctx, hipSetDevice(ctx->device));
+    return PQH_OK;
+}
+
+int pqh_ensure_ws(pqh_ctx* ctx, size_t bytes) {
+    if (bytes <= ctx->ws_bytes) return PQH_OK;
+    if (ctx->ws) {
+        PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        PQH_HIP(ctx, hipFree(ctx->ws));
+        ctx->ws = nullptr;
+    }
+    size_t want = bytes + bytes / 4 + 4096;
+    PQH_HIP(ctx, hipMalloc(&ctx->ws, want));
+    ctx->ws_bytes = want;
+    return PQH_OK;
+}
+
+extern "C" {
+
+int pqh_device_count(int* count) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return n > 0 ? PQH_OK : PQH_ERR_NO_DEVICE;
+}
+
+int pqh_ctx_create(pqh_ctx_t** out, int device) {
+    if (!out) return PQH_ERR_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return PQH_ERR_NO_DEVICE;
+    if (device < 0 || device >= n) return PQH_ERR_ARG;
+    pqh_ctx* ctx = new pqh_ctx();
+    ctx->device = device;
+    if (hipSetDevice(device) != hipSuccess) {
+        delete ctx;
+        return PQH_ERR_HIP;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+        ctx->num_cus = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return PQH_ERR_HIP;
+    }
+    ctx->own_stream = true;
+    if (hipMalloc(&ctx->d_diag, 8 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(ctx->d_diag, 0, 8 * sizeof(unsigned long long)) != hipSuccess) {
+        delete ctx;
+        return PQH_ERR_HIP;
+    }
+    *out = ctx;
+    return PQH_OK;
+}
+
+int pqh_ctx_destroy(pqh_ctx_t* ctx) {
+    if (!ctx) return PQH_OK;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->ws) (void)hipFree(ctx->ws);
+    if (ctx->d_diag) (void)hipFree(ctx->d_diag);
+    if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return PQH_OK;
+}
+
+int pqh_ctx_set_stream(pqh_ctx_t* ctx, void* hip_stream) {
+    if (!ctx) return PQH_ERR_ARG;
+    if (ctx->own_stream) {
+        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipStreamDestroy(ctx->stream);
+        ctx->own_stream = false;
+    }
+    ctx->stream = (hipStream_t)hip_stream;
+    return PQH_OK;
+}
+
+int pqh_ctx_sync(pqh_ctx_t* ctx) {
+    if (!ctx) return PQH_ERR_ARG;
+    PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return PQH_OK;
+}
+
+const char* pqh_ctx_last_error(const pqh_ctx_t* ctx) { return ctx ? ctx->err : "no context"; }
+
+const char* pqh_status_string(int s) {
+    switch (s) {
+        case PQH_OK: return "ok";
+        case PQH_ERR_ARG: return "invalid argument";
+        case PQH_ERR_NO_DEVICE: return "no HIP device";
+        case PQH_ERR_HIP: return "HIP runtime error";
+        case PQH_ERR_UNSUPPORTED: return "unsupported configuration";
+        case PQH_ERR_CODE_TOO_LONG: return "Huffman code longer than 56 bits";
+        case PQH_ERR_CORRUPT: return "corrupt stream";
+        case PQH_ERR_NOMEM: return "out of memory";
+        case PQH_ERR_CAPACITY: return "output buffer too small";
+        default: return "unknown status";
+    }
+}
+
+}  // extern "C"

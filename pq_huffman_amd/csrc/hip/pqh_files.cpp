@@ -1,0 +1,264 @@
+// pqh_files.cpp -- whole-file encode/decode on top of the pqh GPU calls, used by the CLI
+// tools (csrc/tools).  Produces exactly the reference's files (huffman_encoder.c:306-439):
+//   huffman_codebooks.bin  u32 m + m x huffman_codebook_save
+//   huffman_indices.bin    u64 N + stream (zero padded)
+//   huffman_stats.txt      JSON line appended (stats.c)
+// plus the decode sidecar huffman_chunks.bin (pqh extension, see pqh.h).
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "pqh_internal.h"
+#include "stats.h"
+
+namespace {
+
+struct Sidecar {
+    char magic[4];
+    uint32_t version, m, k, context, chunk_vectors, raw_first;
+    uint64_t n, chunks;
+};
+
+struct CtxGuard {
+    pqh_ctx_t* ctx = nullptr;
+    ~CtxGuard() { pqh_ctx_destroy(ctx); }
+};
+
+template <typename T>
+struct DevBuf {
+    T* p = nullptr;
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+    int alloc(pqh_ctx* ctx, size_t count) {
+        PQH_HIP(ctx, hipMalloc(&p, count * sizeof(T) + 16));
+        return PQH_OK;
+    }
+};
+
+std::string path_of(const char* prefix, const char* name) { return std::string(prefix) + name; }
+
+}  // namespace
+
+extern "C" int pqh_encode_files(const unsigned char* codes, long long n, int m,
+                                const pqh_encode_options_t* options, const char* out_prefix) {
+    const int k = 256;
+    pqh_encode_options_t opt = {1, 1, 64, 0};
+    if (options) opt = *options;
+    if (!codes || n < 0 || m <= 0 || m > 16 || !out_prefix) return PQH_ERR_ARG;
+    if (opt.chunk_vectors <= 0) opt.chunk_vectors = 64;
+    if (opt.context && n == 0) return PQH_ERR_ARG;  // the reference asserts (huffman_encoder.c:198)
+    CtxGuard g;
+    int rc = pqh_ctx_create(&g.ctx, 0);
+    if (rc) return rc;
+    pqh_ctx* ctx = g.ctx;
+    const long long items = opt.context ? (long long)k * k : k;
+    DevBuf<unsigned char> d_codes;
+    DevBuf<uint32_t> d_counts;
+    if ((rc = d_codes.alloc(ctx, (size_t)n * m)) || (rc = d_counts.alloc(ctx, (size_t)m * items)))
+        return rc;
+    PQH_HIP(ctx, hipMemcpyAsync(d_codes.p, codes, (size_t)n * m, hipMemcpyHostToDevice, ctx->stream));
+    if (opt.sort) {
+        DevBuf<unsigned char> tmp;
+        if ((rc = tmp.alloc(ctx, (size_t)n * m))) return rc;
+        if ((rc = pqh_sort_rows(ctx, d_codes.p, n, m, tmp.p))) return rc;
+    }
+    PQH_HIP(ctx, hipMemsetAsync(d_counts.p, 0, (size_t)m * items * 4, ctx->stream));
+    if ((rc = pqh_histogram(ctx, d_codes.p, n, m, k, opt.context, nullptr, d_counts.p))) return rc;
+    // codes are built on the GPU from the device histogram (pqh_tables_build); the host
+    // copies feed huffman_codebooks.bin and the stats line
+    pqh_tables_t* tab = nullptr;
+    if ((rc = pqh_tables_alloc(ctx, m, k, opt.context, &tab))) return rc;
+    rc = pqh_tables_build(ctx, tab, d_counts.p);
+    std::vector<huffman_codebook_t> cbs(m);
+    if (!rc) rc = pqh_tables_codebooks(ctx, tab, cbs.data());
+    if (rc) {
+        pqh_tables_destroy(tab);
+        return rc;
+    }
+    std::vector<uint32_t> hc((size_t)m * items);
+    PQH_HIP(ctx, hipMemcpyAsync(hc.data(), d_counts.p, hc.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
+    PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    std::vector<double> counts(hc.begin(), hc.end());
+
+    huffman_stats_t st;
+    huffman_stats_init(&st, n, m, k);
+    st.num_roots = opt.context ? 1 : 0;
+    for (int i = 0; i < m; ++i)
+        huffman_stats_push(&st, i, huffman_estimate_size(&cbs[i], counts.data() + i * items));
+    huffman_stats_print(&st);
+    huffman_stats_print_filename(&st, path_of(out_prefix, "huffman_stats.txt").c_str());
+    huffman_stats_destroy(&st);
+    if (opt.only_estimate) {
+        for (auto& cb : cbs) huffman_codebook_destroy(&cb);
+        pqh_tables_destroy(tab);
+        return PQH_OK;
+    }
+
+    FILE* cf = fopen(path_of(out_prefix, "huffman_codebooks.bin").c_str(), "wb");
+    if (!cf) {
+        pqh_tables_destroy(tab);
+        return pqh_set_error(ctx, PQH_ERR_ARG, "cannot write codebooks");
+    }
+    uint32_t mu = (uint32_t)m;
+    fwrite(&mu, 4, 1, cf);
+    for (int i = 0; i < m; ++i) huffman_codebook_save(&cbs[i], cf);
+    fclose(cf);
+    for (auto& cb : cbs) huffman_codebook_destroy(&cb);
+
+    DevBuf<unsigned long long> d_total;
+    const long long chunks = (n + opt.chunk_vectors - 1) / opt.chunk_vectors;
+    DevBuf<unsigned long long> d_coff;
+    DevBuf<unsigned char> d_cprev;
+    if ((rc = d_total.alloc(ctx, 1)) || (rc = d_coff.alloc(ctx, chunks + 1)) ||
+        (rc = d_cprev.alloc(ctx, (size_t)(chunks + 1) * m))) {
+        pqh_tables_destroy(tab);
+        return rc;
+    }
+    rc = pqh_encode_size(ctx, tab, d_codes.p, n, 1, nullptr, d_total.p);
+    unsigned long long total = 0;
+    if (!rc) {
+        PQH_HIP(ctx, hipMemcpyAsync(&total, d_total.p, 8, hipMemcpyDeviceToHost, ctx->stream));
+        PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    const unsigned long long bytes = (total + 7) / 8, wbytes = ((total + 31) / 32) * 4 + 4;
+    DevBuf<unsigned char> d_out;
+    if (!rc) rc = d_out.alloc(ctx, wbytes);
+    if (!rc) {
+        PQH_HIP(ctx, hipMemsetAsync(d_out.p, 0, wbytes, ctx->stream));
+        rc = pqh_encode_write(ctx, tab, d_codes.p, n, 1, nullptr, 0, d_out.p, wbytes,
+                              opt.chunk_vectors, d_coff.p, d_cprev.p);
+        if (!rc) rc = pqh_encode_status(ctx);
+    }
+    pqh_tables_destroy(tab);
+    if (rc) return rc;
+    std::vector<unsigned char> stream(bytes + 1);
+    std::vector<unsigned long long> coff(chunks + 1);
+    std::vector<unsigned char> cprev((size_t)(chunks + 1) * m);
+    PQH_HIP(ctx, hipMemcpyAsync(stream.data(), d_out.p, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    PQH_HIP(ctx, hipMemcpyAsync(coff.data(), d_coff.p, chunks * 8, hipMemcpyDeviceToHost, ctx->stream));
+    PQH_HIP(ctx, hipMemcpyAsync(cprev.data(), d_cprev.p, (size_t)chunks * m, hipMemcpyDeviceToHost,
+                                ctx->stream));
+    PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+
+    FILE* ef = fopen(path_of(out_prefix, "huffman_indices.bin").c_str(), "wb");
+    if (!ef) return pqh_set_error(ctx, PQH_ERR_ARG, "cannot write indices");
+    unsigned long long nn = (unsigned long long)n;
+    fwrite(&nn, 8, 1, ef);
+    fwrite(stream.data(), 1, bytes, ef);
+    fclose(ef);
+
+    FILE* sf = fopen(path_of(out_prefix, "huffman_chunks.bin").c_str(), "wb");
+    if (sf) {
+        Sidecar h;
+        memcpy(h.magic, "PQHC", 4);
+        h.version = 1;
+        h.m = m;
+        h.k = k;
+        h.context = opt.context;
+        h.chunk_vectors = opt.chunk_vectors;
+        h.raw_first = 1;
+        h.n = n;
+        h.chunks = chunks;
+        fwrite(&h, sizeof(h), 1, sf);
+        fwrite(coff.data(), 8, chunks, sf);
+        if (opt.context) fwrite(cprev.data(), 1, (size_t)chunks * m, sf);
+        fclose(sf);
+    }
+    return PQH_OK;
+}
+
+extern "C" int pqh_decode_files(const char* in_prefix, unsigned char** codes_out, long long* n_out,
+                                int* m_out) {
+    if (!in_prefix || !codes_out || !n_out || !m_out) return PQH_ERR_ARG;
+    *codes_out = nullptr;
+    FILE* cf = fopen(path_of(in_prefix, "huffman_codebooks.bin").c_str(), "rb");
+    if (!cf) return PQH_ERR_ARG;
+    uint32_t m = 0;
+    if (fread(&m, 4, 1, cf) != 1 || m == 0 || m > 16) {
+        fclose(cf);
+        return PQH_ERR_CORRUPT;
+    }
+    std::vector<huffman_codebook_t> cbs(m);
+    for (uint32_t i = 0; i < m; ++i) huffman_codebook_load(&cbs[i], cf);
+    fclose(cf);
+    FILE* ef = fopen(path_of(in_prefix, "huffman_indices.bin").c_str(), "rb");
+    if (!ef) return PQH_ERR_ARG;
+    unsigned long long n = 0;
+    if (fread(&n, 8, 1, ef) != 1) n = 0;
+    fseek(ef, 0, SEEK_END);
+    const long long fsize = ftell(ef);
+    fseek(ef, 8, SEEK_SET);
+    const unsigned long long bytes = fsize > 8 ? (unsigned long long)(fsize - 8) : 0;
+    const unsigned long long wbytes = ((bytes + 3) / 4) * 4 + 8;
+    std::vector<unsigned char> stream(wbytes, 0);
+    if (bytes && fread(stream.data(), 1, bytes, ef) != bytes) {
+        fclose(ef);
+        return PQH_ERR_CORRUPT;
+    }
+    fclose(ef);
+
+    CtxGuard g;
+    int rc = pqh_ctx_create(&g.ctx, 0);
+    if (rc) return rc;
+    pqh_ctx* ctx = g.ctx;
+    pqh_tables_t* tab = nullptr;
+    rc = pqh_tables_create(ctx, cbs.data(), (int)m, &tab);
+    const int context = cbs[0].is_context;
+    const int k = cbs[0].alphabet_size;
+    for (auto& cb : cbs) huffman_codebook_destroy(&cb);
+    if (rc) return rc;
+    const size_t esz = k <= 256 ? 1 : 2;
+
+    // chunk index: sidecar when it matches, else a host walk of the stream
+    int C = 64;
+    std::vector<unsigned long long> coff;
+    std::vector<unsigned char> cprev;
+    bool have = false;
+    FILE* sf = fopen(path_of(in_prefix, "huffman_chunks.bin").c_str(), "rb");
+    if (sf) {
+        Sidecar h;
+        if (fread(&h, sizeof(h), 1, sf) == 1 && !memcmp(h.magic, "PQHC", 4) && h.n == n &&
+            h.m == m && h.context == (uint32_t)context && h.chunk_vectors > 0 && h.raw_first == 1) {
+            C = (int)h.chunk_vectors;
+            coff.resize(h.chunks + 1);
+            cprev.resize((h.chunks + 1) * m * esz);
+            have = fread(coff.data(), 8, h.chunks, sf) == h.chunks;
+            if (have && context) have = fread(cprev.data(), esz, h.chunks * m, sf) == h.chunks * m;
+        }
+        fclose(sf);
+    }
+    const long long chunks = ((long long)n + C - 1) / C;
+    if (!have) {
+        coff.assign(chunks + 1, 0);
+        cprev.assign((chunks + 1) * m * esz, 0);
+        rc = pqh_chunk_index_host(tab, stream.data(), bytes, (long long)n, 1, C, coff.data(),
+                                  cprev.data());
+        if (rc) {
+            pqh_tables_destroy(tab);
+            return rc;
+        }
+    }
+    DevBuf<unsigned char> d_stream, d_cprev, d_codes;
+    DevBuf<unsigned long long> d_coff;
+    if ((rc = d_stream.alloc(ctx, wbytes)) || (rc = d_coff.alloc(ctx, chunks + 1)) ||
+        (rc = d_cprev.alloc(ctx, (chunks + 1) * m * esz)) || (rc = d_codes.alloc(ctx, n * m * esz))) {
+        pqh_tables_destroy(tab);
+        return rc;
+    }
+    PQH_HIP(ctx, hipMemcpyAsync(d_stream.p, stream.data(), wbytes, hipMemcpyHostToDevice, ctx->stream));
+    PQH_HIP(ctx, hipMemcpyAsync(d_coff.p, coff.data(), (chunks + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+    PQH_HIP(ctx, hipMemcpyAsync(d_cprev.p, cprev.data(), (chunks + 1) * m * esz, hipMemcpyHostToDevice,
+                                ctx->stream));
+    rc = pqh_decode(ctx, tab, d_stream.p, wbytes, (long long)n, 1, C, d_coff.p, d_cprev.p, d_codes.p);
+    if (!rc) rc = pqh_decode_status(ctx);
+    pqh_tables_destroy(tab);
+    if (rc) return rc;
+    unsigned char* out = (unsigned char*)malloc(n * m * esz + 1);
+    PQH_HIP(ctx, hipMemcpy(out, d_codes.p, n * m * esz, hipMemcpyDeviceToHost));
+    *codes_out = out;
+    *n_out = (long long)n;
+    *m_out = (int)m;
+    return PQH_OK;
+}

@@ -1,0 +1,83 @@
+// pqh_internal.h -- shared internals of the pq_huffman_amd GPU library (not installed).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+
+#include "pqh.h"
+
+struct pqh_tables;
+
+// encode_size -> encode_write hand-off key: the write pass reuses the size pass's block
+// totals only when they were computed for the same call arguments.
+struct pqh_enc_key {
+    const void* codes = nullptr;
+    long long n = -1;
+    const pqh_tables* t = nullptr;
+    int raw_first = -1;
+    const void* prev = nullptr;
+};
+
+struct pqh_ctx {
+    int device = 0;
+    int num_cus = 256;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    char err[512] = {0};
+    // grow-only scratch (stream ordered use, allocated outside timed regions)
+    void* ws = nullptr;
+    size_t ws_bytes = 0;
+    // [0] rerank count, [1] decode error, [2] encode capacity error, [3] scratch total bits
+    unsigned long long* d_diag = nullptr;
+    pqh_enc_key enc_key;
+};
+
+int pqh_set_error(pqh_ctx* ctx, int code, const char* fmt, ...);
+int pqh_ensure_ws(pqh_ctx* ctx, size_t bytes);
+int pqh_use_device(pqh_ctx* ctx);
+
+#define PQH_HIP(ctx, expr)                                                                \
+    do {                                                                                  \
+        hipError_t _e = (expr);                                                           \
+        if (_e != hipSuccess)                                                             \
+            return pqh_set_error((ctx), PQH_ERR_HIP, "%s:%d %s: %s", __FILE__, __LINE__,  \
+                                 #expr, hipGetErrorString(_e));                          \
+    } while (0)
+
+#define PQH_LAUNCH_CHECK(ctx) PQH_HIP(ctx, hipGetLastError())
+
+// Device-side code tables shared by the encode and decode kernels (pqh_tables.hip).
+//   enc [m][items] u64: (len << 56) | code (right-aligned, len <= 56; 0 = no code)
+//   Decode: two-level lookup per alphabet (tables = m * roots, roots = K in context mode)
+//   lut1 [tables][1 << l1_bits] u16, first W1_t = min(longest code, l1_bits) entries used:
+//        (len << 12) | sym for 1 <= len <= W1_t; (15 << 12) | sub = longer code, subtable
+//        `sub` of this alphabet; 0 = invalid prefix
+//   meta [tables] u32: (first descriptor << 8) | W1_t
+//   desc [..] u32: (offset in lut2 << 4) | w2 -- subtable of 2^w2 entries for the bits
+//        after the W1_t-bit prefix: (len2 << 12) | sym, 15 << 12 = even longer (linear
+//        search in longs), 0 = invalid
+//   longs [tables][k] {code, len, sym}, long_cnt [tables]: codes beyond both levels
+struct pqh_long_code {
+    unsigned long long code;
+    uint32_t len;
+    uint32_t sym;
+};
+
+struct pqh_tables {
+    pqh_ctx* ctx = nullptr;
+    int m = 0, k = 0, context = 0, roots = 1, l1_bits = 9, l2_bits = 8;
+    long long items = 0, tables = 0;
+    long long lut2_cap = 0, desc_cap = 0;
+    unsigned long long* d_enc = nullptr;
+    uint16_t* d_lut1 = nullptr;
+    uint16_t* d_lut2 = nullptr;
+    uint32_t* d_meta = nullptr;
+    uint32_t* d_desc = nullptr;
+    uint32_t* d_scratch = nullptr;   // per-table sizes for the allocation scan
+    pqh_long_code* d_long = nullptr;
+    uint32_t* d_long_cnt = nullptr;
+    uint32_t* d_err = nullptr;       // [0] code too long
+};

@@ -1,0 +1,816 @@
+// pqh_tables.hip -- Huffman code tables built on the GPU, and the chunked stream decoder.
+//
+//  huff_trees   huffman_codebook_init_encoder + collect_codes (huffman_encode.c:33-192,
+//               :100-132) for every (part, previous-symbol) alphabet at once: one lane per
+//               tree simulates the reference's binary heap step for step -- same push
+//               (sift up while strictly lighter), same pop (left child unless the right one
+//               is strictly lighter), leaves pushed in symbol order, first pop = child 0 --
+//               so the tree, and therefore every code, is the reference's.  Heap entries
+//               carry (weight << 16 | node) so a comparison is one LDS read; all per-tree
+//               arrays are interleaved tree-minor so the 32 lanes of a wave hit 32
+//               consecutive LDS words.
+//  lut_plan/alloc/fill  two-level decode tables per alphabet: a first level of up to 2^11
+//               entries (2^9 in context mode, where there are K*m alphabets), second-level
+//               subtables for the prefixes of longer codes, allocated by a device scan.
+//  dec_chunks   huffman_decoder.c:211-255: one lane per chunk of C vectors; a symbol costs
+//               one table load instead of one trie step per bit (huffman_decode.c:137-191).
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "pqh_internal.h"
+
+namespace {
+
+constexpr int kMaxCodeLen = 56;
+constexpr unsigned long long kCodeMask = (1ull << 56) - 1;
+
+// ------------------------------------------------------------------- tree building
+template <int KMAX, int TPW>
+__global__ void __launch_bounds__(64)
+huff_trees(const uint32_t* __restrict__ counts, int k, long long trees,
+           unsigned long long* __restrict__ enc, uint32_t* __restrict__ err) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    unsigned long long* heap = reinterpret_cast<unsigned long long*>(lds);  // [KMAX][TPW]
+    uint32_t* kid = reinterpret_cast<uint32_t*>(heap + KMAX * TPW);          // [KMAX][TPW]
+    uint32_t* smeta = kid + KMAX * TPW;                                       // [KMAX][TPW]
+    uint16_t* lsym = reinterpret_cast<uint16_t*>(smeta + KMAX * TPW);        // [KMAX][TPW]
+    const int t = threadIdx.x;
+    if (t >= TPW) return;  // no barriers in this kernel
+    const long long tree = (long long)blockIdx.x * TPW + t;
+    if (tree >= trees) return;
+    const uint32_t* cnt = counts + tree * k;
+    unsigned long long* out = enc + tree * k;
+#define H(i) heap[(i) * TPW + t]
+    int size = 0;
+    auto push = [&](unsigned long long e) {
+        int i = size++;
+        const unsigned long long w = e >> 16;
+        while (i > 0) {
+            const int p = (i - 1) >> 1;
+            const unsigned long long hp = H(p);
+            if (w >= (hp >> 16)) break;
+            H(i) = hp;
+            i = p;
+        }
+        H(i) = e;
+    };
+    auto pop = [&]() -> unsigned long long {
+        const unsigned long long top = H(0);
+        const unsigned long long last = H(--size);
+        const unsigned long long w = last >> 16;
+        int i = 0;
+        for (;;) {
+            const int l = 2 * i + 1, r = l + 1;
+            int nx = -1;
+            unsigned long long hl = 0, hr = 0;
+            if (l < size) {
+                hl = H(l);
+                if (r < size) {
+                    hr = H(r);
+                    if ((hl >> 16) <= (hr >> 16)) {
+                        if (w > (hl >> 16)) nx = l;
+                    } else if (w > (hr >> 16)) {
+                        nx = r;
+                    }
+                } else if (w > (hl >> 16)) {
+                    nx = l;
+                }
+            }
+            if (nx < 0) break;
+            H(i) = nx == l ? hl : hr;
+            i = nx;
+        }
+        H(i) = last;
+        return top;
+    };
+    int nz = 0;
+    for (int s = 0; s < k; ++s) {
+        const uint32_t c = cnt[s];
+        out[s] = 0;
+        if (c) {
+            lsym[nz * TPW + t] = (uint16_t)s;
+            push(((unsigned long long)c << 16) | (unsigned)nz);
+            ++nz;
+        }
+    }
+    if (nz == 0) return;
+    int next = nz;
+    if (size == 1) {  // lone symbol: code "0" (huffman_encode.c:168-177)
+        const unsigned long long e = pop();
+        kid[(next - nz) * TPW + t] = (uint32_t)(e & 0xFFFFu) | 0xFFFF0000u;
+        push(((e >> 16) << 16) | (unsigned)next);
+        ++next;
+    }
+    while (size > 1) {
+        const unsigned long long a = pop();
+        const unsigned long long b = pop();
+        kid[(next - nz) * TPW + t] = (uint32_t)(a & 0xFFFFu) | ((uint32_t)(b & 0xFFFFu) << 16);
+        push((((a >> 16) + (b >> 16)) << 16) | (unsigned)next);
+        ++next;
+    }
+    // depth-first code assignment; heap slots hold the codes of the stacked nodes
+    int sp = 0;
+    smeta[0 * TPW + t] = (uint32_t)(H(0) & 0xFFFFu);
+    H(0) = 0;
+    sp = 1;
+    bool too_long = false;
+    while (sp) {
+        --sp;
+        const uint32_t meta = smeta[sp * TPW + t];
+        const unsigned long long code = H(sp);
+        const int node = (int)(meta & 0xFFFFu), depth = (int)(meta >> 16);
+        if (node < nz) {
+            if (depth > kMaxCodeLen) too_long = true;
+            else out[lsym[node * TPW + t]] = ((unsigned long long)depth << 56) | code;
+            continue;
+        }
+        const uint32_t kk = kid[(node - nz) * TPW + t];
+        const uint32_t c0 = kk & 0xFFFFu, c1 = kk >> 16;
+        smeta[sp * TPW + t] = c0 | ((uint32_t)(depth + 1) << 16);
+        H(sp) = code << 1;
+        ++sp;
+        if (c1 != 0xFFFFu) {
+            smeta[sp * TPW + t] = c1 | ((uint32_t)(depth + 1) << 16);
+            H(sp) = (code << 1) | 1ull;
+            ++sp;
+        }
+    }
+    if (too_long) atomicOr(err, 1u);
+#undef H
+}
+
+// Two-level decode tables.  Block per alphabet; lut_plan sizes, lut_alloc (one workgroup)
+// scans the sizes into sub-pool offsets, lut_fill writes the entries.
+constexpr int kL1Max = 11;
+
+__device__ void block_w2max(const unsigned long long* e, int k, int w1, int l2_bits,
+                            uint32_t* w2max /* LDS [1 << kL1Max] */) {
+    for (int i = threadIdx.x; i < (1 << w1); i += blockDim.x) w2max[i] = 0;
+    __syncthreads();
+    for (int s = threadIdx.x; s < k; s += blockDim.x) {
+        const unsigned long long v = e[s];
+        const int len = (int)(v >> 56);
+        if (len > w1) {
+            const unsigned p = (unsigned)((v & kCodeMask) >> (len - w1));
+            atomicMax(&w2max[p], (uint32_t)min(len - w1, l2_bits));
+        }
+    }
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(256)
+lut_plan(const unsigned long long* __restrict__ enc, int k, long long tables, int l1_bits,
+         int l2_bits, uint32_t* __restrict__ meta, uint32_t* __restrict__ sizes) {
+    __shared__ uint32_t w2max[1 << kL1Max];
+    __shared__ uint32_t red[4];
+    const long long t = blockIdx.x;
+    const unsigned long long* e = enc + t * k;
+    int mx = 1;
+    for (int s = threadIdx.x; s < k; s += blockDim.x) mx = max(mx, (int)(e[s] >> 56));
+    for (int off = 32; off >= 1; off >>= 1) mx = max(mx, __shfl_xor(mx, off));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = (uint32_t)mx;
+    __syncthreads();
+    const int maxlen = (int)max(max(red[0], red[1]), max(red[2], red[3]));
+    const int w1 = min(maxlen, l1_bits);
+    block_w2max(e, k, w1, l2_bits, w2max);
+    uint32_t nsub = 0, entries = 0;
+    for (int i = threadIdx.x; i < (1 << w1); i += blockDim.x)
+        if (w2max[i]) {
+            ++nsub;
+            entries += 1u << w2max[i];
+        }
+    for (int off = 32; off >= 1; off >>= 1) {
+        nsub += __shfl_xor(nsub, off);
+        entries += __shfl_xor(entries, off);
+    }
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = nsub;
+    __syncthreads();
+    const uint32_t tn = red[0] + red[1] + red[2] + red[3];
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = entries;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        meta[t] = (uint32_t)w1;
+        sizes[t] = tn;
+        sizes[tables + t] = red[0] + red[1] + red[2] + red[3];
+    }
+}
+
+// one workgroup: exclusive scans of descriptor counts and sub-pool entries; an alphabet that
+// does not fit the capacities keeps only its first level (flag 0x80: long codes searched)
+__global__ void __launch_bounds__(1024)
+lut_alloc(long long tables, long long desc_cap, long long lut2_cap, uint32_t* __restrict__ meta,
+          uint32_t* __restrict__ sizes) {
+    __shared__ unsigned long long ws[2][16];
+    __shared__ unsigned long long carry[2];
+    if (threadIdx.x < 2) carry[threadIdx.x] = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (long long base = 0; base < tables; base += blockDim.x) {
+        const long long i = base + threadIdx.x;
+        const unsigned long long a = i < tables ? sizes[i] : 0, b = i < tables ? sizes[tables + i] : 0;
+        unsigned long long ia = a, ib = b;
+        for (int off = 1; off < 64; off <<= 1) {
+            const unsigned long long ya = __shfl_up(ia, off), yb = __shfl_up(ib, off);
+            if (lane >= off) {
+                ia += ya;
+                ib += yb;
+            }
+        }
+        if (lane == 63) {
+            ws[0][wid] = ia;
+            ws[1][wid] = ib;
+        }
+        __syncthreads();
+        unsigned long long ba = carry[0], bb = carry[1];
+        for (int q = 0; q < wid; ++q) {
+            ba += ws[0][q];
+            bb += ws[1][q];
+        }
+        if (i < tables) {
+            const unsigned long long d0 = ba + ia - a, l0 = bb + ib - b;
+            const bool fits = d0 + a <= (unsigned long long)desc_cap && l0 + b <= (unsigned long long)lut2_cap;
+            const uint32_t w1 = meta[i] & 15u;
+            meta[i] = fits ? (uint32_t)((d0 << 8) | w1) : (0x80u | w1);
+            sizes[i] = fits ? (uint32_t)l0 : 0u;   // lut2 offset of this alphabet
+        }
+        __syncthreads();
+        if (threadIdx.x == blockDim.x - 1) {
+            carry[0] = ba + ia;
+            carry[1] = bb + ib;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void __launch_bounds__(256)
+lut_fill(const unsigned long long* __restrict__ enc, int k, int l2_bits, const uint32_t* __restrict__ meta,
+         const uint32_t* __restrict__ sizes, uint16_t* __restrict__ lut1, uint16_t* __restrict__ lut2,
+         uint32_t* __restrict__ desc, pqh_long_code* __restrict__ longs,
+         uint32_t* __restrict__ long_cnt) {
+    __shared__ uint32_t w2max[1 << kL1Max];
+    __shared__ uint32_t sub_id[1 << kL1Max];
+    __shared__ uint32_t sub_off[1 << kL1Max];
+    __shared__ uint32_t nlong;
+    __shared__ uint32_t part[256][2];
+    const long long t = blockIdx.x;
+    const unsigned long long* e = enc + t * k;
+    const uint32_t mt = meta[t];
+    const int w1 = (int)(mt & 15u);
+    const bool subs = !(mt & 0x80u);
+    const uint32_t dbase = mt >> 8, l2base = sizes[t];
+    uint16_t* L1 = lut1 + (t << kL1Max);
+    block_w2max(e, k, w1, l2_bits, w2max);
+    // sub ids and offsets: per-thread chunk of prefixes, then a block scan
+    const int np = 1 << w1;
+    const int per = (np + blockDim.x - 1) / blockDim.x;
+    const int p0 = threadIdx.x * per, p1 = min(np, p0 + per);
+    uint32_t c_id = 0, c_off = 0;
+    for (int p = p0; p < p1; ++p)
+        if (w2max[p]) {
+            ++c_id;
+            c_off += 1u << w2max[p];
+        }
+    part[threadIdx.x][0] = c_id;
+    part[threadIdx.x][1] = c_off;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t a = 0, b = 0;
+        for (int q = 0; q < (int)blockDim.x; ++q) {
+            const uint32_t x = part[q][0], y = part[q][1];
+            part[q][0] = a;
+            part[q][1] = b;
+            a += x;
+            b += y;
+        }
+        nlong = 0;
+    }
+    __syncthreads();
+    c_id = part[threadIdx.x][0];
+    c_off = part[threadIdx.x][1];
+    for (int p = p0; p < p1; ++p) {
+        if (w2max[p]) {
+            sub_id[p] = c_id;
+            sub_off[p] = c_off;
+            if (subs) desc[dbase + c_id] = ((l2base + c_off) << 4) | w2max[p];
+            ++c_id;
+            c_off += 1u << w2max[p];
+        }
+    }
+    for (int i = threadIdx.x; i < np; i += blockDim.x) L1[i] = 0;
+    if (subs) {
+        for (int p = threadIdx.x; p < np; p += blockDim.x)
+            if (w2max[p])
+                for (uint32_t q = 0; q < (1u << w2max[p]); ++q) lut2[l2base + sub_off[p] + q] = 0;
+    }
+    __syncthreads();
+    for (int s = threadIdx.x; s < k; s += blockDim.x) {
+        const unsigned long long v = e[s];
+        const int len = (int)(v >> 56);
+        if (!len) continue;
+        const unsigned long long code = v & kCodeMask;
+        if (len <= w1) {
+            const unsigned first = (unsigned)(code << (w1 - len));
+            const uint16_t val = (uint16_t)((len << 12) | s);
+            for (unsigned j = 0; j < (1u << (w1 - len)); ++j) L1[first + j] = val;
+            continue;
+        }
+        const unsigned p = (unsigned)(code >> (len - w1));
+        const int rem = len - w1;
+        const int w2 = (int)w2max[p];
+        if (subs && rem <= w2) {
+            L1[p] = (uint16_t)((15u << 12) | sub_id[p]);
+            const unsigned rest = (unsigned)(code & ((1ull << rem) - 1));
+            const uint32_t base = l2base + sub_off[p] + (rest << (w2 - rem));
+            const uint16_t val = (uint16_t)((rem << 12) | s);
+            for (unsigned j = 0; j < (1u << (w2 - rem)); ++j) lut2[base + j] = val;
+        } else {
+            if (subs) {
+                L1[p] = (uint16_t)((15u << 12) | sub_id[p]);
+                const unsigned rest = (unsigned)((code >> (rem - w2)) & ((1u << w2) - 1));
+                lut2[l2base + sub_off[p] + rest] = (uint16_t)(15u << 12);
+            } else {
+                L1[p] = (uint16_t)((15u << 12) | 0xFFFu);
+            }
+            const uint32_t idx = atomicAdd(&nlong, 1u);
+            longs[t * k + idx] = {code, (uint32_t)len, (uint32_t)s};
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) long_cnt[t] = nlong;
+}
+
+// ------------------------------------------------------------------- decoding
+struct BitReader {
+    const uint32_t* words;
+    long long nwords;
+    long long next;
+    unsigned long long pos;
+    unsigned long long buf;
+    int have;
+    __device__ __forceinline__ uint32_t load(long long i) const {
+        return i < nwords ? __builtin_bswap32(words[i]) : 0u;
+    }
+    __device__ __forceinline__ void init(const uint32_t* w, long long nw, unsigned long long p) {
+        words = w;
+        nwords = nw;
+        pos = p;
+        const long long wi = (long long)(p >> 5);
+        const int o = (int)(p & 31);
+        buf = (((unsigned long long)load(wi) << 32) | load(wi + 1)) << o;
+        have = 64 - o;
+        next = wi + 2;
+    }
+    __device__ __forceinline__ void skip(int nb) {
+        buf <<= nb;
+        have -= nb;
+        pos += nb;
+        if (have <= 32) {
+            buf |= (unsigned long long)load(next++) << (32 - have);
+            have += 32;
+        }
+    }
+    __device__ __forceinline__ void skip_long(int nb) {   // nb may exceed `have`
+        while (nb > 0) {
+            const int step = nb < 32 ? nb : 32;
+            skip(step);
+            nb -= step;
+        }
+    }
+    __device__ __forceinline__ uint32_t peek(int nb) const { return (uint32_t)(buf >> (64 - nb)); }
+    __device__ unsigned long long peek_long(int nb) const {  // nb <= 56, from memory
+        const long long wi = (long long)(pos >> 5);
+        const int o = (int)(pos & 31);
+        const unsigned long long hi = ((unsigned long long)load(wi) << 32) | load(wi + 1);
+        const unsigned long long lo = load(wi + 2);
+        const unsigned long long w64 = o ? ((hi << o) | (lo >> (32 - o))) : hi;
+        return w64 >> (64 - nb);
+    }
+};
+
+// One lane per chunk of C vectors.  MT = parts per vector at compile time (0 = runtime m,
+// at most 16).  LDS holds the per-alphabet metadata and, when it fits (non-context mode:
+// m alphabets), the first-level tables, so most symbols cost one LDS read.
+template <int MT, typename CodeT, bool L1_IN_LDS>
+__global__ void __launch_bounds__(64)
+dec_chunks(const uint32_t* __restrict__ words, long long nwords, long long n, int m_rt, int k,
+           int context, int raw_first, int chunk_vectors,
+           const unsigned long long* __restrict__ chunk_off, const CodeT* __restrict__ chunk_prev,
+           const uint16_t* __restrict__ lut1_g, const uint16_t* __restrict__ lut2,
+           const uint32_t* __restrict__ meta_g, const uint32_t* __restrict__ desc,
+           long long tables, const pqh_long_code* __restrict__ longs,
+           const uint32_t* __restrict__ long_cnt, CodeT* __restrict__ out,
+           unsigned long long* __restrict__ err) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    uint32_t* meta = reinterpret_cast<uint32_t*>(lds);
+    uint16_t* l1s = reinterpret_cast<uint16_t*>(lds + ((tables * 4 + 15) & ~15ll));
+    for (long long t = threadIdx.x; t < tables; t += blockDim.x) meta[t] = meta_g[t];
+    if constexpr (L1_IN_LDS) {
+        const long long n16 = (tables << kL1Max) * 2 / 16;
+        const uint4* src = reinterpret_cast<const uint4*>(lut1_g);
+        uint4* dst = reinterpret_cast<uint4*>(l1s);
+        for (long long i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
+    }
+    __syncthreads();
+    const uint16_t* lut1 = L1_IN_LDS ? l1s : lut1_g;
+    const int m = MT ? MT : m_rt;
+    const long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long v0 = j * chunk_vectors;
+    if (v0 >= n) return;
+    const long long v1 = min(n, v0 + chunk_vectors);
+    BitReader br;
+    br.init(words, nwords, chunk_off[j]);
+    bool warm = context && j == 0 && raw_first;
+    unsigned prev[MT ? MT : 16];
+#pragma unroll
+    for (int i = 0; i < (MT ? MT : 16); ++i)
+        prev[i] = (i < m && context && !warm) ? (unsigned)chunk_prev[j * m + i] : 0u;
+    int warm_bits = 1;
+    while ((1 << warm_bits) < k) ++warm_bits;
+    const int roots = context ? k : 1;
+    for (long long v = v0; v < v1; ++v) {
+#pragma unroll
+        for (int i = 0; i < (MT ? MT : 16); ++i) {
+            if (!MT && i >= m) break;
+            unsigned sym;
+            if (warm) {
+                sym = br.peek(warm_bits);
+                br.skip(warm_bits);
+            } else {
+                const long long tab = (long long)i * roots + (context ? prev[i] : 0u);
+                const uint32_t mt = meta[tab];
+                const int w1 = (int)(mt & 15u);
+                const uint16_t e = lut1[(tab << kL1Max) + br.peek(w1)];
+                const int len = e >> 12;
+                bool slow = false;
+                sym = e & 0xFFFu;
+                if (len >= 1 && len <= w1) {
+                    br.skip(len);
+                } else if (len == 15 && sym != 0xFFFu) {
+                    const uint32_t d = desc[(mt >> 8) + sym];
+                    const int w2 = (int)(d & 15u);
+                    const uint16_t e2 = lut2[(d >> 4) + (br.peek(w1 + w2) & ((1u << w2) - 1u))];
+                    const int len2 = e2 >> 12;
+                    if (len2 >= 1 && len2 <= w2) {
+                        sym = e2 & 0xFFFu;
+                        br.skip(w1 + len2);
+                    } else if (len2 == 15) {
+                        slow = true;
+                    } else {
+                        atomicOr(err, 1ull);
+                        return;
+                    }
+                } else if (len == 15) {
+                    slow = true;
+                } else {
+                    atomicOr(err, 1ull);
+                    return;
+                }
+                if (slow) {   // codes beyond both levels: rare, linear search
+                    const uint32_t cnt = long_cnt[tab];
+                    bool found = false;
+                    for (uint32_t q = 0; q < cnt; ++q) {
+                        const pqh_long_code lc = longs[tab * k + q];
+                        if (br.peek_long((int)lc.len) == lc.code) {
+                            sym = lc.sym;
+                            br.skip_long((int)lc.len);
+                            found = true;
+                            break;
+                        }
+                    }
+                    if (!found) {
+                        atomicOr(err, 1ull);
+                        return;
+                    }
+                }
+            }
+            prev[i] = sym;
+        }
+        warm = false;
+        CodeT* o = out + v * m;
+        if constexpr (sizeof(CodeT) == 1 && MT % 4 == 0 && MT > 0) {
+#pragma unroll
+            for (int q = 0; q < MT / 4; ++q)
+                reinterpret_cast<uint32_t*>(o)[q] = prev[4 * q] | (prev[4 * q + 1] << 8) |
+                                                    (prev[4 * q + 2] << 16) | (prev[4 * q + 3] << 24);
+        } else {
+#pragma unroll
+            for (int i = 0; i < (MT ? MT : 16); ++i)
+                if (MT || i < m) o[i] = (CodeT)prev[i];
+        }
+    }
+}
+
+
+
+}  // namespace
+
+extern "C" {
+
+int pqh_tables_alloc(pqh_ctx_t* ctx, int m, int k, int context, pqh_tables_t** out) {
+    if (!ctx || !out || m <= 0 || k <= 0 || k > 4096) return PQH_ERR_ARG;
+    if (context && k != 256)
+        return pqh_set_error(ctx, PQH_ERR_UNSUPPORTED,
+                             "context coding needs K=256 (huffman_encoder.c:187,234)");
+    int rc = pqh_use_device(ctx);
+    if (rc) return rc;
+    pqh_tables* t = new pqh_tables();
+    t->ctx = ctx;
+    t->m = m;
+    t->k = k;
+    t->context = context;
+    t->roots = context ? k : 1;
+    t->items = (long long)t->roots * k;
+    t->tables = (long long)m * t->roots;
+    t->l1_bits = context ? 9 : kL1Max;   // 1 KB first level per context alphabet
+    t->l2_bits = 8;
+    t->desc_cap = t->tables * 64 + 1024;
+    t->lut2_cap = t->tables * 2048 + 65536;
+    if (hipMalloc(&t->d_enc, (size_t)m * t->items * 8) != hipSuccess ||
+        hipMalloc(&t->d_lut1, (size_t)(t->tables << kL1Max) * 2) != hipSuccess ||
+        hipMalloc(&t->d_lut2, (size_t)t->lut2_cap * 2) != hipSuccess ||
+        hipMalloc(&t->d_meta, (size_t)t->tables * 4 + 16) != hipSuccess ||
+        hipMalloc(&t->d_desc, (size_t)t->desc_cap * 4) != hipSuccess ||
+        hipMalloc(&t->d_scratch, (size_t)t->tables * 8 + 16) != hipSuccess ||
+        hipMalloc(&t->d_long, (size_t)t->tables * k * sizeof(pqh_long_code)) != hipSuccess ||
+        hipMalloc(&t->d_long_cnt, (size_t)t->tables * 4) != hipSuccess ||
+        hipMalloc(&t->d_err, 16) != hipSuccess) {
+        pqh_tables_destroy(t);
+        return pqh_set_error(ctx, PQH_ERR_NOMEM, "hipMalloc tables");
+    }
+    *out = t;
+    return PQH_OK;
+}
+
+int pqh_tables_destroy(pqh_tables_t* t) {
+    if (!t) return PQH_OK;
+    if (t->ctx) {
+        (void)hipSetDevice(t->ctx->device);
+        (void)hipStreamSynchronize(t->ctx->stream);
+    }
+    void* bufs[] = {t->d_enc, t->d_lut1, t->d_lut2, t->d_meta, t->d_desc, t->d_scratch,
+                    t->d_long, t->d_long_cnt, t->d_err};
+    for (void* b : bufs)
+        if (b) (void)hipFree(b);
+    delete t;
+    return PQH_OK;
+}
+
+static int launch_luts(pqh_ctx* ctx, pqh_tables* t) {
+    hipLaunchKernelGGL(lut_plan, dim3((unsigned)t->tables), dim3(256), 0, ctx->stream, t->d_enc,
+                       t->k, t->tables, t->l1_bits, t->l2_bits, t->d_meta, t->d_scratch);
+    PQH_LAUNCH_CHECK(ctx);
+    hipLaunchKernelGGL(lut_alloc, dim3(1), dim3(1024), 0, ctx->stream, t->tables, t->desc_cap,
+                       t->lut2_cap, t->d_meta, t->d_scratch);
+    PQH_LAUNCH_CHECK(ctx);
+    hipLaunchKernelGGL(lut_fill, dim3((unsigned)t->tables), dim3(256), 0, ctx->stream, t->d_enc,
+                       t->k, t->l2_bits, t->d_meta, t->d_scratch, t->d_lut1, t->d_lut2, t->d_desc,
+                       t->d_long, t->d_long_cnt);
+    PQH_LAUNCH_CHECK(ctx);
+    return PQH_OK;
+}
+
+int pqh_tables_build(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts) {
+    if (!ctx || !t || !d_counts || t->ctx != ctx) return PQH_ERR_ARG;
+    int rc = pqh_use_device(ctx);
+    if (rc) return rc;
+    PQH_HIP(ctx, hipMemsetAsync(t->d_err, 0, 4, ctx->stream));
+    const long long trees = t->tables;
+    if (t->k <= 256) {
+        constexpr int TPW = 32;
+        const size_t lds = (size_t)256 * TPW * (8 + 4 + 4 + 2);
+        PQH_HIP(ctx, hipFuncSetAttribute((const void*)huff_trees<256, TPW>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL((huff_trees<256, TPW>), dim3((unsigned)((trees + TPW - 1) / TPW)), dim3(64),
+                           lds, ctx->stream, d_counts, t->k, trees, t->d_enc, t->d_err);
+    } else {
+        constexpr int TPW = 2;
+        const size_t lds = (size_t)4096 * TPW * (8 + 4 + 4 + 2);
+        PQH_HIP(ctx, hipFuncSetAttribute((const void*)huff_trees<4096, TPW>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL((huff_trees<4096, TPW>), dim3((unsigned)((trees + TPW - 1) / TPW)), dim3(64),
+                           lds, ctx->stream, d_counts, t->k, trees, t->d_enc, t->d_err);
+    }
+    PQH_LAUNCH_CHECK(ctx);
+    return launch_luts(ctx, t);
+}
+
+int pqh_tables_upload(pqh_ctx_t* ctx, pqh_tables_t* t, const huffman_codebook_t* cbs) {
+    if (!ctx || !t || !cbs) return PQH_ERR_ARG;
+    for (int i = 0; i < t->m; ++i)
+        if (cbs[i].alphabet_size != t->k || (cbs[i].is_context ? 1 : 0) != t->context) return PQH_ERR_ARG;
+    int rc = pqh_use_device(ctx);
+    if (rc) return rc;
+    std::vector<unsigned long long> h((size_t)t->m * t->items, 0);
+    for (int i = 0; i < t->m; ++i)
+        for (long long it = 0; it < t->items; ++it) {
+            const huffman_code_item_t& c = cbs[i].items[it];
+            if (c.bit_length <= 0) continue;
+            if (c.bit_length > kMaxCodeLen)
+                return pqh_set_error(ctx, PQH_ERR_CODE_TOO_LONG, "code of %d bits", c.bit_length);
+            unsigned long long v = 0;
+            for (int b = 0; b < c.bit_length; ++b) v = (v << 1) | ((c.code[b >> 3] >> (7 - (b & 7))) & 1u);
+            h[(size_t)i * t->items + it] = ((unsigned long long)c.bit_length << 56) | v;
+        }
+    PQH_HIP(ctx, hipMemsetAsync(t->d_err, 0, 4, ctx->stream));
+    PQH_HIP(ctx, hipMemcpyAsync(t->d_enc, h.data(), h.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+    rc = launch_luts(ctx, t);
+    if (rc) return rc;
+    PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));  // h goes out of scope
+    return PQH_OK;
+}
+
+int pqh_tables_create(pqh_ctx_t* ctx, const huffman_codebook_t* cbs, int m, pqh_tables_t** out) {
+    if (!ctx || !cbs || m <= 0 || !out) return PQH_ERR_ARG;
+    int rc = pqh_tables_alloc(ctx, m, cbs[0].alphabet_size, cbs[0].is_context ? 1 : 0, out);
+    if (rc) return rc;
+    rc = pqh_tables_upload(ctx, *out, cbs);
+    if (rc) {
+        pqh_tables_destroy(*out);
+        *out = nullptr;
+    }
+    return rc;
+}
+
+int pqh_tables_status(pqh_ctx_t* ctx, const pqh_tables_t* t) {
+    if (!ctx || !t) return PQH_ERR_ARG;
+    uint32_t e = 0;
+    PQH_HIP(ctx, hipMemcpyAsync(&e, t->d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
+    PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return e ? pqh_set_error(ctx, PQH_ERR_CODE_TOO_LONG, "a Huffman code exceeds 56 bits") : PQH_OK;
+}
+
+int pqh_tables_codebooks(pqh_ctx_t* ctx, const pqh_tables_t* t, huffman_codebook_t* cbs) {
+    if (!ctx || !t || !cbs) return PQH_ERR_ARG;
+    int rc = pqh_tables_status(ctx, t);
+    if (rc) return rc;
+    std::vector<unsigned long long> h((size_t)t->m * t->items);
+    PQH_HIP(ctx, hipMemcpyAsync(h.data(), t->d_enc, h.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+    PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    for (int i = 0; i < t->m; ++i) {
+        huffman_codebook_t& cb = cbs[i];
+        cb.alphabet_size = t->k;
+        cb.is_context = t->context;
+        cb.num_items = (int)t->items;
+        cb.items = (huffman_code_item_t*)calloc((size_t)t->items, sizeof(huffman_code_item_t));
+        long long bytes = 0;
+        for (long long it = 0; it < t->items; ++it) bytes += ((h[(size_t)i * t->items + it] >> 56) + 7) / 8;
+        cb.codefield = (byte_t*)calloc((size_t)(bytes > 0 ? bytes : 1), 1);
+        byte_t* p = cb.codefield;
+        for (long long it = 0; it < t->items; ++it) {
+            const unsigned long long v = h[(size_t)i * t->items + it];
+            const int L = (int)(v >> 56);
+            cb.items[it].bit_length = L;
+            if (!L) continue;
+            const unsigned long long code = v & kCodeMask;
+            for (int b = 0; b < L; ++b)
+                if ((code >> (L - 1 - b)) & 1ull) p[b >> 3] |= (byte_t)(0x80u >> (b & 7));
+            cb.items[it].code = p;
+            p += (L + 7) / 8;
+        }
+    }
+    return PQH_OK;
+}
+
+int pqh_decode(pqh_ctx_t* ctx, const pqh_tables_t* t, const unsigned char* d_stream,
+               unsigned long long stream_bytes, long long n, int raw_first, int chunk_vectors,
+               const unsigned long long* d_chunk_offsets, const void* d_chunk_prev, void* d_codes) {
+    if (!ctx || !t || n < 0 || chunk_vectors <= 0 ||
+        (n > 0 && (!d_stream || !d_chunk_offsets || !d_codes)))
+        return PQH_ERR_ARG;
+    if (reinterpret_cast<uintptr_t>(d_stream) & 3u) return PQH_ERR_ARG;
+    if (t->context && !raw_first && !d_chunk_prev) return PQH_ERR_ARG;
+    if (t->m > 16) return PQH_ERR_UNSUPPORTED;
+    int rc = pqh_use_device(ctx);
+    if (rc) return rc;
+    if (n == 0) return PQH_OK;
+    PQH_HIP(ctx, hipMemsetAsync(ctx->d_diag + 1, 0, 8, ctx->stream));
+    const long long chunks = (n + chunk_vectors - 1) / chunk_vectors;
+    const long long nwords = (long long)(stream_bytes / 4);
+    const unsigned blocks = (unsigned)((chunks + 63) / 64);
+    if (reinterpret_cast<uintptr_t>(d_codes) & 3u) return PQH_ERR_ARG;
+    const size_t l1_bytes = (size_t)(t->tables << kL1Max) * 2;
+    const size_t meta_bytes = ((size_t)t->tables * 4 + 15) & ~(size_t)15;
+    const bool lds_l1 = meta_bytes + l1_bytes <= 48 * 1024;
+    const size_t lds = meta_bytes + (lds_l1 ? l1_bytes : 0) + 16;
+    if (lds > 64 * 1024) return PQH_ERR_UNSUPPORTED;
+#define PQH_DEC(MT, T, L)                                                                        \
+    hipLaunchKernelGGL((dec_chunks<MT, T, L>), dim3(blocks), dim3(64), lds, ctx->stream,          \
+                       reinterpret_cast<const uint32_t*>(d_stream), nwords, n, t->m, t->k,       \
+                       t->context, raw_first, chunk_vectors, d_chunk_offsets,                    \
+                       static_cast<const T*>(d_chunk_prev), t->d_lut1, t->d_lut2, t->d_meta,     \
+                       t->d_desc, t->tables, t->d_long, t->d_long_cnt, static_cast<T*>(d_codes), \
+                       ctx->d_diag + 1)
+    if (t->k <= 256) {
+        if (t->m == 8) {
+            if (lds_l1) PQH_DEC(8, uint8_t, true); else PQH_DEC(8, uint8_t, false);
+        } else if (t->m == 16) {
+            if (lds_l1) PQH_DEC(16, uint8_t, true); else PQH_DEC(16, uint8_t, false);
+        } else {
+            if (lds_l1) PQH_DEC(0, uint8_t, true); else PQH_DEC(0, uint8_t, false);
+        }
+    } else {
+        if (lds_l1) PQH_DEC(0, uint16_t, true); else PQH_DEC(0, uint16_t, false);
+    }
+#undef PQH_DEC
+    PQH_LAUNCH_CHECK(ctx);
+    return PQH_OK;
+}
+
+int pqh_decode_status(pqh_ctx_t* ctx) {
+    unsigned long long e = 0;
+    PQH_HIP(ctx, hipMemcpyAsync(&e, ctx->d_diag + 1, 8, hipMemcpyDeviceToHost, ctx->stream));
+    PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return e ? pqh_set_error(ctx, PQH_ERR_CORRUPT, "invalid code in stream") : PQH_OK;
+}
+
+// Chunk index of a stream that came without a sidecar: a sequential walk over a HOST copy
+// of the code table (index building only; the symbols are decoded by pqh_decode).
+int pqh_chunk_index_host(const pqh_tables_t* t, const unsigned char* stream,
+                         unsigned long long stream_bytes, long long n, int raw_first,
+                         int chunk_vectors, unsigned long long* chunk_offsets, void* chunk_prev) {
+    if (!t || n < 0 || chunk_vectors <= 0 || (n > 0 && (!stream || !chunk_offsets))) return PQH_ERR_ARG;
+    if (t->context && !chunk_prev) return PQH_ERR_ARG;
+    pqh_ctx* ctx = t->ctx;
+    std::vector<unsigned long long> enc((size_t)t->m * t->items);
+    PQH_HIP(ctx, hipMemcpyAsync(enc.data(), t->d_enc, enc.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+    PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    // per-table canonical lookup: (len, code) -> symbol, via sorted vectors per length
+    const int W = 16;
+    std::vector<int32_t> lut((size_t)t->tables << W, -1);
+    std::vector<std::vector<std::pair<unsigned long long, int>>> longs(t->tables);
+    for (long long tab = 0; tab < t->tables; ++tab)
+        for (int s = 0; s < t->k; ++s) {
+            const unsigned long long v = enc[(size_t)tab * t->k + s];
+            const int L = (int)(v >> 56);
+            if (!L) continue;
+            const unsigned long long code = v & kCodeMask;
+            if (L <= W) {
+                for (unsigned long long e = code << (W - L); e < (code + 1) << (W - L); ++e)
+                    lut[((size_t)tab << W) + e] = (L << 16) | s;
+            } else {
+                longs[tab].push_back({(code << 8) | (unsigned long long)L, s});
+            }
+        }
+    const unsigned long long total = stream_bytes * 8;
+    auto peek = [&](unsigned long long p, int nb) -> unsigned long long {
+        unsigned long long r = 0;
+        for (int b = 0; b < nb; ++b) {
+            const unsigned long long q = p + b;
+            r = (r << 1) | (q < total ? (unsigned long long)((stream[q >> 3] >> (7 - (q & 7))) & 1u) : 0ull);
+        }
+        return r;
+    };
+    std::vector<unsigned> prev(t->m, 0);
+    bool warm = t->context && raw_first;
+    int warm_bits = 1;
+    while ((1 << warm_bits) < t->k) ++warm_bits;
+    unsigned long long pos = 0;
+    for (long long v = 0; v < n; ++v) {
+        if (v % chunk_vectors == 0) {
+            const long long j = v / chunk_vectors;
+            chunk_offsets[j] = pos;
+            if (t->context)
+                for (int i = 0; i < t->m; ++i) {
+                    if (t->k <= 256) static_cast<uint8_t*>(chunk_prev)[j * t->m + i] = (uint8_t)prev[i];
+                    else static_cast<uint16_t*>(chunk_prev)[j * t->m + i] = (uint16_t)prev[i];
+                }
+        }
+        for (int i = 0; i < t->m; ++i) {
+            unsigned sym;
+            if (warm) {
+                sym = (unsigned)peek(pos, warm_bits);
+                pos += warm_bits;
+            } else {
+                const long long tab = (long long)i * t->roots + (t->context ? prev[i] : 0);
+                const int32_t e = lut[((size_t)tab << W) + peek(pos, W)];
+                if (e >= 0) {
+                    pos += (unsigned)e >> 16;
+                    sym = (unsigned)e & 0xFFFFu;
+                } else {
+                    bool found = false;
+                    sym = 0;
+                    for (auto& lc : longs[tab]) {
+                        const int L = (int)(lc.first & 0xFF);
+                        if (peek(pos, L) == (lc.first >> 8)) {
+                            pos += L;
+                            sym = (unsigned)lc.second;
+                            found = true;
+                            break;
+                        }
+                    }
+                    if (!found) return PQH_ERR_CORRUPT;
+                }
+                if (pos > total) return PQH_ERR_CORRUPT;
+            }
+            prev[i] = sym;
+        }
+        warm = false;
+    }
+    return PQH_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,58 @@
+/* huffman_encoder -- CLI-compatible replacement for the reference's src/huffman_encoder.c
+ * (usage and outputs of huffman_encoder.c:42-102,306-439) running histogram, encode and
+ * the sidecar chunk index on the GPU through libpqh.
+ *   huffman_encoder <pq-output-template> <output-template> <m>
+ *                   [--no-sort] [--no-context] [--only-estimate] [--shuffle] [--tree <path>]
+ * --shuffle (time-seeded rand(), not reproducible) and --tree (kNN/MST ordering) are out
+ * of scope of this build and rejected. */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "misc.h"
+#include "pqh.h"
+#include "vecs_io.h"
+
+static void usage(const char* argv0) {
+    fprintf(stderr, "Usage: %s <pq-output-template> <output-template> <m>"
+                    " [--no-sort] [--no-context] [--only-estimate] [--tree <tree path>]\n", argv0);
+    exit(1);
+}
+
+int main(int argc, const char* argv[]) {
+    if (argc < 4) {
+        fprintf(stderr, "Too few positional arguments\n");
+        usage(argv[0]);
+    }
+    pqh_encode_options_t opt = {1, 1, 64, 0};
+    int m = atoi(argv[3]);
+    for (int i = 4; i < argc; ++i) {
+        if (!strcmp(argv[i], "--only-estimate")) opt.only_estimate = 1;
+        else if (!strcmp(argv[i], "--no-sort")) opt.sort = 0;
+        else if (!strcmp(argv[i], "--no-context")) opt.context = 0;
+        else if (!strcmp(argv[i], "--shuffle") || !strcmp(argv[i], "--tree")) {
+            fprintf(stderr, "%s: not supported by this build (see DESIGN.md scope)\n", argv[i]);
+            return 1;
+        } else {
+            fprintf(stderr, "Unknown arg: %s\n", argv[i]);
+            usage(argv[0]);
+        }
+    }
+    char* in = concat(argv[1], "pq_indices.bvecsl");
+    long long n = 0;
+    int d = 0;
+    byte_t* codes = load_vecs_light_filename(in, 1, &n, &d);
+    if (!codes || d != m) {
+        fprintf(stderr, "cannot read %s (or its dimension %d != m %d)\n", in, d, m);
+        return 1;
+    }
+    printf("use %s encoder\n", opt.context ? "context" : "non-context");
+    int rc = pqh_encode_files(codes, n, m, &opt, argv[2]);
+    if (rc) {
+        fprintf(stderr, "huffman_encoder: %s\n", pqh_status_string(rc));
+        return 1;
+    }
+    free(codes);
+    free(in);
+    return 0;
+}

@@ -1,0 +1,219 @@
+"""GPU parity of histogram / encode / decode (C ABI) against the reference-generated golden
+files and the oracle: byte-exact huffman_indices.bin, exact round trips, shard composition,
+full-size properties."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, golden
+import datagen
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    import torch
+    from pq_huffman_amd import codec
+    assert torch.cuda.is_available()
+    return torch, codec, codec.Context(0)
+
+
+def _codebooks_from_gpu_hist(gpu, codes, k, ctx_mode):
+    torch, codec, ctx = gpu
+    codes = np.ascontiguousarray(codes)
+    if codes.dtype == np.uint16:
+        codes = codes.view(np.int16)
+    cd = torch.from_numpy(codes).cuda()
+    counts = codec.histogram(ctx, cd, k, ctx_mode)
+    return cd, codec.Codebooks(codec.counts_to_host(counts), k, ctx_mode)
+
+
+@pytest.mark.parametrize("name", ["m8_n1000", "m16_n1000", "m8_n1", "m3_n2"])
+@pytest.mark.parametrize("mode", ["nosort_ctx", "nosort_noctx"])
+@pytest.mark.parametrize("chunk", [1, 7, 64])
+def test_encode_decode_vs_reference_files(gpu, name, mode, chunk):
+    torch, codec, ctx = gpu
+    g = golden(f"huff_{name}.npz")
+    ctxm = mode == "nosort_ctx"
+    cd, cbs = _codebooks_from_gpu_hist(gpu, g["input"], 256, ctxm)
+    assert cbs.file_bytes() == g[mode + "__codebooks"].tobytes()
+    tabs = codec.Tables.from_codebooks(ctx, cbs)
+    enc = codec.encode(ctx, tabs, cd, chunk_vectors=chunk)
+    assert codec.indices_file_bytes(enc) == g[mode + "__indices"].tobytes()
+    dec = codec.decode(ctx, tabs, enc)
+    codec.decode_status(ctx)
+    assert np.array_equal(dec.cpu().numpy(), g["input"])
+
+
+def test_k4096_noctx_vs_reference(gpu):
+    torch, codec, ctx = gpu
+    g = golden("huff_k4096_m8_n2000.npz")
+    cd, cbs = _codebooks_from_gpu_hist(gpu, g["input"], 4096, False)
+    assert cbs.file_bytes() == g["nosort_noctx__codebooks"].tobytes()
+    tabs = codec.Tables.from_codebooks(ctx, cbs)
+    enc = codec.encode(ctx, tabs, cd, chunk_vectors=16)
+    assert codec.indices_file_bytes(enc) == g["nosort_noctx__indices"].tobytes()
+    dec = codec.decode(ctx, tabs, enc)
+    assert np.array_equal(dec.cpu().numpy().view(np.uint16), g["input"])
+
+
+@pytest.mark.parametrize("ctxm", [True, False])
+def test_histogram_vs_oracle_with_halo(gpu, oracle, ctxm):
+    torch, codec, ctx = gpu
+    codes = datagen.skewed_codes(70001, 8, seed=8)
+    cd = torch.from_numpy(codes).cuda()
+    got = codec.counts_to_host(codec.histogram(ctx, cd, 256, ctxm))
+    assert np.array_equal(got, oracle.histogram(codes, 256, ctxm))
+    if ctxm:  # shard [40000:) with the halo row 39999 == the pairs of the whole array
+        a = codec.histogram(ctx, cd[:40000], 256, True)
+        codec.histogram(ctx, cd[40000:], 256, True, prev_row=cd[39999], counts=a)
+        assert np.array_equal(codec.counts_to_host(a), got)
+
+
+@pytest.mark.parametrize("ctxm", [True, False])
+def test_sharded_encode_composes(gpu, oracle, ctxm):
+    """Two shards written at their global bit offsets into one buffer == one-shot stream
+    (the multi-GPU concatenation rule)."""
+    torch, codec, ctx = gpu
+    codes = datagen.skewed_codes(9000, 8, seed=31)
+    cd, cbs = _codebooks_from_gpu_hist(gpu, codes, 256, ctxm)
+    tabs = codec.Tables.from_codebooks(ctx, cbs)
+    whole = codec.encode(ctx, tabs, cd, chunk_vectors=32)
+    cut = 4321
+    a, b = cd[:cut], cd[cut:]
+    ta = int(codec.encode_size(ctx, tabs, a, 1, None).item())
+    tb = int(codec.encode_size(ctx, tabs, b, 0, cd[cut - 1] if ctxm else None).item())
+    assert ta + tb == whole.bits
+    out = torch.zeros_like(whole.stream)
+    codec.encode_write(ctx, tabs, a, out, 0, 1, None, 0)
+    codec.encode_write(ctx, tabs, b, out, ta, 0, cd[cut - 1] if ctxm else None, 0)
+    assert torch.equal(out, whole.stream)
+    stream, bits = oracle.encode(codes, oracle.build_codebooks(codes, 256, ctxm))
+    assert bits == whole.bits
+    assert out[:len(stream)].cpu().numpy().tobytes() == stream
+
+
+def test_corrupt_stream_is_reported(gpu):
+    torch, codec, ctx = gpu
+    codes = np.zeros((100, 2), np.uint8)
+    codes[::2, 0] = 1
+    cd, cbs = _codebooks_from_gpu_hist(gpu, codes, 256, False)
+    tabs = codec.Tables.from_codebooks(ctx, cbs)
+    enc = codec.encode(ctx, tabs, cd, chunk_vectors=10)
+    # part 1 has a single symbol: code "0"; a 1 bit there is invalid
+    enc.stream[:] = 0xFF
+    codec.decode(ctx, tabs, enc)
+    with pytest.raises(Exception):
+        codec.decode_status(ctx)
+
+
+@pytest.mark.parametrize("ctxm", [True, False])
+def test_full_size_roundtrip_sift1m(gpu, oracle, ctxm):
+    """SIFT1M-shaped: assign (MFMA) -> hist -> codebooks -> encode -> decode; exact round
+    trip, total bits == the codebook estimate, stream byte-equal to the oracle's."""
+    torch, codec, ctx = gpu
+    n = 1_000_000
+    x = datagen.sift_like(n, 128, seed=77)
+    cent = datagen.lloyd_centroids(x, 8, 256, iters=2, sample=20000)
+    pq = codec.PQ(ctx, cent)
+    xd = torch.from_numpy(x).cuda()
+    codes = pq.assign(xd)
+    counts = codec.histogram(ctx, codes, 256, ctxm)
+    cbs = codec.Codebooks(codec.counts_to_host(counts), 256, ctxm)
+    tabs = codec.Tables.from_codebooks(ctx, cbs)
+    enc = codec.encode(ctx, tabs, codes, chunk_vectors=64)
+    dec = codec.decode(ctx, tabs, enc)
+    codec.decode_status(ctx)
+    assert torch.equal(dec, codes)
+    est = cbs.estimate().sum() + (8 * 8 if ctxm else 0)
+    assert enc.bits == int(est)
+    hc = codes.cpu().numpy()
+    stream, bits = oracle.encode(hc, oracle.build_codebooks(hc, 256, ctxm))
+    assert bits == enc.bits
+    assert enc.stream[:len(stream)].cpu().numpy().tobytes() == stream
+    # the PQ codes themselves: oracle on a 20k-row sample
+    sel = np.random.default_rng(0).choice(n, 20000, replace=False)
+    want, _ = oracle.pq_assign(x[sel], cent, threads=0)
+    assert np.array_equal(hc[sel], want)
+
+
+@pytest.mark.parametrize("case", ["enc_test_many", "enc_test_one", "enc_test_zero",
+                                  "ties_small_ints", "ties_all_equal", "ties_powers",
+                                  "single_symbol", "empty", "geometric"])
+def test_gpu_tree_builder_vs_reference_codebooks(gpu, case):
+    """pqh_tables_build (GPU heap simulation) == the reference's codebook bytes."""
+    torch, codec, ctx = gpu
+    g = golden("codebooks.npz")
+    k, c = (int(v) for v in g[case + "__alphabet"])
+    counts = torch.from_numpy(g[case + "__counts"].astype(np.int32)[None]).cuda()
+    tabs = codec.Tables(ctx, 1, k, bool(c)).build(counts)
+    cbs = tabs.codebooks()
+    assert cbs.file_bytes() == np.uint32(1).tobytes() + g[case + "__file"].tobytes()
+
+
+@pytest.mark.parametrize("ctxm", [True, False])
+def test_gpu_tree_builder_vs_host_builder_ties(gpu, ctxm):
+    """2048 tie-heavy context trees (or 8 plain ones): GPU tables == host codebooks."""
+    torch, codec, ctx = gpu
+    rng = np.random.default_rng(17)
+    items = 256 * 256 if ctxm else 256
+    counts = rng.integers(0, 4, (8, items)).astype(np.int64)
+    counts[:, : items // 3] *= rng.integers(0, 50, (8, items // 3))
+    if ctxm:
+        counts[0, 5 * 256:6 * 256] = 0      # an empty context row
+        counts[1, 7 * 256:8 * 256] = 0
+        counts[1, 7 * 256 + 3] = 9          # a one-symbol context row
+    else:
+        counts[2] = 0
+        counts[2, 77] = 5                   # a one-symbol part
+    host = codec.Codebooks(counts.astype(np.float64), 256, ctxm)
+    dev = codec.Tables(ctx, 8, 256, ctxm).build(torch.from_numpy(counts.astype(np.int32)).cuda())
+    assert dev.codebooks().file_bytes() == host.file_bytes()
+
+
+def _run(args, cwd=None):
+    r = subprocess.run(args, capture_output=True, text=True, cwd=cwd)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return r.stdout
+
+
+@pytest.mark.parametrize("mode,flags", [("nosort_ctx", ["--no-sort"]),
+                                        ("nosort_noctx", ["--no-sort", "--no-context"])])
+def test_cli_tools_match_reference_files(tmp_path, mode, flags):
+    g = golden("huff_m8_n1000.npz")
+    bind = os.path.join(ROOT, "pq_huffman_amd", "bin")
+    pqdir, out = tmp_path / "pq", tmp_path / "out"
+    pqdir.mkdir()
+    out.mkdir()
+    datagen.write_vecsl(str(pqdir / "pq_indices.bvecsl"), g["input"])
+    _run([os.path.join(bind, "huffman_encoder"), str(pqdir) + "/", str(out) + "/", "8"] + flags)
+    assert (out / "huffman_codebooks.bin").read_bytes() == g[mode + "__codebooks"].tobytes()
+    assert (out / "huffman_indices.bin").read_bytes() == g[mode + "__indices"].tobytes()
+    assert (out / "huffman_stats.txt").read_text() == g[mode + "__stats"].tobytes().decode()
+    dec = tmp_path / "dec.bin"
+    _run([os.path.join(bind, "huffman_decoder"), str(out) + "/", "--output-file", str(dec),
+          "--check-file", str(pqdir / "pq_indices.bvecsl")])
+    assert np.array_equal(np.fromfile(dec, np.uint8).reshape(1000, 8), g["input"])
+    # without the sidecar the decoder rebuilds the chunk index from the stream
+    (out / "huffman_chunks.bin").unlink()
+    _run([os.path.join(bind, "huffman_decoder"), str(out) + "/", "--output-file", str(dec)])
+    assert np.array_equal(np.fromfile(dec, np.uint8).reshape(1000, 8), g["input"])
+
+
+def test_cli_pq_encoder_fixed_centroids(tmp_path, oracle):
+    g = golden("pq_sift_n1000_m8_k256.npz")
+    bind = os.path.join(ROOT, "pq_huffman_amd", "bin")
+    datagen.write_fvecs(str(tmp_path / "x.fvecs"), g["x"])
+    cfile = tmp_path / "c.fvecsl"
+    datagen.write_vecsl(str(cfile), g["centroids"].reshape(8 * 256, 16))
+    _run([os.path.join(bind, "pq_encoder"), str(tmp_path / "x.fvecs"), str(tmp_path) + "/", "8",
+          "--centroids", str(cfile), "--compute-error"])
+    raw = (tmp_path / "pq_indices.bvecsl").read_bytes()
+    assert np.frombuffer(raw[:8], np.uint32).tolist() == [1000, 8]
+    assert np.array_equal(np.frombuffer(raw[8:], np.uint8).reshape(1000, 8), g["codes"])
+    err = float((tmp_path / "pq_error").read_text().strip())
+    want = oracle.compute_error(g["x"], g["centroids"], g["codes"])
+    assert abs(err - want) <= 1e-6 * want
