@@ -58,6 +58,7 @@ def make_data(torch, n, d, seed, rank, device):
     g = torch.Generator(device=device)
     g.manual_seed(seed)
     centers = 1024
+    torch.manual_seed(seed)    # the Gamma draw uses the default CPU generator
     mu = torch.distributions.Gamma(torch.tensor(1.2), torch.tensor(1 / 30.0)).sample((centers, d))
     mu = mu.to(device)
     w = 1.0 / torch.arange(1, centers + 1, dtype=torch.float64) ** 1.1
@@ -69,7 +70,8 @@ def make_data(torch, n, d, seed, rank, device):
 
 
 def train_centroids(torch, x, m, k, iters=4, sample=50_000, seed=7):
-    """Setup only (not timed): Lloyd iterations on a device sample, float64 accumulation."""
+    """Setup only (not timed): Lloyd iterations on a device sample, float64 accumulation.
+    Centroid sums are taken on the host so the setup is deterministic run to run."""
     n, d = x.shape
     ds = d // m
     g = torch.Generator(device=x.device)
@@ -80,11 +82,13 @@ def train_centroids(torch, x, m, k, iters=4, sample=50_000, seed=7):
         sub = xs[:, j * ds:(j + 1) * ds]
         c = sub[torch.randperm(sub.shape[0], generator=g, device=x.device)[:k]].clone()
         for _ in range(iters):
-            a = torch.cdist(sub, c).argmin(1)
-            s = torch.zeros_like(c).index_add_(0, a, sub)
+            a = torch.cdist(sub, c).argmin(1).cpu()
+            s = torch.zeros((k, ds), dtype=torch.float64).index_add_(0, a, sub.cpu())
             cnt = torch.bincount(a, minlength=k).double()
             nz = cnt > 0
+            c = c.cpu()
             c[nz] = s[nz] / cnt[nz, None]
+            c = c.to(x.device)
         out[j] = c.float().cpu()
     return out.numpy()
 

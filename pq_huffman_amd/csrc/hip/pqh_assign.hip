@@ -119,21 +119,31 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     const long long nblk = (n + 31) / 32;
     unsigned long long slow_count = 0;
 
+    // x slice of a block: lane (r, h) holds vector r's D floats (both half-waves)
+    auto load_x = [&](long long b, float* dst) {
+        const long long vv = b * 32 + r;
+        const bool ok = b < nblk && vv < n;
+        const float* xp = x + (ok ? vv : 0) * ldx + (long long)m * D;
+        if constexpr (D % 4 == 0) {
+#pragma unroll
+            for (int j = 0; j < D; j += 4) {
+                float4 q = ok ? *reinterpret_cast<const float4*>(xp + j) : make_float4(0, 0, 0, 0);
+                dst[j] = q.x; dst[j + 1] = q.y; dst[j + 2] = q.z; dst[j + 3] = q.w;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < D; ++j) dst[j] = ok ? xp[j] : 0.0f;
+        }
+    };
+    float xn[D];
+    load_x(blockIdx.x, xn);
     for (long long blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
         const long long v = blk * 32 + r;
         const bool valid = v < n;
         float xs[D];
-        const float* xp = x + (valid ? v : 0) * ldx + (long long)m * D;
-        if constexpr (D % 4 == 0) {
 #pragma unroll
-            for (int j = 0; j < D; j += 4) {
-                float4 q = valid ? *reinterpret_cast<const float4*>(xp + j) : make_float4(0, 0, 0, 0);
-                xs[j] = q.x; xs[j + 1] = q.y; xs[j + 2] = q.z; xs[j + 3] = q.w;
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < D; ++j) xs[j] = valid ? xp[j] : 0.0f;
-        }
+        for (int j = 0; j < D; ++j) xs[j] = xn[j];
+        load_x(blk + gridDim.x, xn);   // next block's slice in flight during this block
 
         float X = 0.0f;
         bool lo = false;
@@ -150,9 +160,10 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         const bool any_lo = __any(lo);
         const bool finite_x = isfinite(X);
 
-        // error bound of the screening score (DESIGN.md "pq_assign error bound")
+        // error bound of the screening score (DESIGN.md "pq_assign error bound"); when no
+        // x of the block has a bf16 remainder the split error is 2^-15 P instead of 2^-13 P
         const float Pm = sqrtf(X) * sc * 1.00001f;
-        const float E0 = 0x1p-13f * Pm + 0x1p-22f * cm +
+        const float E0 = (any_lo ? 0x1p-13f : 0x1p-15f) * Pm + 0x1p-22f * cm +
                          0x1p-17f * (2.02f * Pm + 1.01f * cm + 1.05f * X);
         const float bv = finite_x ? bf16_up(X + 3.0f * E0 + 1e-30f) : 0.0f;
         const float tau = 2.2f * E0 + 1e-30f;

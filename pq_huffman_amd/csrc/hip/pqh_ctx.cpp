@@ -14,6 +14,15 @@ int pqh_set_error(pqh_ctx* ctx, int code, const char* fmt, ...) {
     return code;
 }
 
+bool pqh_debug_sync() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("PQH_DEBUG_SYNC");
+        v = (e && *e && *e != '0') ? 1 : 0;
+    }
+    return v == 1;
+}
+
 int pqh_use_device(pqh_ctx* ctx) {
     PQH_HIP(ctx, hipSetDevice(ctx->device));
     return PQH_OK;

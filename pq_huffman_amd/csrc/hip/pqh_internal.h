@@ -47,7 +47,14 @@ int pqh_use_device(pqh_ctx* ctx);
                                  #expr, hipGetErrorString(_e));                          \
     } while (0)
 
-#define PQH_LAUNCH_CHECK(ctx) PQH_HIP(ctx, hipGetLastError())
+// PQH_DEBUG_SYNC=1: synchronise and check after every launch, so an asynchronous fault is
+// reported by the call that caused it (diagnostics only).
+bool pqh_debug_sync();
+#define PQH_LAUNCH_CHECK(ctx)                                                             \
+    do {                                                                                  \
+        PQH_HIP(ctx, hipGetLastError());                                                  \
+        if (pqh_debug_sync()) PQH_HIP(ctx, hipStreamSynchronize((ctx)->stream));          \
+    } while (0)
 
 // Device-side code tables shared by the encode and decode kernels (pqh_tables.hip).
 //   enc [m][items] u64: (len << 56) | code (right-aligned, len <= 56; 0 = no code)

@@ -44,7 +44,7 @@ huff_trees(const uint32_t* __restrict__ counts, int k, long long trees,
     unsigned long long* out = enc + tree * k;
 #define H(i) heap[(i) * TPW + t]
     int size = 0;
-    auto push = [&](unsigned long long e) {
+    auto push = [&](unsigned long long e) {   // huffman_encode.c:33-46
         int i = size++;
         const unsigned long long w = e >> 16;
         while (i > 0) {
@@ -56,43 +56,50 @@ huff_trees(const uint32_t* __restrict__ counts, int k, long long trees,
         }
         H(i) = e;
     };
-    auto pop = [&]() -> unsigned long long {
+    auto pop = [&]() -> unsigned long long {  // huffman_encode.c:48-76, branch-free children
         const unsigned long long top = H(0);
         const unsigned long long last = H(--size);
         const unsigned long long w = last >> 16;
+        const int lim = size > 0 ? size - 1 : 0;
         int i = 0;
         for (;;) {
             const int l = 2 * i + 1, r = l + 1;
-            int nx = -1;
-            unsigned long long hl = 0, hr = 0;
-            if (l < size) {
-                hl = H(l);
-                if (r < size) {
-                    hr = H(r);
-                    if ((hl >> 16) <= (hr >> 16)) {
-                        if (w > (hl >> 16)) nx = l;
-                    } else if (w > (hr >> 16)) {
-                        nx = r;
-                    }
-                } else if (w > (hl >> 16)) {
-                    nx = l;
-                }
-            }
-            if (nx < 0) break;
-            H(i) = nx == l ? hl : hr;
-            i = nx;
+            const unsigned long long hl = H(min(l, lim)), hr = H(min(r, lim));
+            const unsigned long long wl = hl >> 16, wr = hr >> 16;
+            const bool lv = l < size, rv = r < size;
+            const bool take_l = lv && w > wl && (!rv || wl <= wr);
+            const bool take_r = !take_l && rv && w > wr && wr <= wl;
+            if (!(take_l || take_r)) break;
+            H(i) = take_l ? hl : hr;
+            i = take_l ? l : r;
         }
         H(i) = last;
         return top;
     };
     int nz = 0;
-    for (int s = 0; s < k; ++s) {
+    const uint4* cnt4 = reinterpret_cast<const uint4*>(cnt);
+    const int kv = (k & 31) ? 0 : k;           // vector part (counts rows are 16-B aligned)
+    for (int s = kv; s < k; ++s) {             // small / odd alphabets
         const uint32_t c = cnt[s];
-        out[s] = 0;
         if (c) {
             lsym[nz * TPW + t] = (uint16_t)s;
             push(((unsigned long long)c << 16) | (unsigned)nz);
             ++nz;
+        }
+    }
+    for (int s0 = 0; s0 < kv; s0 += 32) {       // 128 B of counts in flight per lane
+        uint4 q[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) q[u] = cnt4[(s0 >> 2) + u];
+#pragma unroll
+        for (int u = 0; u < 32; ++u) {
+            const uint32_t c = u % 4 == 0 ? q[u / 4].x : u % 4 == 1 ? q[u / 4].y
+                             : u % 4 == 2 ? q[u / 4].z : q[u / 4].w;
+            if (c) {
+                lsym[nz * TPW + t] = (uint16_t)(s0 + u);
+                push(((unsigned long long)c << 16) | (unsigned)nz);
+                ++nz;
+            }
         }
     }
     if (nz == 0) return;
@@ -117,6 +124,10 @@ huff_trees(const uint32_t* __restrict__ counts, int k, long long trees,
     sp = 1;
     bool too_long = false;
     while (sp) {
+        if (sp > KMAX) {   // cannot happen for a binary tree of <= KMAX leaves
+            too_long = true;
+            break;
+        }
         --sp;
         const uint32_t meta = smeta[sp * TPW + t];
         const unsigned long long code = H(sp);
@@ -249,8 +260,8 @@ lut_alloc(long long tables, long long desc_cap, long long lut2_cap, uint32_t* __
 __global__ void __launch_bounds__(256)
 lut_fill(const unsigned long long* __restrict__ enc, int k, int l2_bits, const uint32_t* __restrict__ meta,
          const uint32_t* __restrict__ sizes, uint16_t* __restrict__ lut1, uint16_t* __restrict__ lut2,
-         uint32_t* __restrict__ desc, pqh_long_code* __restrict__ longs,
-         uint32_t* __restrict__ long_cnt) {
+         uint32_t* __restrict__ desc, long long desc_cap, long long lut2_cap,
+         pqh_long_code* __restrict__ longs, uint32_t* __restrict__ long_cnt) {
     __shared__ uint32_t w2max[1 << kL1Max];
     __shared__ uint32_t sub_id[1 << kL1Max];
     __shared__ uint32_t sub_off[1 << kL1Max];
@@ -295,7 +306,7 @@ lut_fill(const unsigned long long* __restrict__ enc, int k, int l2_bits, const u
         if (w2max[p]) {
             sub_id[p] = c_id;
             sub_off[p] = c_off;
-            if (subs) desc[dbase + c_id] = ((l2base + c_off) << 4) | w2max[p];
+            if (subs && dbase + c_id < desc_cap) desc[dbase + c_id] = ((l2base + c_off) << 4) | w2max[p];
             ++c_id;
             c_off += 1u << w2max[p];
         }
@@ -304,7 +315,8 @@ lut_fill(const unsigned long long* __restrict__ enc, int k, int l2_bits, const u
     if (subs) {
         for (int p = threadIdx.x; p < np; p += blockDim.x)
             if (w2max[p])
-                for (uint32_t q = 0; q < (1u << w2max[p]); ++q) lut2[l2base + sub_off[p] + q] = 0;
+                for (uint32_t q = 0; q < (1u << w2max[p]); ++q)
+                    if (l2base + sub_off[p] + q < lut2_cap) lut2[l2base + sub_off[p] + q] = 0;
     }
     __syncthreads();
     for (int s = threadIdx.x; s < k; s += blockDim.x) {
@@ -326,12 +338,13 @@ lut_fill(const unsigned long long* __restrict__ enc, int k, int l2_bits, const u
             const unsigned rest = (unsigned)(code & ((1ull << rem) - 1));
             const uint32_t base = l2base + sub_off[p] + (rest << (w2 - rem));
             const uint16_t val = (uint16_t)((rem << 12) | s);
-            for (unsigned j = 0; j < (1u << (w2 - rem)); ++j) lut2[base + j] = val;
+            for (unsigned j = 0; j < (1u << (w2 - rem)); ++j)
+                if (base + j < lut2_cap) lut2[base + j] = val;
         } else {
             if (subs) {
                 L1[p] = (uint16_t)((15u << 12) | sub_id[p]);
                 const unsigned rest = (unsigned)((code >> (rem - w2)) & ((1u << w2) - 1));
-                lut2[l2base + sub_off[p] + rest] = (uint16_t)(15u << 12);
+                if (l2base + sub_off[p] + rest < lut2_cap) lut2[l2base + sub_off[p] + rest] = (uint16_t)(15u << 12);
             } else {
                 L1[p] = (uint16_t)((15u << 12) | 0xFFFu);
             }
@@ -401,7 +414,8 @@ dec_chunks(const uint32_t* __restrict__ words, long long nwords, long long n, in
            const unsigned long long* __restrict__ chunk_off, const CodeT* __restrict__ chunk_prev,
            const uint16_t* __restrict__ lut1_g, const uint16_t* __restrict__ lut2,
            const uint32_t* __restrict__ meta_g, const uint32_t* __restrict__ desc,
-           long long tables, const pqh_long_code* __restrict__ longs,
+           long long tables, long long desc_cap, long long lut2_cap,
+           const pqh_long_code* __restrict__ longs,
            const uint32_t* __restrict__ long_cnt, CodeT* __restrict__ out,
            unsigned long long* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -443,6 +457,10 @@ dec_chunks(const uint32_t* __restrict__ words, long long nwords, long long n, in
                 const long long tab = (long long)i * roots + (context ? prev[i] : 0u);
                 const uint32_t mt = meta[tab];
                 const int w1 = (int)(mt & 15u);
+                if (w1 < 1 || w1 > kL1Max) {
+                    atomicOr(err, 1ull);
+                    return;
+                }
                 const uint16_t e = lut1[(tab << kL1Max) + br.peek(w1)];
                 const int len = e >> 12;
                 bool slow = false;
@@ -450,9 +468,19 @@ dec_chunks(const uint32_t* __restrict__ words, long long nwords, long long n, in
                 if (len >= 1 && len <= w1) {
                     br.skip(len);
                 } else if (len == 15 && sym != 0xFFFu) {
-                    const uint32_t d = desc[(mt >> 8) + sym];
+                    const long long di = (long long)(mt >> 8) + sym;
+                    if (di >= desc_cap) {
+                        atomicOr(err, 1ull);
+                        return;
+                    }
+                    const uint32_t d = desc[di];
                     const int w2 = (int)(d & 15u);
-                    const uint16_t e2 = lut2[(d >> 4) + (br.peek(w1 + w2) & ((1u << w2) - 1u))];
+                    const long long li = (long long)(d >> 4) + (br.peek(w1 + w2) & ((1u << w2) - 1u));
+                    if (w2 < 1 || w2 > 12 || li >= lut2_cap) {
+                        atomicOr(err, 1ull);
+                        return;
+                    }
+                    const uint16_t e2 = lut2[li];
                     const int len2 = e2 >> 12;
                     if (len2 >= 1 && len2 <= w2) {
                         sym = e2 & 0xFFFu;
@@ -486,6 +514,10 @@ dec_chunks(const uint32_t* __restrict__ words, long long nwords, long long n, in
                         return;
                     }
                 }
+            }
+            if (sym >= (unsigned)k) {   // never from a well-formed table: stop, do not index
+                atomicOr(err, 1ull);
+                return;
             }
             prev[i] = sym;
         }
@@ -568,7 +600,7 @@ static int launch_luts(pqh_ctx* ctx, pqh_tables* t) {
     PQH_LAUNCH_CHECK(ctx);
     hipLaunchKernelGGL(lut_fill, dim3((unsigned)t->tables), dim3(256), 0, ctx->stream, t->d_enc,
                        t->k, t->l2_bits, t->d_meta, t->d_scratch, t->d_lut1, t->d_lut2, t->d_desc,
-                       t->d_long, t->d_long_cnt);
+                       t->desc_cap, t->lut2_cap, t->d_long, t->d_long_cnt);
     PQH_LAUNCH_CHECK(ctx);
     return PQH_OK;
 }
@@ -578,6 +610,8 @@ int pqh_tables_build(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts) 
     int rc = pqh_use_device(ctx);
     if (rc) return rc;
     PQH_HIP(ctx, hipMemsetAsync(t->d_err, 0, 4, ctx->stream));
+    if (reinterpret_cast<uintptr_t>(d_counts) & 15u) return PQH_ERR_ARG;
+    PQH_HIP(ctx, hipMemsetAsync(t->d_enc, 0, (size_t)t->m * t->items * 8, ctx->stream));
     const long long trees = t->tables;
     if (t->k <= 256) {
         constexpr int TPW = 32;
@@ -702,7 +736,8 @@ int pqh_decode(pqh_ctx_t* ctx, const pqh_tables_t* t, const unsigned char* d_str
                        reinterpret_cast<const uint32_t*>(d_stream), nwords, n, t->m, t->k,       \
                        t->context, raw_first, chunk_vectors, d_chunk_offsets,                    \
                        static_cast<const T*>(d_chunk_prev), t->d_lut1, t->d_lut2, t->d_meta,     \
-                       t->d_desc, t->tables, t->d_long, t->d_long_cnt, static_cast<T*>(d_codes), \
+                       t->d_desc, t->tables, t->desc_cap, t->lut2_cap, t->d_long, t->d_long_cnt,  \
+                       static_cast<T*>(d_codes),                                                 \
                        ctx->d_diag + 1)
     if (t->k <= 256) {
         if (t->m == 8) {
