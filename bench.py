@@ -36,6 +36,25 @@ METRIC = "Mvec/s encode+decode round-trip, 128-d fp32 M=8 K=256; % HBM-read roof
 HBM_PEAK_GBS = 8000.0
 BYTES_PER_VEC_READ = 512          # 128 fp32
 BYTES_PER_VEC_WRITE = 8           # M=8 uint8 codes
+ROOT = os.path.dirname(os.path.abspath(__file__))
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/<round>_pmc_summary.json, written by profiles/summarize.py from a separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE pass of this same bench command)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")),
+                   key=lambda f: int(os.path.basename(f)[1:].split("_")[0]))
+    for f in reversed(files):
+        try:
+            ks = json.load(open(f))["kernels"]
+        except (OSError, ValueError, KeyError):
+            continue
+        for name, e in ks.items():
+            if name.startswith(kernel) and "hbm_bytes" in e:
+                return e["hbm_bytes"], os.path.relpath(f, ROOT)
+    return None, None
 
 
 def parse():
@@ -235,6 +254,8 @@ def main():
     if rank == 0:
         t_assign = acc["assign"] / args.steps
         achieved = (BYTES_PER_VEC_READ + BYTES_PER_VEC_WRITE) * n / t_assign / 1e9
+        traffic, traffic_src = pmc_traffic("pq_assign_mfma")
+        t_enc = (acc["assign"] + acc["hist"] + acc["codebook"] + acc["encode"]) / args.steps
         res = {
             "metric": METRIC,
             "value": round(world * n * args.steps / elapsed / 1e6, 2),
@@ -257,10 +278,13 @@ def main():
                        "chunk_vectors": args.chunk, "parallelism": f"dp{world} row shards"},
             "roofline": {"kernel": "pq_assign_mfma", "bound": "hbm",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "bytes_per_vector": BYTES_PER_VEC_READ + BYTES_PER_VEC_WRITE,
                          "avg_ms": round(t_assign * 1e3, 4)},
             "stages_ms": {s: round(v / args.steps * 1e3, 4) for s, v in acc.items()},
+            # encode-side HBM-read roofline = 512 B/vec x N / t_encode / 8 TB/s
+            "encode_read_roofline_frac": round(BYTES_PER_VEC_READ * n / t_enc / 1e9 / HBM_PEAK_GBS, 4),
             "bits_per_vector": round(bits_per_vec, 3),
             "rerank_fraction": round(rerank / (n * m), 6),
         }

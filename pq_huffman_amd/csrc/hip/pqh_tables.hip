@@ -27,67 +27,88 @@ constexpr int kMaxCodeLen = 56;
 constexpr unsigned long long kCodeMask = (1ull << 56) - 1;
 
 // ------------------------------------------------------------------- tree building
-template <int KMAX, int TPW>
-__global__ void __launch_bounds__(64)
-huff_trees(const uint32_t* __restrict__ counts, int k, long long trees,
-           unsigned long long* __restrict__ enc, uint32_t* __restrict__ err) {
-    extern __shared__ __attribute__((aligned(16))) char lds[];
-    unsigned long long* heap = reinterpret_cast<unsigned long long*>(lds);  // [KMAX][TPW]
-    uint32_t* kid = reinterpret_cast<uint32_t*>(heap + KMAX * TPW);          // [KMAX][TPW]
-    uint32_t* smeta = kid + KMAX * TPW;                                       // [KMAX][TPW]
-    uint16_t* lsym = reinterpret_cast<uint16_t*>(smeta + KMAX * TPW);        // [KMAX][TPW]
-    const int t = threadIdx.x;
-    if (t >= TPW) return;  // no barriers in this kernel
-    const long long tree = (long long)blockIdx.x * TPW + t;
-    if (tree >= trees) return;
-    const uint32_t* cnt = counts + tree * k;
-    unsigned long long* out = enc + tree * k;
-#define H(i) heap[(i) * TPW + t]
-    int size = 0;
-    auto push = [&](unsigned long long e) {   // huffman_encode.c:33-46
+// A tree's heap lives in LDS, interleaved tree-minor (entry i of lane t at [i * TPW + t]) so
+// the lanes of a wave touch consecutive words.  Keys are (weight << NB | node): a 32-bit key
+// (NB = 9) when the tree's total weight is below 2^23, else 64-bit (NB = 16).  Comparisons
+// use the weight only, exactly as the reference heap does.
+template <typename Key, int NB, int TPW, int CAP>
+struct LdsHeap {
+    Key* h;
+    int size;
+    __device__ __forceinline__ Key get(int i) const { return h[i * TPW]; }
+    __device__ __forceinline__ void set(int i, Key v) { h[i * TPW] = v; }
+    // huffman_encode.c:33-46: sift up while strictly lighter than the parent.  The first
+    // three ancestors are read in one round trip (most pushes stop within them).
+    __device__ __forceinline__ void push(Key e) {
         int i = size++;
-        const unsigned long long w = e >> 16;
-        while (i > 0) {
-            const int p = (i - 1) >> 1;
-            const unsigned long long hp = H(p);
-            if (w >= (hp >> 16)) break;
-            H(i) = hp;
-            i = p;
+        const Key w = e >> NB;
+        const int p1 = (i - 1) >> 1, p2 = (p1 - 1) >> 1, p3 = (p2 - 1) >> 1;
+        Key a1 = get(max(p1, 0)), a2 = get(max(p2, 0)), a3 = get(max(p3, 0));
+        asm volatile("" : "+v"(a1), "+v"(a2), "+v"(a3));   // one wait for all three
+        if (i > 0 && w < (a1 >> NB)) {
+            set(i, a1);
+            i = p1;
+            if (i > 0 && w < (a2 >> NB)) {
+                set(i, a2);
+                i = p2;
+                if (i > 0 && w < (a3 >> NB)) {
+                    set(i, a3);
+                    i = p3;
+                    while (i > 0) {
+                        const int p = (i - 1) >> 1;
+                        const Key hp = get(p);
+                        if (w >= (hp >> NB)) break;
+                        set(i, hp);
+                        i = p;
+                    }
+                }
+            }
         }
-        H(i) = e;
-    };
-    auto pop = [&]() -> unsigned long long {  // huffman_encode.c:48-76, branch-free children
-        const unsigned long long top = H(0);
-        const unsigned long long last = H(--size);
-        const unsigned long long w = last >> 16;
-        const int lim = size > 0 ? size - 1 : 0;
+        set(i, e);
+    }
+    // huffman_encode.c:48-76: the last entry sifts down from the root; at each level the
+    // left child is the candidate unless the right one is strictly lighter, and the entry
+    // moves while strictly heavier than the candidate.  Children and grandchildren are read
+    // together, so two levels cost one LDS round trip.
+    __device__ __forceinline__ Key pop() {
+        const Key top = get(0);
+        const Key last = get(--size);
+        const Key w = last >> NB;
+        constexpr int lim = CAP - 1;
         int i = 0;
         for (;;) {
-            const int l = 2 * i + 1, r = l + 1;
-            const unsigned long long hl = H(min(l, lim)), hr = H(min(r, lim));
-            const unsigned long long wl = hl >> 16, wr = hr >> 16;
-            const bool lv = l < size, rv = r < size;
-            const bool take_l = lv && w > wl && (!rv || wl <= wr);
-            const bool take_r = !take_l && rv && w > wr && wr <= wl;
-            if (!(take_l || take_r)) break;
-            H(i) = take_l ? hl : hr;
-            i = take_l ? l : r;
+            const int l = 2 * i + 1;
+            if (l >= size) break;
+            const int g = 2 * l + 1;
+            const Key kl = get(l), kr = get(min(l + 1, lim));
+            Key g0 = get(min(g, lim)), g1 = get(min(g + 1, lim));
+            Key g2 = get(min(g + 2, lim)), g3 = get(min(g + 3, lim));
+            asm volatile("" : "+v"(g0), "+v"(g1), "+v"(g2), "+v"(g3));   // keep the loads together
+            const bool pr = l + 1 < size && (kr >> NB) < (kl >> NB);
+            const Key kc = pr ? kr : kl;
+            if (!(w > (kc >> NB))) break;
+            set(i, kc);
+            i = l + (pr ? 1 : 0);
+            const int l2 = 2 * i + 1;
+            if (l2 >= size) break;
+            const Key a = pr ? g2 : g0, b = pr ? g3 : g1;
+            const bool pr2 = l2 + 1 < size && (b >> NB) < (a >> NB);
+            const Key kc2 = pr2 ? b : a;
+            if (!(w > (kc2 >> NB))) break;
+            set(i, kc2);
+            i = l2 + (pr2 ? 1 : 0);
         }
-        H(i) = last;
+        set(i, last);
         return top;
-    };
-    int nz = 0;
-    const uint4* cnt4 = reinterpret_cast<const uint4*>(cnt);
-    const int kv = (k & 31) ? 0 : k;           // vector part (counts rows are 16-B aligned)
-    for (int s = kv; s < k; ++s) {             // small / odd alphabets
-        const uint32_t c = cnt[s];
-        if (c) {
-            lsym[nz * TPW + t] = (uint16_t)s;
-            push(((unsigned long long)c << 16) | (unsigned)nz);
-            ++nz;
-        }
     }
-    for (int s0 = 0; s0 < kv; s0 += 32) {       // 128 B of counts in flight per lane
+};
+
+// Count scan: calls f(symbol, count) for every nonzero count in symbol order.
+template <typename F>
+__device__ __forceinline__ void scan_counts(const uint32_t* __restrict__ cnt, int k, F&& f) {
+    const int kv = (k & 31) ? 0 : k;           // vector part (count rows are 16-B aligned)
+    const uint4* cnt4 = reinterpret_cast<const uint4*>(cnt);
+    for (int s0 = 0; s0 < kv; s0 += 32) {      // 128 B of counts in flight per lane
         uint4 q[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) q[u] = cnt4[(s0 >> 2) + u];
@@ -95,61 +116,97 @@ huff_trees(const uint32_t* __restrict__ counts, int k, long long trees,
         for (int u = 0; u < 32; ++u) {
             const uint32_t c = u % 4 == 0 ? q[u / 4].x : u % 4 == 1 ? q[u / 4].y
                              : u % 4 == 2 ? q[u / 4].z : q[u / 4].w;
-            if (c) {
-                lsym[nz * TPW + t] = (uint16_t)(s0 + u);
-                push(((unsigned long long)c << 16) | (unsigned)nz);
-                ++nz;
-            }
+            if (c) f(s0 + u, c);
         }
     }
-    if (nz == 0) return;
+    for (int s = kv; s < k; ++s) {             // small / odd alphabets
+        const uint32_t c = cnt[s];
+        if (c) f(s, c);
+    }
+}
+
+// Merge loop of huffman_codebook_init_encoder (huffman_encode.c:150-190) on one lane's heap:
+// the nz leaves (counts lcnt, in symbol order) are pushed, then pop two / push their sum
+// until one node is left.  Returns the node count; kid[q - nz] = children of internal node q.
+template <typename Key, int NB, int TPW, int CAP>
+__device__ __forceinline__ int merge_tree(Key* heap_base, const uint32_t* lcnt, int nz,
+                                          uint32_t* kid) {
+    LdsHeap<Key, NB, TPW, CAP> hp{heap_base, 0};
+    for (int j = 0; j < nz; ++j) hp.push(((Key)lcnt[j * TPW] << NB) | (Key)j);
     int next = nz;
-    if (size == 1) {  // lone symbol: code "0" (huffman_encode.c:168-177)
-        const unsigned long long e = pop();
-        kid[(next - nz) * TPW + t] = (uint32_t)(e & 0xFFFFu) | 0xFFFF0000u;
-        push(((e >> 16) << 16) | (unsigned)next);
+    const Key nmask = ((Key)1 << NB) - 1;
+    if (hp.size == 1) {  // lone symbol: code "0" (huffman_encode.c:168-177)
+        const Key e = hp.pop();
+        kid[0] = (uint32_t)(e & nmask) | 0xFFFF0000u;
+        hp.push(((e >> NB) << NB) | (Key)next);
         ++next;
     }
-    while (size > 1) {
-        const unsigned long long a = pop();
-        const unsigned long long b = pop();
-        kid[(next - nz) * TPW + t] = (uint32_t)(a & 0xFFFFu) | ((uint32_t)(b & 0xFFFFu) << 16);
-        push((((a >> 16) + (b >> 16)) << 16) | (unsigned)next);
+    while (hp.size > 1) {
+        const Key a = hp.pop();
+        const Key b = hp.pop();
+        kid[(next - nz) * TPW] = (uint32_t)(a & nmask) | ((uint32_t)(b & nmask) << 16);
+        hp.push((((a >> NB) + (b >> NB)) << NB) | (Key)next);
         ++next;
     }
-    // depth-first code assignment; heap slots hold the codes of the stacked nodes
-    int sp = 0;
-    smeta[0 * TPW + t] = (uint32_t)(H(0) & 0xFFFFu);
-    H(0) = 0;
-    sp = 1;
+    return next;
+}
+
+template <int KMAX, int TPW>
+__global__ void __launch_bounds__(64)
+huff_trees(const uint32_t* __restrict__ counts, int k, long long trees,
+           unsigned long long* __restrict__ enc, uint32_t* __restrict__ err) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    // per tree: ncode u64 [2 KMAX] (the heap aliases its start), kid u32 [KMAX], lsym u16 [KMAX]
+    unsigned long long* ncode_all = reinterpret_cast<unsigned long long*>(lds);
+    uint32_t* kid_all = reinterpret_cast<uint32_t*>(ncode_all + 2 * KMAX * TPW);
+    uint16_t* lsym_all = reinterpret_cast<uint16_t*>(kid_all + KMAX * TPW);
+    const int t = threadIdx.x;
+    if (t >= TPW) return;  // no barriers in this kernel
+    const long long tree = (long long)blockIdx.x * TPW + t;
+    if (tree >= trees) return;
+    const uint32_t* cnt = counts + tree * k;
+    unsigned long long* out = enc + tree * k;
+    unsigned long long* ncode = ncode_all + t;
+    uint32_t* kid = kid_all + t;
+    uint16_t* lsym = lsym_all + t;
+
+    // nonzero symbols in symbol order; their counts are staged past the heap's storage
+    uint32_t* lcnt = reinterpret_cast<uint32_t*>(ncode_all) + 2 * KMAX * TPW + t;
+    unsigned long long total = 0;
+    int nz = 0;
+    scan_counts(cnt, k, [&](int s, uint32_t c) {
+        lsym[nz * TPW] = (uint16_t)s;
+        lcnt[nz * TPW] = c;
+        total += c;
+        ++nz;
+    });
+    if (nz == 0) return;
+    int next;
+    if (KMAX <= 256 && total < (1ull << 23))
+        next = merge_tree<uint32_t, 9, TPW, KMAX>(reinterpret_cast<uint32_t*>(ncode_all) + t,
+                                                  lcnt, nz, kid);
+    else
+        next = merge_tree<unsigned long long, 16, TPW, KMAX>(ncode, lcnt, nz, kid);
+
+    // codes top-down in reverse creation order (parents are created after their children):
+    // ncode[q] = depth << 56 | code, child 0 appends bit 0 (huffman_encode.c:100-132)
+    constexpr unsigned long long kMask = (1ull << 56) - 1;
+    ncode[(next - 1) * TPW] = 0;   // root: the heap is dead, its storage is reused
+    for (int q = next - 1; q >= nz; --q) {
+        const unsigned long long e = ncode[q * TPW];
+        const uint32_t kk = kid[(q - nz) * TPW];
+        const unsigned long long d = min((e >> 56) + 1, 255ull);
+        const unsigned long long c = (e & kMask) << 1;
+        ncode[(kk & 0xFFFFu) * TPW] = (d << 56) | (c & kMask);
+        if ((kk >> 16) != 0xFFFFu) ncode[(kk >> 16) * TPW] = (d << 56) | ((c | 1ull) & kMask);
+    }
     bool too_long = false;
-    while (sp) {
-        if (sp > KMAX) {   // cannot happen for a binary tree of <= KMAX leaves
-            too_long = true;
-            break;
-        }
-        --sp;
-        const uint32_t meta = smeta[sp * TPW + t];
-        const unsigned long long code = H(sp);
-        const int node = (int)(meta & 0xFFFFu), depth = (int)(meta >> 16);
-        if (node < nz) {
-            if (depth > kMaxCodeLen) too_long = true;
-            else out[lsym[node * TPW + t]] = ((unsigned long long)depth << 56) | code;
-            continue;
-        }
-        const uint32_t kk = kid[(node - nz) * TPW + t];
-        const uint32_t c0 = kk & 0xFFFFu, c1 = kk >> 16;
-        smeta[sp * TPW + t] = c0 | ((uint32_t)(depth + 1) << 16);
-        H(sp) = code << 1;
-        ++sp;
-        if (c1 != 0xFFFFu) {
-            smeta[sp * TPW + t] = c1 | ((uint32_t)(depth + 1) << 16);
-            H(sp) = (code << 1) | 1ull;
-            ++sp;
-        }
+    for (int j = 0; j < nz; ++j) {
+        const unsigned long long e = ncode[j * TPW];
+        if ((e >> 56) > (unsigned long long)kMaxCodeLen) too_long = true;
+        else out[lsym[j * TPW]] = e;
     }
     if (too_long) atomicOr(err, 1u);
-#undef H
 }
 
 // Two-level decode tables.  Block per alphabet; lut_plan sizes, lut_alloc (one workgroup)
@@ -614,15 +671,15 @@ int pqh_tables_build(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts) 
     PQH_HIP(ctx, hipMemsetAsync(t->d_enc, 0, (size_t)t->m * t->items * 8, ctx->stream));
     const long long trees = t->tables;
     if (t->k <= 256) {
-        constexpr int TPW = 32;
-        const size_t lds = (size_t)256 * TPW * (8 + 4 + 4 + 2);
+        constexpr int TPW = 16;
+        const size_t lds = (size_t)256 * TPW * (16 + 4 + 2);
         PQH_HIP(ctx, hipFuncSetAttribute((const void*)huff_trees<256, TPW>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         hipLaunchKernelGGL((huff_trees<256, TPW>), dim3((unsigned)((trees + TPW - 1) / TPW)), dim3(64),
                            lds, ctx->stream, d_counts, t->k, trees, t->d_enc, t->d_err);
     } else {
-        constexpr int TPW = 2;
-        const size_t lds = (size_t)4096 * TPW * (8 + 4 + 4 + 2);
+        constexpr int TPW = 1;
+        const size_t lds = (size_t)4096 * TPW * (16 + 4 + 2);
         PQH_HIP(ctx, hipFuncSetAttribute((const void*)huff_trees<4096, TPW>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         hipLaunchKernelGGL((huff_trees<4096, TPW>), dim3((unsigned)((trees + TPW - 1) / TPW)), dim3(64),

@@ -1,0 +1,44 @@
+"""Micro-benchmark of the GPU code-table build (trees + decode tables) on a realistic
+context histogram: SIFT-like codes -> histogram -> Tables.build timed with HIP events.
+Diagnostic tool (not part of the product path)."""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+from pq_huffman_amd import codec  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    n, m, k = 1_000_000, 8, 256
+    g = torch.Generator(device=dev)
+    g.manual_seed(1)
+    # Markov-ish skewed codes: next code near the previous one with Zipf jumps
+    z = torch.distributions.Zipf if hasattr(torch.distributions, "Zipf") else None
+    base = torch.randint(0, k, (n, m), generator=g, device=dev)
+    skew = (torch.rand((n, m), generator=g, device=dev) ** 3 * k).long()
+    codes = ((base // 16) * 16 + skew % 16).clamp(0, k - 1).to(torch.uint8)
+    ctx = codec.Context(0)
+    for mode in (True, False):
+        items = k * k if mode else k
+        counts = torch.zeros((m, items), dtype=torch.int32, device=dev)
+        codec.histogram(ctx, codes, k, mode, counts=counts)
+        tabs = codec.Tables(ctx, m, k, mode)
+        for _ in range(3):
+            tabs.build(counts)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 20
+        e0.record()
+        for _ in range(reps):
+            tabs.build(counts)
+        e1.record()
+        torch.cuda.synchronize()
+        print(f"phase={os.environ.get('PQH_TREE_PHASE', '0')} ctx={mode} build_ms={e0.elapsed_time(e1) / reps:.4f}",
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
