@@ -138,7 +138,7 @@ def main():
     args = parse()
     import torch
     import torch.distributed as dist
-    from pq_huffman_amd import codec
+    from pq_huffman_amd import codec, shard
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -165,8 +165,6 @@ def main():
     coff = torch.empty(chunks, dtype=torch.int64, device=dev)
     cprev = torch.empty((chunks, m), dtype=torch.uint8, device=dev) if ctxm else None
     out = torch.zeros(n * m * 56 // 8 + 64, dtype=torch.uint8, device=dev)  # worst case
-    halo_all = torch.zeros((world, m), dtype=torch.uint8, device=dev)
-    tot_all = torch.zeros(world, dtype=torch.int64, device=dev)
 
     ev = {s: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for s in ("assign", "hist", "codebook", "encode", "decode")}
@@ -181,31 +179,26 @@ def main():
         rec("assign", 0)
         pq.assign(x, codes)
         rec("assign", 1)
-        prev_row = None
         tc = time.perf_counter()
-        if world > 1 and ctxm:
-            dist.all_gather_into_tensor(halo_all, codes[-1].contiguous())
-            prev_row = halo_all[rank - 1] if rank > 0 else None
+        prev_row = shard.exchange_halo(codes[-1], world, rank) if ctxm else None
         acc_coll = time.perf_counter() - tc
         rec("hist", 0)
         counts.zero_()
         codec.histogram(ctx, codes, k, ctxm, prev_row=prev_row, counts=counts)
         rec("hist", 1)
         tc = time.perf_counter()
-        if world > 1:
-            dist.all_reduce(counts)
+        shard.reduce_counts(counts, world)
         acc_coll += time.perf_counter() - tc
         rec("codebook", 0)
         tabs.build(counts)                        # GPU trees + lookup tables, no host trip
         rec("codebook", 1)
-        raw_first = 1 if rank == 0 else 0
+        raw_first = shard.raw_first(rank)
         rec("encode", 0)
         total = codec.encode_size(ctx, tabs, codes, raw_first, prev_row)
         tc = time.perf_counter()
-        if world > 1:
-            dist.all_gather_into_tensor(tot_all, total)
-            offs = torch.cumsum(tot_all, 0) - tot_all
-            bit_off = int(offs[rank].item()) % 32     # word-aligned with the global stream
+        if world > 1:   # place the shard in the global stream (word-aligned buffer)
+            goff, _ = shard.bit_offsets(total, world, rank)
+            bit_off = shard.local_bit_offset(goff)
         else:
             bit_off = 0
         acc_coll += time.perf_counter() - tc
