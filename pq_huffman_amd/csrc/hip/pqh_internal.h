@@ -59,13 +59,12 @@ bool pqh_debug_sync();
 // Device-side code tables shared by the encode and decode kernels (pqh_tables.hip).
 //   enc [m][items] u64: (len << 56) | code (right-aligned, len <= 56; 0 = no code)
 //   Decode: two-level lookup per alphabet (tables = m * roots, roots = K in context mode)
-//   lut1 [tables][1 << l1_bits] u16, first W1_t = min(longest code, l1_bits) entries used:
-//        (len << 12) | sym for 1 <= len <= W1_t; (15 << 12) | sub = longer code, subtable
-//        `sub` of this alphabet; 0 = invalid prefix
-//   meta [tables] u32: (first descriptor << 8) | W1_t
-//   desc [..] u32: (offset in lut2 << 4) | w2 -- subtable of 2^w2 entries for the bits
-//        after the W1_t-bit prefix: (len2 << 12) | sym, 15 << 12 = even longer (linear
-//        search in longs), 0 = invalid
+//   lut1 [tables][1 << kL1Max] u16, the first 2^l1_bits entries used (W1 = l1_bits for
+//        every alphabet): (len << 12) | sym for 1 <= len <= W1 (replicated);
+//        (15 << 12) | sub = a longer code, subtable `sub` of this alphabet; 0 = invalid
+//   meta [tables] u32: l2base << 9 | noL2 << 8 | w2 << 4 | W1 -- the alphabet's subtables
+//        are 2^w2-entry blocks at lut2[l2base + (sub << w2)] holding (len2 << 12) | sym,
+//        15 << 12 = even longer (linear search in longs), 0 = invalid
 //   longs [tables][k] {code, len, sym}, long_cnt [tables]: codes beyond both levels
 struct pqh_long_code {
     unsigned long long code;
@@ -77,12 +76,11 @@ struct pqh_tables {
     pqh_ctx* ctx = nullptr;
     int m = 0, k = 0, context = 0, roots = 1, l1_bits = 9, l2_bits = 8;
     long long items = 0, tables = 0;
-    long long lut2_cap = 0, desc_cap = 0;
+    long long lut2_cap = 0;
     unsigned long long* d_enc = nullptr;
     uint16_t* d_lut1 = nullptr;
     uint16_t* d_lut2 = nullptr;
     uint32_t* d_meta = nullptr;
-    uint32_t* d_desc = nullptr;
     uint32_t* d_scratch = nullptr;   // per-table sizes for the allocation scan
     pqh_long_code* d_long = nullptr;
     uint32_t* d_long_cnt = nullptr;

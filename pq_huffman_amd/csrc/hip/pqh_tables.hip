@@ -151,27 +151,103 @@ __device__ __forceinline__ int merge_tree(Key* heap_base, const uint32_t* lcnt, 
     return next;
 }
 
+// Sentinel heap for K <= 256 and tree totals below 2^22 (the common case): u32 keys
+// weight << 10 | tie << 9 | node.  Every slot past the heap holds 0xFFFFFFFF, so children
+// need no bounds checks.  The reference rules (huffman_encode.c:33-76) become single
+// integer ops: "left child unless the right one is strictly lighter" is
+// min(left, right | TIE) (the tie bit makes an equal-weight right child lose), and "move
+// while strictly heavier" is child < (last & ~LOW) (weights compared, low bits ignored).
+template <int TPW>
+struct SentinelHeap {
+    static constexpr uint32_t kTie = 1u << 9, kLow = (1u << 10) - 1, kMax = 0xFFFFFFFFu;
+    static constexpr int kSlots = 1024;        // children of every node < 256, and theirs
+    uint32_t* h;                               // this lane's slot 0 (stride TPW)
+    int size;
+    __device__ __forceinline__ uint32_t get(int i) const { return h[i * TPW]; }
+    __device__ __forceinline__ void set(int i, uint32_t v) { h[i * TPW] = v; }
+    // sift up while strictly lighter than the parent; three ancestors per LDS round trip
+    __device__ __forceinline__ void push(uint32_t e) {
+        int i = size++;
+        bool act = true;
+        while (true) {
+            const int p1 = (i - 1) >> 1, p2 = (p1 - 1) >> 1, p3 = (p2 - 1) >> 1;
+            uint32_t a1 = get(max(p1, 0)), a2 = get(max(p2, 0)), a3 = get(max(p3, 0));
+            asm volatile("" : "+v"(a1), "+v"(a2), "+v"(a3));
+            bool mv = act && i > 0 && e < (a1 & ~kLow);
+            if (mv) { set(i, a1); i = p1; }
+            act = mv;
+            mv = act && i > 0 && e < (a2 & ~kLow);
+            if (mv) { set(i, a2); i = p2; }
+            act = mv;
+            mv = act && i > 0 && e < (a3 & ~kLow);
+            if (mv) { set(i, a3); i = p3; }
+            act = mv;
+            if (!__any(act)) break;
+        }
+        set(i, e);
+    }
+    __device__ __forceinline__ uint32_t pop() {
+        const uint32_t top = get(0);
+        const uint32_t last = get(--size);
+        set(size, kMax);                       // the vacated slot becomes a sentinel
+        const uint32_t lw = last & ~kLow;      // child < lw  <=>  child weight < last weight
+        int i = 0;
+        bool act = true;
+        while (true) {
+            const int c = 2 * i + 1, g = 4 * i + 3;
+            uint32_t kl = get(c), kr = get(c + 1);
+            uint32_t g0 = get(g), g1 = get(g + 1), g2 = get(g + 2), g3 = get(g + 3);
+            asm volatile("" : "+v"(kl), "+v"(kr), "+v"(g0), "+v"(g1), "+v"(g2), "+v"(g3));
+            const uint32_t kc = min(kl, kr | kTie);
+            const bool pr = (kc & kTie) != 0;
+            bool mv = act && kc < lw;
+            if (mv) { set(i, kc & ~kTie); i = c + (int)pr; }
+            act = mv;
+            const uint32_t kc2 = min(pr ? g2 : g0, (pr ? g3 : g1) | kTie);
+            mv = act && kc2 < lw;
+            if (mv) { set(i, kc2 & ~kTie); i = 2 * i + 1 + (int)((kc2 & kTie) != 0); }
+            act = mv;
+            if (!__any(act)) break;
+        }
+        set(i, last);
+        return top;
+    }
+};
+
+// diagnostics: s_memtime stamps of tree 0's phases (read with pqh_debug_tree_stamps)
+__device__ unsigned long long g_tree_stamps[8];
+
 template <int KMAX, int TPW>
 __global__ void __launch_bounds__(64)
 huff_trees(const uint32_t* __restrict__ counts, int k, long long trees,
            unsigned long long* __restrict__ enc, uint32_t* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
-    // per tree: ncode u64 [2 KMAX] (the heap aliases its start), kid u32 [KMAX], lsym u16 [KMAX]
+    // per tree: ncode u64 [2 KMAX] (the heap aliases it), kid u32 [KMAX], lcnt u32 [KMAX],
+    // lsym u16 [KMAX]; all interleaved tree-minor
     unsigned long long* ncode_all = reinterpret_cast<unsigned long long*>(lds);
     uint32_t* kid_all = reinterpret_cast<uint32_t*>(ncode_all + 2 * KMAX * TPW);
-    uint16_t* lsym_all = reinterpret_cast<uint16_t*>(kid_all + KMAX * TPW);
+    uint32_t* lcnt_all = kid_all + KMAX * TPW;
+    uint16_t* lsym_all = reinterpret_cast<uint16_t*>(lcnt_all + KMAX * TPW);
     const int t = threadIdx.x;
-    if (t >= TPW) return;  // no barriers in this kernel
+    if (KMAX <= 256) {   // the whole workgroup fills the sentinel-heap slots (ncode region)
+        uint4* z = reinterpret_cast<uint4*>(ncode_all);
+        for (int q = t; q < 2 * KMAX * TPW / 2; q += blockDim.x)
+            z[q] = make_uint4(~0u, ~0u, ~0u, ~0u);
+        __syncthreads();
+    }
+    if (t >= TPW) return;  // no barriers below
     const long long tree = (long long)blockIdx.x * TPW + t;
     if (tree >= trees) return;
     const uint32_t* cnt = counts + tree * k;
     unsigned long long* out = enc + tree * k;
     unsigned long long* ncode = ncode_all + t;
+    const bool stamp = tree == 0;
+    if (stamp) g_tree_stamps[0] = __builtin_amdgcn_s_memtime();
     uint32_t* kid = kid_all + t;
     uint16_t* lsym = lsym_all + t;
 
-    // nonzero symbols in symbol order; their counts are staged past the heap's storage
-    uint32_t* lcnt = reinterpret_cast<uint32_t*>(ncode_all) + 2 * KMAX * TPW + t;
+    // nonzero symbols in symbol order, with their counts
+    uint32_t* lcnt = lcnt_all + t;
     unsigned long long total = 0;
     int nz = 0;
     scan_counts(cnt, k, [&](int s, uint32_t c) {
@@ -181,13 +257,35 @@ huff_trees(const uint32_t* __restrict__ counts, int k, long long trees,
         ++nz;
     });
     if (nz == 0) return;
+    if (stamp) g_tree_stamps[1] = __builtin_amdgcn_s_memtime();
     int next;
-    if (KMAX <= 256 && total < (1ull << 23))
+    if (KMAX <= 256 && total < (1ull << 22)) {
+        // sentinel heap in the ncode region (1024 u32 slots per lane = 4 KB = ncode's 512 u64)
+        SentinelHeap<TPW> hp{reinterpret_cast<uint32_t*>(ncode_all) + t, 0};   // pre-filled
+        for (int j = 0; j < nz; ++j) hp.push((lcnt[j * TPW] << 10) | (uint32_t)j);
+        if (stamp) g_tree_stamps[2] = __builtin_amdgcn_s_memtime();
+        next = nz;
+        if (hp.size == 1) {  // lone symbol: code "0" (huffman_encode.c:168-177)
+            const uint32_t e = hp.pop();
+            kid[0] = (e & 511u) | 0xFFFF0000u;
+            hp.push((e & ~1023u) | (uint32_t)next);
+            ++next;
+        }
+        while (hp.size > 1) {
+            const uint32_t a = hp.pop();
+            const uint32_t b = hp.pop();
+            kid[(next - nz) * TPW] = (a & 511u) | ((b & 511u) << 16);
+            hp.push(((a & ~1023u) + (b & ~1023u)) | (uint32_t)next);
+            ++next;
+        }
+    } else if (KMAX <= 256 && total < (1ull << 23)) {
         next = merge_tree<uint32_t, 9, TPW, KMAX>(reinterpret_cast<uint32_t*>(ncode_all) + t,
                                                   lcnt, nz, kid);
-    else
+    } else {
         next = merge_tree<unsigned long long, 16, TPW, KMAX>(ncode, lcnt, nz, kid);
+    }
 
+    if (stamp) g_tree_stamps[3] = __builtin_amdgcn_s_memtime();
     // codes top-down in reverse creation order (parents are created after their children):
     // ncode[q] = depth << 56 | code, child 0 appends bit 0 (huffman_encode.c:100-132)
     constexpr unsigned long long kMask = (1ull << 56) - 1;
@@ -207,12 +305,27 @@ huff_trees(const uint32_t* __restrict__ counts, int k, long long trees,
         else out[lsym[j * TPW]] = e;
     }
     if (too_long) atomicOr(err, 1u);
+    if (stamp) {
+        g_tree_stamps[4] = __builtin_amdgcn_s_memtime();
+        g_tree_stamps[5] = (unsigned long long)nz;
+        g_tree_stamps[6] = (unsigned long long)next;
+    }
 }
 
-// Two-level decode tables.  Block per alphabet; lut_plan sizes, lut_alloc (one workgroup)
-// scans the sizes into sub-pool offsets, lut_fill writes the entries.
+// Two-level decode tables, one block per alphabet.
+//   L1: 2^W1 u16 entries per alphabet, W1 fixed for the table set (9 in context mode, 11
+//       otherwise) so a lookup never waits for per-alphabet metadata:
+//       (len << 12) | sym for codes of len <= W1 (replicated), 15 << 12 | sub for the
+//       prefix of longer codes, 0 for bit patterns no code starts with.
+//   L2: per alphabet `nsub` subtables of one width w2 (the widest prefix needs, <= 8):
+//       entry (rem << 12) | sym, or 15 << 12 for codes longer than W1 + w2 (long list).
+//   meta[alphabet] = l2base << 9 | noL2 << 8 | w2 << 4 | W1   (l2base < 2^23)
+// lut_plan sizes every alphabet, lut_alloc (one workgroup) scans the sizes into pool
+// offsets, lut_fill writes the entries.
 constexpr int kL1Max = 11;
+constexpr long long kL2BaseMax = 1ll << 23;
 
+// per W1-prefix: widest remainder (capped at l2_bits) of the codes longer than W1
 __device__ void block_w2max(const unsigned long long* e, int k, int w1, int l2_bits,
                             uint32_t* w2max /* LDS [1 << kL1Max] */) {
     for (int i = threadIdx.x; i < (1 << w1); i += blockDim.x) w2max[i] = 0;
@@ -228,152 +341,124 @@ __device__ void block_w2max(const unsigned long long* e, int k, int w1, int l2_b
     __syncthreads();
 }
 
+__device__ __forceinline__ uint32_t block_sum_u32(uint32_t v, uint32_t* red /* LDS [4] */) {
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    return red[0] + red[1] + red[2] + red[3];
+}
+
+__device__ __forceinline__ uint32_t block_max_u32(uint32_t v, uint32_t* red /* LDS [4] */) {
+    for (int off = 32; off >= 1; off >>= 1) v = max(v, (uint32_t)__shfl_xor(v, off));
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    return max(max(red[0], red[1]), max(red[2], red[3]));
+}
+
 __global__ void __launch_bounds__(256)
-lut_plan(const unsigned long long* __restrict__ enc, int k, long long tables, int l1_bits,
-         int l2_bits, uint32_t* __restrict__ meta, uint32_t* __restrict__ sizes) {
+lut_plan(const unsigned long long* __restrict__ enc, int k, int w1, int l2_bits,
+         uint32_t* __restrict__ meta, uint32_t* __restrict__ sizes) {
     __shared__ uint32_t w2max[1 << kL1Max];
     __shared__ uint32_t red[4];
     const long long t = blockIdx.x;
-    const unsigned long long* e = enc + t * k;
-    int mx = 1;
-    for (int s = threadIdx.x; s < k; s += blockDim.x) mx = max(mx, (int)(e[s] >> 56));
-    for (int off = 32; off >= 1; off >>= 1) mx = max(mx, __shfl_xor(mx, off));
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = (uint32_t)mx;
-    __syncthreads();
-    const int maxlen = (int)max(max(red[0], red[1]), max(red[2], red[3]));
-    const int w1 = min(maxlen, l1_bits);
-    block_w2max(e, k, w1, l2_bits, w2max);
-    uint32_t nsub = 0, entries = 0;
+    block_w2max(enc + t * k, k, w1, l2_bits, w2max);
+    uint32_t nsub = 0, w2 = 0;
     for (int i = threadIdx.x; i < (1 << w1); i += blockDim.x)
         if (w2max[i]) {
             ++nsub;
-            entries += 1u << w2max[i];
+            w2 = max(w2, w2max[i]);
         }
-    for (int off = 32; off >= 1; off >>= 1) {
-        nsub += __shfl_xor(nsub, off);
-        entries += __shfl_xor(entries, off);
-    }
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = nsub;
-    __syncthreads();
-    const uint32_t tn = red[0] + red[1] + red[2] + red[3];
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = entries;
-    __syncthreads();
+    nsub = block_sum_u32(nsub, red);
+    w2 = block_max_u32(w2, red);
     if (threadIdx.x == 0) {
-        meta[t] = (uint32_t)w1;
-        sizes[t] = tn;
-        sizes[tables + t] = red[0] + red[1] + red[2] + red[3];
+        meta[t] = (w2 << 4) | (uint32_t)w1;
+        sizes[t] = nsub < 4095 ? nsub << w2 : 0xFFFFFFFFu;   // sub ids must fit 12 bits
     }
 }
 
-// one workgroup: exclusive scans of descriptor counts and sub-pool entries; an alphabet that
-// does not fit the capacities keeps only its first level (flag 0x80: long codes searched)
+// one workgroup: exclusive scan of the L2 entry counts; an alphabet that does not fit (or
+// has too many subtables) keeps only L1 (noL2 flag: its long codes go to the long list)
 __global__ void __launch_bounds__(1024)
-lut_alloc(long long tables, long long desc_cap, long long lut2_cap, uint32_t* __restrict__ meta,
+lut_alloc(long long tables, long long lut2_cap, uint32_t* __restrict__ meta,
           uint32_t* __restrict__ sizes) {
-    __shared__ unsigned long long ws[2][16];
-    __shared__ unsigned long long carry[2];
-    if (threadIdx.x < 2) carry[threadIdx.x] = 0;
+    __shared__ unsigned long long ws[16];
+    __shared__ unsigned long long carry;
+    if (threadIdx.x == 0) carry = 0;
     __syncthreads();
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     for (long long base = 0; base < tables; base += blockDim.x) {
         const long long i = base + threadIdx.x;
-        const unsigned long long a = i < tables ? sizes[i] : 0, b = i < tables ? sizes[tables + i] : 0;
-        unsigned long long ia = a, ib = b;
+        const uint32_t sz = i < tables ? sizes[i] : 0u;
+        const unsigned long long b = sz == 0xFFFFFFFFu ? 0ull : sz;
+        unsigned long long inc = b;
         for (int off = 1; off < 64; off <<= 1) {
-            const unsigned long long ya = __shfl_up(ia, off), yb = __shfl_up(ib, off);
-            if (lane >= off) {
-                ia += ya;
-                ib += yb;
-            }
+            const unsigned long long y = __shfl_up(inc, off);
+            if (lane >= off) inc += y;
         }
-        if (lane == 63) {
-            ws[0][wid] = ia;
-            ws[1][wid] = ib;
-        }
+        if (lane == 63) ws[wid] = inc;
         __syncthreads();
-        unsigned long long ba = carry[0], bb = carry[1];
-        for (int q = 0; q < wid; ++q) {
-            ba += ws[0][q];
-            bb += ws[1][q];
-        }
+        unsigned long long before = carry;
+        for (int q = 0; q < wid; ++q) before += ws[q];
         if (i < tables) {
-            const unsigned long long d0 = ba + ia - a, l0 = bb + ib - b;
-            const bool fits = d0 + a <= (unsigned long long)desc_cap && l0 + b <= (unsigned long long)lut2_cap;
-            const uint32_t w1 = meta[i] & 15u;
-            meta[i] = fits ? (uint32_t)((d0 << 8) | w1) : (0x80u | w1);
-            sizes[i] = fits ? (uint32_t)l0 : 0u;   // lut2 offset of this alphabet
+            const unsigned long long l0 = before + inc - b;
+            const bool fits = sz != 0xFFFFFFFFu && l0 + b <= (unsigned long long)lut2_cap;
+            const uint32_t low = meta[i] & 0xFFu;
+            meta[i] = fits ? (uint32_t)((l0 << 9) | low) : (0x100u | low);
         }
         __syncthreads();
-        if (threadIdx.x == blockDim.x - 1) {
-            carry[0] = ba + ia;
-            carry[1] = bb + ib;
-        }
+        if (threadIdx.x == blockDim.x - 1) carry = before + inc;
         __syncthreads();
     }
 }
 
 __global__ void __launch_bounds__(256)
-lut_fill(const unsigned long long* __restrict__ enc, int k, int l2_bits, const uint32_t* __restrict__ meta,
-         const uint32_t* __restrict__ sizes, uint16_t* __restrict__ lut1, uint16_t* __restrict__ lut2,
-         uint32_t* __restrict__ desc, long long desc_cap, long long lut2_cap,
-         pqh_long_code* __restrict__ longs, uint32_t* __restrict__ long_cnt) {
+lut_fill(const unsigned long long* __restrict__ enc, int k, int l2_bits,
+         const uint32_t* __restrict__ meta, uint16_t* __restrict__ lut1,
+         uint16_t* __restrict__ lut2, long long lut2_cap, pqh_long_code* __restrict__ longs,
+         uint32_t* __restrict__ long_cnt) {
     __shared__ uint32_t w2max[1 << kL1Max];
     __shared__ uint32_t sub_id[1 << kL1Max];
-    __shared__ uint32_t sub_off[1 << kL1Max];
-    __shared__ uint32_t nlong;
-    __shared__ uint32_t part[256][2];
+    __shared__ uint32_t nlong, nsub;
+    __shared__ uint32_t part[256];
     const long long t = blockIdx.x;
     const unsigned long long* e = enc + t * k;
     const uint32_t mt = meta[t];
     const int w1 = (int)(mt & 15u);
-    const bool subs = !(mt & 0x80u);
-    const uint32_t dbase = mt >> 8, l2base = sizes[t];
+    const int w2 = (int)((mt >> 4) & 15u);
+    const bool subs = !(mt & 0x100u) && w2 > 0;
+    const long long l2base = (long long)(mt >> 9);
     uint16_t* L1 = lut1 + (t << kL1Max);
     block_w2max(e, k, w1, l2_bits, w2max);
-    // sub ids and offsets: per-thread chunk of prefixes, then a block scan
+    // subtable ids in prefix order: per-thread chunk counts, then a serial scan of 256
     const int np = 1 << w1;
     const int per = (np + blockDim.x - 1) / blockDim.x;
     const int p0 = threadIdx.x * per, p1 = min(np, p0 + per);
-    uint32_t c_id = 0, c_off = 0;
-    for (int p = p0; p < p1; ++p)
-        if (w2max[p]) {
-            ++c_id;
-            c_off += 1u << w2max[p];
-        }
-    part[threadIdx.x][0] = c_id;
-    part[threadIdx.x][1] = c_off;
+    uint32_t c_id = 0;
+    for (int p = p0; p < p1; ++p) c_id += w2max[p] ? 1u : 0u;
+    part[threadIdx.x] = c_id;
     __syncthreads();
     if (threadIdx.x == 0) {
-        uint32_t a = 0, b = 0;
+        uint32_t a = 0;
         for (int q = 0; q < (int)blockDim.x; ++q) {
-            const uint32_t x = part[q][0], y = part[q][1];
-            part[q][0] = a;
-            part[q][1] = b;
+            const uint32_t x = part[q];
+            part[q] = a;
             a += x;
-            b += y;
         }
+        nsub = a;
         nlong = 0;
     }
     __syncthreads();
-    c_id = part[threadIdx.x][0];
-    c_off = part[threadIdx.x][1];
-    for (int p = p0; p < p1; ++p) {
-        if (w2max[p]) {
-            sub_id[p] = c_id;
-            sub_off[p] = c_off;
-            if (subs && dbase + c_id < desc_cap) desc[dbase + c_id] = ((l2base + c_off) << 4) | w2max[p];
-            ++c_id;
-            c_off += 1u << w2max[p];
-        }
-    }
+    c_id = part[threadIdx.x];
+    for (int p = p0; p < p1; ++p)
+        if (w2max[p]) sub_id[p] = c_id++;
     for (int i = threadIdx.x; i < np; i += blockDim.x) L1[i] = 0;
-    if (subs) {
-        for (int p = threadIdx.x; p < np; p += blockDim.x)
-            if (w2max[p])
-                for (uint32_t q = 0; q < (1u << w2max[p]); ++q)
-                    if (l2base + sub_off[p] + q < lut2_cap) lut2[l2base + sub_off[p] + q] = 0;
+    __syncthreads();
+    if (subs) {   // zero this alphabet's subtables
+        const long long entries = (long long)nsub << w2;
+        for (long long q = threadIdx.x; q < entries; q += blockDim.x)
+            if (l2base + q < lut2_cap) lut2[l2base + q] = 0;
     }
     __syncthreads();
     for (int s = threadIdx.x; s < k; s += blockDim.x) {
@@ -389,61 +474,64 @@ lut_fill(const unsigned long long* __restrict__ enc, int k, int l2_bits, const u
         }
         const unsigned p = (unsigned)(code >> (len - w1));
         const int rem = len - w1;
-        const int w2 = (int)w2max[p];
-        if (subs && rem <= w2) {
+        if (subs) {
             L1[p] = (uint16_t)((15u << 12) | sub_id[p]);
-            const unsigned rest = (unsigned)(code & ((1ull << rem) - 1));
-            const uint32_t base = l2base + sub_off[p] + (rest << (w2 - rem));
-            const uint16_t val = (uint16_t)((rem << 12) | s);
-            for (unsigned j = 0; j < (1u << (w2 - rem)); ++j)
-                if (base + j < lut2_cap) lut2[base + j] = val;
-        } else {
-            if (subs) {
-                L1[p] = (uint16_t)((15u << 12) | sub_id[p]);
-                const unsigned rest = (unsigned)((code >> (rem - w2)) & ((1u << w2) - 1));
-                if (l2base + sub_off[p] + rest < lut2_cap) lut2[l2base + sub_off[p] + rest] = (uint16_t)(15u << 12);
-            } else {
-                L1[p] = (uint16_t)((15u << 12) | 0xFFFu);
+            const long long sb = l2base + ((long long)sub_id[p] << w2);
+            if (rem <= w2) {
+                const unsigned rest = (unsigned)(code & ((1ull << rem) - 1));
+                const long long base = sb + ((long long)rest << (w2 - rem));
+                const uint16_t val = (uint16_t)((rem << 12) | s);
+                for (unsigned j = 0; j < (1u << (w2 - rem)); ++j)
+                    if (base + j < lut2_cap) lut2[base + j] = val;
+                continue;
             }
-            const uint32_t idx = atomicAdd(&nlong, 1u);
-            longs[t * k + idx] = {code, (uint32_t)len, (uint32_t)s};
+            const unsigned rest = (unsigned)((code >> (rem - w2)) & ((1u << w2) - 1));
+            if (sb + rest < lut2_cap) lut2[sb + rest] = (uint16_t)(15u << 12);
+        } else {
+            L1[p] = (uint16_t)((15u << 12) | 0xFFFu);
         }
+        const uint32_t idx = atomicAdd(&nlong, 1u);
+        longs[t * k + idx] = {code, (uint32_t)len, (uint32_t)s};
     }
     __syncthreads();
     if (threadIdx.x == 0) long_cnt[t] = nlong;
 }
 
 // ------------------------------------------------------------------- decoding
+// Bit reader over a word array: a 64-bit MSB-first buffer refilled one 32-bit word at a
+// time, branch-free (the next word is always read; the array is readable up to `lim`).
+// WIN = the words are this workgroup's LDS window (the compiler then emits ds_read).
 struct BitReader {
     const uint32_t* words;
-    long long nwords;
-    long long next;
-    unsigned long long pos;
+    long long lim;             // last readable index
+    long long next;            // next word to load
     unsigned long long buf;
     int have;
     __device__ __forceinline__ uint32_t load(long long i) const {
-        return i < nwords ? __builtin_bswap32(words[i]) : 0u;
+        return __builtin_bswap32(words[min(i, lim)]);
     }
-    __device__ __forceinline__ void init(const uint32_t* w, long long nw, unsigned long long p) {
+    __device__ __forceinline__ void init(const uint32_t* w, long long l, unsigned long long p) {
         words = w;
-        nwords = nw;
-        pos = p;
+        lim = l;
         const long long wi = (long long)(p >> 5);
         const int o = (int)(p & 31);
         buf = (((unsigned long long)load(wi) << 32) | load(wi + 1)) << o;
         have = 64 - o;
         next = wi + 2;
     }
-    __device__ __forceinline__ void skip(int nb) {
+    __device__ __forceinline__ unsigned long long pos() const {
+        return (unsigned long long)next * 32 - (unsigned long long)have;
+    }
+    __device__ __forceinline__ void skip(int nb) {   // nb <= 32
+        const uint32_t w = load(next);
         buf <<= nb;
         have -= nb;
-        pos += nb;
-        if (have <= 32) {
-            buf |= (unsigned long long)load(next++) << (32 - have);
-            have += 32;
-        }
+        const bool need = have <= 32;
+        buf |= need ? ((unsigned long long)w << (32 - have)) : 0ull;
+        next += need ? 1 : 0;
+        have += need ? 32 : 0;
     }
-    __device__ __forceinline__ void skip_long(int nb) {   // nb may exceed `have`
+    __device__ __forceinline__ void skip_long(int nb) {   // nb may exceed 32
         while (nb > 0) {
             const int step = nb < 32 ? nb : 32;
             skip(step);
@@ -451,9 +539,10 @@ struct BitReader {
         }
     }
     __device__ __forceinline__ uint32_t peek(int nb) const { return (uint32_t)(buf >> (64 - nb)); }
-    __device__ unsigned long long peek_long(int nb) const {  // nb <= 56, from memory
-        const long long wi = (long long)(pos >> 5);
-        const int o = (int)(pos & 31);
+    __device__ unsigned long long peek_long(int nb) const {  // nb <= 56
+        const unsigned long long p = pos();
+        const long long wi = (long long)(p >> 5);
+        const int o = (int)(p & 31);
         const unsigned long long hi = ((unsigned long long)load(wi) << 32) | load(wi + 1);
         const unsigned long long lo = load(wi + 2);
         const unsigned long long w64 = o ? ((hi << o) | (lo >> (32 - o))) : hi;
@@ -461,139 +550,215 @@ struct BitReader {
     }
 };
 
-// One lane per chunk of C vectors.  MT = parts per vector at compile time (0 = runtime m,
-// at most 16).  LDS holds the per-alphabet metadata and, when it fits (non-context mode:
-// m alphabets), the first-level tables, so most symbols cost one LDS read.
+// Decoder tables as seen by one workgroup.
+struct DecTables {
+    const uint32_t* meta;      // LDS copy
+    const uint16_t* lut1;      // LDS copy (non-context) or global
+    const uint16_t* lut2;
+    long long lut2_cap;
+    const pqh_long_code* longs;
+    const uint32_t* long_cnt;
+    int k;
+    int w1;                    // fixed first-level width of the table set
+};
+
+// one symbol of alphabet `tab` (huffman_decode.c:137-191 as table lookups); false = invalid.
+// The L1 lookup depends only on (tab, next W1 bits); the metadata read runs beside it and
+// is needed only for the second level.
+__device__ __forceinline__ bool dec_symbol(BitReader& br, const DecTables& T, long long tab,
+                                           unsigned& sym) {
+    const int w1 = T.w1;
+    const uint16_t e = T.lut1[(tab << kL1Max) + br.peek(w1)];
+    const uint32_t mt = T.meta[tab];
+    const int len = e >> 12;
+    sym = e & 0xFFFu;
+    if (len >= 1 && len <= w1) {
+        br.skip(len);
+        return sym < (unsigned)T.k;
+    }
+    if (len != 15) return false;
+    bool slow = true;
+    if (sym != 0xFFFu) {
+        const int w2 = (int)((mt >> 4) & 15u);
+        const long long li = (long long)(mt >> 9) + ((long long)sym << w2) +
+                             (br.peek(w1 + w2) & ((1u << w2) - 1u));
+        if (w2 < 1 || (mt & 0x100u) || li >= T.lut2_cap) return false;
+        const uint16_t e2 = T.lut2[li];
+        const int len2 = e2 >> 12;
+        if (len2 >= 1 && len2 <= w2) {
+            sym = e2 & 0xFFFu;
+            br.skip(w1 + len2);
+            slow = false;
+        } else if (len2 != 15) {
+            return false;
+        }
+    }
+    if (slow) {   // codes beyond both levels: rare, linear search
+        const uint32_t cnt = T.long_cnt[tab];
+        bool found = false;
+        for (uint32_t q = 0; q < cnt; ++q) {
+            const pqh_long_code lc = T.longs[tab * T.k + q];
+            if (br.peek_long((int)lc.len) == lc.code) {
+                sym = lc.sym;
+                br.skip_long((int)lc.len);
+                found = true;
+                break;
+            }
+        }
+        if (!found) return false;
+    }
+    return sym < (unsigned)T.k;   // never false for a well-formed table
+}
+
+// Per-lane decode of [v0, v1) in batches of S vectors staged in LDS; every lane of the
+// workgroup runs the batch loop (barriers).  `src` is the LDS window or the global stream.
+template <int MT, typename CodeT>
+__device__ __forceinline__ void decode_lanes(const uint32_t* src, long long src_lim,
+                                             unsigned long long start, bool live, long long j,
+                                             long long j0, long long jn, long long n, int m,
+                                             int k, int context, int raw_first,
+                                             int chunk_vectors, int S,
+                                             const CodeT* __restrict__ chunk_prev,
+                                             const DecTables& T, CodeT* stage,
+                                             CodeT* __restrict__ out, bool& ok) {
+    const int lane = threadIdx.x;
+    const long long v0 = j * chunk_vectors;
+    const long long v1 = min(n, v0 + chunk_vectors);
+    BitReader br;
+    br.init(src, src_lim, live ? start : 0);
+    unsigned prev[MT ? MT : 16];
+    bool warm = context && j == 0 && raw_first && live;
+#pragma unroll
+    for (int i = 0; i < (MT ? MT : 16); ++i)
+        prev[i] = (live && i < m && context && !warm) ? (unsigned)chunk_prev[j * m + i] : 0u;
+    const int roots = context ? k : 1;
+    const long long run = (long long)S * m;   // staged codes per lane per batch
+
+    for (int s0 = 0; s0 < chunk_vectors; s0 += S) {
+        long long va = v0 + s0;
+        const long long vb = live ? min(v1, va + S) : va;
+        if (warm && va < vb) {   // global row 0 of a context stream: ceil(log2 K) raw bits
+            int warm_bits = 1;   // per part (huffman_decode.c:73-76; the encoder writes 8)
+            while ((1 << warm_bits) < k) ++warm_bits;
+            for (int i = 0; i < m; ++i) {
+                prev[i] = br.peek(warm_bits);
+                br.skip(warm_bits);
+            }
+            CodeT* o = stage + lane * run;
+            for (int i = 0; i < m; ++i) o[i] = (CodeT)prev[i];
+            ++va;
+            warm = false;
+        }
+        for (long long v = va; v < vb && ok; ++v) {
+#pragma unroll
+            for (int i = 0; i < (MT ? MT : 16); ++i) {
+                if (!MT && i >= m) break;
+                const long long tab = (long long)i * roots + (context ? prev[i] : 0u);
+                unsigned sym;
+                if (!dec_symbol(br, T, tab, sym)) {
+                    ok = false;
+                    break;
+                }
+                prev[i] = sym;
+            }
+            CodeT* o = stage + lane * run + (v - v0 - s0) * m;
+            if constexpr (sizeof(CodeT) == 1 && MT % 4 == 0 && MT > 0) {
+#pragma unroll
+                for (int q = 0; q < MT / 4; ++q)
+                    reinterpret_cast<uint32_t*>(o)[q] = prev[4 * q] | (prev[4 * q + 1] << 8) |
+                                                        (prev[4 * q + 2] << 16) | (prev[4 * q + 3] << 24);
+            } else {
+#pragma unroll
+                for (int i = 0; i < (MT ? MT : 16); ++i)
+                    if (MT || i < m) o[i] = (CodeT)prev[i];
+            }
+        }
+        __syncthreads();
+        // write back: lane-run r holds rows (j0 + r) * C + s0 ... of at most S rows
+        if (S == chunk_vectors && (run * (long long)sizeof(CodeT)) % 4 == 0) {
+            // runs are contiguous: one linear copy of the workgroup's rows
+            const long long rows = min(n, (j0 + 64) * chunk_vectors) - j0 * chunk_vectors;
+            const long long nbytes = rows * m * (long long)sizeof(CodeT);
+            char* dst = reinterpret_cast<char*>(out + j0 * chunk_vectors * m);
+            const long long n4 = nbytes / 4;
+            for (long long q = lane; q < n4; q += 64)
+                __builtin_nontemporal_store(reinterpret_cast<const uint32_t*>(stage)[q],
+                                            reinterpret_cast<uint32_t*>(dst) + q);
+            for (long long q = n4 * 4 + lane; q < nbytes; q += 64)
+                dst[q] = reinterpret_cast<const char*>(stage)[q];
+        } else {
+            for (long long q = lane; q < 64 * run; q += 64) {
+                const long long r = q / run, w = q % run;
+                const long long row = (j0 + r) * chunk_vectors + s0 + w / m;
+                if (r < jn && s0 + w / m < chunk_vectors && row < n) out[row * m + w % m] = stage[q];
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// One lane per chunk of C vectors (huffman_decoder.c:211-255).  The workgroup's 64 chunks
+// are contiguous in the stream, so their bits are first copied into an LDS window with
+// coalesced non-temporal loads (global fallback when the window is too small); decoded
+// codes are staged in LDS and written back coalesced, S vectors per lane at a time.  The
+// only global loads in the symbol loop are then the table lookups, and no store sits in
+// front of them in the vmcnt queue.  MT = parts at compile time (0 = runtime m <= 16).
 template <int MT, typename CodeT, bool L1_IN_LDS>
 __global__ void __launch_bounds__(64)
 dec_chunks(const uint32_t* __restrict__ words, long long nwords, long long n, int m_rt, int k,
            int context, int raw_first, int chunk_vectors,
            const unsigned long long* __restrict__ chunk_off, const CodeT* __restrict__ chunk_prev,
            const uint16_t* __restrict__ lut1_g, const uint16_t* __restrict__ lut2,
-           const uint32_t* __restrict__ meta_g, const uint32_t* __restrict__ desc,
-           long long tables, long long desc_cap, long long lut2_cap,
+           const uint32_t* __restrict__ meta_g, int w1, long long tables, long long lut2_cap,
            const pqh_long_code* __restrict__ longs,
            const uint32_t* __restrict__ long_cnt, CodeT* __restrict__ out,
-           unsigned long long* __restrict__ err) {
+           unsigned long long* __restrict__ err, int win_words, int S) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
+    const int m = MT ? MT : m_rt;
+    const long long meta_b = (tables * 4 + 15) & ~15ll;
+    const long long l1_b = L1_IN_LDS ? (((tables << kL1Max) * 2 + 15) & ~15ll) : 0;
     uint32_t* meta = reinterpret_cast<uint32_t*>(lds);
-    uint16_t* l1s = reinterpret_cast<uint16_t*>(lds + ((tables * 4 + 15) & ~15ll));
-    for (long long t = threadIdx.x; t < tables; t += blockDim.x) meta[t] = meta_g[t];
+    uint16_t* l1s = reinterpret_cast<uint16_t*>(lds + meta_b);
+    uint32_t* win = reinterpret_cast<uint32_t*>(lds + meta_b + l1_b);
+    CodeT* stage = reinterpret_cast<CodeT*>(lds + meta_b + l1_b + ((long long)win_words + 4) * 4);
+    const int lane = threadIdx.x;
+    for (long long t = lane; t < tables; t += 64) meta[t] = meta_g[t];
     if constexpr (L1_IN_LDS) {
         const long long n16 = (tables << kL1Max) * 2 / 16;
         const uint4* src = reinterpret_cast<const uint4*>(lut1_g);
         uint4* dst = reinterpret_cast<uint4*>(l1s);
-        for (long long i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
+        for (long long i = lane; i < n16; i += 64) dst[i] = src[i];
+    }
+    const long long chunks = (n + chunk_vectors - 1) / chunk_vectors;
+    const long long j0 = (long long)blockIdx.x * 64;
+    const long long jn = min(chunks - j0, 64ll);
+    // stream window of this workgroup's chunks
+    const unsigned long long b_lo = chunk_off[j0];
+    const unsigned long long b_hi = j0 + 64 < chunks ? chunk_off[j0 + 64] : (unsigned long long)nwords * 32;
+    const long long w_lo = (long long)(b_lo >> 5);
+    const long long w_hi = min(nwords, (long long)((b_hi + 31) >> 5) + 2);
+    const bool in_lds = w_hi - w_lo <= win_words;
+    if (in_lds) {   // streamed once: non-temporal, so the code tables keep the L2
+        for (long long w = w_lo + lane; w < w_hi; w += 64)
+            win[w - w_lo] = __builtin_nontemporal_load(words + w);
+        if (lane < 4) win[w_hi - w_lo + lane] = 0;   // zero pad read past the window
     }
     __syncthreads();
-    const uint16_t* lut1 = L1_IN_LDS ? l1s : lut1_g;
-    const int m = MT ? MT : m_rt;
-    const long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    const long long v0 = j * chunk_vectors;
-    if (v0 >= n) return;
-    const long long v1 = min(n, v0 + chunk_vectors);
-    BitReader br;
-    br.init(words, nwords, chunk_off[j]);
-    bool warm = context && j == 0 && raw_first;
-    unsigned prev[MT ? MT : 16];
-#pragma unroll
-    for (int i = 0; i < (MT ? MT : 16); ++i)
-        prev[i] = (i < m && context && !warm) ? (unsigned)chunk_prev[j * m + i] : 0u;
-    int warm_bits = 1;
-    while ((1 << warm_bits) < k) ++warm_bits;
-    const int roots = context ? k : 1;
-    for (long long v = v0; v < v1; ++v) {
-#pragma unroll
-        for (int i = 0; i < (MT ? MT : 16); ++i) {
-            if (!MT && i >= m) break;
-            unsigned sym;
-            if (warm) {
-                sym = br.peek(warm_bits);
-                br.skip(warm_bits);
-            } else {
-                const long long tab = (long long)i * roots + (context ? prev[i] : 0u);
-                const uint32_t mt = meta[tab];
-                const int w1 = (int)(mt & 15u);
-                if (w1 < 1 || w1 > kL1Max) {
-                    atomicOr(err, 1ull);
-                    return;
-                }
-                const uint16_t e = lut1[(tab << kL1Max) + br.peek(w1)];
-                const int len = e >> 12;
-                bool slow = false;
-                sym = e & 0xFFFu;
-                if (len >= 1 && len <= w1) {
-                    br.skip(len);
-                } else if (len == 15 && sym != 0xFFFu) {
-                    const long long di = (long long)(mt >> 8) + sym;
-                    if (di >= desc_cap) {
-                        atomicOr(err, 1ull);
-                        return;
-                    }
-                    const uint32_t d = desc[di];
-                    const int w2 = (int)(d & 15u);
-                    const long long li = (long long)(d >> 4) + (br.peek(w1 + w2) & ((1u << w2) - 1u));
-                    if (w2 < 1 || w2 > 12 || li >= lut2_cap) {
-                        atomicOr(err, 1ull);
-                        return;
-                    }
-                    const uint16_t e2 = lut2[li];
-                    const int len2 = e2 >> 12;
-                    if (len2 >= 1 && len2 <= w2) {
-                        sym = e2 & 0xFFFu;
-                        br.skip(w1 + len2);
-                    } else if (len2 == 15) {
-                        slow = true;
-                    } else {
-                        atomicOr(err, 1ull);
-                        return;
-                    }
-                } else if (len == 15) {
-                    slow = true;
-                } else {
-                    atomicOr(err, 1ull);
-                    return;
-                }
-                if (slow) {   // codes beyond both levels: rare, linear search
-                    const uint32_t cnt = long_cnt[tab];
-                    bool found = false;
-                    for (uint32_t q = 0; q < cnt; ++q) {
-                        const pqh_long_code lc = longs[tab * k + q];
-                        if (br.peek_long((int)lc.len) == lc.code) {
-                            sym = lc.sym;
-                            br.skip_long((int)lc.len);
-                            found = true;
-                            break;
-                        }
-                    }
-                    if (!found) {
-                        atomicOr(err, 1ull);
-                        return;
-                    }
-                }
-            }
-            if (sym >= (unsigned)k) {   // never from a well-formed table: stop, do not index
-                atomicOr(err, 1ull);
-                return;
-            }
-            prev[i] = sym;
-        }
-        warm = false;
-        CodeT* o = out + v * m;
-        if constexpr (sizeof(CodeT) == 1 && MT % 4 == 0 && MT > 0) {
-#pragma unroll
-            for (int q = 0; q < MT / 4; ++q)
-                reinterpret_cast<uint32_t*>(o)[q] = prev[4 * q] | (prev[4 * q + 1] << 8) |
-                                                    (prev[4 * q + 2] << 16) | (prev[4 * q + 3] << 24);
-        } else {
-#pragma unroll
-            for (int i = 0; i < (MT ? MT : 16); ++i)
-                if (MT || i < m) o[i] = (CodeT)prev[i];
-        }
-    }
+
+    DecTables T{meta, L1_IN_LDS ? l1s : lut1_g, lut2, lut2_cap, longs, long_cnt, k, w1};
+    const long long j = j0 + lane;
+    const bool live = lane < jn;
+    bool ok = true;
+    const unsigned long long start = live ? chunk_off[j] : 0;
+    if (in_lds)
+        decode_lanes<MT, CodeT>(win, w_hi - w_lo + 3, live ? start - (unsigned long long)w_lo * 32 : 0,
+                                live, j, j0, jn, n, m, k, context, raw_first, chunk_vectors, S,
+                                chunk_prev, T, stage, out, ok);
+    else
+        decode_lanes<MT, CodeT>(words, nwords - 1, start, live, j, j0, jn, n, m, k, context,
+                                raw_first, chunk_vectors, S, chunk_prev, T, stage, out, ok);
+    if (!ok) atomicOr(err, 1ull);
 }
-
-
 
 }  // namespace
 
@@ -616,13 +781,11 @@ int pqh_tables_alloc(pqh_ctx_t* ctx, int m, int k, int context, pqh_tables_t** o
     t->tables = (long long)m * t->roots;
     t->l1_bits = context ? 9 : kL1Max;   // 1 KB first level per context alphabet
     t->l2_bits = 8;
-    t->desc_cap = t->tables * 64 + 1024;
-    t->lut2_cap = t->tables * 2048 + 65536;
+    t->lut2_cap = std::min<long long>(t->tables * 2048 + 65536, kL2BaseMax - 1);
     if (hipMalloc(&t->d_enc, (size_t)m * t->items * 8) != hipSuccess ||
         hipMalloc(&t->d_lut1, (size_t)(t->tables << kL1Max) * 2) != hipSuccess ||
         hipMalloc(&t->d_lut2, (size_t)t->lut2_cap * 2) != hipSuccess ||
         hipMalloc(&t->d_meta, (size_t)t->tables * 4 + 16) != hipSuccess ||
-        hipMalloc(&t->d_desc, (size_t)t->desc_cap * 4) != hipSuccess ||
         hipMalloc(&t->d_scratch, (size_t)t->tables * 8 + 16) != hipSuccess ||
         hipMalloc(&t->d_long, (size_t)t->tables * k * sizeof(pqh_long_code)) != hipSuccess ||
         hipMalloc(&t->d_long_cnt, (size_t)t->tables * 4) != hipSuccess ||
@@ -640,7 +803,7 @@ int pqh_tables_destroy(pqh_tables_t* t) {
         (void)hipSetDevice(t->ctx->device);
         (void)hipStreamSynchronize(t->ctx->stream);
     }
-    void* bufs[] = {t->d_enc, t->d_lut1, t->d_lut2, t->d_meta, t->d_desc, t->d_scratch,
+    void* bufs[] = {t->d_enc, t->d_lut1, t->d_lut2, t->d_meta, t->d_scratch,
                     t->d_long, t->d_long_cnt, t->d_err};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -650,14 +813,14 @@ int pqh_tables_destroy(pqh_tables_t* t) {
 
 static int launch_luts(pqh_ctx* ctx, pqh_tables* t) {
     hipLaunchKernelGGL(lut_plan, dim3((unsigned)t->tables), dim3(256), 0, ctx->stream, t->d_enc,
-                       t->k, t->tables, t->l1_bits, t->l2_bits, t->d_meta, t->d_scratch);
+                       t->k, t->l1_bits, t->l2_bits, t->d_meta, t->d_scratch);
     PQH_LAUNCH_CHECK(ctx);
-    hipLaunchKernelGGL(lut_alloc, dim3(1), dim3(1024), 0, ctx->stream, t->tables, t->desc_cap,
-                       t->lut2_cap, t->d_meta, t->d_scratch);
+    hipLaunchKernelGGL(lut_alloc, dim3(1), dim3(1024), 0, ctx->stream, t->tables, t->lut2_cap,
+                       t->d_meta, t->d_scratch);
     PQH_LAUNCH_CHECK(ctx);
     hipLaunchKernelGGL(lut_fill, dim3((unsigned)t->tables), dim3(256), 0, ctx->stream, t->d_enc,
-                       t->k, t->l2_bits, t->d_meta, t->d_scratch, t->d_lut1, t->d_lut2, t->d_desc,
-                       t->desc_cap, t->lut2_cap, t->d_long, t->d_long_cnt);
+                       t->k, t->l2_bits, t->d_meta, t->d_lut1, t->d_lut2, t->lut2_cap, t->d_long,
+                       t->d_long_cnt);
     PQH_LAUNCH_CHECK(ctx);
     return PQH_OK;
 }
@@ -672,14 +835,14 @@ int pqh_tables_build(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts) 
     const long long trees = t->tables;
     if (t->k <= 256) {
         constexpr int TPW = 16;
-        const size_t lds = (size_t)256 * TPW * (16 + 4 + 2);
+        const size_t lds = (size_t)256 * TPW * (16 + 4 + 4 + 2);
         PQH_HIP(ctx, hipFuncSetAttribute((const void*)huff_trees<256, TPW>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         hipLaunchKernelGGL((huff_trees<256, TPW>), dim3((unsigned)((trees + TPW - 1) / TPW)), dim3(64),
                            lds, ctx->stream, d_counts, t->k, trees, t->d_enc, t->d_err);
     } else {
         constexpr int TPW = 1;
-        const size_t lds = (size_t)4096 * TPW * (16 + 4 + 2);
+        const size_t lds = (size_t)4096 * TPW * (16 + 4 + 4 + 2);
         PQH_HIP(ctx, hipFuncSetAttribute((const void*)huff_trees<4096, TPW>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         hipLaunchKernelGGL((huff_trees<4096, TPW>), dim3((unsigned)((trees + TPW - 1) / TPW)), dim3(64),
@@ -687,6 +850,14 @@ int pqh_tables_build(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts) 
     }
     PQH_LAUNCH_CHECK(ctx);
     return launch_luts(ctx, t);
+}
+
+// diagnostics only: phase stamps (s_memtime) of tree 0 of the last huff_trees launch
+int pqh_debug_tree_stamps(pqh_ctx_t* ctx, unsigned long long* out8) {
+    if (!ctx || !out8) return PQH_ERR_ARG;
+    PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    PQH_HIP(ctx, hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_tree_stamps), 8 * sizeof(unsigned long long)));
+    return PQH_OK;
 }
 
 int pqh_tables_upload(pqh_ctx_t* ctx, pqh_tables_t* t, const huffman_codebook_t* cbs) {
@@ -786,16 +957,29 @@ int pqh_decode(pqh_ctx_t* ctx, const pqh_tables_t* t, const unsigned char* d_str
     const size_t l1_bytes = (size_t)(t->tables << kL1Max) * 2;
     const size_t meta_bytes = ((size_t)t->tables * 4 + 15) & ~(size_t)15;
     const bool lds_l1 = meta_bytes + l1_bytes <= 48 * 1024;
-    const size_t lds = meta_bytes + (lds_l1 ? l1_bytes : 0) + 16;
-    if (lds > 64 * 1024) return PQH_ERR_UNSUPPORTED;
+    const size_t esz = t->k <= 256 ? 1 : 2;
+    // stream window: 16 KB (a workgroup's 64 chunks; larger windows fall back to global
+    // reads); staging: S vectors per lane, at most 16 KB
+    const int win_words = 4096;
+    int S = chunk_vectors;
+    while (S > 1 && (size_t)64 * S * t->m * esz > 16 * 1024) S = (S + 1) / 2;
+    const size_t lds = meta_bytes + (lds_l1 ? ((l1_bytes + 15) & ~(size_t)15) : 0) +
+                       ((size_t)win_words + 4) * 4 + (size_t)64 * S * t->m * esz + 16;
+    if (lds > 160 * 1024) return PQH_ERR_UNSUPPORTED;
 #define PQH_DEC(MT, T, L)                                                                        \
-    hipLaunchKernelGGL((dec_chunks<MT, T, L>), dim3(blocks), dim3(64), lds, ctx->stream,          \
-                       reinterpret_cast<const uint32_t*>(d_stream), nwords, n, t->m, t->k,       \
-                       t->context, raw_first, chunk_vectors, d_chunk_offsets,                    \
-                       static_cast<const T*>(d_chunk_prev), t->d_lut1, t->d_lut2, t->d_meta,     \
-                       t->d_desc, t->tables, t->desc_cap, t->lut2_cap, t->d_long, t->d_long_cnt,  \
-                       static_cast<T*>(d_codes),                                                 \
-                       ctx->d_diag + 1)
+    do {                                                                                         \
+        if (lds > 64 * 1024)                                                                     \
+            PQH_HIP(ctx, hipFuncSetAttribute((const void*)(dec_chunks<MT, T, L>),                \
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,         \
+                                             (int)lds));                                         \
+        hipLaunchKernelGGL((dec_chunks<MT, T, L>), dim3(blocks), dim3(64), lds, ctx->stream,      \
+                           reinterpret_cast<const uint32_t*>(d_stream), nwords, n, t->m, t->k,   \
+                           t->context, raw_first, chunk_vectors, d_chunk_offsets,                \
+                           static_cast<const T*>(d_chunk_prev), t->d_lut1, t->d_lut2, t->d_meta, \
+                           t->l1_bits, t->tables, t->lut2_cap, t->d_long,                        \
+                           t->d_long_cnt, static_cast<T*>(d_codes), ctx->d_diag + 1, win_words,  \
+                           S);                                                                   \
+    } while (0)
     if (t->k <= 256) {
         if (t->m == 8) {
             if (lds_l1) PQH_DEC(8, uint8_t, true); else PQH_DEC(8, uint8_t, false);

@@ -36,9 +36,24 @@ def main():
             tabs.build(counts)
         e1.record()
         torch.cuda.synchronize()
-        print(f"phase={os.environ.get('PQH_TREE_PHASE', '0')} ctx={mode} build_ms={e0.elapsed_time(e1) / reps:.4f}",
-              flush=True)
+        L, out = stamps()
+        L.pqh_debug_tree_stamps(ctx.ptr, out)
+        st = list(out)
+        print(f"ctx={mode} build_ms={e0.elapsed_time(e1) / reps:.4f} "
+              f"tree0 cycles: scan={st[1]-st[0]} leaves={st[2]-st[1]} merges={st[3]-st[2]} "
+              f"codes={st[4]-st[3]} nz={st[5]} nodes={st[6]}", flush=True)
+
+
+def stamps():
+    """Phase cycle counts of tree 0 (s_memtime) after a ctx build."""
+    import ctypes
+    from pq_huffman_amd.capi import lib
+    L = lib()
+    L.pqh_debug_tree_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    out = (ctypes.c_ulonglong * 8)()
+    return L, out
 
 
 if __name__ == "__main__":
     main()
+
