@@ -5,6 +5,7 @@ huffman_decoder, gluing CLI programs through files.  Here the same stages run as
 calls on device-resident data:
 
     PQ.assign            pq_encoder.c:270-272 (yael kmeans assignment) + :192-205
+    sort_rows            huffman_encoder.c:301-317 (default sort mode)
     histogram            huffman_encoder.c:139-205
     build_codebooks      huffman_encoder.c:377-388 (huffman_codebook_[context_]encode_init)
     encode               huffman_encoder.c:413-428 (+ sidecar chunk index)
@@ -281,6 +282,14 @@ def histogram(ctx: Context, codes, k: int, context: bool, prev_row=None, counts=
     check(lib().pqh_histogram(ctx.ptr, _ptr(codes), n, m, k, int(context), _ptr(prev_row),
                               _ptr(counts)), "pqh_histogram")
     return counts
+
+
+def sort_rows(ctx: Context, codes, tmp=None):
+    """In-place stable sort of uint8 code rows in strncmp order -- the reference encoder's
+    default mode (huffman_encoder.c:301-317).  `tmp`: optional n*m byte device scratch."""
+    n, m = codes.shape
+    check(lib().pqh_sort_rows(ctx.ptr, _ptr(codes), n, m, _ptr(tmp)), "pqh_sort_rows")
+    return codes
 
 
 def counts_to_host(counts) -> np.ndarray:

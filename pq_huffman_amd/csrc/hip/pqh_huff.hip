@@ -375,9 +375,4 @@ int pqh_codebooks_build(const double* counts, int m, int k, int context,
     return PQH_OK;
 }
 
-int pqh_sort_rows(pqh_ctx_t* ctx, void* d_codes, long long n, int m, void* d_tmp) {
-    (void)d_codes; (void)n; (void)m; (void)d_tmp;
-    return pqh_set_error(ctx, PQH_ERR_UNSUPPORTED, "pqh_sort_rows: not built yet");
-}
-
 }  // extern "C"

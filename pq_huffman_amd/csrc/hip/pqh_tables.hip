@@ -214,8 +214,9 @@ struct SentinelHeap {
     }
 };
 
-// diagnostics: s_memtime stamps of tree 0's phases (read with pqh_debug_tree_stamps)
-__device__ unsigned long long g_tree_stamps[8];
+// diagnostics: s_memtime stamps of the first workgroup's phases (pqh_debug_stamps):
+// [0..6] huff_trees tree 0, [8..13] dec_chunks workgroup 0 lane 0
+__device__ unsigned long long g_tree_stamps[16];
 
 template <int KMAX, int TPW>
 __global__ void __launch_bounds__(64)
@@ -722,6 +723,8 @@ dec_chunks(const uint32_t* __restrict__ words, long long nwords, long long n, in
     uint32_t* win = reinterpret_cast<uint32_t*>(lds + meta_b + l1_b);
     CodeT* stage = reinterpret_cast<CodeT*>(lds + meta_b + l1_b + ((long long)win_words + 4) * 4);
     const int lane = threadIdx.x;
+    const bool stamp = blockIdx.x == 0 && lane == 0;
+    if (stamp) g_tree_stamps[8] = __builtin_amdgcn_s_memtime();
     for (long long t = lane; t < tables; t += 64) meta[t] = meta_g[t];
     if constexpr (L1_IN_LDS) {
         const long long n16 = (tables << kL1Max) * 2 / 16;
@@ -732,6 +735,7 @@ dec_chunks(const uint32_t* __restrict__ words, long long nwords, long long n, in
     const long long chunks = (n + chunk_vectors - 1) / chunk_vectors;
     const long long j0 = (long long)blockIdx.x * 64;
     const long long jn = min(chunks - j0, 64ll);
+    if (stamp) g_tree_stamps[9] = __builtin_amdgcn_s_memtime();
     // stream window of this workgroup's chunks
     const unsigned long long b_lo = chunk_off[j0];
     const unsigned long long b_hi = j0 + 64 < chunks ? chunk_off[j0 + 64] : (unsigned long long)nwords * 32;
@@ -739,12 +743,28 @@ dec_chunks(const uint32_t* __restrict__ words, long long nwords, long long n, in
     const long long w_hi = min(nwords, (long long)((b_hi + 31) >> 5) + 2);
     const bool in_lds = w_hi - w_lo <= win_words;
     if (in_lds) {   // streamed once: non-temporal, so the code tables keep the L2
-        for (long long w = w_lo + lane; w < w_hi; w += 64)
-            win[w - w_lo] = __builtin_nontemporal_load(words + w);
-        if (lane < 4) win[w_hi - w_lo + lane] = 0;   // zero pad read past the window
+        const long long nw = w_hi - w_lo;
+        for (long long w0 = 0; w0 < nw; w0 += 8 * 64) {   // 8 loads in flight per lane
+            uint32_t r[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const long long w = w0 + u * 64 + lane;
+                r[u] = w < nw ? __builtin_nontemporal_load(words + w_lo + w) : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const long long w = w0 + u * 64 + lane;
+                if (w < nw) win[w] = r[u];
+            }
+        }
+        if (lane < 4) win[nw + lane] = 0;   // zero pad read past the window
     }
     __syncthreads();
 
+    if (stamp) {
+        g_tree_stamps[10] = __builtin_amdgcn_s_memtime();
+        g_tree_stamps[13] = in_lds;
+    }
     DecTables T{meta, L1_IN_LDS ? l1s : lut1_g, lut2, lut2_cap, longs, long_cnt, k, w1};
     const long long j = j0 + lane;
     const bool live = lane < jn;
@@ -757,6 +777,7 @@ dec_chunks(const uint32_t* __restrict__ words, long long nwords, long long n, in
     else
         decode_lanes<MT, CodeT>(words, nwords - 1, start, live, j, j0, jn, n, m, k, context,
                                 raw_first, chunk_vectors, S, chunk_prev, T, stage, out, ok);
+    if (stamp) g_tree_stamps[11] = __builtin_amdgcn_s_memtime();
     if (!ok) atomicOr(err, 1ull);
 }
 
@@ -853,10 +874,10 @@ int pqh_tables_build(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts) 
 }
 
 // diagnostics only: phase stamps (s_memtime) of tree 0 of the last huff_trees launch
-int pqh_debug_tree_stamps(pqh_ctx_t* ctx, unsigned long long* out8) {
-    if (!ctx || !out8) return PQH_ERR_ARG;
+int pqh_debug_tree_stamps(pqh_ctx_t* ctx, unsigned long long* out16) {
+    if (!ctx || !out16) return PQH_ERR_ARG;
     PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    PQH_HIP(ctx, hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_tree_stamps), 8 * sizeof(unsigned long long)));
+    PQH_HIP(ctx, hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_tree_stamps), 16 * sizeof(unsigned long long)));
     return PQH_OK;
 }
 
@@ -958,9 +979,12 @@ int pqh_decode(pqh_ctx_t* ctx, const pqh_tables_t* t, const unsigned char* d_str
     const size_t meta_bytes = ((size_t)t->tables * 4 + 15) & ~(size_t)15;
     const bool lds_l1 = meta_bytes + l1_bytes <= 48 * 1024;
     const size_t esz = t->k <= 256 ? 1 : 2;
-    // stream window: 16 KB (a workgroup's 64 chunks; larger windows fall back to global
-    // reads); staging: S vectors per lane, at most 16 KB
-    const int win_words = 4096;
+    // stream window: the workgroup's 64 chunks at up to 12 (K <= 256; Huffman averages
+    // at most ~8.x bits) or 14 bits per symbol, at most 16 KB -- a larger span reads the
+    // global stream instead; staging: S vectors per lane, at most 16 KB
+    const long long sym_bits = t->k <= 256 ? 12 : 14;
+    const int win_words = (int)std::min<long long>(4096, std::max<long long>(
+        256, (64ll * chunk_vectors * t->m * sym_bits + 31) / 32 + 8));
     int S = chunk_vectors;
     while (S > 1 && (size_t)64 * S * t->m * esz > 16 * 1024) S = (S + 1) / 2;
     const size_t lds = meta_bytes + (lds_l1 ? ((l1_bytes + 15) & ~(size_t)15) : 0) +

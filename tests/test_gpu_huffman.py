@@ -180,7 +180,8 @@ def _run(args, cwd=None):
     return r.stdout
 
 
-@pytest.mark.parametrize("mode,flags", [("nosort_ctx", ["--no-sort"]),
+@pytest.mark.parametrize("mode,flags", [("sort_ctx", []),
+                                        ("nosort_ctx", ["--no-sort"]),
                                         ("nosort_noctx", ["--no-sort", "--no-context"])])
 def test_cli_tools_match_reference_files(tmp_path, mode, flags):
     g = golden("huff_m8_n1000.npz")
@@ -196,11 +197,12 @@ def test_cli_tools_match_reference_files(tmp_path, mode, flags):
     dec = tmp_path / "dec.bin"
     _run([os.path.join(bind, "huffman_decoder"), str(out) + "/", "--output-file", str(dec),
           "--check-file", str(pqdir / "pq_indices.bvecsl")])
-    assert np.array_equal(np.fromfile(dec, np.uint8).reshape(1000, 8), g["input"])
+    want = g[mode + "__decoded"].reshape(1000, 8)      # sort mode decodes the sorted rows
+    assert np.array_equal(np.fromfile(dec, np.uint8).reshape(1000, 8), want)
     # without the sidecar the decoder rebuilds the chunk index from the stream
     (out / "huffman_chunks.bin").unlink()
     _run([os.path.join(bind, "huffman_decoder"), str(out) + "/", "--output-file", str(dec)])
-    assert np.array_equal(np.fromfile(dec, np.uint8).reshape(1000, 8), g["input"])
+    assert np.array_equal(np.fromfile(dec, np.uint8).reshape(1000, 8), want)
 
 
 def test_cli_pq_encoder_fixed_centroids(tmp_path, oracle):
@@ -217,3 +219,51 @@ def test_cli_pq_encoder_fixed_centroids(tmp_path, oracle):
     err = float((tmp_path / "pq_error").read_text().strip())
     want = oracle.compute_error(g["x"], g["centroids"], g["codes"])
     assert abs(err - want) <= 1e-6 * want
+
+
+def _zero_heavy_rows(n, m, seed):
+    """Rows that exercise the strncmp key: many zeros at every position, repeated rows and
+    rows equal up to their first zero (whose tails must keep input order)."""
+    rng = np.random.default_rng(seed)
+    a = rng.integers(0, 4, size=(n, m)).astype(np.uint8)
+    a[rng.random((n, m)) < 0.3] = 0
+    half = a[1::4]
+    a[1::4] = a[0::4][: len(half)]          # exact duplicates
+    a[2::4, 0] = 0                          # ties decided by input order alone
+    return np.ascontiguousarray(a)
+
+
+@pytest.mark.parametrize("n,m", [(1, 8), (2, 8), (1000, 8), (1000, 16), (777, 3), (513, 12),
+                                 (300, 1), (2000, 24)])
+def test_gpu_sort_rows_vs_oracle(gpu, oracle, n, m):
+    torch, codec, ctx = gpu
+    for seed in (1, 2):
+        a = _zero_heavy_rows(n, m, seed)
+        d = torch.from_numpy(a.copy()).cuda()
+        codec.sort_rows(ctx, d)
+        assert np.array_equal(d.cpu().numpy(), oracle.sort_rows(a))
+
+
+def test_gpu_sort_full_size_vs_oracle(gpu, oracle):
+    torch, codec, ctx = gpu
+    a = datagen.skewed_codes(1_000_000, 8, 256, seed=5)
+    d = torch.from_numpy(a).cuda()
+    tmp = torch.empty_like(d)
+    codec.sort_rows(ctx, d, tmp)
+    assert np.array_equal(d.cpu().numpy(), oracle.sort_rows(a))
+
+
+@pytest.mark.parametrize("name", ["m8_n1000", "m16_n1000", "m8_n1", "m3_n2"])
+def test_sort_ctx_mode_vs_reference_files(gpu, name):
+    """Default reference mode: GPU sort, then the GPU histogram / codebooks / encode."""
+    torch, codec, ctx = gpu
+    g = golden(f"huff_{name}.npz")
+    cd = torch.from_numpy(np.ascontiguousarray(g["input"])).cuda()
+    codec.sort_rows(ctx, cd)
+    assert np.array_equal(cd.cpu().numpy(), g["sort_ctx__decoded"].reshape(g["input"].shape))
+    counts = codec.histogram(ctx, cd, 256, True)
+    cbs = codec.Codebooks(codec.counts_to_host(counts), 256, True)
+    assert cbs.file_bytes() == g["sort_ctx__codebooks"].tobytes()
+    tabs = codec.Tables.from_codebooks(ctx, cbs)
+    enc = codec.encode(ctx, tabs, cd, chunk_vectors=16)
+    assert codec.indices_file_bytes(enc) == g["sort_ctx__indices"].tobytes()
