@@ -165,6 +165,7 @@ def main():
     coff = torch.empty(chunks, dtype=torch.int64, device=dev)
     cprev = torch.empty((chunks, m), dtype=torch.uint8, device=dev) if ctxm else None
     out = torch.zeros(n * m * 56 // 8 + 64, dtype=torch.uint8, device=dev)  # worst case
+    tot_dev = torch.zeros(1, dtype=torch.int64, device=dev)
 
     ev = {s: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for s in ("assign", "hist", "codebook", "encode", "decode")}
@@ -194,17 +195,19 @@ def main():
         rec("codebook", 1)
         raw_first = shard.raw_first(rank)
         rec("encode", 0)
-        total = codec.encode_size(ctx, tabs, codes, raw_first, prev_row)
         tc = time.perf_counter()
-        if world > 1:   # place the shard in the global stream (word-aligned buffer)
+        if world > 1:   # place the shard in the global stream before writing it
+            total = codec.encode_size(ctx, tabs, codes, raw_first, prev_row)
             goff, _ = shard.bit_offsets(total, world, rank)
             bit_off = shard.local_bit_offset(goff)
+            out[:4].zero_()   # bits before bit_off belong to the previous shard: kept zero
         else:
             bit_off = 0
         acc_coll += time.perf_counter() - tc
-        out.zero_()
+        # one pass: look-back offsets, every word stored once (no zeroing of `out`)
         codec.encode_write(ctx, tabs, codes, out, bit_off, raw_first, prev_row, args.chunk,
-                           coff, cprev)
+                           coff, cprev, total=tot_dev)
+        total = tot_dev
         rec("encode", 1)
         enc = codec.Encoded(out, -1, args.chunk, coff, cprev, n, raw_first)
         rec("decode", 0)

@@ -118,20 +118,25 @@ int pqh_codebooks_build(const double* counts, int m, int k, int context,
                         huffman_codebook_t* codebooks, int num_threads);
 
 /* ---- encode (huffman_encoder.c:207-238 + bitstream.c:71-150) --------------------- */
-/* Phase 1: bits of every vector block; total bits (device, u64) written to d_total_bits.
+/* Total bits of the stream (device, u64) without writing it -- for placing shards before
+ * they are written (multi-GPU); pqh_encode_write does not need it.
  * raw_first: context mode writes row 0 raw (8 bits per part, huffman_encoder.c:234) --
  * set for the shard holding global row 0; other shards pass d_prev_row instead. */
 int pqh_encode_size(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes, long long n,
                     int raw_first, const void* d_prev_row, unsigned long long* d_total_bits);
-/* Phase 2: write the stream at bit offset `bit_offset` of d_out (bytes, caller-zeroed
- * over [bit_offset/8, end)).  Words are OR-ed at the two ends so shards written at
- * adjacent offsets into one buffer compose.  chunk_vectors > 0 also emits the chunk
- * index: d_chunk_offsets[ceil(n/C)] (bit offsets relative to d_out bit 0) and, in context
- * mode, d_chunk_prev[ceil(n/C)][m] codes.  Must follow pqh_encode_size on the same data. */
+/* Write the stream at bit offset `bit_offset` of d_out in ONE pass (no pqh_encode_size
+ * needed): workgroups find their bit offsets by a decoupled look-back and store every word
+ * of [bit_offset, bit_offset + bits) exactly once, zero padding the last word -- the buffer
+ * needs no zeroing.  Bits of d_out before bit_offset in the first word are kept (they are
+ * merged), so shards written at adjacent offsets into one buffer compose.
+ * chunk_vectors > 0 also emits the chunk index: d_chunk_offsets[ceil(n/C)] (bit offsets
+ * relative to d_out bit 0) and, in context mode, d_chunk_prev[ceil(n/C)][m] codes.
+ * d_total_bits (optional, device u64): the number of bits written. */
 int pqh_encode_write(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes, long long n,
                      int raw_first, const void* d_prev_row, unsigned long long bit_offset,
                      unsigned char* d_out, unsigned long long out_bytes, int chunk_vectors,
-                     unsigned long long* d_chunk_offsets, void* d_chunk_prev);
+                     unsigned long long* d_chunk_offsets, void* d_chunk_prev,
+                     unsigned long long* d_total_bits);
 
 /* Synchronises; PQH_ERR_CAPACITY if a pqh_encode_write since the last call had to drop
  * words because out_bytes was too small (nothing is written out of bounds). */

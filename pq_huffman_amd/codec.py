@@ -322,11 +322,16 @@ def encode_size(ctx: Context, tables: Tables, codes, raw_first: int = 1, prev_ro
 
 
 def encode_write(ctx: Context, tables: Tables, codes, out, bit_offset: int = 0, raw_first: int = 1,
-                 prev_row=None, chunk_vectors: int = 64, chunk_offsets=None, chunk_prev=None):
+                 prev_row=None, chunk_vectors: int = 64, chunk_offsets=None, chunk_prev=None,
+                 total=None):
+    """One-pass encode into `out` at `bit_offset` (no zeroing needed; bits of the first word
+    before bit_offset are kept).  total: optional device int64[1] receiving the bit count."""
     check(lib().pqh_encode_write(ctx.ptr, tables.ptr, _ptr(codes), codes.shape[0], raw_first,
                                  _ptr(prev_row), bit_offset, _ptr(out), out.numel(),
-                                 chunk_vectors, _ptr(chunk_offsets), _ptr(chunk_prev)),
+                                 chunk_vectors, _ptr(chunk_offsets), _ptr(chunk_prev),
+                                 _ptr(total)),
           "pqh_encode_write: " + ctx.last_error())
+    return total
 
 
 def encode(ctx: Context, tables: Tables, codes, chunk_vectors: int = 64, raw_first: int = 1,

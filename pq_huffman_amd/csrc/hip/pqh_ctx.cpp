@@ -85,6 +85,7 @@ int pqh_ctx_destroy(pqh_ctx_t* ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->d_diag) (void)hipFree(ctx->d_diag);
+    if (ctx->lb_state) (void)hipFree(ctx->lb_state);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return PQH_OK;

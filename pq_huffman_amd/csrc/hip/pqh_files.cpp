@@ -128,7 +128,7 @@ extern "C" int pqh_encode_files(const unsigned char* codes, long long n, int m,
     if (!rc) {
         PQH_HIP(ctx, hipMemsetAsync(d_out.p, 0, wbytes, ctx->stream));
         rc = pqh_encode_write(ctx, tab, d_codes.p, n, 1, nullptr, 0, d_out.p, wbytes,
-                              opt.chunk_vectors, d_coff.p, d_cprev.p);
+                              opt.chunk_vectors, d_coff.p, d_cprev.p, nullptr);
         if (!rc) rc = pqh_encode_status(ctx);
     }
     pqh_tables_destroy(tab);

@@ -20,7 +20,7 @@
 
 namespace {
 
-constexpr int kEncBlock = 256;   // vectors per encode workgroup (one thread each)
+constexpr int kEncBlock = 512;   // vectors per encode workgroup (one thread each)
 constexpr int kMaxCodeLen = 56;
 constexpr int kHistChunk = 32768; // vectors per context-histogram workgroup (< 65536)
 
@@ -153,41 +153,203 @@ scan_blocks(const uint32_t* __restrict__ block_bits, long long nb,
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
-template <typename CodeT>
+// decoupled look-back state words: epoch (16 bits) | status (2) | value (46)
+constexpr unsigned long long kLbAgg = 1ull << 46, kLbPrefix = 2ull << 46;
+constexpr unsigned long long kLbValue = (1ull << 46) - 1;
+__device__ __forceinline__ unsigned long long lb_pack(unsigned epoch, unsigned long long status,
+                                                      unsigned long long v) {
+    return ((unsigned long long)epoch << 48) | status | v;
+}
+// Every value handed between workgroups travels inside the 64-bit atomic word itself, so
+// relaxed agent-scope atomics suffice (coherent sc1 accesses): release/acquire would add a
+// whole-L2 writeback (buffer_wbl2) per publish and an L2 invalidate (buffer_inv) per poll.
+__device__ __forceinline__ void lb_store(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long lb_load(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// tail word of a block: epoch | ready (bit 32) | the word's bits from blocks <= it
+__device__ __forceinline__ uint32_t lb_wait_tail(const unsigned long long* tails, long long b,
+                                                 unsigned epoch) {
+    for (;;) {
+        const unsigned long long t = lb_load(tails + b);
+        if ((unsigned)(t >> 48) == epoch && (t >> 32 & 1ull)) return (uint32_t)t;
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+// m codes of row v (MAXM >= m) with wide loads when the row is 8-byte aligned
+template <typename CodeT, int MAXM>
+__device__ __forceinline__ void load_row(const CodeT* __restrict__ codes, long long v, int m,
+                                         unsigned (&out)[MAXM]) {
+    const CodeT* row = codes + v * m;
+    if (m * (int)sizeof(CodeT) == 8 * ((m * (int)sizeof(CodeT)) / 8) &&
+        !(reinterpret_cast<uintptr_t>(row) & 7)) {
+        constexpr int per = 8 / sizeof(CodeT);
+        unsigned long long w[(MAXM * sizeof(CodeT) + 7) / 8];
+#pragma unroll
+        for (int q = 0; q < (MAXM * (int)sizeof(CodeT) + 7) / 8; ++q)
+            w[q] = q * 8 < m * (int)sizeof(CodeT) ? reinterpret_cast<const unsigned long long*>(row)[q] : 0ull;
+#pragma unroll
+        for (int i = 0; i < MAXM; ++i)
+            out[i] = (unsigned)((w[i / per] >> (8 * sizeof(CodeT) * (i % per))) &
+                                ((1ull << (8 * sizeof(CodeT))) - 1));
+    } else {
+#pragma unroll
+        for (int i = 0; i < MAXM; ++i) out[i] = i < m ? (unsigned)row[i] : 0u;
+    }
+}
+
+// The m (code, length) entries of vector v, all table loads issued together
+// (huffman_encoder.c:207-238: context index (prev << 8) + cur; context row 0 raw 8 bits)
+template <typename CodeT, int MAXM>
+__device__ __forceinline__ void gather_entries(const CodeT* __restrict__ codes, long long v, int m,
+                                               int k, int context, int raw_first,
+                                               const CodeT* __restrict__ prev_row,
+                                               const unsigned long long* __restrict__ enc,
+                                               const uint32_t* __restrict__ enc32,
+                                               long long items, unsigned long long (&ent)[MAXM]) {
+    unsigned cur[MAXM], prv[MAXM];
+    load_row<CodeT, MAXM>(codes, v, m, cur);
+    const bool raw = context && v == 0 && (raw_first || !prev_row);
+    if (context && v > 0) {
+        load_row<CodeT, MAXM>(codes, v - 1, m, prv);
+    } else {
+#pragma unroll
+        for (int i = 0; i < MAXM; ++i) prv[i] = (context && prev_row && i < m) ? (unsigned)prev_row[i] : 0u;
+    }
+    uint32_t e32[MAXM];
+    long long idx[MAXM];
+#pragma unroll
+    for (int i = 0; i < MAXM; ++i) {
+        const bool ok = i < m && cur[i] < (unsigned)k && (!context || prv[i] < (unsigned)k) && !raw;
+        idx[i] = ok ? (long long)i * items +
+                          (context ? (long long)prv[i] * k + cur[i] : (long long)cur[i])
+                    : -1;
+        e32[i] = ok ? enc32[idx[i]] : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < MAXM; ++i)
+        ent[i] = e32[i] == ~0u ? enc[idx[i]]   // codes longer than 26 bits: rare
+                               : ((unsigned long long)(e32[i] >> 26) << 56) | (e32[i] & ((1u << 26) - 1));
+    if (raw) {
+#pragma unroll
+        for (int i = 0; i < MAXM; ++i) ent[i] = i < m ? ((8ull << 56) | (cur[i] & 0xFFu)) : 0ull;
+    }
+}
+
+// One-pass encoder (huffman_encoder.c:207-238 + the bit cursor of bitstream.c:71-101).
+// Workgroups take tickets in launch order (so every predecessor has started), sum their
+// 256 vectors' code lengths, and find their bit offset by a decoupled look-back over the
+// predecessors' published aggregates / prefixes.  Each workgroup ORs its codes into an LDS
+// image of its bit range and stores every word it owns exactly once: the word it shares with
+// its successor is published as a "tail" instead, and the successor merges it into its own
+// first word.  So no word is written twice, nothing needs zeroing and no global atomics are
+// used; the call's first word is merged with the memory content when bit_offset is not
+// word-aligned (shards composed into one buffer).  MAXM > 0 keeps the m table entries of a
+// vector in registers (m <= MAXM).
+// diagnostics: s_memtime phase stamps of one mid-grid workgroup (pqh_debug_enc_stamps)
+__device__ unsigned long long g_enc_stamps[8];
+
+template <typename CodeT, int MAXM>
 __global__ void __launch_bounds__(kEncBlock)
-enc_write(const CodeT* __restrict__ codes, long long n, int m_total, int k, int context,
-          int raw_first, const CodeT* __restrict__ prev_row, const unsigned long long* __restrict__ enc,
-          long long items, const unsigned long long* __restrict__ block_off,
-          const uint32_t* __restrict__ block_bits, unsigned long long bit_offset,
-          uint32_t* __restrict__ out_words, long long out_words_cap, int chunk_vectors,
-          unsigned long long* __restrict__ chunk_off, CodeT* __restrict__ chunk_prev,
-          unsigned long long* __restrict__ err) {
+enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, int context,
+            int raw_first, const CodeT* __restrict__ prev_row,
+            const unsigned long long* __restrict__ enc, const uint32_t* __restrict__ enc32,
+            long long items,
+            unsigned long long bit_offset, uint32_t* __restrict__ out_words, long long cap_words,
+            int chunk_vectors, unsigned long long* __restrict__ chunk_off,
+            CodeT* __restrict__ chunk_prev, unsigned long long* __restrict__ err,
+            unsigned long long* __restrict__ state, unsigned long long* __restrict__ tails,
+            unsigned long long* __restrict__ ticket, unsigned long long ticket_base,
+            unsigned epoch, long long nb, unsigned long long* __restrict__ total_out) {
     extern __shared__ uint32_t img[];   // LDS image of this block's bit range
     __shared__ uint32_t wsum[kEncBlock / 64];
-    const long long v = (long long)blockIdx.x * kEncBlock + threadIdx.x;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const unsigned long long b0 = bit_offset + block_off[blockIdx.x];
-    const unsigned long long b1 = b0 + block_bits[blockIdx.x];
-    const long long w0 = (long long)(b0 >> 5);
-    const long long nwords = b1 > b0 ? (long long)((b1 - 1) >> 5) - w0 + 1 : 0;
-    for (long long w = threadIdx.x; w < nwords; w += blockDim.x) img[w] = 0;
+    __shared__ long long s_id;
+    __shared__ unsigned long long s_excl;
+    __shared__ uint32_t s_head;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    if (tid == 0) s_id = (long long)(atomicAdd(ticket, 1ull) - ticket_base);
+    __syncthreads();
+    const long long id = s_id;
+    const long long v = id * kEncBlock + tid;
+    const bool stamp = id == nb / 2 && tid == 0;
+    if (stamp) g_enc_stamps[0] = __builtin_amdgcn_s_memtime();
 
+    // code entries of this vector (gathered once)
+    unsigned long long ent[MAXM > 0 ? MAXM : 1];
     uint32_t bits = 0;
-    if (v < n)
-        for (int i = 0; i < m_total; ++i)
-            bits += (uint32_t)(sym_entry(codes, v, i, m_total, k, context, raw_first, prev_row,
-                                         enc, items) >> 56);
+    if (v < n) {
+        if constexpr (MAXM > 0) {
+            gather_entries<CodeT, MAXM>(codes, v, m_total, k, context, raw_first, prev_row, enc,
+                                        enc32, items, ent);
+#pragma unroll
+            for (int i = 0; i < MAXM; ++i) bits += (uint32_t)(ent[i] >> 56);
+        } else {
+            for (int i = 0; i < m_total; ++i)
+                bits += (uint32_t)(sym_entry(codes, v, i, m_total, k, context, raw_first,
+                                             prev_row, enc, items) >> 56);
+        }
+    }
     uint32_t incl = bits;
     for (int off = 1; off < 64; off <<= 1) {
-        uint32_t y = __shfl_up(incl, off);
+        const uint32_t y = __shfl_up(incl, off);
         if (lane >= off) incl += y;
     }
     if (lane == 63) wsum[wid] = incl;
     __syncthreads();
-    uint32_t before = 0;
-    for (int w = 0; w < wid; ++w) before += wsum[w];
-    unsigned long long pos = b0 + before + incl - bits;
+    if (stamp) g_enc_stamps[1] = __builtin_amdgcn_s_memtime();
+    uint32_t before = 0, block_bits = 0;
+    for (int w = 0; w < kEncBlock / 64; ++w) {
+        before += w < wid ? wsum[w] : 0u;
+        block_bits += wsum[w];
+    }
+    // decoupled look-back, one wave wide: lane l inspects predecessor p - l; the walk stops
+    // at the nearest published inclusive prefix, adding the aggregates in front of it
+    if (wid == 0) {
+        unsigned long long excl = 0;
+        if (id == 0) {
+            if (lane == 0) lb_store(state, lb_pack(epoch, kLbPrefix, block_bits));
+        } else {
+            if (lane == 0) lb_store(state + id, lb_pack(epoch, kLbAgg, block_bits));
+            long long p = id - 1;
+            for (;;) {
+                const long long q = p - lane;
+                const unsigned long long st = q >= 0 ? lb_load(state + q) : lb_pack(epoch, kLbPrefix, 0);
+                const bool ready = (unsigned)(st >> 48) == epoch && (st & (3ull << 46));
+                const unsigned long long pref = __ballot(ready && (st & kLbPrefix));
+                const unsigned long long notready = __ballot(!ready);
+                // lanes up to the nearest prefix (or all 64) must be ready
+                const int f = pref ? __ffsll((long long)pref) - 1 : 63;
+                const unsigned long long need = f == 63 ? ~0ull : ((2ull << f) - 1);
+                if (notready & need) {
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                unsigned long long v = lane <= f ? (st & kLbValue) : 0ull;
+                for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+                excl += v;
+                if (pref) break;
+                p -= 64;
+            }
+            if (lane == 0) lb_store(state + id, lb_pack(epoch, kLbPrefix, excl + block_bits));
+        }
+        if (lane == 0) s_excl = excl;
+    }
+    __syncthreads();
+    if (stamp) g_enc_stamps[2] = __builtin_amdgcn_s_memtime();
+    const unsigned long long bs = bit_offset + s_excl, be = bs + block_bits;
+    const long long wa = (long long)(bs >> 5);
+    const long long wz = block_bits ? (long long)((be - 1) >> 5) : wa;
+    const long long nwords = block_bits ? wz - wa + 1 : 0;
+    const bool head_pred = (bs & 31) && bs > bit_offset;    // earlier blocks' bits in word wa
+    const bool head_mem = (bs & 31) && bs == bit_offset;    // the caller's bits in word wa
+    const bool overflow = nwords > 0 && wz >= cap_words;
+    for (long long w = tid; w < nwords; w += kEncBlock) img[w] = 0;
+    __syncthreads();
 
+    unsigned long long pos = bs + before + incl - bits;
     if (v < n) {
         if (chunk_vectors > 0 && v % chunk_vectors == 0) {
             const long long j = v / chunk_vectors;
@@ -197,34 +359,87 @@ enc_write(const CodeT* __restrict__ codes, long long n, int m_total, int k, int 
                     chunk_prev[j * m_total + i] =
                         v > 0 ? codes[(v - 1) * m_total + i] : (prev_row ? prev_row[i] : (CodeT)0);
         }
-        for (int i = 0; i < m_total; ++i) {
-            const unsigned long long e = sym_entry(codes, v, i, m_total, k, context, raw_first,
-                                                   prev_row, enc, items);
-            int len = (int)(e >> 56);
-            const unsigned long long code = e & ((1ull << 56) - 1);
-            while (len > 0) {
-                const int o = (int)(pos & 31);
-                const int take = min(len, 32 - o);
-                const uint32_t piece = (uint32_t)((code >> (len - take)) & ((1ull << take) - 1));
-                atomicOr(&img[(long long)(pos >> 5) - w0], piece << (32 - o - take));
-                pos += take;
-                len -= take;
+        // assemble this vector's bits in registers: words wholly inside its range are
+        // plain LDS stores (no other thread touches them); only the first and the last,
+        // shared with the neighbouring vectors, are OR-ed
+        long long w = (long long)(pos >> 5) - wa;
+        unsigned long long acc = 0;   // pending bits, right-aligned
+        int nacc = (int)(pos & 31);   // (the bits before `pos` in the first word are zeros)
+        bool first = true;
+        auto emit = [&](uint32_t word) {
+            if (first) atomicOr(&img[w], word);
+            else img[w] = word;
+            first = false;
+            ++w;
+        };
+        auto append = [&](unsigned long long code, int len) {   // len <= 32
+            acc = (acc << len) | code;
+            nacc += len;
+            if (nacc >= 32) {
+                emit((uint32_t)(acc >> (nacc - 32)));
+                nacc -= 32;
+                acc &= (1ull << nacc) - 1;
             }
+        };
+        auto put = [&](unsigned long long e) {
+            const int len = (int)(e >> 56);
+            const unsigned long long code = e & ((1ull << 56) - 1);
+            if (len > 32) {
+                append(code >> 32, len - 32);
+                append(code & 0xFFFFFFFFull, 32);
+            } else if (len > 0) {
+                append(code, len);
+            }
+        };
+        if constexpr (MAXM > 0) {
+#pragma unroll
+            for (int i = 0; i < MAXM; ++i) put(ent[i]);   // length 0 past m_total
+        } else {
+            for (int i = 0; i < m_total; ++i)
+                put(sym_entry(codes, v, i, m_total, k, context, raw_first, prev_row, enc, items));
         }
+        if (nacc > 0) atomicOr(&img[w], (uint32_t)(acc << (32 - nacc)));
+        pos += bits;
     }
     __syncthreads();
-    if (w0 + nwords > out_words_cap) {   // caller's buffer too small: write nothing, flag
-        if (threadIdx.x == 0) atomicOr(err, 2ull);
-        return;
-    }
-    for (long long w = threadIdx.x; w < nwords; w += blockDim.x) {
-        const uint32_t val = bswap32(img[w]);
-        if (w == 0 || w == nwords - 1) {
-            if (val) atomicOr(&out_words[w0 + w], val);
+    if (stamp) g_enc_stamps[3] = __builtin_amdgcn_s_memtime();
+    // tail / head exchange with the neighbours (one lane)
+    if (tid == 0) {
+        const bool tail_open = (be & 31) != 0;   // last word not complete: successor's head
+        uint32_t pred = 0;
+        if (head_mem) pred = bswap32(out_words[wa]);   // nobody else writes word wa yet
+        if (nwords == 0) {
+            // empty block: forward the open word unchanged
+            if (head_pred) pred = lb_wait_tail(tails, id - 1, epoch);
+            lb_store(tails + id, ((unsigned long long)epoch << 48) | (1ull << 32) | pred);
+            s_head = pred;
+        } else if (nwords > 1) {
+            // the tail does not depend on the predecessor: publish it first
+            lb_store(tails + id, ((unsigned long long)epoch << 48) | (1ull << 32) |
+                                     (tail_open ? img[nwords - 1] : 0u));
+            if (head_pred) pred = lb_wait_tail(tails, id - 1, epoch);
+            s_head = img[0] | pred;
         } else {
-            out_words[w0 + w] = val;
+            if (head_pred) pred = lb_wait_tail(tails, id - 1, epoch);
+            s_head = img[0] | pred;
+            lb_store(tails + id, ((unsigned long long)epoch << 48) | (1ull << 32) |
+                                     (tail_open ? s_head : 0u));
         }
+        if (id == nb - 1) *total_out = be - bit_offset;
+        if (overflow) atomicOr(err, 2ull);
     }
+    __syncthreads();
+    if (stamp) g_enc_stamps[4] = __builtin_amdgcn_s_memtime();
+    const bool last = id == nb - 1;
+    if (!overflow) {
+        // words this block owns: [wa, wz], minus an open last word unless this is the last block
+        const long long wend = ((be & 31) && !last) ? nwords - 1 : nwords;
+        for (long long w = tid; w < wend; w += kEncBlock)
+            __builtin_nontemporal_store(bswap32(w == 0 ? s_head : img[w]), out_words + wa + w);
+        if (nwords == 0 && last && (be & 31) && tid == 0)   // empty last block closes the word
+            out_words[wa] = bswap32(s_head);
+    }
+    if (stamp) g_enc_stamps[5] = __builtin_amdgcn_s_memtime();
 }
 
 }  // namespace
@@ -288,7 +503,6 @@ static int run_size(pqh_ctx* ctx, const pqh_tables* t, const void* d_codes, long
     PQH_LAUNCH_CHECK(ctx);
     hipLaunchKernelGGL(scan_blocks, dim3(1), dim3(1024), 0, ctx->stream, bb, nb, bo, d_total);
     PQH_LAUNCH_CHECK(ctx);
-    ctx->enc_key = {d_codes, n, t, raw_first, d_prev_row};
     return PQH_OK;
 }
 
@@ -307,41 +521,76 @@ int pqh_encode_size(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes, 
 int pqh_encode_write(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes, long long n,
                      int raw_first, const void* d_prev_row, unsigned long long bit_offset,
                      unsigned char* d_out, unsigned long long out_bytes, int chunk_vectors,
-                     unsigned long long* d_chunk_offsets, void* d_chunk_prev) {
+                     unsigned long long* d_chunk_offsets, void* d_chunk_prev,
+                     unsigned long long* d_total_bits) {
     if (!ctx || !t || n < 0 || (n > 0 && (!d_codes || !d_out))) return PQH_ERR_ARG;
     if ((reinterpret_cast<uintptr_t>(d_out) & 3u) || (out_bytes & 3u))
         return pqh_set_error(ctx, PQH_ERR_ARG, "stream buffer must be 4-byte aligned and sized");
     if (chunk_vectors > 0 && !d_chunk_offsets) return PQH_ERR_ARG;
     int rc = pqh_use_device(ctx);
     if (rc) return rc;
-    if (n == 0) return PQH_OK;
-    const pqh_enc_key& key = ctx->enc_key;
-    if (key.codes != d_codes || key.n != n || key.t != t || key.raw_first != raw_first ||
-        key.prev != d_prev_row) {
-        rc = run_size(ctx, t, d_codes, n, raw_first, d_prev_row, ctx->d_diag + 3);
-        if (rc) return rc;
+    if (n == 0) {
+        if (d_total_bits) PQH_HIP(ctx, hipMemsetAsync(d_total_bits, 0, 8, ctx->stream));
+        return PQH_OK;
     }
-    uint32_t* bb;
-    unsigned long long* bo;
-    rc = enc_ws(ctx, n, &bb, &bo);
-    if (rc) return rc;
     const long long nb = (n + kEncBlock - 1) / kEncBlock;
     const size_t lds = ((size_t)kEncBlock * t->m * kMaxCodeLen / 32 + 4) * 4;
-    if (lds > 64 * 1024) return PQH_ERR_UNSUPPORTED;
+    if (lds > 160 * 1024) return PQH_ERR_UNSUPPORTED;
+    // look-back state: grow-only, epoch-tagged so it never needs clearing between calls
+    if (nb > ctx->lb_cap) {
+        PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));   // no launch may still use it
+        if (ctx->lb_state) (void)hipFree(ctx->lb_state);
+        ctx->lb_state = nullptr;
+        const long long cap = nb + nb / 4 + 64;
+        PQH_HIP(ctx, hipMalloc(&ctx->lb_state, (size_t)(2 * cap + 1) * 8));
+        PQH_HIP(ctx, hipMemsetAsync(ctx->lb_state, 0, (size_t)(2 * cap + 1) * 8, ctx->stream));
+        ctx->lb_cap = cap;
+        ctx->lb_epoch = 0;
+        ctx->lb_ticket_base = 0;
+    }
+    if (++ctx->lb_epoch >= 0xFFFF) {   // wrap: clear the tags (never matched by a new epoch)
+        PQH_HIP(ctx, hipMemsetAsync(ctx->lb_state, 0, (size_t)(2 * ctx->lb_cap) * 8, ctx->stream));
+        ctx->lb_epoch = 1;
+    }
+    unsigned long long* st = ctx->lb_state;
+    unsigned long long* tails = st + ctx->lb_cap;
+    unsigned long long* ticket = st + 2 * ctx->lb_cap;
+    unsigned long long* total = d_total_bits ? d_total_bits : ctx->d_diag + 3;
     uint32_t* words = reinterpret_cast<uint32_t*>(d_out);
-    if (t->k <= 256)
-        hipLaunchKernelGGL(enc_write<uint8_t>, dim3((unsigned)nb), dim3(kEncBlock), lds, ctx->stream,
-                           static_cast<const uint8_t*>(d_codes), n, t->m, t->k, t->context,
-                           raw_first, static_cast<const uint8_t*>(d_prev_row), t->d_enc, t->items, bo,
-                           bb, bit_offset, words, (long long)(out_bytes / 4), chunk_vectors,
-                           d_chunk_offsets, static_cast<uint8_t*>(d_chunk_prev), ctx->d_diag + 2);
-    else
-        hipLaunchKernelGGL(enc_write<uint16_t>, dim3((unsigned)nb), dim3(kEncBlock), lds, ctx->stream,
-                           static_cast<const uint16_t*>(d_codes), n, t->m, t->k, t->context,
-                           raw_first, static_cast<const uint16_t*>(d_prev_row), t->d_enc, t->items, bo,
-                           bb, bit_offset, words, (long long)(out_bytes / 4), chunk_vectors,
-                           d_chunk_offsets, static_cast<uint16_t*>(d_chunk_prev), ctx->d_diag + 2);
+#define PQH_ENC(T, MAXM)                                                                          \
+    do {                                                                                          \
+        if (lds > 64 * 1024)                                                                      \
+            PQH_HIP(ctx, hipFuncSetAttribute((const void*)(enc_onepass<T, MAXM>),                 \
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,          \
+                                             (int)lds));                                          \
+        hipLaunchKernelGGL((enc_onepass<T, MAXM>), dim3((unsigned)nb), dim3(kEncBlock), lds,       \
+                           ctx->stream, static_cast<const T*>(d_codes), n, t->m, t->k,            \
+                           t->context, raw_first, static_cast<const T*>(d_prev_row), t->d_enc,    \
+                           t->d_enc32, t->items, bit_offset, words, (long long)(out_bytes / 4),               \
+                           chunk_vectors, d_chunk_offsets, static_cast<T*>(d_chunk_prev),         \
+                           ctx->d_diag + 2, st, tails, ticket, ctx->lb_ticket_base,               \
+                           (unsigned)ctx->lb_epoch, nb, total);                                   \
+    } while (0)
+    if (t->k <= 256) {
+        if (t->m <= 8) PQH_ENC(uint8_t, 8);
+        else if (t->m <= 16) PQH_ENC(uint8_t, 16);
+        else PQH_ENC(uint8_t, 0);
+    } else {
+        if (t->m <= 8) PQH_ENC(uint16_t, 8);
+        else if (t->m <= 16) PQH_ENC(uint16_t, 16);
+        else PQH_ENC(uint16_t, 0);
+    }
+#undef PQH_ENC
     PQH_LAUNCH_CHECK(ctx);
+    ctx->lb_ticket_base += (unsigned long long)nb;
+    return PQH_OK;
+}
+
+// diagnostics only: phase stamps of the mid-grid workgroup of the last one-pass encode
+int pqh_debug_enc_stamps(pqh_ctx_t* ctx, unsigned long long* out8) {
+    if (!ctx || !out8) return PQH_ERR_ARG;
+    PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    PQH_HIP(ctx, hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_enc_stamps), 8 * sizeof(unsigned long long)));
     return PQH_OK;
 }
 

@@ -11,16 +11,6 @@
 
 struct pqh_tables;
 
-// encode_size -> encode_write hand-off key: the write pass reuses the size pass's block
-// totals only when they were computed for the same call arguments.
-struct pqh_enc_key {
-    const void* codes = nullptr;
-    long long n = -1;
-    const pqh_tables* t = nullptr;
-    int raw_first = -1;
-    const void* prev = nullptr;
-};
-
 struct pqh_ctx {
     int device = 0;
     int num_cus = 256;
@@ -32,7 +22,11 @@ struct pqh_ctx {
     size_t ws_bytes = 0;
     // [0] rerank count, [1] decode error, [2] encode capacity error, [3] scratch total bits
     unsigned long long* d_diag = nullptr;
-    pqh_enc_key enc_key;
+    // one-pass encoder look-back state: [lb_cap] block states, [lb_cap] tails, ticket
+    unsigned long long* lb_state = nullptr;
+    long long lb_cap = 0;
+    unsigned lb_epoch = 0;
+    unsigned long long lb_ticket_base = 0;
 };
 
 int pqh_set_error(pqh_ctx* ctx, int code, const char* fmt, ...);
@@ -58,6 +52,7 @@ bool pqh_debug_sync();
 
 // Device-side code tables shared by the encode and decode kernels (pqh_tables.hip).
 //   enc [m][items] u64: (len << 56) | code (right-aligned, len <= 56; 0 = no code)
+//   enc32 [m][items] u32: the same entry as len << 26 | code when len <= 26, else ~0u
 //   Decode: two-level lookup per alphabet (tables = m * roots, roots = K in context mode)
 //   lut1 [tables][1 << kL1Max] u16, the first 2^l1_bits entries used (W1 = l1_bits for
 //        every alphabet): (len << 12) | sym for 1 <= len <= W1 (replicated);
@@ -78,6 +73,8 @@ struct pqh_tables {
     long long items = 0, tables = 0;
     long long lut2_cap = 0;
     unsigned long long* d_enc = nullptr;
+    uint32_t* d_enc32 = nullptr;     // [m][items] len << 26 | code (len <= 26), else ~0u
+                                     // (escape: read d_enc) -- the encoder's gather table
     uint16_t* d_lut1 = nullptr;
     uint16_t* d_lut2 = nullptr;
     uint32_t* d_meta = nullptr;

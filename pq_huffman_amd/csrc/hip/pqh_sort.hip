@@ -73,7 +73,6 @@ int pqh_sort_rows(pqh_ctx_t* ctx, void* d_codes, long long n, int m, void* d_tmp
     int rc = pqh_use_device(ctx);
     if (rc) return rc;
     if (n <= 1) return PQH_OK;
-    ctx->enc_key = pqh_enc_key{};   // the shared workspace is reused below
     // workspace: keys in/out (u64), index in/out (u32), rocPRIM temp, row buffer if no d_tmp
     size_t temp = 0;
     if (rocprim::radix_sort_pairs(nullptr, temp, (unsigned long long*)nullptr,

@@ -415,8 +415,8 @@ lut_alloc(long long tables, long long lut2_cap, uint32_t* __restrict__ meta,
 }
 
 __global__ void __launch_bounds__(256)
-lut_fill(const unsigned long long* __restrict__ enc, int k, int l2_bits,
-         const uint32_t* __restrict__ meta, uint16_t* __restrict__ lut1,
+lut_fill(const unsigned long long* __restrict__ enc, uint32_t* __restrict__ enc32, int k,
+         int l2_bits, const uint32_t* __restrict__ meta, uint16_t* __restrict__ lut1,
          uint16_t* __restrict__ lut2, long long lut2_cap, pqh_long_code* __restrict__ longs,
          uint32_t* __restrict__ long_cnt) {
     __shared__ uint32_t w2max[1 << kL1Max];
@@ -465,6 +465,8 @@ lut_fill(const unsigned long long* __restrict__ enc, int k, int l2_bits,
     for (int s = threadIdx.x; s < k; s += blockDim.x) {
         const unsigned long long v = e[s];
         const int len = (int)(v >> 56);
+        enc32[t * k + s] = len <= 26 ? (uint32_t)(((unsigned long long)len << 26) | (v & kCodeMask))
+                                     : ~0u;
         if (!len) continue;
         const unsigned long long code = v & kCodeMask;
         if (len <= w1) {
@@ -804,6 +806,7 @@ int pqh_tables_alloc(pqh_ctx_t* ctx, int m, int k, int context, pqh_tables_t** o
     t->l2_bits = 8;
     t->lut2_cap = std::min<long long>(t->tables * 2048 + 65536, kL2BaseMax - 1);
     if (hipMalloc(&t->d_enc, (size_t)m * t->items * 8) != hipSuccess ||
+        hipMalloc(&t->d_enc32, (size_t)m * t->items * 4) != hipSuccess ||
         hipMalloc(&t->d_lut1, (size_t)(t->tables << kL1Max) * 2) != hipSuccess ||
         hipMalloc(&t->d_lut2, (size_t)t->lut2_cap * 2) != hipSuccess ||
         hipMalloc(&t->d_meta, (size_t)t->tables * 4 + 16) != hipSuccess ||
@@ -824,7 +827,7 @@ int pqh_tables_destroy(pqh_tables_t* t) {
         (void)hipSetDevice(t->ctx->device);
         (void)hipStreamSynchronize(t->ctx->stream);
     }
-    void* bufs[] = {t->d_enc, t->d_lut1, t->d_lut2, t->d_meta, t->d_scratch,
+    void* bufs[] = {t->d_enc, t->d_enc32, t->d_lut1, t->d_lut2, t->d_meta, t->d_scratch,
                     t->d_long, t->d_long_cnt, t->d_err};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -840,7 +843,7 @@ static int launch_luts(pqh_ctx* ctx, pqh_tables* t) {
                        t->d_meta, t->d_scratch);
     PQH_LAUNCH_CHECK(ctx);
     hipLaunchKernelGGL(lut_fill, dim3((unsigned)t->tables), dim3(256), 0, ctx->stream, t->d_enc,
-                       t->k, t->l2_bits, t->d_meta, t->d_lut1, t->d_lut2, t->lut2_cap, t->d_long,
+                       t->d_enc32, t->k, t->l2_bits, t->d_meta, t->d_lut1, t->d_lut2, t->lut2_cap, t->d_long,
                        t->d_long_cnt);
     PQH_LAUNCH_CHECK(ctx);
     return PQH_OK;
