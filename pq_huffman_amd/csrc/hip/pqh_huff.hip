@@ -28,10 +28,13 @@ template <typename CodeT>
 __device__ __forceinline__ unsigned ld_code(const CodeT* c, long long i) { return (unsigned)c[i]; }
 
 // ---------------------------------------------------------------- histograms
+// Context histogram, pass 1: workgroup (chunk of kHistChunk vectors, part) counts its
+// (prev, cur) pairs in LDS as u16 pairs (a chunk cannot overflow 16 bits) and stores the
+// packed counters as its private partial -- plain coalesced stores, no global atomics.
 template <typename CodeT>
 __global__ void __launch_bounds__(1024)
 hist_ctx(const CodeT* __restrict__ codes, long long n, int m_total, int k,
-         const CodeT* __restrict__ prev_row, uint32_t* __restrict__ counts) {
+         const CodeT* __restrict__ prev_row, uint32_t* __restrict__ partial) {
     extern __shared__ uint32_t pairs[];   // k*k u16 counters packed two per word
     const int m = blockIdx.y;
     const int words = (k * k + 1) / 2;
@@ -50,12 +53,34 @@ hist_ctx(const CodeT* __restrict__ codes, long long n, int m_total, int k,
         atomicAdd(&pairs[bin >> 1], 1u << ((bin & 1u) * 16));
     }
     __syncthreads();
-    uint32_t* out = counts + (long long)m * k * k;
-    for (int w = threadIdx.x; w < words; w += blockDim.x) {
-        const uint32_t c = pairs[w];
-        if (c & 0xFFFFu) atomicAdd(&out[2 * w], c & 0xFFFFu);
-        if (c >> 16) atomicAdd(&out[2 * w + 1], c >> 16);
+    uint32_t* out = partial + ((long long)m * gridDim.x + blockIdx.x) * words;
+    if ((words & 3) == 0) {
+        const uint4* src = reinterpret_cast<const uint4*>(pairs);
+        uint4* dst = reinterpret_cast<uint4*>(out);
+        for (int w = threadIdx.x; w < words / 4; w += blockDim.x) dst[w] = src[w];
+    } else {
+        for (int w = threadIdx.x; w < words; w += blockDim.x) out[w] = pairs[w];
     }
+}
+
+// Context histogram, pass 2: counts[m][bin] += sum of the chunks' partials (one thread per
+// packed word, so every counter has a single writer)
+__global__ void __launch_bounds__(256)
+hist_ctx_reduce(const uint32_t* __restrict__ partial, int chunks, int words, long long items,
+                uint32_t* __restrict__ counts) {
+    const int m = blockIdx.y;
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= words) return;
+    const uint32_t* p = partial + (long long)m * chunks * words + w;
+    uint32_t lo = 0, hi = 0;
+    for (int c = 0; c < chunks; ++c) {
+        const uint32_t x = p[(long long)c * words];
+        lo += x & 0xFFFFu;
+        hi += x >> 16;
+    }
+    uint32_t* out = counts + (long long)m * items;
+    if (lo) out[2 * w] += lo;
+    if (hi && 2 * w + 1 < items) out[2 * w + 1] += hi;
 }
 
 template <typename CodeT>
@@ -241,15 +266,15 @@ __device__ __forceinline__ void gather_entries(const CodeT* __restrict__ codes, 
 
 // One-pass encoder (huffman_encoder.c:207-238 + the bit cursor of bitstream.c:71-101).
 // Workgroups take tickets in launch order (so every predecessor has started), sum their
-// 256 vectors' code lengths, and find their bit offset by a decoupled look-back over the
+// kEncBlock vectors' code lengths, and find their bit offset by a decoupled look-back over the
 // predecessors' published aggregates / prefixes.  Each workgroup ORs its codes into an LDS
 // image of its bit range and stores every word it owns exactly once: the word it shares with
 // its successor is published as a "tail" instead, and the successor merges it into its own
 // first word.  So no word is written twice, nothing needs zeroing and no global atomics are
 // used; the call's first word is merged with the memory content when bit_offset is not
 // word-aligned (shards composed into one buffer).  MAXM > 0 keeps the m table entries of a
-// vector in registers (m <= MAXM).
-// diagnostics: s_memtime phase stamps of one mid-grid workgroup (pqh_debug_enc_stamps)
+// vector in registers (m <= MAXM).  (Diagnostics: g_enc_stamps holds s_memtime phase
+// stamps of the mid-grid workgroup, read by pqh_debug_enc_stamps.)
 __device__ unsigned long long g_enc_stamps[8];
 
 template <typename CodeT, int MAXM>
@@ -455,12 +480,19 @@ int pqh_histogram(pqh_ctx_t* ctx, const void* d_codes, long long n, int m, int k
     if (n == 0) return PQH_OK;
     if (context) {
         const unsigned chunks = (unsigned)((n + kHistChunk - 1) / kHistChunk);
-        const size_t lds = (size_t)((k * k + 1) / 2) * 4;
+        const int words = (k * k + 1) / 2;
+        const size_t lds = (size_t)words * 4;
+        rc = pqh_ensure_ws(ctx, (size_t)m * chunks * words * 4);
+        if (rc) return rc;
+        uint32_t* partial = static_cast<uint32_t*>(ctx->ws);
         PQH_HIP(ctx, hipFuncSetAttribute((const void*)hist_ctx<uint8_t>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         hipLaunchKernelGGL(hist_ctx<uint8_t>, dim3(chunks, m), dim3(1024), lds, ctx->stream,
                            static_cast<const uint8_t*>(d_codes), n, m, k,
-                           static_cast<const uint8_t*>(d_prev_row), d_counts);
+                           static_cast<const uint8_t*>(d_prev_row), partial);
+        PQH_LAUNCH_CHECK(ctx);
+        hipLaunchKernelGGL(hist_ctx_reduce, dim3((unsigned)((words + 255) / 256), m), dim3(256), 0,
+                           ctx->stream, partial, (int)chunks, words, (long long)k * k, d_counts);
     } else {
         const unsigned blocks = (unsigned)std::min<long long>((n + 4095) / 4096, 512);
         if (k <= 256)
