@@ -155,6 +155,10 @@ def main():
 
     x = make_data(torch, n, d, 0x5EED, rank, dev)
     cent = train_centroids(torch, make_data(torch, 200_000, d, 0x5EED, 0, dev), m, k)
+    if world > 1:   # one quantizer for the whole job: rank 0's centroids
+        ct = torch.from_numpy(cent).to(dev)
+        dist.broadcast(ct, 0)
+        cent = ct.cpu().numpy()
     ctx = codec.Context(local)
     pq = codec.PQ(ctx, cent)
     items = k * k if ctxm else k

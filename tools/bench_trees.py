@@ -50,7 +50,7 @@ def stamps():
     from pq_huffman_amd.capi import lib
     L = lib()
     L.pqh_debug_tree_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-    out = (ctypes.c_ulonglong * 8)()
+    out = (ctypes.c_ulonglong * 16)()
     return L, out
 
 
