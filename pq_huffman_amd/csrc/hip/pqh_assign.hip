@@ -23,6 +23,7 @@
 //    from the winner the winner IS the fp32 direct-form argmin; otherwise (and for any
 //    non-finite input) the wave re-ranks all K centroids of that vector with the exact
 //    fp32 direct form and first-index tie break.
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -119,37 +120,41 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     const long long nblk = (n + 31) / 32;
     unsigned long long slow_count = 0;
 
-    // x slice of a block: lane (r, h) holds vector r's D floats (both half-waves)
+    // x slice of a block.  D == 16 (SIFT): lane (r, h) holds dims [8h, 8h + 8) of vector r
+    // -- exactly the B-fragment slots it feeds -- so each lane splits 8 values and no
+    // half-wave selects are needed; other D: both half-waves hold all D dims.
+    constexpr bool HALF = D == 16;
+    constexpr int XD = HALF ? 8 : D;
     auto load_x = [&](long long b, float* dst) {
         const long long vv = b * 32 + r;
         const bool ok = b < nblk && vv < n;
-        const float* xp = x + (ok ? vv : 0) * ldx + (long long)m * D;
-        if constexpr (D % 4 == 0) {
+        const float* xp = x + (ok ? vv : 0) * ldx + (long long)m * D + (HALF ? 8 * h : 0);
+        if constexpr (XD % 4 == 0) {
 #pragma unroll
-            for (int j = 0; j < D; j += 4) {
+            for (int j = 0; j < XD; j += 4) {
                 float4 q = ok ? *reinterpret_cast<const float4*>(xp + j) : make_float4(0, 0, 0, 0);
                 dst[j] = q.x; dst[j + 1] = q.y; dst[j + 2] = q.z; dst[j + 3] = q.w;
             }
         } else {
 #pragma unroll
-            for (int j = 0; j < D; ++j) dst[j] = ok ? xp[j] : 0.0f;
+            for (int j = 0; j < XD; ++j) dst[j] = ok ? xp[j] : 0.0f;
         }
     };
-    float xn[D];
+    float xn[XD];
     load_x(blockIdx.x, xn);
     for (long long blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
         const long long v = blk * 32 + r;
         const bool valid = v < n;
-        float xs[D];
+        float xs[XD];
 #pragma unroll
-        for (int j = 0; j < D; ++j) xs[j] = xn[j];
+        for (int j = 0; j < XD; ++j) xs[j] = xn[j];
         load_x(blk + gridDim.x, xn);   // next block's slice in flight during this block
 
         float X = 0.0f;
         bool lo = false;
-        float xh[D], xl[D];
+        float xh[XD], xl[XD];
 #pragma unroll
-        for (int j = 0; j < D; ++j) {
+        for (int j = 0; j < XD; ++j) {
             X = fmaf(xs[j], xs[j], X);
             __bf16 hb = (__bf16)xs[j];
             xh[j] = (float)hb;
@@ -157,6 +162,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
             xl[j] = (float)(__bf16)rem;
             lo |= rem != 0.0f;
         }
+        if constexpr (HALF) X += __shfl_xor(X, 32);   // the other half-wave's 8 dims
         const bool any_lo = __any(lo);
         const bool finite_x = isfinite(X);
 
@@ -170,28 +176,41 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
 
         // B fragments
         bf16x8 Bm[P::PM];
-#pragma unroll
-        for (int p = 0; p < P::PM; ++p)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                float v0 = main_slot<D>(16 * p + j, xh, bv);
-                float v1 = main_slot<D>(16 * p + 8 + j, xh, bv);
-                Bm[p][j] = (__bf16)(h ? v1 : v0);
-            }
         bf16x8 Bl[P::PL];
-#pragma unroll
-        for (int p = 0; p < P::PL; ++p)
+        if constexpr (HALF) {
+            // slots 16p + 8h + j: p = 0, 1 -> xh[8h + j]; p = 2 -> aux (h = 0) / zero (h = 1)
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                int s0 = 16 * p + j, s1 = 16 * p + 8 + j;
-                float v0 = s0 < D ? xl[s0 < D ? s0 : 0] : 0.0f;
-                float v1 = s1 < D ? xl[s1 < D ? s1 : 0] : 0.0f;
-                Bl[p][j] = (__bf16)(h ? v1 : v0);
+                Bm[0][j] = (__bf16)xh[j];
+                Bl[0][j] = (__bf16)xl[j];
             }
-
-        unsigned m1 = 0xFFFFFFFFu, m2 = 0xFFFFFFFFu, mt = 0;
+            Bm[1] = Bm[0];
 #pragma unroll
-        for (int t = 0; t < kTiles; ++t) {
+            for (int j = 0; j < 8; ++j)
+                Bm[2][j] = (__bf16)(h ? 0.0f : (j < 3 ? 1.0f : (j == 3 ? bv : 0.0f)));
+        } else {
+#pragma unroll
+            for (int p = 0; p < P::PM; ++p)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    float v0 = main_slot<D>(16 * p + j, xh, bv);
+                    float v1 = main_slot<D>(16 * p + 8 + j, xh, bv);
+                    Bm[p][j] = (__bf16)(h ? v1 : v0);
+                }
+#pragma unroll
+            for (int p = 0; p < P::PL; ++p)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    int s0 = 16 * p + j, s1 = 16 * p + 8 + j;
+                    float v0 = s0 < D ? xl[s0 < D ? s0 : 0] : 0.0f;
+                    float v1 = s1 < D ? xl[s1 < D ? s1 : 0] : 0.0f;
+                    Bl[p][j] = (__bf16)(h ? v1 : v0);
+                }
+        }
+
+        // tiles, software-pipelined: tile t + 1's MFMAs are issued before tile t's keys are
+        // reduced, so the matrix core and the VALU work side by side
+        auto tile_acc = [&](int t) {
             f32x16 acc = {0};
 #pragma unroll
             for (int p = 0; p < P::PM; ++p)
@@ -203,6 +222,14 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
                     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, Bl[p], acc, 0, 0, 0);
                 }
             }
+            return acc;
+        };
+        unsigned m1 = 0xFFFFFFFFu, m2 = 0xFFFFFFFFu, mt = 0;
+        f32x16 acc = tile_acc(0);
+#pragma unroll
+        for (int t = 0; t < kTiles; ++t) {
+            f32x16 nxt;
+            if (t + 1 < kTiles) nxt = tile_acc(t + 1);
             unsigned k0 = (__float_as_uint(acc[0]) & ~15u);
             unsigned k1 = (__float_as_uint(acc[1]) & ~15u) | 1u;
             unsigned t1 = min(k0, k1), t2 = max(k0, k1);
@@ -216,6 +243,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
             mt = t1 < m1 ? (unsigned)t : mt;
             m1 = min(m1, t1);
             m2 = nm2;
+            if (t + 1 < kTiles) acc = nxt;
         }
         // merge the two half-waves (lanes l and l^32 hold the same vector)
         unsigned o1 = __shfl_xor(m1, 32), o2 = __shfl_xor(m2, 32), ot = __shfl_xor(mt, 32);
@@ -239,8 +267,11 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
                 todo &= todo - 1;
                 float xv[D];
 #pragma unroll
-                for (int j = 0; j < D; ++j)
-                    xv[j] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xs[j]), rs));
+                for (int j = 0; j < D; ++j) {   // HALF: dims 8.. live in the partner lane
+                    const int src = HALF && j >= XD ? rs + 32 : rs;
+                    xv[j] = __int_as_float(__builtin_amdgcn_readlane(
+                        __float_as_int(xs[HALF && j >= XD ? j - XD : j]), src));
+                }
                 float best = INFINITY;
                 int bidx = 0x7FFFFFFF;
 #pragma unroll
@@ -444,17 +475,24 @@ int launch_mfma(pqh_pq* pq, const float* x, long long n, long long ldx, CodeT* c
     pqh_ctx* ctx = pq->ctx;
     const long long nblk = (n + 31) / 32;
     const int groups = (pq->m + kWavesPerWG - 1) / kWavesPerWG;
-    long long gx = (long long)ctx->num_cus * 2 / groups;
-    if (gx < 1) gx = 1;
-    if (gx > nblk) gx = nblk;
-    dim3 grid((unsigned)gx, (unsigned)groups), block(64 * kWavesPerWG);
+    dim3 block(64 * kWavesPerWG);
     unsigned long long* rr = ctx->d_diag;
+    // grid = the workgroups that are resident at once (persistent, grid-stride over the
+    // 32-vector blocks): more would only queue behind the first wave of workgroups
 #define PQH_CASE(DD)                                                                        \
-    case DD:                                                                                \
-        hipLaunchKernelGGL((pq_assign_mfma<DD, CodeT>), grid, block, 0, ctx->stream, x, n, \
-                           ldx, pq->m, pq->d_afrag, pq->d_cent, pq->d_cmax, pq->d_sqc,      \
-                           codes, counts, rr);                                              \
-        break;
+    case DD: {                                                                              \
+        int per_cu = 1;                                                                     \
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(                                   \
+                &per_cu, (const void*)(pq_assign_mfma<DD, CodeT>), (int)block.x, 0) !=      \
+                hipSuccess || per_cu < 1)                                                   \
+            per_cu = 1;                                                                     \
+        long long gx = (long long)ctx->num_cus * per_cu / groups;                           \
+        gx = std::max(1ll, std::min(gx, nblk));                                             \
+        hipLaunchKernelGGL((pq_assign_mfma<DD, CodeT>), dim3((unsigned)gx, (unsigned)groups), \
+                           block, 0, ctx->stream, x, n, ldx, pq->m, pq->d_afrag, pq->d_cent, \
+                           pq->d_cmax, pq->d_sqc, codes, counts, rr);                       \
+        break;                                                                              \
+    }
     switch (pq->dsub) {
         PQH_CASE(4)
         PQH_CASE(6)
