@@ -44,6 +44,10 @@ float* fvecs_load(const char* filename, long long* num_vectors, int* num_dimensi
 /* codes: n x M, uint8 when K <= 256 else uint16 (row-major, pq_indices.bvecsl order). */
 int pq_encode(const centroids_codebook_t* codebook, const float* x, long long n, int d,
               void* codes);
+/* Train the codebook in place on the GPU: `iters` deterministic Lloyd iterations
+ * (pqh_kmeans_train) from the centroids it holds -- the build's replacement for the
+ * training done by yael kmeans at pq_encoder.c:265-274. */
+int pq_train(centroids_codebook_t* codebook, const float* x, long long n, int d, int iters);
 /* mean over vectors of the summed squared reconstruction error (double). */
 int pq_compute_error(const centroids_codebook_t* codebook, const float* x, long long n, int d,
                      const void* codes, double* error_out);

@@ -81,6 +81,15 @@ int pqh_pq_error(pqh_ctx_t* ctx, const pqh_pq_t* pq, const float* d_x, long long
 int pqh_pq_reconstruct(pqh_ctx_t* ctx, const pqh_pq_t* pq, const void* d_codes, long long n,
                        float* d_out, long long ld_out);
 
+/* ---- k-means training (replaces the training half of yael kmeans, pq_encoder.c:265-274) */
+/* `iters` Lloyd iterations per subspace on the GPU: exact fp32 assignment (as
+ * pqh_pq_assign) then centroid means; an empty cluster keeps its centroid.  Sums are
+ * 64-bit fixed point (x * 2^s, s = 61 - ceil(log2(max|x| * n))), so the result is exact
+ * and the same on every run.  centroids: host [m][k][dsub], initial in, trained out.
+ * d_x rows are ld_x floats apart (subspace i = columns [i*dsub, (i+1)*dsub)).  Synchronous. */
+int pqh_kmeans_train(pqh_ctx_t* ctx, const float* d_x, long long n, long long ld_x, int m,
+                     int k, int dsub, int iters, float* centroids);
+
 /* ---- symbol histograms (huffman_encoder.c:139-205) ------------------------------- */
 /* counts += histogram of codes.  context: pairs (codes[v-1][i], codes[v][i]) for v >= 1,
  * plus (d_prev_row[i], codes[0][i]) when d_prev_row != NULL (the one-vector halo of a

@@ -39,6 +39,9 @@ def lib():
         L.orc_decode.restype = I
         L.orc_sort_rows.argtypes = [P, LL, I]
         L.orc_pq_assign.argtypes = [P, LL, I, I, I, P, P, I, P, I]
+        L.orc_kmeans.argtypes = [P, LL, I, I, I, I, P, I]
+        L.orc_kmeans_shift.argtypes = [ctypes.c_float, LL]
+        L.orc_kmeans_shift.restype = I
         L.orc_compute_error.argtypes = [P, LL, I, I, I, P, P, I]
         L.orc_compute_error.restype = ctypes.c_double
         L.orc_estimate_size.argtypes = [P, P, LL]
@@ -157,6 +160,15 @@ def sort_rows(codes: np.ndarray) -> np.ndarray:
     out = np.ascontiguousarray(codes, np.uint8).copy()
     lib().orc_sort_rows(_p(out), out.shape[0], out.shape[1])
     return out
+
+
+def kmeans(x: np.ndarray, init: np.ndarray, iters: int, threads: int = 0) -> np.ndarray:
+    """Deterministic fixed-point Lloyd (the build's training definition); init [m][k][ds]."""
+    x = np.ascontiguousarray(x, np.float32)
+    cent = np.ascontiguousarray(init, np.float32).copy()
+    m, k, ds = cent.shape
+    lib().orc_kmeans(_p(x), x.shape[0], x.shape[1], m, k, iters, _p(cent), threads)
+    return cent
 
 
 def pq_assign(x: np.ndarray, centroids: np.ndarray, threads: int = 1):

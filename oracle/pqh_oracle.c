@@ -429,6 +429,57 @@ void orc_pq_assign(const float* x, long long n, int d, int m, int k, const float
     }
 }
 
+/* Deterministic Lloyd k-means (the build's replacement for yael's training, SURVEY 8f-2;
+ * NOT the reference's algorithm -- yael is absent): iters x { exact assignment as
+ * orc_pq_assign; centroid = mean of its members, accumulated in 64-bit fixed point
+ * x * 2^s, s = 61 - ceil(log2(max|x| * n)) clamped to [-126, 100]; empty clusters keep
+ * their centroid }.  The GPU trainer (pqh_kmeans.hip) must match this bit for bit. */
+int orc_kmeans_shift(float max_abs, long long n) {
+    if (!(max_abs > 0.0f) || n <= 0) return 40;
+    if (isinf(max_abs)) return -126;
+    double b = (double)max_abs * (double)n;
+    int s = 61 - (int)ceil(log2(b));
+    if (s < -126) s = -126;
+    if (s > 100) s = 100;
+    return s;
+}
+
+void orc_kmeans(const float* x, long long n, int d, int m, int k, int iters, float* cent,
+                int threads) {
+    int ds = d / m;
+    float mx = 0.0f;
+    for (long long e = 0; e < n * d; ++e) {
+        float a = fabsf(x[e]);
+        if (isnan(a)) a = INFINITY;
+        if (a > mx) mx = a;
+    }
+    int s = orc_kmeans_shift(mx, n);
+    int esize = k <= 256 ? 1 : 2;
+    void* codes = malloc((size_t)n * m * esize + 1);
+    long long* sums = (long long*)malloc(sizeof(long long) * (size_t)m * k * ds);
+    unsigned long long* cnt = (unsigned long long*)malloc(sizeof(unsigned long long) * (size_t)m * k);
+    for (int it = 0; it < iters; ++it) {
+        orc_pq_assign(x, n, d, m, k, cent, codes, esize, NULL, threads);
+        memset(sums, 0, sizeof(long long) * (size_t)m * k * ds);
+        memset(cnt, 0, sizeof(unsigned long long) * (size_t)m * k);
+        for (long long v = 0; v < n; ++v)
+            for (int i = 0; i < m; ++i) {
+                unsigned c = orc_sym(codes, esize, v * m + i);
+                cnt[(size_t)i * k + c]++;
+                for (int j = 0; j < ds; ++j)
+                    sums[((size_t)i * k + c) * ds + j] +=
+                        llrint(ldexp((double)x[v * d + (long long)i * ds + j], s));
+            }
+        for (size_t q = 0; q < (size_t)m * k; ++q)
+            if (cnt[q])
+                for (int j = 0; j < ds; ++j)
+                    cent[q * ds + j] = (float)ldexp((double)sums[q * ds + j] / (double)cnt[q], -s);
+    }
+    free(codes);
+    free(sums);
+    free(cnt);
+}
+
 /* compute_error (pq_encoder.c:82-119): mean over vectors of sum (double) of squared fp32
  * deltas. */
 double orc_compute_error(const float* x, long long n, int d, int m, int k, const float* cent,

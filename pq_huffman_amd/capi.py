@@ -90,6 +90,7 @@ SIGNATURES = [
     ("centroids_codebook_save", I, [P, S]), ("centroids_codebook_load", I, [P, S, I, I]),
     ("fvecs_load_meta", I, [S, P, P]), ("fvecs_load", P, [S, P, P]),
     ("pq_encode", I, [P, P, LL, I, P]), ("pq_compute_error", I, [P, P, LL, I, P, P]),
+    ("pq_train", I, [P, P, LL, I, I]),
     # pqh.h
     ("pqh_ctx_create", I, [P, I]), ("pqh_ctx_destroy", I, [P]), ("pqh_ctx_set_stream", I, [P, P]),
     ("pqh_ctx_sync", I, [P]), ("pqh_status_string", S, [I]), ("pqh_ctx_last_error", S, [P]),
@@ -99,6 +100,7 @@ SIGNATURES = [
     ("pqh_pq_last_rerank_count", I, [P, P]),
     ("pqh_pq_error", I, [P, P, P, LL, LL, P, P]),
     ("pqh_pq_reconstruct", I, [P, P, P, LL, P, LL]),
+    ("pqh_kmeans_train", I, [P, P, LL, LL, I, I, I, I, P]),
     ("pqh_histogram", I, [P, P, LL, I, I, I, P, P]),
     ("pqh_tables_create", I, [P, P, I, P]), ("pqh_tables_destroy", I, [P]),
     ("pqh_tables_alloc", I, [P, I, I, I, P]), ("pqh_tables_build", I, [P, P, P]),

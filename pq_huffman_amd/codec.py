@@ -5,6 +5,7 @@ huffman_decoder, gluing CLI programs through files.  Here the same stages run as
 calls on device-resident data:
 
     PQ.assign            pq_encoder.c:270-272 (yael kmeans assignment) + :192-205
+    kmeans_train         pq_encoder.c:265-274 (training, deterministic Lloyd on the GPU)
     sort_rows            huffman_encoder.c:301-317 (default sort mode)
     histogram            huffman_encoder.c:139-205
     build_codebooks      huffman_encoder.c:377-388 (huffman_codebook_[context_]encode_init)
@@ -144,6 +145,16 @@ class PQ:
             self.close()
         except Exception:
             pass
+
+
+def kmeans_train(ctx: Context, x, init: np.ndarray, iters: int) -> np.ndarray:
+    """Lloyd k-means of every subspace on the GPU (pqh_kmeans_train): exact assignment and
+    fixed-point centroid means, deterministic; init [m][k][dsub] -> trained centroids."""
+    cent = np.ascontiguousarray(init, np.float32).copy()
+    m, k, ds = cent.shape
+    check(lib().pqh_kmeans_train(ctx.ptr, _ptr(x), x.shape[0], x.stride(0), m, k, ds, iters,
+                                 _ptr(cent)), "pqh_kmeans_train")
+    return cent
 
 
 class Codebooks:

@@ -2,6 +2,9 @@
 #include <cstdlib>
 #include <cstring>
 
+#include <algorithm>
+#include <cmath>
+
 #include "pqh_internal.h"
 
 int pqh_set_error(pqh_ctx* ctx, int code, const char* fmt, ...) {
@@ -12,6 +15,16 @@ int pqh_set_error(pqh_ctx* ctx, int code, const char* fmt, ...) {
         va_end(ap);
     }
     return code;
+}
+
+// fixed-point exponent of the k-means sums: s = 61 - ceil(log2(max|x| * n)), clamped, so
+// that n values of magnitude <= max|x| scaled by 2^s stay below 2^61 (pqh_kmeans.hip)
+int pqh_kmeans_fixed_shift(float max_abs, long long n) {
+    if (!(max_abs > 0.0f) || n <= 0) return 40;
+    if (std::isinf(max_abs)) return -126;
+    const double b = (double)max_abs * (double)n;
+    int s = 61 - (int)std::ceil(std::log2(b));
+    return std::max(-126, std::min(100, s));
 }
 
 bool pqh_debug_sync() {

@@ -32,6 +32,7 @@ struct pqh_ctx {
 int pqh_set_error(pqh_ctx* ctx, int code, const char* fmt, ...);
 int pqh_ensure_ws(pqh_ctx* ctx, size_t bytes);
 int pqh_use_device(pqh_ctx* ctx);
+int pqh_kmeans_fixed_shift(float max_abs, long long n);
 
 #define PQH_HIP(ctx, expr)                                                                \
     do {                                                                                  \

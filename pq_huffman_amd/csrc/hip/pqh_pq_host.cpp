@@ -72,3 +72,20 @@ extern "C" int pq_compute_error(const centroids_codebook_t* cb, const float* x, 
     (void)hipFree(dc);
     return rc;
 }
+
+// k-means training of the whole codebook on the GPU (pqh_kmeans_train); the codebook holds
+// the initial centroids on entry and the trained ones on return
+extern "C" int pq_train(centroids_codebook_t* cb, const float* x, long long n, int d, int iters) {
+    if (!cb || !x || n < 0 || iters < 0 || d != cb->num_parts * cb->num_dimensions) return PQH_ERR_ARG;
+    Ctx g;
+    int rc = pqh_ctx_create(&g.c, 0);
+    if (rc) return rc;
+    float* dx = nullptr;
+    if (hipMalloc(&dx, (size_t)n * d * 4 + 16) != hipSuccess) return PQH_ERR_NOMEM;
+    rc = hipMemcpy(dx, x, (size_t)n * d * 4, hipMemcpyHostToDevice) == hipSuccess ? PQH_OK : PQH_ERR_HIP;
+    if (!rc)
+        rc = pqh_kmeans_train(g.c, dx, n, d, cb->num_parts, cb->num_clusters, cb->num_dimensions,
+                              iters, cb->centroids_pool);
+    (void)hipFree(dx);
+    return rc;
+}

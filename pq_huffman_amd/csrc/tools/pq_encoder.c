@@ -2,10 +2,10 @@
  * (usage pq_encoder.c:121-175; outputs :207-213, :248-255, :290-295).
  *   pq_encoder <input.fvecs> <output template> <m> [--num-threads t] [--compute-error]
  *              [--kmeans-iterations n] [--centroids <pq_centroids.fvecsl>] [--seed s]
- * Assignment runs on the GPU (libpqh).  Training: deterministic Lloyd iterations
- * (seeded sample init; yael's time-seeded Berkeley init is not reproducible) with GPU
- * assignment and host centroid means; --centroids skips training.  --num-threads is
- * accepted for compatibility. */
+ * Assignment and training run on the GPU (libpqh).  Training: deterministic Lloyd
+ * iterations on the GPU (pq_train: exact assignment, fixed-point centroid means) from a
+ * seeded sample init (yael's time-seeded Berkeley init is not reproducible); --centroids
+ * skips training.  --num-threads is accepted for compatibility. */
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -66,32 +66,11 @@ int main(int argc, const char* argv[]) {
             for (int i = 0; i < m; ++i)
                 memcpy(cb.centroids[i] + (size_t)c * ds, x + v * d + (long long)i * ds, ds * sizeof(float));
         }
-        double* sums = (double*)malloc(sizeof(double) * (size_t)m * k * ds);
-        long long* cnt = (long long*)malloc(sizeof(long long) * (size_t)m * k);
-        for (int it = 0; it < iters; ++it) {
-            printf("Starting iteration %d\n", it);
-            int rc = pq_encode(&cb, x, n, d, codes);
-            if (rc) {
-                fprintf(stderr, "pq_encode failed: %d\n", rc);
-                return 1;
-            }
-            memset(sums, 0, sizeof(double) * (size_t)m * k * ds);
-            memset(cnt, 0, sizeof(long long) * (size_t)m * k);
-            for (long long v = 0; v < n; ++v)
-                for (int i = 0; i < m; ++i) {
-                    int c = codes[v * m + i];
-                    cnt[i * k + c]++;
-                    for (int j = 0; j < ds; ++j) sums[((size_t)i * k + c) * ds + j] += x[v * d + i * ds + j];
-                }
-            for (int i = 0; i < m; ++i)
-                for (int c = 0; c < k; ++c)
-                    if (cnt[i * k + c])
-                        for (int j = 0; j < ds; ++j)
-                            cb.centroids[i][(size_t)c * ds + j] =
-                                (float)(sums[((size_t)i * k + c) * ds + j] / cnt[i * k + c]);
+        int trc = pq_train(&cb, x, n, d, iters);   /* GPU Lloyd, fixed-point means */
+        if (trc) {
+            fprintf(stderr, "pq_train failed: %d\n", trc);
+            return 1;
         }
-        free(sums);
-        free(cnt);
     }
     int rc = pq_encode(&cb, x, n, d, codes);
     if (rc) {

@@ -114,3 +114,66 @@ def test_error_and_reconstruct(gpu, oracle):
     c = g["centroids"]
     ref = np.concatenate([c[i][g["codes"][:, i]] for i in range(8)], axis=1)
     assert np.array_equal(rec, ref)
+
+
+def _init_from_rows(x, m, k, seed):
+    rng = np.random.default_rng(seed)
+    rows = rng.choice(x.shape[0], k, replace=False)
+    ds = x.shape[1] // m
+    return np.ascontiguousarray(x[rows].reshape(k, m, ds).transpose(1, 0, 2))
+
+
+@pytest.mark.parametrize("n,d,m,k,iters", [(3000, 32, 4, 16, 5), (20000, 128, 8, 256, 3),
+                                           (4000, 96, 16, 256, 2), (2500, 64, 8, 300, 2)])
+def test_kmeans_train_vs_oracle(gpu, oracle, n, d, m, k, iters):
+    """GPU Lloyd (fixed-point sums) equals the oracle's sequential restatement bit for bit."""
+    torch, codec, ctx = gpu
+    x = datagen.sift_like(n, d, seed=3) if d == 128 else \
+        np.random.default_rng(4).normal(0, 1, (n, d)).astype(np.float32)
+    init = _init_from_rows(x, m, k, 7)
+    got = codec.kmeans_train(ctx, torch.from_numpy(x).cuda(), init, iters)
+    want = oracle.kmeans(x, init, iters, threads=0)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+def test_kmeans_train_reduces_error(gpu, oracle):
+    torch, codec, ctx = gpu
+    x = datagen.sift_like(20000, 128, seed=9)
+    init = _init_from_rows(x, 8, 256, 1)
+    xd = torch.from_numpy(x).cuda()
+    errs = []
+    for it in (0, 1, 4):
+        c = codec.kmeans_train(ctx, xd, init, it)
+        codes, _ = oracle.pq_assign(x, c, threads=0)
+        errs.append(oracle.compute_error(x, c, codes))
+    assert errs[0] > errs[1] > errs[2]
+
+
+def test_cli_pq_encoder_trains_on_gpu(gpu, oracle, tmp_path):
+    """pq_encoder without --centroids: seeded row init (the CLI's xorshift sampler), GPU
+    training, then GPU assignment -- equal to the oracle's training from the same init."""
+    import os
+    import subprocess
+    from conftest import ROOT
+    x = datagen.sift_like(5000, 128, seed=2)
+    datagen.write_fvecs(str(tmp_path / "x.fvecs"), x)
+    bind = os.path.join(ROOT, "pq_huffman_amd", "bin")
+    subprocess.run([os.path.join(bind, "pq_encoder"), str(tmp_path / "x.fvecs"),
+                    str(tmp_path) + "/", "8", "--kmeans-iterations", "3"], check=True,
+                   capture_output=True, timeout=300)
+    state = 0x9E3779B97F4A7C15
+    mask = (1 << 64) - 1
+    rows = []
+    for _ in range(256):                       # tools/pq_encoder.c rng_next
+        state ^= (state << 13) & mask
+        state ^= state >> 7
+        state ^= (state << 17) & mask
+        rows.append(state % 5000)
+    init = np.ascontiguousarray(x[rows].reshape(256, 8, 16).transpose(1, 0, 2))
+    want = oracle.kmeans(x, init, 3, threads=0)
+    raw = (tmp_path / "pq_centroids.fvecsl").read_bytes()
+    got = np.frombuffer(raw[8:], np.float32).reshape(8, 256, 16)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    codes_raw = (tmp_path / "pq_indices.bvecsl").read_bytes()
+    want_codes, _ = oracle.pq_assign(x, want, threads=0)
+    assert np.array_equal(np.frombuffer(codes_raw[8:], np.uint8).reshape(5000, 8), want_codes)
