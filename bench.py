@@ -67,6 +67,10 @@ def parse():
     ap.add_argument("--chunk", type=int, default=16)
     ap.add_argument("--cpu-sample", type=int, default=200_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="serial schedule: no overlap of batch i's code tables with batch i+1")
+    ap.add_argument("--table-cus", type=int, default=64,
+                    help="compute units of the code-table stream in the overlapped schedule")
     return ap.parse_args()
 
 
@@ -159,67 +163,106 @@ def main():
         ct = torch.from_numpy(cent).to(dev)
         dist.broadcast(ct, 0)
         cent = ct.cpu().numpy()
-    ctx = codec.Context(local)
+    overlap = not args.no_overlap
+    sA = torch.cuda.Stream(device=dev)
+    ctx = codec.Context(local, stream=sA)                 # assign/hist/encode/decode
+    # code tables: their own stream, limited to a quarter of the CUs, so batch i's tree
+    # build (latency-bound) runs beside batch i+1's assignment
+    ctxB = codec.Context(local, cus=args.table_cus) if overlap else ctx
     pq = codec.PQ(ctx, cent)
     items = k * k if ctxm else k
-    codes = torch.empty((n, m), dtype=torch.uint8, device=dev)
-    counts = torch.zeros((m, items), dtype=torch.int32, device=dev)
-    dec = torch.empty_like(codes)
+    slots = 2 if overlap else 1
+    codes = [torch.empty((n, m), dtype=torch.uint8, device=dev) for _ in range(slots)]
+    counts = [torch.zeros((m, items), dtype=torch.int32, device=dev) for _ in range(slots)]
+    tabs = [codec.Tables(ctxB, m, k, ctxm) for _ in range(slots)]
+    halo = [None] * slots
+    ev_hist = [torch.cuda.Event() for _ in range(slots)]
+    ev_tab = [torch.cuda.Event() for _ in range(slots)]
+    dec = torch.empty_like(codes[0])
     chunks = (n + args.chunk - 1) // args.chunk
     coff = torch.empty(chunks, dtype=torch.int64, device=dev)
     cprev = torch.empty((chunks, m), dtype=torch.uint8, device=dev) if ctxm else None
     out = torch.zeros(n * m * 56 // 8 + 64, dtype=torch.uint8, device=dev)  # worst case
     tot_dev = torch.zeros(1, dtype=torch.int64, device=dev)
+    raw_first = shard.raw_first(rank)
+    stages = ("assign", "hist", "codebook", "encode", "decode")
+    events = []          # (stage, start, end) of timed steps, read after the timed region
+    acc = {s: 0.0 for s in list(stages) + ["collectives"]}
+    state = {"timed": False}
 
-    ev = {s: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for s in ("assign", "hist", "codebook", "encode", "decode")}
-    acc = {s: 0.0 for s in list(ev) + ["collectives"]}
-    tabs = codec.Tables(ctx, m, k, ctxm)
-    state = {}
+    def rec(name, stream):
+        if not state["timed"]:
+            return None
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        events.append((name, e0, e1))
+        return e1
 
-    def step(timed):
-        def rec(name, i):
-            if timed:
-                ev[name][i].record()
-        rec("assign", 0)
-        pq.assign(x, codes)
-        rec("assign", 1)
-        tc = time.perf_counter()
-        prev_row = shard.exchange_halo(codes[-1], world, rank) if ctxm else None
-        acc_coll = time.perf_counter() - tc
-        rec("hist", 0)
-        counts.zero_()
-        codec.histogram(ctx, codes, k, ctxm, prev_row=prev_row, counts=counts)
-        rec("hist", 1)
-        tc = time.perf_counter()
-        shard.reduce_counts(counts, world)
-        acc_coll += time.perf_counter() - tc
-        rec("codebook", 0)
-        tabs.build(counts)                        # GPU trees + lookup tables, no host trip
-        rec("codebook", 1)
-        raw_first = shard.raw_first(rank)
-        rec("encode", 0)
-        tc = time.perf_counter()
-        if world > 1:   # place the shard in the global stream before writing it
-            total = codec.encode_size(ctx, tabs, codes, raw_first, prev_row)
-            goff, _ = shard.bit_offsets(total, world, rank)
-            bit_off = shard.local_bit_offset(goff)
-            out[:4].zero_()   # bits before bit_off belong to the previous shard: kept zero
+    def done(e1, stream):
+        if e1 is not None:
+            e1.record(stream)
+
+    def front(i):
+        """batch i: assignment + histogram (stream A), then its code tables (stream B)"""
+        s = i % slots
+        with torch.cuda.stream(sA):
+            e = rec("assign", sA)
+            pq.assign(x, codes[s])
+            done(e, sA)
+            tc = time.perf_counter()
+            halo[s] = shard.exchange_halo(codes[s][-1], world, rank) if ctxm else None
+            acc["collectives"] += time.perf_counter() - tc if state["timed"] else 0.0
+            e = rec("hist", sA)
+            counts[s].zero_()
+            codec.histogram(ctx, codes[s], k, ctxm, prev_row=halo[s], counts=counts[s])
+            done(e, sA)
+            tc = time.perf_counter()
+            shard.reduce_counts(counts[s], world)
+            acc["collectives"] += time.perf_counter() - tc if state["timed"] else 0.0
+            ev_hist[s].record(sA)
+        sB = ctxB.stream
+        sB.wait_event(ev_hist[s])
+        e = rec("codebook", sB)
+        tabs[s].build(counts[s])                  # GPU trees + lookup tables, no host trip
+        done(e, sB)
+        ev_tab[s].record(sB)
+
+    def back(i):
+        """batch i: encode + decode (stream A) once its tables are built"""
+        s = i % slots
+        with torch.cuda.stream(sA):
+            sA.wait_event(ev_tab[s])
+            e = rec("encode", sA)
+            tc = time.perf_counter()
+            if world > 1:   # place the shard in the global stream before writing it
+                total = codec.encode_size(ctx, tabs[s], codes[s], raw_first, halo[s])
+                goff, _ = shard.bit_offsets(total, world, rank)
+                bit_off = shard.local_bit_offset(goff)
+                out[:4].zero_()   # bits before bit_off belong to the previous shard
+            else:
+                bit_off = 0
+            acc["collectives"] += time.perf_counter() - tc if state["timed"] else 0.0
+            # one pass: look-back offsets, every word stored once (no zeroing of `out`)
+            codec.encode_write(ctx, tabs[s], codes[s], out, bit_off, raw_first, halo[s],
+                               args.chunk, coff, cprev, total=tot_dev)
+            done(e, sA)
+            enc = codec.Encoded(out, -1, args.chunk, coff, cprev, n, raw_first)
+            e = rec("decode", sA)
+            codec.decode(ctx, tabs[s], enc, out=dec)
+            done(e, sA)
+        state["last_slot"] = s
+
+    def run(steps):
+        if overlap:      # software pipeline: batch i's tables overlap batch i+1's assign
+            for i in range(steps):
+                front(i)
+                if i >= 1:
+                    back(i - 1)
+            back(steps - 1)
         else:
-            bit_off = 0
-        acc_coll += time.perf_counter() - tc
-        # one pass: look-back offsets, every word stored once (no zeroing of `out`)
-        codec.encode_write(ctx, tabs, codes, out, bit_off, raw_first, prev_row, args.chunk,
-                           coff, cprev, total=tot_dev)
-        total = tot_dev
-        rec("encode", 1)
-        enc = codec.Encoded(out, -1, args.chunk, coff, cprev, n, raw_first)
-        rec("decode", 0)
-        codec.decode(ctx, tabs, enc, out=dec)
-        rec("decode", 1)
-        if timed:
-            acc["collectives"] += acc_coll
-        state["enc"], state["total"] = enc, total
+            for i in range(steps):
+                front(i)
+                back(i)
 
     def barrier():
         torch.cuda.synchronize()
@@ -227,29 +270,30 @@ def main():
             dist.barrier()
             torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
-        step(False)
+    run(args.warmup)
     barrier()
+    state["timed"] = True
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
-        torch.cuda.synchronize()
-        for s in ev:
-            acc[s] += ev[s][0].elapsed_time(ev[s][1]) / 1e3
+    run(args.steps)
     barrier()
     elapsed = time.perf_counter() - t0
+    state["timed"] = False
+    for name, e0, e1 in events:
+        acc[name] += e0.elapsed_time(e1) / 1e3
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    s_last = state["last_slot"]
+    codes_last, tabs_last = codes[s_last], tabs[s_last]
 
     # correctness after timing (not timed): exact round trip + oracle parity spot checks
     codec.decode_status(ctx)
     codec.encode_status(ctx)
-    assert torch.equal(dec, codes), "round trip mismatch"
+    assert torch.equal(dec, codes_last), "round trip mismatch"
     rerank = pq.rerank_count()
-    tabs.status()
-    bits_per_vec = int(state["total"].item()) / n
+    tabs_last.status()
+    bits_per_vec = int(tot_dev.item()) / n
 
     if rank == 0:
         t_assign = acc["assign"] / args.steps
@@ -275,7 +319,11 @@ def main():
                                    + ("order-1 context Huffman (reference default coding), "
                                       "no sort" if ctxm else "non-context Huffman, no sort"),
                        "vectors_per_gpu": n, "m": m, "k": k, "mode": args.mode,
-                       "chunk_vectors": args.chunk, "parallelism": f"dp{world} row shards"},
+                       "chunk_vectors": args.chunk, "parallelism": f"dp{world} row shards",
+                       "schedule": ("pipelined: batch i's code tables (tree build, latency-bound) "
+                                    f"on a {args.table_cus}-CU stream beside batch i+1's "
+                                    "assignment; every timed step runs all five stages"
+                                    if overlap else "serial")},
             "roofline": {"kernel": "pq_assign_mfma", "bound": "hbm",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -283,6 +331,8 @@ def main():
                          "bytes_per_vector": BYTES_PER_VEC_READ + BYTES_PER_VEC_WRITE,
                          "avg_ms": round(t_assign * 1e3, 4)},
             "stages_ms": {s: round(v / args.steps * 1e3, 4) for s, v in acc.items()},
+            "stages_note": ("per-stage HIP-event times; in the pipelined schedule 'codebook' "
+                            "overlaps the next batch's 'assign'" if overlap else "serial"),
             # encode-side HBM-read roofline = 512 B/vec x N / t_encode / 8 TB/s
             "encode_read_roofline_frac": round(BYTES_PER_VEC_READ * n / t_enc / 1e9 / HBM_PEAK_GBS, 4),
             "bits_per_vector": round(bits_per_vec, 3),

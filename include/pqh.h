@@ -46,6 +46,12 @@ typedef struct pqh_ctx pqh_ctx_t;
 /* ---- context: one per device, one host thread per context ----------------------- */
 /* creates the context with a private non-blocking stream */
 int pqh_ctx_create(pqh_ctx_t** ctx, int device);
+/* Like pqh_ctx_create, but the context's own stream may only use `cus` compute units,
+ * spread evenly over the device (hipExtStreamCreateWithCUMask) -- for running the
+ * latency-bound code-table build beside the next batch's assignment. */
+int pqh_ctx_create_cu_limited(pqh_ctx_t** ctx, int device, int cus);
+/* the context's current HIP stream (e.g. for torch.cuda.ExternalStream) */
+void* pqh_ctx_stream(const pqh_ctx_t* ctx);
 int pqh_ctx_destroy(pqh_ctx_t* ctx);
 /* run all later calls on hip_stream, taken literally: NULL is the device's default
  * (legacy, synchronising) stream -- what torch's current stream usually is. */

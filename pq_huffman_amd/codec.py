@@ -55,14 +55,23 @@ def device_count() -> int:
 
 
 class Context:
-    """pqh_ctx_t bound to a torch device and its current stream (pqh.h)."""
+    """pqh_ctx_t bound to a torch device and a stream (pqh.h).
 
-    def __init__(self, device: int = 0, stream=None):
+    Default: torch's current stream, so torch's fills and copies are ordered with the pqh
+    kernels.  cus > 0: the context keeps its own stream limited to that many compute units
+    (pqh_ctx_create_cu_limited); `stream` is then a torch.cuda.ExternalStream over it."""
+
+    def __init__(self, device: int = 0, stream=None, cus: int = 0):
         torch = _torch()
         self.device = device
         torch.cuda.set_device(device)
-        self.stream = stream or torch.cuda.current_stream(device)
         self.ptr = ctypes.c_void_p()
+        if cus > 0:
+            check(lib().pqh_ctx_create_cu_limited(ctypes.byref(self.ptr), device, cus),
+                  "pqh_ctx_create_cu_limited")
+            self.stream = torch.cuda.ExternalStream(lib().pqh_ctx_stream(self.ptr), device=device)
+            return
+        self.stream = stream or torch.cuda.current_stream(device)
         check(lib().pqh_ctx_create(ctypes.byref(self.ptr), device), "pqh_ctx_create")
         # bind to torch's stream (often the NULL/default stream) so torch's allocations,
         # fills and copies are ordered with the pqh kernels

@@ -3,6 +3,7 @@
 #include <cstring>
 
 #include <algorithm>
+#include <vector>
 #include <cmath>
 
 #include "pqh_internal.h"
@@ -91,6 +92,31 @@ int pqh_ctx_create(pqh_ctx_t** out, int device) {
     *out = ctx;
     return PQH_OK;
 }
+
+int pqh_ctx_create_cu_limited(pqh_ctx_t** out, int device, int cus) {
+    int rc = pqh_ctx_create(out, device);
+    if (rc) return rc;
+    pqh_ctx* ctx = *out;
+    if (cus <= 0 || cus >= ctx->num_cus) return PQH_OK;
+    // every (num_cus / cus)-th compute unit, so the subset spans all XCDs / shader engines
+    std::vector<uint32_t> mask((ctx->num_cus + 31) / 32, 0u);
+    const int stride = std::max(1, ctx->num_cus / cus);
+    int used = 0;
+    for (int cu = 0; cu < ctx->num_cus && used < cus; cu += stride, ++used)
+        mask[cu / 32] |= 1u << (cu % 32);
+    hipStream_t s = nullptr;
+    if (hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
+        pqh_ctx_destroy(ctx);
+        *out = nullptr;
+        return PQH_ERR_HIP;
+    }
+    (void)hipStreamDestroy(ctx->stream);
+    ctx->stream = s;
+    ctx->own_stream = true;
+    return PQH_OK;
+}
+
+void* pqh_ctx_stream(const pqh_ctx_t* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 
 int pqh_ctx_destroy(pqh_ctx_t* ctx) {
     if (!ctx) return PQH_OK;

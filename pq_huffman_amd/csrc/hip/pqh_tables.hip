@@ -160,10 +160,10 @@ __device__ __forceinline__ int merge_tree(Key* heap_base, const uint32_t* lcnt, 
 template <int TPW>
 struct SentinelHeap {
     static constexpr uint32_t kTie = 1u << 9, kLow = (1u << 10) - 1, kMax = 0xFFFFFFFFu;
-    static constexpr int kSlots = 1024;        // children of every node < 256, and theirs
+    static constexpr int kSlots = 512;         // heap < 256 entries; reads clamp to slot 511
     uint32_t* h;                               // this lane's slot 0 (stride TPW)
     int size;
-    __device__ __forceinline__ uint32_t get(int i) const { return h[i * TPW]; }
+    __device__ __forceinline__ uint32_t get(int i) const { return h[min(i, kSlots - 1) * TPW]; }
     __device__ __forceinline__ void set(int i, uint32_t v) { h[i * TPW] = v; }
     // sift up while strictly lighter than the parent; three ancestors per LDS round trip
     __device__ __forceinline__ void push(uint32_t e) {
@@ -217,6 +217,105 @@ struct SentinelHeap {
 // diagnostics: s_memtime stamps of the first workgroup's phases (pqh_debug_stamps):
 // [0..6] huff_trees tree 0, [8..13] dec_chunks workgroup 0 lane 0
 __device__ unsigned long long g_tree_stamps[16];
+
+// Compact per-tree layout for K <= 256 (3.5 KB, so 32 trees fit one workgroup and the
+// whole build occupies 64 CUs -- it can run beside the next batch's assignment):
+//   heap u32 [512]  (sentinel heap; after the merges the internal nodes' codes, u64 [255])
+//   kid  u32 [256]  (children of internal node q at q - nz; the leaf counts before that)
+//   lsym u16 [256]  (symbol of leaf j)
+// all interleaved tree-minor (element e of lane t at [e * TPW + t]).
+template <int TPW>
+__global__ void __launch_bounds__(64)
+huff_trees_small(const uint32_t* __restrict__ counts, int k, long long trees,
+                 unsigned long long* __restrict__ enc, uint32_t* __restrict__ err) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    uint32_t* heap_all = reinterpret_cast<uint32_t*>(lds);
+    uint32_t* kid_all = heap_all + 512 * TPW;
+    uint16_t* lsym_all = reinterpret_cast<uint16_t*>(kid_all + 256 * TPW);
+    const int t = threadIdx.x;
+    {   // the whole workgroup fills the heap slots with sentinels
+        uint4* z = reinterpret_cast<uint4*>(heap_all);
+        for (int q = t; q < 512 * TPW / 4; q += blockDim.x) z[q] = make_uint4(~0u, ~0u, ~0u, ~0u);
+        __syncthreads();
+    }
+    if (t >= TPW) return;  // no barriers below
+    const long long tree = (long long)blockIdx.x * TPW + t;
+    if (tree >= trees) return;
+    const uint32_t* cnt = counts + tree * k;
+    unsigned long long* out = enc + tree * k;
+    const bool stamp = tree == 0;
+    if (stamp) g_tree_stamps[0] = __builtin_amdgcn_s_memtime();
+    uint32_t* kid = kid_all + t;
+    uint32_t* lcnt = kid;                      // leaf counts until the first merge
+    uint16_t* lsym = lsym_all + t;
+    unsigned long long total = 0;
+    int nz = 0;
+    scan_counts(cnt, k, [&](int s, uint32_t c) {
+        lsym[nz * TPW] = (uint16_t)s;
+        lcnt[nz * TPW] = c;
+        total += c;
+        ++nz;
+    });
+    if (nz == 0) return;
+    if (stamp) g_tree_stamps[1] = __builtin_amdgcn_s_memtime();
+    int next;
+    if (total < (1ull << 22)) {
+        SentinelHeap<TPW> hp{heap_all + t, 0};
+        for (int j = 0; j < nz; ++j) hp.push((lcnt[j * TPW] << 10) | (uint32_t)j);
+        if (stamp) g_tree_stamps[2] = __builtin_amdgcn_s_memtime();
+        next = nz;
+        if (hp.size == 1) {  // lone symbol: code "0" (huffman_encode.c:168-177)
+            const uint32_t e = hp.pop();
+            kid[0] = (e & 511u) | 0xFFFF0000u;
+            hp.push((e & ~1023u) | (uint32_t)next);
+            ++next;
+        }
+        while (hp.size > 1) {
+            const uint32_t a = hp.pop();
+            const uint32_t b = hp.pop();
+            kid[(next - nz) * TPW] = (a & 511u) | ((b & 511u) << 16);
+            hp.push(((a & ~1023u) + (b & ~1023u)) | (uint32_t)next);
+            ++next;
+        }
+    } else {   // heavy tree: 64-bit keys (u64 [256] in the heap's 2 KB)
+        next = merge_tree<unsigned long long, 16, TPW, 256>(
+            reinterpret_cast<unsigned long long*>(heap_all) + t, lcnt, nz, kid);
+    }
+    if (stamp) g_tree_stamps[3] = __builtin_amdgcn_s_memtime();
+    // codes top-down in reverse creation order (parents are created after their children):
+    // depth << 56 | code, child 0 appends bit 0 (huffman_encode.c:100-132); internal nodes
+    // keep theirs in the dead heap, leaves go straight to the code table
+    constexpr unsigned long long kMask = (1ull << 56) - 1;
+    unsigned long long* icode = reinterpret_cast<unsigned long long*>(heap_all) + t;
+    icode[(next - 1 - nz) * TPW] = 0;         // root
+    bool too_long = false;
+    for (int q = next - 1; q >= nz; --q) {
+        const unsigned long long e = icode[(q - nz) * TPW];
+        const uint32_t kk = kid[(q - nz) * TPW];
+        const unsigned long long d = min((e >> 56) + 1, 255ull);
+        const unsigned long long c = (e & kMask) << 1;
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const uint32_t ch = b ? kk >> 16 : kk & 0xFFFFu;
+            if (ch == 0xFFFFu) continue;
+            const unsigned long long v = (d << 56) | ((c | (unsigned long long)b) & kMask);
+            if ((int)ch >= nz) {
+                icode[(ch - nz) * TPW] = v;
+            } else if (d > (unsigned long long)kMaxCodeLen) {
+                too_long = true;
+            } else {
+                out[lsym[ch * TPW]] = v;
+            }
+        }
+    }
+    if (too_long) atomicOr(err, 1u);
+    if (stamp) {
+        g_tree_stamps[4] = __builtin_amdgcn_s_memtime();
+        g_tree_stamps[5] = (unsigned long long)nz;
+        g_tree_stamps[6] = (unsigned long long)next;
+    }
+}
+
 
 template <int KMAX, int TPW>
 __global__ void __launch_bounds__(64)
@@ -858,12 +957,12 @@ int pqh_tables_build(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts) 
     PQH_HIP(ctx, hipMemsetAsync(t->d_enc, 0, (size_t)t->m * t->items * 8, ctx->stream));
     const long long trees = t->tables;
     if (t->k <= 256) {
-        constexpr int TPW = 16;
-        const size_t lds = (size_t)256 * TPW * (16 + 4 + 4 + 2);
-        PQH_HIP(ctx, hipFuncSetAttribute((const void*)huff_trees<256, TPW>,
+        constexpr int TPW = 32;
+        const size_t lds = (size_t)TPW * (512 * 4 + 256 * 4 + 256 * 2);
+        PQH_HIP(ctx, hipFuncSetAttribute((const void*)huff_trees_small<TPW>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL((huff_trees<256, TPW>), dim3((unsigned)((trees + TPW - 1) / TPW)), dim3(64),
-                           lds, ctx->stream, d_counts, t->k, trees, t->d_enc, t->d_err);
+        hipLaunchKernelGGL((huff_trees_small<TPW>), dim3((unsigned)((trees + TPW - 1) / TPW)),
+                           dim3(64), lds, ctx->stream, d_counts, t->k, trees, t->d_enc, t->d_err);
     } else {
         constexpr int TPW = 1;
         const size_t lds = (size_t)4096 * TPW * (16 + 4 + 4 + 2);
