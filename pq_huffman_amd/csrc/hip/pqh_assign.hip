@@ -90,7 +90,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
                const bf16x8* __restrict__ afrag, const float* __restrict__ cent,
                const float* __restrict__ cmax, const float* __restrict__ sqrt_cmax,
                CodeT* __restrict__ codes, uint32_t* __restrict__ counts,
-               unsigned long long* __restrict__ rerank) {
+               unsigned long long* __restrict__ rerank, uint32_t* __restrict__ sched) {
     using P = Plan<D>;
     constexpr int K = kTiles * 32;
     __shared__ uint32_t hist[kWavesPerWG][K];
@@ -140,15 +140,45 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
             for (int j = 0; j < XD; ++j) dst[j] = ok ? xp[j] : 0.0f;
         }
     };
+    // Block schedule.  sched == nullptr: static grid stride.  Otherwise a dynamic queue per
+    // subspace hands out chunks of kChunk consecutive blocks (chunk q = blocks [kChunk q,
+    // kChunk q + kChunk)): each wave starts on chunk blockIdx.x and then takes chunk
+    // gridDim.x + ticket, so waves that share their CU with other work (a concurrent stream)
+    // simply take fewer chunks.  The ticket for the next chunk is requested one chunk ahead,
+    // after the x prefetch, so neither its latency nor its place in vmcnt order stalls a load.
+    constexpr int kChunk = 2;
+    uint32_t* head = sched ? sched + m * kSchedStride : nullptr;
+    auto ticket = [&]() -> unsigned {
+        unsigned t = 0;
+        if (lane == 0)
+            t = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return t;
+    };
+    long long blk = head ? (long long)blockIdx.x * kChunk : blockIdx.x;
+    int in_chunk = 0;
+    unsigned traw = head ? ticket() : 0u;
     float xn[XD];
-    load_x(blockIdx.x, xn);
-    for (long long blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+    load_x(blk, xn);
+    while (blk < nblk) {
         const long long v = blk * 32 + r;
         const bool valid = v < n;
+        long long nb;
+        bool refill = false;
+        if (!head) {
+            nb = blk + gridDim.x;
+        } else if (in_chunk + 1 < kChunk) {
+            nb = blk + 1;
+            ++in_chunk;
+        } else {
+            nb = ((long long)gridDim.x + (unsigned)__builtin_amdgcn_readfirstlane(traw)) * kChunk;
+            in_chunk = 0;
+            refill = true;
+        }
         float xs[XD];
 #pragma unroll
         for (int j = 0; j < XD; ++j) xs[j] = xn[j];
-        load_x(blk + gridDim.x, xn);   // next block's slice in flight during this block
+        load_x(nb, xn);   // next block's slice in flight during this block
+        if (refill) traw = ticket();
 
         float X = 0.0f;
         bool lo = false;
@@ -295,6 +325,22 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         if (valid && h == 0) {
             codes[v * m_total + m] = (CodeT)code;
             if (counts) atomicAdd(&hist[wave][code], 1u);
+        }
+        blk = nb;
+    }
+    if (head && lane == 0) {
+        // the last wave to finish resets every queue for the next launch on this context
+        // (all waves' tickets have returned: each consumed its last one, or waits here)
+        (void)__builtin_amdgcn_readfirstlane(traw);
+        __builtin_amdgcn_s_waitcnt(0);
+        uint32_t* done = sched + kSchedMax * kSchedStride;
+        const unsigned waves = gridDim.x * (unsigned)m_total;
+        if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            waves - 1) {
+            for (int i = 0; i < m_total; ++i)
+                __hip_atomic_store(sched + i * kSchedStride, 0u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     if (counts) {
@@ -477,6 +523,7 @@ int launch_mfma(pqh_pq* pq, const float* x, long long n, long long ldx, CodeT* c
     const int groups = (pq->m + kWavesPerWG - 1) / kWavesPerWG;
     dim3 block(64 * kWavesPerWG);
     unsigned long long* rr = ctx->d_diag;
+    uint32_t* sched = pq->m <= kSchedMax ? ctx->d_sched : nullptr;
     // grid = the workgroups that are resident at once (persistent, grid-stride over the
     // 32-vector blocks): more would only queue behind the first wave of workgroups
 #define PQH_CASE(DD)                                                                        \
@@ -487,10 +534,10 @@ int launch_mfma(pqh_pq* pq, const float* x, long long n, long long ldx, CodeT* c
                 hipSuccess || per_cu < 1)                                                   \
             per_cu = 1;                                                                     \
         long long gx = (long long)ctx->num_cus * per_cu / groups;                           \
-        gx = std::max(1ll, std::min(gx, nblk));                                             \
+        gx = std::max(1ll, std::min(gx, sched ? (nblk + 1) / 2 : nblk));                    \
         hipLaunchKernelGGL((pq_assign_mfma<DD, CodeT>), dim3((unsigned)gx, (unsigned)groups), \
                            block, 0, ctx->stream, x, n, ldx, pq->m, pq->d_afrag, pq->d_cent, \
-                           pq->d_cmax, pq->d_sqc, codes, counts, rr);                       \
+                           pq->d_cmax, pq->d_sqc, codes, counts, rr, sched);                \
         break;                                                                              \
     }
     switch (pq->dsub) {

@@ -27,7 +27,13 @@ struct pqh_ctx {
     long long lb_cap = 0;
     unsigned lb_epoch = 0;
     unsigned long long lb_ticket_base = 0;
+    // dynamic work queues of the assignment kernel: kSchedMax per-subspace chunk heads
+    // kSchedStride bytes apart (own L2 lines) + one finish counter; every launch leaves
+    // them zero (the last wave to finish resets them)
+    uint32_t* d_sched = nullptr;
 };
+constexpr int kSchedMax = 64;
+constexpr int kSchedStride = 64;   // u32 words = 256 B
 
 int pqh_set_error(pqh_ctx* ctx, int code, const char* fmt, ...);
 int pqh_ensure_ws(pqh_ctx* ctx, size_t bytes);
