@@ -11,6 +11,8 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libpqh.so")
+# diagnostics only: an alternative in-tree build of the same library (tools/ A/B runs)
+LIB_PATH = os.environ.get("PQH_LIB", LIB_PATH)
 
 P = ctypes.c_void_p
 I = ctypes.c_int

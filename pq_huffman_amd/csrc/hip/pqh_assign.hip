@@ -37,7 +37,19 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 namespace {
 
 constexpr int kTiles = 8;        // K = 256 centroids = 8 tiles of 32 rows
-constexpr int kWavesPerWG = 8;   // subspace waves per workgroup
+#ifndef PQH_ASSIGN_WPG
+#define PQH_ASSIGN_WPG 4
+#endif
+#ifndef PQH_ASSIGN_OCC
+#define PQH_ASSIGN_OCC 4
+#endif
+#ifndef PQH_ASSIGN_DEFER
+#define PQH_ASSIGN_DEFER 1
+#endif
+#ifndef PQH_ASSIGN_PIPE
+#define PQH_ASSIGN_PIPE 0
+#endif
+constexpr int kWavesPerWG = PQH_ASSIGN_WPG;   // subspace waves per workgroup
 
 template <int D>
 struct Plan {
@@ -50,7 +62,7 @@ struct Plan {
 
 __device__ __forceinline__ unsigned med3u(unsigned a, unsigned b, unsigned c) {
     unsigned r;
-    asm volatile("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
 }
 
@@ -85,34 +97,35 @@ __device__ __forceinline__ float exact_dist(const float* x, const float* c) {
 }
 
 template <int D, typename CodeT>
-__global__ void __launch_bounds__(64 * kWavesPerWG)
+__global__ void __launch_bounds__(64 * kWavesPerWG, PQH_ASSIGN_OCC)
 pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_total,
                const bf16x8* __restrict__ afrag, const float* __restrict__ cent,
                const float* __restrict__ cmax, const float* __restrict__ sqrt_cmax,
                CodeT* __restrict__ codes, uint32_t* __restrict__ counts,
-               unsigned long long* __restrict__ rerank, uint32_t* __restrict__ sched) {
+               unsigned long long* __restrict__ rerank, uint32_t* __restrict__ sched,
+               uint32_t* __restrict__ rq, int rq_seg, uint32_t* __restrict__ rq_cnt) {
     using P = Plan<D>;
     constexpr int K = kTiles * 32;
     __shared__ uint32_t hist[kWavesPerWG][K];
+    // the subspace's A fragments, shared by the workgroup's waves (24 KB at D = 16): keeping
+    // them out of VGPRs is what lets 4 waves share each SIMD
+    __shared__ uint4 As[P::PA * kTiles * 64];
 
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int m = blockIdx.y * kWavesPerWG + wave;
-    if (m >= m_total) return;  // whole wave leaves; no workgroup barriers below
+    const int m = blockIdx.y;   // one subspace per workgroup
     const int r = lane & 31;
     const int h = lane >> 5;
-
-    if (counts) {
-        for (int i = lane; i < K; i += 64) hist[wave][i] = 0;
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(afrag) + (long long)m * P::PA * kTiles * 64;
+        for (int i = threadIdx.x; i < P::PA * kTiles * 64; i += blockDim.x) As[i] = src[i];
+        if (counts)
+            for (int i = lane; i < K; i += 64) hist[wave][i] = 0;
+        __syncthreads();   // the only workgroup barrier
     }
-
-    // resident A fragments of this subspace: PA passes x 8 tiles x 4 VGPRs
-    bf16x8 A[P::PA][kTiles];
-#pragma unroll
-    for (int p = 0; p < P::PA; ++p)
-#pragma unroll
-        for (int t = 0; t < kTiles; ++t)
-            A[p][t] = afrag[(((long long)m * P::PA + p) * kTiles + t) * 64 + lane];
+    auto lda = [&](int p, int t) -> bf16x8 {
+        return *reinterpret_cast<const bf16x8*>(&As[(p * kTiles + t) * 64 + lane]);
+    };
 
     const float cm = cmax[m];
     const float sc = sqrt_cmax[m];
@@ -125,61 +138,53 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     // half-wave selects are needed; other D: both half-waves hold all D dims.
     constexpr bool HALF = D == 16;
     constexpr int XD = HALF ? 8 : D;
+    // Branch-free loads (the row index is clamped; the block's validity is applied when
+    // the slice is used), so the prefetch stays in flight across a whole block.
     auto load_x = [&](long long b, float* dst) {
-        const long long vv = b * 32 + r;
-        const bool ok = b < nblk && vv < n;
-        const float* xp = x + (ok ? vv : 0) * ldx + (long long)m * D + (HALF ? 8 * h : 0);
+        long long vv = b * 32 + r;
+        vv = vv < n ? vv : n - 1;
+#ifdef PQH_ASSIGN_CONTIG   // diagnostic: same bytes, read as one contiguous 2 KB per wave
+        const float* xp = x + (b < nblk - 1 ? b : nblk - 2) * 32 * ldx + (long long)m * 512 + lane * 8;
+#else
+        const float* xp = x + vv * ldx + (long long)m * D + (HALF ? 8 * h : 0);
+#endif
         if constexpr (XD % 4 == 0) {
 #pragma unroll
             for (int j = 0; j < XD; j += 4) {
-                float4 q = ok ? *reinterpret_cast<const float4*>(xp + j) : make_float4(0, 0, 0, 0);
+                float4 q = *reinterpret_cast<const float4*>(xp + j);
                 dst[j] = q.x; dst[j + 1] = q.y; dst[j + 2] = q.z; dst[j + 3] = q.w;
             }
         } else {
 #pragma unroll
-            for (int j = 0; j < XD; ++j) dst[j] = ok ? xp[j] : 0.0f;
+            for (int j = 0; j < XD; ++j) dst[j] = xp[j];
         }
     };
-    // Block schedule.  sched == nullptr: static grid stride.  Otherwise a dynamic queue per
-    // subspace hands out chunks of kChunk consecutive blocks (chunk q = blocks [kChunk q,
-    // kChunk q + kChunk)): each wave starts on chunk blockIdx.x and then takes chunk
-    // gridDim.x + ticket, so waves that share their CU with other work (a concurrent stream)
-    // simply take fewer chunks.  The ticket for the next chunk is requested one chunk ahead,
-    // after the x prefetch, so neither its latency nor its place in vmcnt order stalls a load.
-    constexpr int kChunk = 2;
-    uint32_t* head = sched ? sched + m * kSchedStride : nullptr;
-    auto ticket = [&]() -> unsigned {
-        unsigned t = 0;
-        if (lane == 0)
-            t = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return t;
-    };
-    long long blk = head ? (long long)blockIdx.x * kChunk : blockIdx.x;
-    int in_chunk = 0;
-    unsigned traw = head ? ticket() : 0u;
-    float xn[XD];
-    load_x(blk, xn);
-    while (blk < nblk) {
+    // Deferred re-rank: a vector whose screening gap is too small is appended to this wave's
+    // segment of the re-rank queue (no atomics: the segment is private) and finished by
+    // pq_rerank_fix; only when the segment is full does the wave re-rank inline.
+    const unsigned seg_id = (blockIdx.y * gridDim.x + blockIdx.x) * kWavesPerWG + wave;
+    uint32_t* my_rq = rq ? rq + (long long)seg_id * rq_seg : nullptr;
+    unsigned qn = 0;
+
+    auto body = [&](long long blk, const float* xin) {
         const long long v = blk * 32 + r;
         const bool valid = v < n;
-        long long nb;
-        bool refill = false;
-        if (!head) {
-            nb = blk + gridDim.x;
-        } else if (in_chunk + 1 < kChunk) {
-            nb = blk + 1;
-            ++in_chunk;
-        } else {
-            nb = ((long long)gridDim.x + (unsigned)__builtin_amdgcn_readfirstlane(traw)) * kChunk;
-            in_chunk = 0;
-            refill = true;
-        }
         float xs[XD];
 #pragma unroll
-        for (int j = 0; j < XD; ++j) xs[j] = xn[j];
-        load_x(nb, xn);   // next block's slice in flight during this block
-        if (refill) traw = ticket();
-
+        for (int j = 0; j < XD; ++j) xs[j] = valid ? xin[j] : 0.0f;
+#ifdef PQH_ASSIGN_NOCOMPUTE   // diagnostic: the kernel's memory traffic alone
+        {
+            float q = 0.0f;
+#pragma unroll
+            for (int j = 0; j < XD; ++j) q += xs[j];
+#ifdef PQH_ASSIGN_NOSTORE
+            if (q == 1234.5f) codes[v * m_total + m] = (CodeT)(int)q;
+#else
+            if (valid && h == 0) codes[v * m_total + m] = (CodeT)(int)q;
+#endif
+            return;
+        }
+#endif
         float X = 0.0f;
         bool lo = false;
         float xh[XD], xl[XD];
@@ -244,39 +249,45 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
             f32x16 acc = {0};
 #pragma unroll
             for (int p = 0; p < P::PM; ++p)
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[p][t], Bm[p], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lda(p, t), Bm[p], acc, 0, 0, 0);
             if (any_lo) {
 #pragma unroll
                 for (int p = 0; p < P::PL; ++p) {
-                    const bf16x8 a = P::REUSE ? A[0][t] : A[P::PM + (P::REUSE ? 0 : p)][t];
+                    const bf16x8 a = P::REUSE ? lda(0, t) : lda(P::PM + (P::REUSE ? 0 : p), t);
                     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, Bl[p], acc, 0, 0, 0);
                 }
             }
             return acc;
         };
+        // Keys: float bits with the low 4 mantissa bits replaced by the accumulator register
+        // i.  One running (min, second-min) over all 128 values of the lane; values go in
+        // groups of three: the group's top two by min3/med3, then (m1, m2) <- (min(m1, g1),
+        // med3(m1, g1, min(m2, g2))).  The winner's tile is the last tile that lowered m1.
         unsigned m1 = 0xFFFFFFFFu, m2 = 0xFFFFFFFFu, mt = 0;
         f32x16 acc = tile_acc(0);
 #pragma unroll
         for (int t = 0; t < kTiles; ++t) {
             f32x16 nxt;
-            if (t + 1 < kTiles) nxt = tile_acc(t + 1);
-            unsigned k0 = (__float_as_uint(acc[0]) & ~15u);
-            unsigned k1 = (__float_as_uint(acc[1]) & ~15u) | 1u;
-            unsigned t1 = min(k0, k1), t2 = max(k0, k1);
+            if (PQH_ASSIGN_PIPE && t + 1 < kTiles) nxt = tile_acc(t + 1);
+            unsigned kk[16];
 #pragma unroll
-            for (int i = 2; i < 16; ++i) {
-                unsigned key = (__float_as_uint(acc[i]) & ~15u) | (unsigned)i;
-                t2 = med3u(t1, t2, key);
-                t1 = min(t1, key);
+            for (int i = 0; i < 16; ++i) kk[i] = (__float_as_uint(acc[i]) & ~15u) | (unsigned)i;
+            const unsigned prev = m1;
+#pragma unroll
+            for (int g = 0; g < 5; ++g) {
+                const unsigned a0 = kk[3 * g], a1 = kk[3 * g + 1], a2 = kk[3 * g + 2];
+                const unsigned g1 = min(min(a0, a1), a2);
+                const unsigned g2 = med3u(a0, a1, a2);
+                m2 = med3u(m1, g1, min(m2, g2));
+                m1 = min(m1, g1);
             }
-            unsigned nm2 = min(min(m2, t2), max(m1, t1));
-            mt = t1 < m1 ? (unsigned)t : mt;
-            m1 = min(m1, t1);
-            m2 = nm2;
-            if (t + 1 < kTiles) acc = nxt;
+            m2 = med3u(m1, m2, kk[15]);
+            m1 = min(m1, kk[15]);
+            mt = m1 != prev ? (unsigned)t : mt;
+            if (t + 1 < kTiles) acc = PQH_ASSIGN_PIPE ? nxt : tile_acc(t + 1);
         }
         // merge the two half-waves (lanes l and l^32 hold the same vector)
-        unsigned o1 = __shfl_xor(m1, 32), o2 = __shfl_xor(m2, 32), ot = __shfl_xor(mt, 32);
+        const unsigned o1 = __shfl_xor(m1, 32), o2 = __shfl_xor(m2, 32), ot = __shfl_xor(mt, 32);
         const bool other = o1 < m1;
         const unsigned w_h = other ? (unsigned)(1 - h) : (unsigned)h;
         const unsigned w_t = other ? ot : mt;
@@ -289,8 +300,18 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         const bool slow = !(gap > tau + 0x1p-15f * K2) || !finite_x;
 
         unsigned long long need = __ballot(slow && valid && h == 0);
+        bool deferred = false;
         if (need) {
             slow_count += __popcll(need);
+            const unsigned cnt = (unsigned)__popcll(need);
+            if (my_rq && qn + cnt <= (unsigned)rq_seg) {
+                if (slow && valid && h == 0)
+                    my_rq[qn + __builtin_amdgcn_mbcnt_hi((unsigned)(need >> 32),
+                                 __builtin_amdgcn_mbcnt_lo((unsigned)need, 0u))] = (uint32_t)v;
+                qn += cnt;
+                deferred = true;
+                need = 0;
+            }
             unsigned long long todo = need;
             while (todo) {
                 const int rs = __ffsll((long long)todo) - 1;
@@ -304,8 +325,8 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
                 }
                 float best = INFINITY;
                 int bidx = 0x7FFFFFFF;
-#pragma unroll
-                for (int q = 0; q < K / 64; ++q) {
+#pragma unroll 1
+                for (int q = 0; q < K / 64; ++q) {   // rare path: keep its registers few
                     const int c = lane + 64 * q;
                     float cv[D];
 #pragma unroll
@@ -322,27 +343,76 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
                 if (lane == rs) code = bidx == 0x7FFFFFFF ? 0 : bidx;
             }
         }
-        if (valid && h == 0) {
+        if (valid && h == 0 && !(deferred && slow)) {
             codes[v * m_total + m] = (CodeT)code;
             if (counts) atomicAdd(&hist[wave][code], 1u);
         }
+    };
+
+    // Block schedule, two blocks (one chunk) per step.  Wave w of the subspace (w = blockIdx.x
+    // * kWavesPerWG + wave) starts on chunk w.  sched == nullptr: static stride over chunks.
+    // Otherwise the remaining chunks are handed out by tickets, so waves that share their CU
+    // with other work (a concurrent stream) simply take fewer chunks.  The dynamic region is
+    // split into kXcds ranges with a head each; a wave drains the range of the XCD it runs on
+    // first (XCC_ID; placement only affects speed), then moves on to the next range -- one
+    // shared head per subspace saturated at a few dequeues per microsecond.  The ticket for
+    // the next chunk is requested a whole step ahead.
+    const long long wave_id = (long long)blockIdx.x * kWavesPerWG + wave;   // within subspace
+    const long long waves_m = (long long)gridDim.x * kWavesPerWG;
+    const long long nchunk = (nblk + 1) / 2;
+    const long long R = nchunk > waves_m ? (nchunk - waves_m + kXcds - 1) / kXcds : 0;
+    uint32_t* head = sched ? sched + (long long)m * kXcds * kSchedStride : nullptr;
+    int xr = head ? (int)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & (kXcds - 1)) : 0;
+    int tries = head && R > 0 ? 0 : kXcds;
+    auto ticket = [&]() -> unsigned {
+        unsigned t = __builtin_nondeterministic_value(0u);   // lane 0 only: no select,
+                                                             // so no wait at the join
+        if (lane == 0)
+            t = __hip_atomic_fetch_add(head + xr * kSchedStride, 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+        return t;
+    };
+    unsigned traw = 0;
+    if (tries < kXcds) traw = ticket();
+    auto next_dyn = [&]() -> long long {   // the next dynamic chunk, -1 once all are taken
+        while (tries < kXcds) {
+            const long long t = (unsigned)__builtin_amdgcn_readfirstlane(traw);
+            const long long lo = waves_m + xr * R;
+            if (t < std::min(R, nchunk - lo)) {
+                traw = ticket();           // prefetch the one after
+                return lo + t;
+            }
+            if (++tries < kXcds) {         // this range is empty: the next XCD's
+                xr = (xr + 1) & (kXcds - 1);
+                traw = ticket();
+            }
+        }
+        return -1;
+    };
+    long long blk = 2ll * wave_id;
+    float xn[XD];
+    load_x(blk, xn);
+    while (blk < nblk) {
+        float xa[XD];
+#pragma unroll
+        for (int j = 0; j < XD; ++j) xa[j] = xn[j];
+        load_x(blk + 1, xn);   // the chunk's second block in flight during the first
+        body(blk, xa);
+        if (blk + 1 >= nblk) break;
+        long long nb;
+        if (!head) {
+            nb = blk + 2ll * waves_m;
+        } else {
+            const long long c = next_dyn();
+            nb = c < 0 ? nblk : 2ll * c;
+        }
+#pragma unroll
+        for (int j = 0; j < XD; ++j) xa[j] = xn[j];
+        load_x(nb, xn);        // the next chunk's first block in flight during the second
+        body(blk + 1, xa);
         blk = nb;
     }
-    if (head && lane == 0) {
-        // the last wave to finish resets every queue for the next launch on this context
-        // (all waves' tickets have returned: each consumed its last one, or waits here)
-        (void)__builtin_amdgcn_readfirstlane(traw);
-        __builtin_amdgcn_s_waitcnt(0);
-        uint32_t* done = sched + kSchedMax * kSchedStride;
-        const unsigned waves = gridDim.x * (unsigned)m_total;
-        if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-            waves - 1) {
-            for (int i = 0; i < m_total; ++i)
-                __hip_atomic_store(sched + i * kSchedStride, 0u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
+    if (rq && lane == 0) rq_cnt[seg_id] = qn;
     if (counts) {
         __builtin_amdgcn_wave_barrier();
         for (int i = lane; i < K; i += 64) {
@@ -351,6 +421,59 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         }
     }
     if (lane == 0 && slow_count) atomicAdd(rerank, slow_count);
+}
+
+// Deferred re-rank (pq_assign_mfma's queue): segment s belongs to wave s of the assignment
+// grid (subspace m = its workgroup row * kWavesPerWG + its wave); `split` waves share a
+// segment.  Each vector is re-ranked exactly as the inline path does it -- fp32 direct form,
+// lane c + 64 q, strict <, then the (distance, index) butterfly -- so the code is identical.
+template <int D, typename CodeT>
+__global__ void __launch_bounds__(256)
+pq_rerank_fix(const float* __restrict__ x, long long ldx, int m_total,
+              const float* __restrict__ cent, const uint32_t* __restrict__ rq, int rq_seg,
+              const uint32_t* __restrict__ rq_cnt, unsigned segs, unsigned gx, int split,
+              CodeT* __restrict__ codes, uint32_t* __restrict__ counts) {
+    constexpr int K = kTiles * 32;
+    const int lane = threadIdx.x & 63;
+    const unsigned gw = (unsigned)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const unsigned s = gw / (unsigned)split;
+    const int part = (int)(gw % (unsigned)split);
+    if (s >= segs) return;
+    const int m = (int)(s / (gx * kWavesPerWG));
+    if (m >= m_total) return;
+    const unsigned cnt = rq_cnt[s];
+    if ((unsigned)part >= cnt) return;
+    const float* cbase = cent + (long long)m * K * D;
+    float cv[K / 64][D];
+#pragma unroll
+    for (int q = 0; q < K / 64; ++q)
+#pragma unroll
+        for (int j = 0; j < D; ++j) cv[q][j] = cbase[(long long)(lane + 64 * q) * D + j];
+    for (unsigned e = (unsigned)part; e < cnt; e += (unsigned)split) {
+        const long long v = (long long)__builtin_amdgcn_readfirstlane(rq[(long long)s * rq_seg + e]);
+        const float* xp = x + v * ldx + (long long)m * D;
+        float xv[D];
+#pragma unroll
+        for (int j = 0; j < D; ++j) xv[j] = xp[j];
+        float best = INFINITY;
+        int bidx = 0x7FFFFFFF;
+#pragma unroll
+        for (int q = 0; q < K / 64; ++q) {
+            const float dd = exact_dist<D>(xv, cv[q]);
+            if (dd < best) { best = dd; bidx = lane + 64 * q; }
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const float ob = __shfl_xor(best, off);
+            const int oi = __shfl_xor(bidx, off);
+            if (ob < best || (ob == best && oi < bidx)) { best = ob; bidx = oi; }
+        }
+        if (lane == 0) {
+            const int code = bidx == 0x7FFFFFFF ? 0 : bidx;
+            codes[v * m_total + m] = (CodeT)code;
+            if (counts) atomicAdd(&counts[(long long)m * K + code], 1u);
+        }
+    }
 }
 
 // Exact VALU kernel: one thread per (vector, part); any K, any dsub.  Used for shapes the
@@ -520,10 +643,29 @@ int launch_mfma(pqh_pq* pq, const float* x, long long n, long long ldx, CodeT* c
                 uint32_t* counts) {
     pqh_ctx* ctx = pq->ctx;
     const long long nblk = (n + 31) / 32;
-    const int groups = (pq->m + kWavesPerWG - 1) / kWavesPerWG;
+    const int groups = pq->m;   // grid y: one subspace per workgroup
     dim3 block(64 * kWavesPerWG);
     unsigned long long* rr = ctx->d_diag;
+#ifdef PQH_ASSIGN_STATIC   // diagnostic: static chunk stride, no work queues
+    uint32_t* sched = nullptr;
+#else
     uint32_t* sched = pq->m <= kSchedMax ? ctx->d_sched : nullptr;
+#endif
+    // re-rank queue: one segment of kRqSeg entries per wave of the grid (sized below)
+    constexpr int kRqSeg = 1024;
+    auto rq_ensure = [&](long long segs) -> int {
+        if (segs <= ctx->rq_segs) return PQH_OK;
+        if (ctx->d_rq) PQH_HIP(ctx, hipFree(ctx->d_rq));
+        if (ctx->d_rq_cnt) PQH_HIP(ctx, hipFree(ctx->d_rq_cnt));
+        ctx->d_rq = nullptr;
+        ctx->d_rq_cnt = nullptr;
+        ctx->rq_segs = 0;
+        PQH_HIP(ctx, hipMalloc(&ctx->d_rq, (size_t)segs * kRqSeg * sizeof(uint32_t)));
+        PQH_HIP(ctx, hipMalloc(&ctx->d_rq_cnt, (size_t)segs * sizeof(uint32_t)));
+        ctx->rq_segs = segs;
+        return PQH_OK;
+    };
+    const bool use_rq = PQH_ASSIGN_DEFER && n <= 0xFFFFFFFFll;   // entries: u32 vector ids
     // grid = the workgroups that are resident at once (persistent, grid-stride over the
     // 32-vector blocks): more would only queue behind the first wave of workgroups
 #define PQH_CASE(DD)                                                                        \
@@ -534,10 +676,28 @@ int launch_mfma(pqh_pq* pq, const float* x, long long n, long long ldx, CodeT* c
                 hipSuccess || per_cu < 1)                                                   \
             per_cu = 1;                                                                     \
         long long gx = (long long)ctx->num_cus * per_cu / groups;                           \
-        gx = std::max(1ll, std::min(gx, sched ? (nblk + 1) / 2 : nblk));                    \
+        gx = std::max(1ll, std::min(gx, ((nblk + 1) / 2 + kWavesPerWG - 1) / kWavesPerWG)); \
+        const long long segs = gx * groups * kWavesPerWG;                                   \
+        if (use_rq) {                                                                       \
+            int rc = rq_ensure(segs);                                                       \
+            if (rc) return rc;                                                              \
+        }                                                                                   \
+        if (sched)                                                                          \
+            PQH_HIP(ctx, hipMemsetAsync(sched, 0, (size_t)pq->m * kXcds * kSchedStride * 4,  \
+                                        ctx->stream));                                      \
         hipLaunchKernelGGL((pq_assign_mfma<DD, CodeT>), dim3((unsigned)gx, (unsigned)groups), \
                            block, 0, ctx->stream, x, n, ldx, pq->m, pq->d_afrag, pq->d_cent, \
-                           pq->d_cmax, pq->d_sqc, codes, counts, rr, sched);                \
+                           pq->d_cmax, pq->d_sqc, codes, counts, rr, sched,                 \
+                           use_rq ? ctx->d_rq : nullptr, kRqSeg, ctx->d_rq_cnt);            \
+        PQH_LAUNCH_CHECK(ctx);                                                              \
+        if (use_rq) {                                                                       \
+            constexpr int kSplit = 4;                                                       \
+            const long long waves = segs * kSplit;                                          \
+            hipLaunchKernelGGL((pq_rerank_fix<DD, CodeT>), dim3((unsigned)((waves + 3) / 4)), \
+                               dim3(256), 0, ctx->stream, x, ldx, pq->m, pq->d_cent,        \
+                               ctx->d_rq, kRqSeg, ctx->d_rq_cnt, (unsigned)segs,            \
+                               (unsigned)gx, kSplit, codes, counts);                        \
+        }                                                                                   \
         break;                                                                              \
     }
     switch (pq->dsub) {

@@ -27,12 +27,16 @@ struct pqh_ctx {
     long long lb_cap = 0;
     unsigned lb_epoch = 0;
     unsigned long long lb_ticket_base = 0;
-    // dynamic work queues of the assignment kernel: kSchedMax per-subspace chunk heads
-    // kSchedStride bytes apart (own L2 lines) + one finish counter; every launch leaves
-    // them zero (the last wave to finish resets them)
+    // work-queue heads of the assignment kernel: kXcds per subspace, kSchedStride words
+    // apart, zeroed before every launch
     uint32_t* d_sched = nullptr;
+    // deferred re-rank queue of the assignment kernel: rq_segs segments (one per wave)
+    uint32_t* d_rq = nullptr;
+    uint32_t* d_rq_cnt = nullptr;
+    long long rq_segs = 0;
 };
-constexpr int kSchedMax = 64;
+constexpr int kSchedMax = 64;      // subspaces with a work queue (more: static schedule)
+constexpr int kXcds = 8;
 constexpr int kSchedStride = 64;   // u32 words = 256 B
 
 int pqh_set_error(pqh_ctx* ctx, int code, const char* fmt, ...);

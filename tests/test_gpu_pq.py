@@ -63,6 +63,24 @@ def test_assign_ties_first_index(gpu, oracle):
     assert rr > 0                             # ties must have gone to the exact re-rank
 
 
+def test_assign_rerank_queue_overflow(gpu, oracle):
+    """Every vector ties (duplicated centroids), so each wave's deferred re-rank segment
+    (1024 entries) overflows and the rest is re-ranked inline; codes and the fused
+    histogram must still match the oracle."""
+    torch, codec, ctx = gpu
+    rng = np.random.default_rng(17)
+    n = 300_000
+    x = rng.integers(0, 40, (n, 32)).astype(np.float32)
+    cent = rng.integers(0, 40, (2, 256, 16)).astype(np.float32)
+    cent[:, 128:] = cent[:, :128]
+    want, _ = oracle.pq_assign(x, cent, threads=0)
+    counts = torch.zeros((2, 256), dtype=torch.int32, device="cuda")
+    got, rr = _assign(gpu, x, cent, 0, counts)
+    assert np.array_equal(got, want), (got != want).sum()
+    assert rr >= n                            # every vector re-ranked at least in one part
+    assert np.array_equal(codec.counts_to_host(counts), oracle.histogram(got, 256, False))
+
+
 def test_assign_nonfinite_rows(gpu, oracle):
     x = datagen.sift_like(300, 128, seed=2)
     cent = datagen.lloyd_centroids(x, 8, 256, iters=1, sample=300)
