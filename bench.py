@@ -70,7 +70,11 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true",
                     help="serial schedule: no overlap of batch i's code tables with batch i+1")
     ap.add_argument("--table-cus", type=int, default=64,
-                    help="compute units of the code-table stream in the overlapped schedule")
+                    help="compute units of the code-table streams in the overlapped schedule")
+    ap.add_argument("--depth", type=int, default=2,
+                    help="overlapped schedule: batches whose code tables are in flight at "
+                         "once (one CU-limited stream each); batch i is encoded and decoded "
+                         "after batch i+depth's assignment has been queued")
     return ap.parse_args()
 
 
@@ -168,13 +172,15 @@ def main():
     ctx = codec.Context(local, stream=sA)                 # assign/hist/encode/decode
     # code tables: their own stream, limited to a quarter of the CUs, so batch i's tree
     # build (latency-bound) runs beside batch i+1's assignment
-    ctxB = codec.Context(local, cus=args.table_cus) if overlap else ctx
+    # (latency-bound: consecutive batches' builds overlap each other on `depth` streams)
+    depth = max(1, args.depth) if overlap else 0
+    ctxB = [codec.Context(local, cus=args.table_cus) for _ in range(depth)] or [ctx]
     pq = codec.PQ(ctx, cent)
     items = k * k if ctxm else k
-    slots = 2 if overlap else 1
+    slots = depth + 1
     codes = [torch.empty((n, m), dtype=torch.uint8, device=dev) for _ in range(slots)]
     counts = [torch.zeros((m, items), dtype=torch.int32, device=dev) for _ in range(slots)]
-    tabs = [codec.Tables(ctxB, m, k, ctxm) for _ in range(slots)]
+    tabs = [codec.Tables(ctx, m, k, ctxm) for _ in range(slots)]
     halo = [None] * slots
     ev_hist = [torch.cuda.Event() for _ in range(slots)]
     ev_tab = [torch.cuda.Event() for _ in range(slots)]
@@ -220,10 +226,11 @@ def main():
             shard.reduce_counts(counts[s], world)
             acc["collectives"] += time.perf_counter() - tc if state["timed"] else 0.0
             ev_hist[s].record(sA)
-        sB = ctxB.stream
+        cB = ctxB[i % len(ctxB)]
+        sB = cB.stream
         sB.wait_event(ev_hist[s])
         e = rec("codebook", sB)
-        tabs[s].build(counts[s])                  # GPU trees + lookup tables, no host trip
+        tabs[s].build(counts[s], cB)              # GPU trees + lookup tables, no host trip
         done(e, sB)
         ev_tab[s].record(sB)
 
@@ -253,12 +260,13 @@ def main():
         state["last_slot"] = s
 
     def run(steps):
-        if overlap:      # software pipeline: batch i's tables overlap batch i+1's assign
-            for i in range(steps):
+        if overlap:      # software pipeline: batch i's tables overlap the assignment of
+            for i in range(steps):          # batches i+1 .. i+depth and each other
                 front(i)
-                if i >= 1:
-                    back(i - 1)
-            back(steps - 1)
+                if i >= depth:
+                    back(i - depth)
+            for i in range(max(0, steps - depth), steps):
+                back(i)
         else:
             for i in range(steps):
                 front(i)
@@ -321,9 +329,10 @@ def main():
                        "vectors_per_gpu": n, "m": m, "k": k, "mode": args.mode,
                        "chunk_vectors": args.chunk, "parallelism": f"dp{world} row shards",
                        "schedule": ("pipelined: batch i's code tables (tree build, latency-bound) "
-                                    f"on a {args.table_cus}-CU stream beside batch i+1's "
-                                    "assignment; every timed step runs all five stages"
-                                    if overlap else "serial")},
+                                    f"on one of {depth} {args.table_cus}-CU streams beside the "
+                                    f"assignment of batches i+1..i+{depth}; every timed step "
+                                    "runs all five stages, the pipeline fills and drains inside "
+                                    "the timed region" if overlap else "serial")},
             "roofline": {"kernel": "pq_assign_mfma", "bound": "hbm",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

@@ -113,7 +113,8 @@ int pqh_tables_destroy(pqh_tables_t* tables);
 /* Build every code on the GPU from device counts (pqh_histogram layout) -- the reference
  * codebook construction (huffman_codebook_[context_]encode_init, huffman_encode.c:141-269)
  * with its exact heap tie-breaks, one lane per alphabet; asynchronous, no host round trip.
- * Codes longer than 56 bits set an error reported by pqh_tables_status. */
+ * Codes longer than 56 bits set an error reported by pqh_tables_status.  `ctx` may be any
+ * context on the tables' device; the build is ordered on ctx's stream. */
 int pqh_tables_build(pqh_ctx_t* ctx, pqh_tables_t* tables, const uint32_t* d_counts);
 /* Load codes from m host codebooks (e.g. huffman_codebooks.bin read by huffman_codebook_load). */
 int pqh_tables_upload(pqh_ctx_t* ctx, pqh_tables_t* tables, const huffman_codebook_t* codebooks);

@@ -263,9 +263,11 @@ class Tables:
             raise PqhError(st, "pqh_tables_upload: " + ctx.last_error())
         return t
 
-    def build(self, counts) -> "Tables":
-        """GPU codebook construction from device counts (async)."""
-        check(lib().pqh_tables_build(self.ctx.ptr, self.ptr, _ptr(counts)), "pqh_tables_build")
+    def build(self, counts, ctx: Context = None) -> "Tables":
+        """GPU codebook construction from device counts (async, on `ctx`'s stream: any
+        context of the same device, default the one the tables were allocated with)."""
+        c = ctx or self.ctx
+        check(lib().pqh_tables_build(c.ptr, self.ptr, _ptr(counts)), "pqh_tables_build")
         return self
 
     def status(self) -> None:

@@ -96,6 +96,113 @@ __device__ __forceinline__ float exact_dist(const float* x, const float* c) {
     return acc;
 }
 
+// diagnostics (PQH_ASSIGN_STAMPS builds only): per wave of the last pq_assign_mfma launch,
+// {s_memrealtime at start, at end, blocks done | s_memtime lifetime << 16, XCC id}
+constexpr int kStampWaves = 8192;
+__device__ unsigned long long g_assign_stamps[kStampWaves][4];
+
+// ---- screening steps shared by pq_assign_mfma and pq_rerank_window: a deferred vector is
+// re-screened by the same instruction sequence, so its scores are bitwise the same.
+template <int D>
+struct Slice {
+    static constexpr bool HALF = D == 16;   // lane (r, h) holds dims [8h, 8h + 8) of vector r
+    static constexpr int XD = HALF ? 8 : D;
+};
+
+// ||x||^2 (fp32 fma chain; HALF: plus the partner half-wave's), the bf16 split x = xh + xl
+// (+ r), and whether this lane's slice has any bf16 remainder.
+template <int D>
+__device__ __forceinline__ void split_x(const float* xs, float& X, bool& lo, float* xh, float* xl) {
+    constexpr int XD = Slice<D>::XD;
+    X = 0.0f;
+    lo = false;
+#pragma unroll
+    for (int j = 0; j < XD; ++j) {
+        X = fmaf(xs[j], xs[j], X);
+        __bf16 hb = (__bf16)xs[j];
+        xh[j] = (float)hb;
+        float rem = xs[j] - xh[j];
+        xl[j] = (float)(__bf16)rem;
+        lo |= rem != 0.0f;
+    }
+    if constexpr (Slice<D>::HALF) X += __shfl_xor(X, 32);   // the other half-wave's 8 dims
+}
+
+// error bound of the screening score (DESIGN.md "pq_assign error bound"); when no x of the
+// block has a bf16 remainder the split error is 2^-15 P instead of 2^-13 P.  Returns the
+// per-vector bias b_v (keeps every score positive) and the acceptance gap tau.
+__device__ __forceinline__ void screen_bound(float X, bool finite_x, bool any_lo, float cm,
+                                             float sc, float& bv, float& tau) {
+    const float Pm = sqrtf(X) * sc * 1.00001f;
+    const float E0 = (any_lo ? 0x1p-13f : 0x1p-15f) * Pm + 0x1p-22f * cm +
+                     0x1p-17f * (2.02f * Pm + 1.01f * cm + 1.05f * X);
+    bv = finite_x ? bf16_up(X + 3.0f * E0 + 1e-30f) : 0.0f;
+    tau = 2.2f * E0 + 1e-30f;
+}
+
+template <int D>
+__device__ __forceinline__ void build_b(const float* xh, const float* xl, float bv, int h,
+                                        bf16x8* Bm, bf16x8* Bl) {
+    using P = Plan<D>;
+    if constexpr (Slice<D>::HALF) {
+        // slots 16p + 8h + j: p = 0, 1 -> xh[8h + j]; p = 2 -> aux (h = 0) / zero (h = 1)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            Bm[0][j] = (__bf16)xh[j];
+            Bl[0][j] = (__bf16)xl[j];
+        }
+        Bm[1] = Bm[0];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            Bm[2][j] = (__bf16)(h ? 0.0f : (j < 3 ? 1.0f : (j == 3 ? bv : 0.0f)));
+    } else {
+#pragma unroll
+        for (int p = 0; p < P::PM; ++p)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                float v0 = main_slot<D>(16 * p + j, xh, bv);
+                float v1 = main_slot<D>(16 * p + 8 + j, xh, bv);
+                Bm[p][j] = (__bf16)(h ? v1 : v0);
+            }
+#pragma unroll
+        for (int p = 0; p < P::PL; ++p)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                int s0 = 16 * p + j, s1 = 16 * p + 8 + j;
+                float v0 = s0 < D ? xl[s0 < D ? s0 : 0] : 0.0f;
+                float v1 = s1 < D ? xl[s1 < D ? s1 : 0] : 0.0f;
+                Bl[p][j] = (__bf16)(h ? v1 : v0);
+            }
+    }
+}
+
+// the 32 x 32 score tile t: centroid rows 32t.. (A, from LDS) x the block's vectors (B)
+template <int D>
+__device__ __forceinline__ f32x16 tile_scores(const uint4* As, int lane, int t, const bf16x8* Bm,
+                                              const bf16x8* Bl, bool lo_pass) {
+    using P = Plan<D>;
+    auto lda = [&](int p) -> bf16x8 {
+        return *reinterpret_cast<const bf16x8*>(&As[(p * kTiles + t) * 64 + lane]);
+    };
+    f32x16 acc = {0};
+#pragma unroll
+    for (int p = 0; p < P::PM; ++p)
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lda(p), Bm[p], acc, 0, 0, 0);
+    if (lo_pass) {
+#pragma unroll
+        for (int p = 0; p < P::PL; ++p) {
+            const bf16x8 a = P::REUSE ? lda(0) : lda(P::PM + (P::REUSE ? 0 : p));
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, Bl[p], acc, 0, 0, 0);
+        }
+    }
+    return acc;
+}
+
+// centroid row of accumulator register i of tile t for half-wave h (32x32x16 output layout)
+__device__ __forceinline__ int tile_row(int t, int i, int h) {
+    return 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
+}
+
 template <int D, typename CodeT>
 __global__ void __launch_bounds__(64 * kWavesPerWG, PQH_ASSIGN_OCC)
 pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_total,
@@ -103,7 +210,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
                const float* __restrict__ cmax, const float* __restrict__ sqrt_cmax,
                CodeT* __restrict__ codes, uint32_t* __restrict__ counts,
                unsigned long long* __restrict__ rerank, uint32_t* __restrict__ sched,
-               uint32_t* __restrict__ rq, int rq_seg, uint32_t* __restrict__ rq_cnt) {
+               uint2* __restrict__ rq, int rq_seg, uint32_t* __restrict__ rq_cnt, int gx) {
     using P = Plan<D>;
     constexpr int K = kTiles * 32;
     __shared__ uint32_t hist[kWavesPerWG][K];
@@ -113,7 +220,17 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
 
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int m = blockIdx.y;   // one subspace per workgroup
+    // One subspace per workgroup, gx workgroups per subspace, 1-D grid.  Workgroup L is
+    // placed on XCD L % 8 and, within it, round robin over the CUs, so L, L + 256, L + 512 ...
+    // tend to share a CU.  The waves of a SIMD run at very different speeds (VALU issue goes
+    // to the oldest wave first); only waves of the SAME subspace can even that out through
+    // the subspace's work queue, so with gx % 8 == 0 subspace m = (L / 8) % m_total, which
+    // gives every CU's resident workgroups one subspace (speed only -- any bijection is
+    // correct).
+    const int L = blockIdx.x;
+    const bool inter = (gx & 7) == 0;
+    const int m = inter ? (L >> 3) % m_total : L / gx;
+    const int bx = inter ? (L / (8 * m_total)) * 8 + (L & 7) : L % gx;
     const int r = lane & 31;
     const int h = lane >> 5;
     {
@@ -123,10 +240,11 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
             for (int i = lane; i < K; i += 64) hist[wave][i] = 0;
         __syncthreads();   // the only workgroup barrier
     }
-    auto lda = [&](int p, int t) -> bf16x8 {
-        return *reinterpret_cast<const bf16x8*>(&As[(p * kTiles + t) * 64 + lane]);
-    };
-
+#ifdef PQH_ASSIGN_STAMPS
+    const unsigned long long st0 = __builtin_amdgcn_s_memtime();
+    const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long nbdone = 0;
+#endif
     const float cm = cmax[m];
     const float sc = sqrt_cmax[m];
     const float* cbase = cent + (long long)m * K * D;
@@ -136,8 +254,8 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     // x slice of a block.  D == 16 (SIFT): lane (r, h) holds dims [8h, 8h + 8) of vector r
     // -- exactly the B-fragment slots it feeds -- so each lane splits 8 values and no
     // half-wave selects are needed; other D: both half-waves hold all D dims.
-    constexpr bool HALF = D == 16;
-    constexpr int XD = HALF ? 8 : D;
+    constexpr bool HALF = Slice<D>::HALF;
+    constexpr int XD = Slice<D>::XD;
     // Branch-free loads (the row index is clamped; the block's validity is applied when
     // the slice is used), so the prefetch stays in flight across a whole block.
     auto load_x = [&](long long b, float* dst) {
@@ -162,8 +280,8 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     // Deferred re-rank: a vector whose screening gap is too small is appended to this wave's
     // segment of the re-rank queue (no atomics: the segment is private) and finished by
     // pq_rerank_fix; only when the segment is full does the wave re-rank inline.
-    const unsigned seg_id = (blockIdx.y * gridDim.x + blockIdx.x) * kWavesPerWG + wave;
-    uint32_t* my_rq = rq ? rq + (long long)seg_id * rq_seg : nullptr;
+    const unsigned seg_id = (unsigned)((m * gx + bx) * kWavesPerWG + wave);
+    uint2* my_rq = rq ? rq + (long long)seg_id * rq_seg : nullptr;
     unsigned qn = 0;
 
     auto body = [&](long long blk, const float* xin) {
@@ -185,80 +303,19 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
             return;
         }
 #endif
-        float X = 0.0f;
-        bool lo = false;
+        float X;
+        bool lo;
         float xh[XD], xl[XD];
-#pragma unroll
-        for (int j = 0; j < XD; ++j) {
-            X = fmaf(xs[j], xs[j], X);
-            __bf16 hb = (__bf16)xs[j];
-            xh[j] = (float)hb;
-            float rem = xs[j] - xh[j];
-            xl[j] = (float)(__bf16)rem;
-            lo |= rem != 0.0f;
-        }
-        if constexpr (HALF) X += __shfl_xor(X, 32);   // the other half-wave's 8 dims
+        split_x<D>(xs, X, lo, xh, xl);
         const bool any_lo = __any(lo);
         const bool finite_x = isfinite(X);
-
-        // error bound of the screening score (DESIGN.md "pq_assign error bound"); when no
-        // x of the block has a bf16 remainder the split error is 2^-15 P instead of 2^-13 P
-        const float Pm = sqrtf(X) * sc * 1.00001f;
-        const float E0 = (any_lo ? 0x1p-13f : 0x1p-15f) * Pm + 0x1p-22f * cm +
-                         0x1p-17f * (2.02f * Pm + 1.01f * cm + 1.05f * X);
-        const float bv = finite_x ? bf16_up(X + 3.0f * E0 + 1e-30f) : 0.0f;
-        const float tau = 2.2f * E0 + 1e-30f;
-
-        // B fragments
+        float bv, tau;
+        screen_bound(X, finite_x, any_lo, cm, sc, bv, tau);
         bf16x8 Bm[P::PM];
         bf16x8 Bl[P::PL];
-        if constexpr (HALF) {
-            // slots 16p + 8h + j: p = 0, 1 -> xh[8h + j]; p = 2 -> aux (h = 0) / zero (h = 1)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                Bm[0][j] = (__bf16)xh[j];
-                Bl[0][j] = (__bf16)xl[j];
-            }
-            Bm[1] = Bm[0];
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                Bm[2][j] = (__bf16)(h ? 0.0f : (j < 3 ? 1.0f : (j == 3 ? bv : 0.0f)));
-        } else {
-#pragma unroll
-            for (int p = 0; p < P::PM; ++p)
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    float v0 = main_slot<D>(16 * p + j, xh, bv);
-                    float v1 = main_slot<D>(16 * p + 8 + j, xh, bv);
-                    Bm[p][j] = (__bf16)(h ? v1 : v0);
-                }
-#pragma unroll
-            for (int p = 0; p < P::PL; ++p)
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    int s0 = 16 * p + j, s1 = 16 * p + 8 + j;
-                    float v0 = s0 < D ? xl[s0 < D ? s0 : 0] : 0.0f;
-                    float v1 = s1 < D ? xl[s1 < D ? s1 : 0] : 0.0f;
-                    Bl[p][j] = (__bf16)(h ? v1 : v0);
-                }
-        }
-
-        // tiles, software-pipelined: tile t + 1's MFMAs are issued before tile t's keys are
-        // reduced, so the matrix core and the VALU work side by side
-        auto tile_acc = [&](int t) {
-            f32x16 acc = {0};
-#pragma unroll
-            for (int p = 0; p < P::PM; ++p)
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lda(p, t), Bm[p], acc, 0, 0, 0);
-            if (any_lo) {
-#pragma unroll
-                for (int p = 0; p < P::PL; ++p) {
-                    const bf16x8 a = P::REUSE ? lda(0, t) : lda(P::PM + (P::REUSE ? 0 : p), t);
-                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, Bl[p], acc, 0, 0, 0);
-                }
-            }
-            return acc;
-        };
+        build_b<D>(xh, xl, bv, h, Bm, Bl);
+        // (PQH_ASSIGN_PIPE: tile t + 1's MFMAs are issued before tile t's keys are reduced)
+        auto tile_acc = [&](int t) { return tile_scores<D>(As, lane, t, Bm, Bl, any_lo); };
         // Keys: float bits with the low 4 mantissa bits replaced by the accumulator register
         // i.  One running (min, second-min) over all 128 values of the lane; values go in
         // groups of three: the group's top two by min3/med3, then (m1, m2) <- (min(m1, g1),
@@ -294,7 +351,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         const unsigned b2 = min(min(m2, o2), max(m1, o1));
         const unsigned b1 = min(m1, o1);
         const unsigned reg = b1 & 15u;
-        int code = (int)(32u * w_t + (reg & 3u) + 8u * (reg >> 2) + 4u * w_h);
+        int code = tile_row((int)w_t, (int)reg, (int)w_h);
         const float K1 = __uint_as_float(b1 & ~15u), K2 = __uint_as_float(b2 & ~15u);
         const float gap = K2 - K1;
         const bool slow = !(gap > tau + 0x1p-15f * K2) || !finite_x;
@@ -303,14 +360,21 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         bool deferred = false;
         if (need) {
             slow_count += __popcll(need);
-            const unsigned cnt = (unsigned)__popcll(need);
-            if (my_rq && qn + cnt <= (unsigned)rq_seg) {
-                if (slow && valid && h == 0)
-                    my_rq[qn + __builtin_amdgcn_mbcnt_hi((unsigned)(need >> 32),
-                                 __builtin_amdgcn_mbcnt_lo((unsigned)need, 0u))] = (uint32_t)v;
+            // finite vectors go to the queue with their candidate window: every centroid
+            // that can be the fp32 argmin (or tie with it) screens below
+            // (K1 + tau)(1 + 2^-16) -- see pq_rerank_window; non-finite ones stay inline
+            const unsigned long long fin = need & __ballot(finite_x);
+            const unsigned cnt = (unsigned)__popcll(fin);
+            if (my_rq && cnt && qn + cnt <= (unsigned)rq_seg) {
+                if (slow && valid && h == 0 && finite_x) {
+                    const float thr = (K1 + tau) * (1.0f + 0x1p-16f);
+                    my_rq[qn + __builtin_amdgcn_mbcnt_hi((unsigned)(fin >> 32),
+                                 __builtin_amdgcn_mbcnt_lo((unsigned)fin, 0u))] =
+                        make_uint2((uint32_t)v | (any_lo ? 0x80000000u : 0u), __float_as_uint(thr));
+                }
                 qn += cnt;
-                deferred = true;
-                need = 0;
+                deferred = finite_x;
+                need &= ~fin;
             }
             unsigned long long todo = need;
             while (todo) {
@@ -349,7 +413,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         }
     };
 
-    // Block schedule, two blocks (one chunk) per step.  Wave w of the subspace (w = blockIdx.x
+    // Block schedule, two blocks (one chunk) per step.  Wave w of the subspace (w = bx
     // * kWavesPerWG + wave) starts on chunk w.  sched == nullptr: static stride over chunks.
     // Otherwise the remaining chunks are handed out by tickets, so waves that share their CU
     // with other work (a concurrent stream) simply take fewer chunks.  The dynamic region is
@@ -357,8 +421,8 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     // first (XCC_ID; placement only affects speed), then moves on to the next range -- one
     // shared head per subspace saturated at a few dequeues per microsecond.  The ticket for
     // the next chunk is requested a whole step ahead.
-    const long long wave_id = (long long)blockIdx.x * kWavesPerWG + wave;   // within subspace
-    const long long waves_m = (long long)gridDim.x * kWavesPerWG;
+    const long long wave_id = (long long)bx * kWavesPerWG + wave;   // within subspace
+    const long long waves_m = (long long)gx * kWavesPerWG;
     const long long nchunk = (nblk + 1) / 2;
     const long long R = nchunk > waves_m ? (nchunk - waves_m + kXcds - 1) / kXcds : 0;
     uint32_t* head = sched ? sched + (long long)m * kXcds * kSchedStride : nullptr;
@@ -398,6 +462,9 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         for (int j = 0; j < XD; ++j) xa[j] = xn[j];
         load_x(blk + 1, xn);   // the chunk's second block in flight during the first
         body(blk, xa);
+#ifdef PQH_ASSIGN_STAMPS
+        nbdone += 2;
+#endif
         if (blk + 1 >= nblk) break;
         long long nb;
         if (!head) {
@@ -413,6 +480,17 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         blk = nb;
     }
     if (rq && lane == 0) rq_cnt[seg_id] = qn;
+#ifdef PQH_ASSIGN_STAMPS
+    {
+        const unsigned gw = seg_id;
+        if (lane == 0 && gw < (unsigned)kStampWaves) {
+            g_assign_stamps[gw][0] = rt0;   // 100 MHz, chip-wide
+            g_assign_stamps[gw][1] = __builtin_amdgcn_s_memrealtime();
+            g_assign_stamps[gw][2] = nbdone | ((__builtin_amdgcn_s_memtime() - st0) << 16);
+            g_assign_stamps[gw][3] = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 15;
+        }
+    }
+#endif
     if (counts) {
         __builtin_amdgcn_wave_barrier();
         for (int i = lane; i < K; i += 64) {
@@ -423,52 +501,149 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     if (lane == 0 && slow_count) atomicAdd(rerank, slow_count);
 }
 
-// Deferred re-rank (pq_assign_mfma's queue): segment s belongs to wave s of the assignment
-// grid (subspace m = its workgroup row * kWavesPerWG + its wave); `split` waves share a
-// segment.  Each vector is re-ranked exactly as the inline path does it -- fp32 direct form,
-// lane c + 64 q, strict <, then the (distance, index) butterfly -- so the code is identical.
+// Deferred re-rank (pq_assign_mfma's queue).  Entry = (vector | any_lo << 31, thr): the
+// vector's screening gap was too small, and thr = (K1 + tau)(1 + 2^-16) bounds the screened
+// score of every centroid whose fp32 direct-form distance can equal the minimum
+// (S_k <= D_k + b + E0 <= D_min + b + E0 <= S_k1 + 2 E0 <= K1 (1 + 2^-19) + 2 E0 < thr).
+// Vectors are re-screened 32 at a time with the main kernel's own instruction sequence
+// (bitwise the same scores; E0 with the main block's any_lo, carried in the entry), the
+// centroids screening below thr are collected per lane, and only those few are evaluated in
+// exact fp32 direct form (first index among equal distances) -- instead of all K.
+// grid (G, m): the workgroups of subspace m walk the concatenation of its waves' segments.
 template <int D, typename CodeT>
-__global__ void __launch_bounds__(256)
-pq_rerank_fix(const float* __restrict__ x, long long ldx, int m_total,
-              const float* __restrict__ cent, const uint32_t* __restrict__ rq, int rq_seg,
-              const uint32_t* __restrict__ rq_cnt, unsigned segs, unsigned gx, int split,
-              CodeT* __restrict__ codes, uint32_t* __restrict__ counts) {
+__global__ void __launch_bounds__(256, 2)
+pq_rerank_window(const float* __restrict__ x, long long ldx, int m_total,
+                 const bf16x8* __restrict__ afrag, const float* __restrict__ cent,
+                 const float* __restrict__ cmax, const float* __restrict__ sqrt_cmax,
+                 const uint2* __restrict__ rq, int rq_seg, const uint32_t* __restrict__ rq_cnt,
+                 int segs_m, CodeT* __restrict__ codes, uint32_t* __restrict__ counts) {
+    using P = Plan<D>;
     constexpr int K = kTiles * 32;
-    const int lane = threadIdx.x & 63;
-    const unsigned gw = (unsigned)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-    const unsigned s = gw / (unsigned)split;
-    const int part = (int)(gw % (unsigned)split);
-    if (s >= segs) return;
-    const int m = (int)(s / (gx * kWavesPerWG));
-    if (m >= m_total) return;
-    const unsigned cnt = rq_cnt[s];
-    if ((unsigned)part >= cnt) return;
-    const float* cbase = cent + (long long)m * K * D;
-    float cv[K / 64][D];
+    constexpr int XD = Slice<D>::XD;
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    uint4* As = reinterpret_cast<uint4*>(lds);
+    float* cl = reinterpret_cast<float*>(As + P::PA * kTiles * 64);   // [K][D]
+    uint32_t* scan = reinterpret_cast<uint32_t*>(cl + K * D);         // [segs_m + 1]
+    __shared__ uint32_t part[256];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int m = blockIdx.y, r = lane & 31, h = lane >> 5;
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(afrag) + (long long)m * P::PA * kTiles * 64;
+        for (int i = tid; i < P::PA * kTiles * 64; i += 256) As[i] = src[i];
+        const float* cb = cent + (long long)m * K * D;
+        for (int i = tid; i < K * D; i += 256) cl[i] = cb[i];
+        // exclusive scan of the subspace's segment counts: per-thread runs, then the runs
+        const uint32_t* cnt = rq_cnt + (long long)m * segs_m;
+        const int run = (segs_m + 255) / 256, b0 = tid * run;
+        uint32_t sum = 0;
+        for (int i = 0; i < run; ++i) sum += b0 + i < segs_m ? cnt[b0 + i] : 0u;
+        part[tid] = sum;
+        __syncthreads();
+        if (tid < 64) {   // wave 0: scan of the 256 run sums, 4 per lane
+            uint32_t a0 = part[4 * tid], a1 = part[4 * tid + 1], a2 = part[4 * tid + 2],
+                     a3 = part[4 * tid + 3];
+            uint32_t tot = a0 + a1 + a2 + a3, inc = tot;
 #pragma unroll
-    for (int q = 0; q < K / 64; ++q)
-#pragma unroll
-        for (int j = 0; j < D; ++j) cv[q][j] = cbase[(long long)(lane + 64 * q) * D + j];
-    for (unsigned e = (unsigned)part; e < cnt; e += (unsigned)split) {
-        const long long v = (long long)__builtin_amdgcn_readfirstlane(rq[(long long)s * rq_seg + e]);
-        const float* xp = x + v * ldx + (long long)m * D;
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t o = __shfl_up(inc, off);
+                if (lane >= off) inc += o;
+            }
+            uint32_t ex = inc - tot;
+            part[4 * tid] = ex;
+            part[4 * tid + 1] = ex + a0;
+            part[4 * tid + 2] = ex + a0 + a1;
+            part[4 * tid + 3] = ex + a0 + a1 + a2;
+        }
+        __syncthreads();
+        uint32_t acc = part[tid];
+        for (int i = 0; i < run; ++i)
+            if (b0 + i < segs_m) { scan[b0 + i] = acc; acc += cnt[b0 + i]; }
+        if (b0 < segs_m && b0 + run >= segs_m) scan[segs_m] = acc;   // total
+        __syncthreads();
+    }
+    const uint32_t total = scan[segs_m];
+    const float cm = cmax[m], sc = sqrt_cmax[m];
+    const long long nb = ((long long)total + 31) / 32;
+    const long long W = (long long)gridDim.x * 4;
+    for (long long b = (long long)blockIdx.x * 4 + wave; b < nb; b += W) {
+        const long long f = b * 32 + r;
+        const bool valid = f < (long long)total;
+        uint2 e = make_uint2(0u, 0u);
+        if (valid) {   // segment s with scan[s] <= f < scan[s + 1] (the last such s)
+            int lo = 0, hi = segs_m - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (scan[mid] <= (uint32_t)f) lo = mid; else hi = mid - 1;
+            }
+            e = rq[((long long)m * segs_m + lo) * rq_seg + ((uint32_t)f - scan[lo])];
+        }
+        const long long v = (long long)(e.x & 0x7FFFFFFFu);
+        const bool e0_lo = (e.x >> 31) != 0;
+        const float thr = __uint_as_float(e.y);
+        // the full sub-vector (exact distances) and this lane's screening slice
         float xv[D];
+        const float* xp = x + v * ldx + (long long)m * D;
+        if constexpr (D % 4 == 0) {
 #pragma unroll
-        for (int j = 0; j < D; ++j) xv[j] = xp[j];
+            for (int j = 0; j < D; j += 4) {
+                const float4 q = *reinterpret_cast<const float4*>(xp + j);
+                xv[j] = q.x; xv[j + 1] = q.y; xv[j + 2] = q.z; xv[j + 3] = q.w;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < D; ++j) xv[j] = xp[j];
+        }
+        float xs[XD];
+#pragma unroll
+        for (int j = 0; j < XD; ++j)
+            xs[j] = valid ? xv[Slice<D>::HALF ? (h ? 8 + j : j) : j] : 0.0f;
+        float X;
+        bool lo;
+        float xh[XD], xl[XD];
+        split_x<D>(xs, X, lo, xh, xl);
+        float bv, tau;
+        screen_bound(X, true, e0_lo, cm, sc, bv, tau);
+        bf16x8 Bm[P::PM];
+        bf16x8 Bl[P::PL];
+        build_b<D>(xh, xl, bv, h, Bm, Bl);
+        const bool lo_pass = __any(lo);
+        // candidates: bit (t & 1) * 16 + i of word t >> 1
+        uint32_t cw[kTiles / 2];
+#pragma unroll
+        for (int t = 0; t < kTiles; ++t) {
+            const f32x16 acc = tile_scores<D>(As, lane, t, Bm, Bl, lo_pass);
+            uint32_t bits = 0;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) bits |= (acc[i] <= thr ? 1u : 0u) << i;
+            if (t & 1) cw[t >> 1] |= bits << 16; else cw[t >> 1] = bits;
+        }
+        if (!valid) {
+#pragma unroll
+            for (int w = 0; w < kTiles / 2; ++w) cw[w] = 0;
+        }
         float best = INFINITY;
         int bidx = 0x7FFFFFFF;
-#pragma unroll
-        for (int q = 0; q < K / 64; ++q) {
-            const float dd = exact_dist<D>(xv, cv[q]);
-            if (dd < best) { best = dd; bidx = lane + 64 * q; }
+        while (true) {
+            const uint32_t any = cw[0] | cw[1] | cw[2] | cw[3];
+            if (!__any(any != 0)) break;
+            if (any) {
+                const int w = cw[0] ? 0 : cw[1] ? 1 : cw[2] ? 2 : 3;
+                const uint32_t word = w == 0 ? cw[0] : w == 1 ? cw[1] : w == 2 ? cw[2] : cw[3];
+                const int bit = __builtin_ctz(word);
+                const uint32_t rest = word & (word - 1);
+                cw[0] = w == 0 ? rest : cw[0];
+                cw[1] = w == 1 ? rest : cw[1];
+                cw[2] = w == 2 ? rest : cw[2];
+                cw[3] = w == 3 ? rest : cw[3];
+                const int k = tile_row(2 * w + (bit >> 4), bit & 15, h);
+                const float dd = exact_dist<D>(xv, cl + k * D);
+                if (dd < best || (dd == best && k < bidx)) { best = dd; bidx = k; }
+            }
         }
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-            const float ob = __shfl_xor(best, off);
-            const int oi = __shfl_xor(bidx, off);
-            if (ob < best || (ob == best && oi < bidx)) { best = ob; bidx = oi; }
-        }
-        if (lane == 0) {
+        const float ob = __shfl_xor(best, 32);
+        const int oi = __shfl_xor(bidx, 32);
+        if (ob < best || (ob == best && oi < bidx)) { best = ob; bidx = oi; }
+        if (valid && h == 0) {
             const int code = bidx == 0x7FFFFFFF ? 0 : bidx;
             codes[v * m_total + m] = (CodeT)code;
             if (counts) atomicAdd(&counts[(long long)m * K + code], 1u);
@@ -660,12 +835,14 @@ int launch_mfma(pqh_pq* pq, const float* x, long long n, long long ldx, CodeT* c
         ctx->d_rq = nullptr;
         ctx->d_rq_cnt = nullptr;
         ctx->rq_segs = 0;
-        PQH_HIP(ctx, hipMalloc(&ctx->d_rq, (size_t)segs * kRqSeg * sizeof(uint32_t)));
+        PQH_HIP(ctx, hipMalloc(&ctx->d_rq, (size_t)segs * kRqSeg * sizeof(uint2)));
         PQH_HIP(ctx, hipMalloc(&ctx->d_rq_cnt, (size_t)segs * sizeof(uint32_t)));
         ctx->rq_segs = segs;
         return PQH_OK;
     };
-    const bool use_rq = PQH_ASSIGN_DEFER && n <= 0xFFFFFFFFll;   // entries: u32 vector ids
+    // entries carry the vector id in 31 bits; more segments than the window kernel's LDS
+    // scan holds (only with very small m on a large grid) fall back to inline re-ranking
+    const bool use_rq = PQH_ASSIGN_DEFER && n < 0x80000000ll;
     // grid = the workgroups that are resident at once (persistent, grid-stride over the
     // 32-vector blocks): more would only queue behind the first wave of workgroups
 #define PQH_CASE(DD)                                                                        \
@@ -677,26 +854,36 @@ int launch_mfma(pqh_pq* pq, const float* x, long long n, long long ldx, CodeT* c
             per_cu = 1;                                                                     \
         long long gx = (long long)ctx->num_cus * per_cu / groups;                           \
         gx = std::max(1ll, std::min(gx, ((nblk + 1) / 2 + kWavesPerWG - 1) / kWavesPerWG)); \
-        const long long segs = gx * groups * kWavesPerWG;                                   \
-        if (use_rq) {                                                                       \
+        if (gx >= 16) gx &= ~7ll;   /* CU-uniform subspace placement (see the kernel) */   \
+        const long long segs_m = gx * kWavesPerWG;                                          \
+        const long long segs = segs_m * groups;                                             \
+        const size_t fix_lds = (size_t)Plan<DD>::PA * kTiles * 64 * 16 +                    \
+                               (size_t)256 * DD * 4 + (size_t)(segs_m + 1) * 4;             \
+        const bool rq_on = use_rq && fix_lds <= 64 * 1024;                                  \
+        if (rq_on) {                                                                        \
             int rc = rq_ensure(segs);                                                       \
             if (rc) return rc;                                                              \
         }                                                                                   \
         if (sched)                                                                          \
             PQH_HIP(ctx, hipMemsetAsync(sched, 0, (size_t)pq->m * kXcds * kSchedStride * 4,  \
                                         ctx->stream));                                      \
-        hipLaunchKernelGGL((pq_assign_mfma<DD, CodeT>), dim3((unsigned)gx, (unsigned)groups), \
-                           block, 0, ctx->stream, x, n, ldx, pq->m, pq->d_afrag, pq->d_cent, \
+        hipLaunchKernelGGL((pq_assign_mfma<DD, CodeT>), dim3((unsigned)(gx * groups)), block, \
+                           0, ctx->stream, x, n, ldx, pq->m, pq->d_afrag, pq->d_cent,       \
                            pq->d_cmax, pq->d_sqc, codes, counts, rr, sched,                 \
-                           use_rq ? ctx->d_rq : nullptr, kRqSeg, ctx->d_rq_cnt);            \
+                           rq_on ? reinterpret_cast<uint2*>(ctx->d_rq) : nullptr, kRqSeg,   \
+                           ctx->d_rq_cnt, (int)gx);                                         \
         PQH_LAUNCH_CHECK(ctx);                                                              \
-        if (use_rq) {                                                                       \
-            constexpr int kSplit = 4;                                                       \
-            const long long waves = segs * kSplit;                                          \
-            hipLaunchKernelGGL((pq_rerank_fix<DD, CodeT>), dim3((unsigned)((waves + 3) / 4)), \
-                               dim3(256), 0, ctx->stream, x, ldx, pq->m, pq->d_cent,        \
-                               ctx->d_rq, kRqSeg, ctx->d_rq_cnt, (unsigned)segs,            \
-                               (unsigned)gx, kSplit, codes, counts);                        \
+        if (rq_on) {                                                                        \
+            /* ~2k waves in all: each takes a few 32-vector batches of the queue */         \
+            const unsigned gf = (unsigned)std::max(1ll, std::min(64ll, 512ll / groups + 1)); \
+            PQH_HIP(ctx, hipFuncSetAttribute((const void*)pq_rerank_window<DD, CodeT>,      \
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,    \
+                                             (int)fix_lds));                                \
+            hipLaunchKernelGGL((pq_rerank_window<DD, CodeT>), dim3(gf, (unsigned)groups),   \
+                               dim3(256), fix_lds, ctx->stream, x, ldx, pq->m, pq->d_afrag, \
+                               pq->d_cent, pq->d_cmax, pq->d_sqc,                           \
+                               reinterpret_cast<const uint2*>(ctx->d_rq), kRqSeg,           \
+                               ctx->d_rq_cnt, (int)segs_m, codes, counts);                  \
         }                                                                                   \
         break;                                                                              \
     }
@@ -810,6 +997,16 @@ int pqh_pq_assign(pqh_ctx_t* ctx, const pqh_pq_t* cpq, const float* d_x, long lo
                     : launch_exact(pq, d_x, n, ld_x, c, d_counts);
     }
     return launch_exact(pq, d_x, n, ld_x, static_cast<uint16_t*>(d_codes), d_counts);
+}
+
+// diagnostics: the per-wave stamps of the last assignment launch (PQH_ASSIGN_STAMPS builds;
+// zeros otherwise); out holds max_waves * 4 values
+int pqh_debug_assign_stamps(pqh_ctx_t* ctx, unsigned long long* out, int max_waves) {
+    if (!ctx || !out || max_waves <= 0) return PQH_ERR_ARG;
+    PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    const int w = std::min(max_waves, kStampWaves);
+    PQH_HIP(ctx, hipMemcpyFromSymbol(out, HIP_SYMBOL(g_assign_stamps), (size_t)w * 4 * 8));
+    return PQH_OK;
 }
 
 int pqh_pq_last_rerank_count(pqh_ctx_t* ctx, unsigned long long* count) {

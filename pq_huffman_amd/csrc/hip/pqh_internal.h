@@ -31,7 +31,7 @@ struct pqh_ctx {
     // apart, zeroed before every launch
     uint32_t* d_sched = nullptr;
     // deferred re-rank queue of the assignment kernel: rq_segs segments (one per wave)
-    uint32_t* d_rq = nullptr;
+    void* d_rq = nullptr;          // uint2 entries (vector | any_lo << 31, threshold)
     uint32_t* d_rq_cnt = nullptr;
     long long rq_segs = 0;
 };

@@ -949,7 +949,9 @@ static int launch_luts(pqh_ctx* ctx, pqh_tables* t) {
 }
 
 int pqh_tables_build(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts) {
-    if (!ctx || !t || !d_counts || t->ctx != ctx) return PQH_ERR_ARG;
+    // any context of the tables' device may run the build (on its own stream), so the
+    // builds of consecutive batches can overlap on different streams
+    if (!ctx || !t || !d_counts || !t->ctx || t->ctx->device != ctx->device) return PQH_ERR_ARG;
     int rc = pqh_use_device(ctx);
     if (rc) return rc;
     PQH_HIP(ctx, hipMemsetAsync(t->d_err, 0, 4, ctx->stream));

@@ -1,0 +1,50 @@
+"""Per-wave timeline of pq_assign_mfma (diagnostic; needs a PQH_ASSIGN_STAMPS build, see
+tools/build_variants.sh): start/end spread, lifetime and blocks per wave, per XCD."""
+import ctypes
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import bench  # noqa: E402
+from pq_huffman_amd import codec  # noqa: E402
+from pq_huffman_amd.capi import lib  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    n, d, m, k = 1_000_000, 128, 8, 256
+    x = bench.make_data(torch, n, d, 1234, 0, dev)
+    cent = bench.train_centroids(torch, x, m, k)
+    ctx = codec.Context(0)
+    pq = codec.PQ(ctx, cent)
+    codes = torch.empty((n, m), dtype=torch.uint8, device=dev)
+    for _ in range(5):
+        pq.assign(x, codes)
+    torch.cuda.synchronize()
+    W = 8192
+    buf = (ctypes.c_ulonglong * (W * 4))()
+    lib().pqh_debug_assign_stamps(ctx.ptr, buf, W)
+    a = np.frombuffer(buf, dtype=np.uint64).reshape(W, 4).astype(np.int64)
+    a = a[a[:, 1] > 0]
+    t0 = a[:, 0].min()
+    st, en, nb, xcc = a[:, 0] - t0, a[:, 1] - t0, a[:, 2] & 0xFFFF, a[:, 3]
+    cyc = a[:, 2] >> 16          # s_memtime lifetime (shader clock)
+    life = en - st               # s_memrealtime: 100 MHz ticks, comparable across CUs
+    print(f"waves {len(a)}  span {en.max()} ticks of 10 ns")
+    for name, v in (("start", st), ("end", en), ("life", life), ("blocks", nb), ("cycles", cyc)):
+        q = np.percentile(v, [0, 5, 25, 50, 75, 95, 100]).astype(int)
+        print(f"{name:7s} p0/5/25/50/75/95/100: {list(q)}")
+    for c in range(8):
+        sel = xcc == c
+        if sel.any():
+            print(f"xcc {c}: waves {sel.sum()} blocks {nb[sel].sum()} start p50/max {int(np.median(st[sel]))}/"
+                  f"{st[sel].max()} end p5/p50/max {int(np.percentile(en[sel], 5))}/{int(np.median(en[sel]))}/"
+                  f"{en[sel].max()}")
+    print("clock GHz (cycles / life):", round(float(np.median(cyc / np.maximum(life, 1))) / 10, 3))
+    print("ticks per block (median life/blocks):", int(np.median(life / np.maximum(nb, 1))))
+
+
+if __name__ == "__main__":
+    main()
