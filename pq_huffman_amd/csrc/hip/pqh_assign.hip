@@ -40,16 +40,20 @@ constexpr int kTiles = 8;        // K = 256 centroids = 8 tiles of 32 rows
 #ifndef PQH_ASSIGN_WPG
 #define PQH_ASSIGN_WPG 4
 #endif
+#ifndef PQH_ASSIGN_NB
+#define PQH_ASSIGN_NB 2
+#endif
 #ifndef PQH_ASSIGN_OCC
-#define PQH_ASSIGN_OCC 4
+#define PQH_ASSIGN_OCC (PQH_ASSIGN_NB == 1 ? 4 : 3)
 #endif
 #ifndef PQH_ASSIGN_DEFER
 #define PQH_ASSIGN_DEFER 1
 #endif
-#ifndef PQH_ASSIGN_PIPE
-#define PQH_ASSIGN_PIPE 0
+#ifndef PQH_ASSIGN_RED
+#define PQH_ASSIGN_RED 0
 #endif
 constexpr int kWavesPerWG = PQH_ASSIGN_WPG;   // subspace waves per workgroup
+constexpr int kNB = PQH_ASSIGN_NB;            // 32-vector blocks screened together per step
 
 template <int D>
 struct Plan {
@@ -63,6 +67,12 @@ struct Plan {
 __device__ __forceinline__ unsigned med3u(unsigned a, unsigned b, unsigned c) {
     unsigned r;
     asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+__device__ __forceinline__ unsigned min3u(unsigned a, unsigned b, unsigned c) {
+    unsigned r;
+    asm("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
 }
 
@@ -125,19 +135,31 @@ __device__ __forceinline__ void split_x(const float* xs, float& X, bool& lo, flo
         xl[j] = (float)(__bf16)rem;
         lo |= rem != 0.0f;
     }
-    if constexpr (Slice<D>::HALF) X += __shfl_xor(X, 32);   // the other half-wave's 8 dims
+    if constexpr (Slice<D>::HALF) {   // + the other half-wave's 8 dims (lower + upper, so
+        // both halves round the same sum); a VALU lane swap, no LDS round trip
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(X), __float_as_uint(X),
+                                                         false, false);
+        X = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+    }
 }
 
-// error bound of the screening score (DESIGN.md "pq_assign error bound"); when no x of the
-// block has a bf16 remainder the split error is 2^-15 P instead of 2^-13 P.  Returns the
-// per-vector bias b_v (keeps every score positive) and the acceptance gap tau.
-__device__ __forceinline__ void screen_bound(float X, bool finite_x, bool any_lo, float cm,
-                                             float sc, float& bv, float& tau) {
+// Per-vector bias b_v of the screening score: keeps every score positive, so scores order
+// as unsigned integers.  Needs b_v >= X + 3 E0; with P = sqrt(X Cmax) <= (X + Cmax) / 2,
+// E0 (below) <= 7.7e-5 (X + Cmax), so X + 2^-10 (X + Cmax) suffices -- no square root on
+// the way to the first MFMA.  b_v <= 1.0078 X + 0.001 Cmax stays inside the accumulation
+// term of E0 (1.05 X + 1.01 Cmax).
+__device__ __forceinline__ float screen_bias(float X, bool finite_x, float cm) {
+    return finite_x ? bf16_up(X + 0x1p-10f * (X + cm) + 1e-30f) : 0.0f;
+}
+
+// error bound E0 of the screening score against the fp32 direct-form distance (DESIGN.md
+// "pq_assign error bound"); when no x of the block has a bf16 remainder the split error is
+// 2^-15 P instead of 2^-13 P.  Returns the acceptance gap tau = 2.2 E0.
+__device__ __forceinline__ float screen_tau(float X, bool any_lo, float cm, float sc) {
     const float Pm = sqrtf(X) * sc * 1.00001f;
     const float E0 = (any_lo ? 0x1p-13f : 0x1p-15f) * Pm + 0x1p-22f * cm +
                      0x1p-17f * (2.02f * Pm + 1.01f * cm + 1.05f * X);
-    bv = finite_x ? bf16_up(X + 3.0f * E0 + 1e-30f) : 0.0f;
-    tau = 2.2f * E0 + 1e-30f;
+    return 2.2f * E0 + 1e-30f;
 }
 
 template <int D>
@@ -176,26 +198,34 @@ __device__ __forceinline__ void build_b(const float* xh, const float* xl, float 
     }
 }
 
-// the 32 x 32 score tile t: centroid rows 32t.. (A, from LDS) x the block's vectors (B)
+// the 32 x 32 score tile: centroid rows (A fragments a[0 .. PA)) x the block's vectors (B)
+template <int D>
+__device__ __forceinline__ f32x16 tile_scores_a(const bf16x8* a, const bf16x8* Bm,
+                                                const bf16x8* Bl, bool lo_pass) {
+    using P = Plan<D>;
+    f32x16 acc = {0};
+#pragma unroll
+    for (int p = 0; p < P::PM; ++p)
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[p], Bm[p], acc, 0, 0, 0);
+    if (lo_pass) {
+#pragma unroll
+        for (int p = 0; p < P::PL; ++p)
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[P::REUSE ? 0 : P::PM + p], Bl[p],
+                                                          acc, 0, 0, 0);
+    }
+    return acc;
+}
+
+// tile t with its A fragments read from the LDS copy
 template <int D>
 __device__ __forceinline__ f32x16 tile_scores(const uint4* As, int lane, int t, const bf16x8* Bm,
                                               const bf16x8* Bl, bool lo_pass) {
     using P = Plan<D>;
-    auto lda = [&](int p) -> bf16x8 {
-        return *reinterpret_cast<const bf16x8*>(&As[(p * kTiles + t) * 64 + lane]);
-    };
-    f32x16 acc = {0};
+    bf16x8 a[P::PA];
 #pragma unroll
-    for (int p = 0; p < P::PM; ++p)
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lda(p), Bm[p], acc, 0, 0, 0);
-    if (lo_pass) {
-#pragma unroll
-        for (int p = 0; p < P::PL; ++p) {
-            const bf16x8 a = P::REUSE ? lda(0) : lda(P::PM + (P::REUSE ? 0 : p));
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, Bl[p], acc, 0, 0, 0);
-        }
-    }
-    return acc;
+    for (int p = 0; p < P::PA; ++p)
+        a[p] = *reinterpret_cast<const bf16x8*>(&As[(p * kTiles + t) * 64 + lane]);
+    return tile_scores_a<D>(a, Bm, Bl, lo_pass);
 }
 
 // centroid row of accumulator register i of tile t for half-wave h (32x32x16 output layout)
@@ -261,11 +291,10 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     auto load_x = [&](long long b, float* dst) {
         long long vv = b * 32 + r;
         vv = vv < n ? vv : n - 1;
-#ifdef PQH_ASSIGN_CONTIG   // diagnostic: same bytes, read as one contiguous 2 KB per wave
-        const float* xp = x + (b < nblk - 1 ? b : nblk - 2) * 32 * ldx + (long long)m * 512 + lane * 8;
-#else
-        const float* xp = x + vv * ldx + (long long)m * D + (HALF ? 8 * h : 0);
+#ifdef PQH_ASSIGN_L2X   // diagnostic: compute-bound time, x re-read from an L2-resident 64 KB
+        vv &= 1023;
 #endif
+        const float* xp = x + vv * ldx + (long long)m * D + (HALF ? 8 * h : 0);
         if constexpr (XD % 4 == 0) {
 #pragma unroll
             for (int j = 0; j < XD; j += 4) {
@@ -284,146 +313,179 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     uint2* my_rq = rq ? rq + (long long)seg_id * rq_seg : nullptr;
     unsigned qn = 0;
 
-    auto body = [&](long long blk, const float* xin) {
-        const long long v = blk * 32 + r;
-        const bool valid = v < n;
-        float xs[XD];
+    // One step = a chunk of kNB consecutive 32-vector blocks, screened together: each tile's
+    // A fragments are read from LDS once for all kNB blocks, and the kNB independent MFMA
+    // chains and key reductions give the SIMD work to overlap.
+    auto body = [&](long long blk0, float (*xin)[XD]) {
+        long long v[kNB];
+        bool valid[kNB], any_lo[kNB], finite_x[kNB];
+        float xs[kNB][XD], X[kNB];
+        bf16x8 Bm[kNB][P::PM], Bl[kNB][P::PL];
 #pragma unroll
-        for (int j = 0; j < XD; ++j) xs[j] = valid ? xin[j] : 0.0f;
+        for (int b = 0; b < kNB; ++b) {
+            v[b] = (blk0 + b) * 32 + r;
+            valid[b] = v[b] < n;
+#pragma unroll
+            for (int j = 0; j < XD; ++j) xs[b][j] = valid[b] ? xin[b][j] : 0.0f;
+        }
 #ifdef PQH_ASSIGN_NOCOMPUTE   // diagnostic: the kernel's memory traffic alone
-        {
+#pragma unroll
+        for (int b = 0; b < kNB; ++b) {
             float q = 0.0f;
 #pragma unroll
-            for (int j = 0; j < XD; ++j) q += xs[j];
-#ifdef PQH_ASSIGN_NOSTORE
-            if (q == 1234.5f) codes[v * m_total + m] = (CodeT)(int)q;
-#else
-            if (valid && h == 0) codes[v * m_total + m] = (CodeT)(int)q;
-#endif
-            return;
+            for (int j = 0; j < XD; ++j) q += xs[b][j];
+            if (valid[b] && h == 0) codes[v[b] * m_total + m] = (CodeT)(int)q;
         }
+        return;
 #endif
-        float X;
-        bool lo;
-        float xh[XD], xl[XD];
-        split_x<D>(xs, X, lo, xh, xl);
-        const bool any_lo = __any(lo);
-        const bool finite_x = isfinite(X);
-        float bv, tau;
-        screen_bound(X, finite_x, any_lo, cm, sc, bv, tau);
-        bf16x8 Bm[P::PM];
-        bf16x8 Bl[P::PL];
-        build_b<D>(xh, xl, bv, h, Bm, Bl);
-        // (PQH_ASSIGN_PIPE: tile t + 1's MFMAs are issued before tile t's keys are reduced)
-        auto tile_acc = [&](int t) { return tile_scores<D>(As, lane, t, Bm, Bl, any_lo); };
+#pragma unroll
+        for (int b = 0; b < kNB; ++b) {
+            bool lo;
+            float xh[XD], xl[XD];
+            split_x<D>(xs[b], X[b], lo, xh, xl);
+            any_lo[b] = __any(lo);
+            finite_x[b] = isfinite(X[b]);
+            build_b<D>(xh, xl, screen_bias(X[b], finite_x[b], cm), h, Bm[b], Bl[b]);
+        }
         // Keys: float bits with the low 4 mantissa bits replaced by the accumulator register
-        // i.  One running (min, second-min) over all 128 values of the lane; values go in
-        // groups of three: the group's top two by min3/med3, then (m1, m2) <- (min(m1, g1),
+        // i.  One running (min, second-min) per block over the lane's 128 values; values go
+        // in groups of three: the group's top two by min3/med3, then (m1, m2) <- (min(m1, g1),
         // med3(m1, g1, min(m2, g2))).  The winner's tile is the last tile that lowered m1.
-        unsigned m1 = 0xFFFFFFFFu, m2 = 0xFFFFFFFFu, mt = 0;
-        f32x16 acc = tile_acc(0);
+        unsigned m1[kNB], m2[kNB], mt[kNB];
+#pragma unroll
+        for (int b = 0; b < kNB; ++b) { m1[b] = 0xFFFFFFFFu; m2[b] = 0xFFFFFFFFu; mt[b] = 0; }
 #pragma unroll
         for (int t = 0; t < kTiles; ++t) {
-            f32x16 nxt;
-            if (PQH_ASSIGN_PIPE && t + 1 < kTiles) nxt = tile_acc(t + 1);
-            unsigned kk[16];
+            bf16x8 a[P::PA];
 #pragma unroll
-            for (int i = 0; i < 16; ++i) kk[i] = (__float_as_uint(acc[i]) & ~15u) | (unsigned)i;
-            const unsigned prev = m1;
+            for (int p = 0; p < P::PA; ++p)
+                a[p] = *reinterpret_cast<const bf16x8*>(&As[(p * kTiles + t) * 64 + lane]);
+            f32x16 acc[kNB];
+#ifdef PQH_ASSIGN_NOMFMA   // diagnostic timing only: no matrix work, scores from the B data
 #pragma unroll
-            for (int g = 0; g < 5; ++g) {
-                const unsigned a0 = kk[3 * g], a1 = kk[3 * g + 1], a2 = kk[3 * g + 2];
-                const unsigned g1 = min(min(a0, a1), a2);
-                const unsigned g2 = med3u(a0, a1, a2);
-                m2 = med3u(m1, g1, min(m2, g2));
-                m1 = min(m1, g1);
+            for (int b = 0; b < kNB; ++b)
+#pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    acc[b][i] = (float)Bm[b][i & 7][i >> 3] + (float)a[0][i & 7] * (float)(t + 1);
+#else
+#pragma unroll
+            for (int b = 0; b < kNB; ++b) acc[b] = tile_scores_a<D>(a, Bm[b], Bl[b], any_lo[b]);
+#endif
+#pragma unroll
+            for (int b = 0; b < kNB; ++b) {
+                unsigned kk[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    kk[i] = (__float_as_uint(acc[b][i]) & ~15u) | (unsigned)i;
+                const unsigned prev = m1[b];
+#if PQH_ASSIGN_RED == 3   // diagnostic timing only: MFMA + overhead, no key reduction
+                m1[b] = min3u(m1[b], __float_as_uint(acc[b][0]), __float_as_uint(acc[b][15]));
+                m2[b] = m1[b] + 100000;
+#elif PQH_ASSIGN_RED == 2   // diagnostic timing only (wrong codes): min over raw bits
+#pragma unroll
+                for (int q = 0; q < 8; ++q) m1[b] = min3u(m1[b], kk[2 * q], kk[2 * q + 1]);
+                m2[b] = m1[b] + 100000;
+#else
+#pragma unroll
+                for (int g = 0; g < 5; ++g) {
+                    const unsigned a0 = kk[3 * g], a1 = kk[3 * g + 1], a2 = kk[3 * g + 2];
+                    const unsigned g1 = min3u(a0, a1, a2);
+                    const unsigned g2 = med3u(a0, a1, a2);
+                    m2[b] = med3u(m1[b], g1, min(m2[b], g2));
+                    m1[b] = min(m1[b], g1);
+                }
+                m2[b] = med3u(m1[b], m2[b], kk[15]);
+                m1[b] = min(m1[b], kk[15]);
+#endif
+                mt[b] = m1[b] != prev ? (unsigned)t : mt[b];
             }
-            m2 = med3u(m1, m2, kk[15]);
-            m1 = min(m1, kk[15]);
-            mt = m1 != prev ? (unsigned)t : mt;
-            if (t + 1 < kTiles) acc = PQH_ASSIGN_PIPE ? nxt : tile_acc(t + 1);
         }
-        // merge the two half-waves (lanes l and l^32 hold the same vector)
-        const unsigned o1 = __shfl_xor(m1, 32), o2 = __shfl_xor(m2, 32), ot = __shfl_xor(mt, 32);
-        const bool other = o1 < m1;
-        const unsigned w_h = other ? (unsigned)(1 - h) : (unsigned)h;
-        const unsigned w_t = other ? ot : mt;
-        const unsigned b2 = min(min(m2, o2), max(m1, o1));
-        const unsigned b1 = min(m1, o1);
-        const unsigned reg = b1 & 15u;
-        int code = tile_row((int)w_t, (int)reg, (int)w_h);
-        const float K1 = __uint_as_float(b1 & ~15u), K2 = __uint_as_float(b2 & ~15u);
-        const float gap = K2 - K1;
-        const bool slow = !(gap > tau + 0x1p-15f * K2) || !finite_x;
+#pragma unroll
+        for (int b = 0; b < kNB; ++b) {
+            // merge the two half-waves (lanes l and l^32 hold the same vector)
+            const unsigned o1 = __shfl_xor(m1[b], 32), o2 = __shfl_xor(m2[b], 32),
+                           ot = __shfl_xor(mt[b], 32);
+            const bool other = o1 < m1[b];
+            const unsigned w_h = other ? (unsigned)(1 - h) : (unsigned)h;
+            const unsigned w_t = other ? ot : mt[b];
+            const unsigned b2 = min(min(m2[b], o2), max(m1[b], o1));
+            const unsigned b1 = min(m1[b], o1);
+            int code = tile_row((int)w_t, (int)(b1 & 15u), (int)w_h);
+            const float tau = screen_tau(X[b], any_lo[b], cm, sc);
+            const float K1 = __uint_as_float(b1 & ~15u), K2 = __uint_as_float(b2 & ~15u);
+            const bool slow = !(K2 - K1 > tau + 0x1p-15f * K2) || !finite_x[b];
 
-        unsigned long long need = __ballot(slow && valid && h == 0);
-        bool deferred = false;
-        if (need) {
-            slow_count += __popcll(need);
-            // finite vectors go to the queue with their candidate window: every centroid
-            // that can be the fp32 argmin (or tie with it) screens below
-            // (K1 + tau)(1 + 2^-16) -- see pq_rerank_window; non-finite ones stay inline
-            const unsigned long long fin = need & __ballot(finite_x);
-            const unsigned cnt = (unsigned)__popcll(fin);
-            if (my_rq && cnt && qn + cnt <= (unsigned)rq_seg) {
-                if (slow && valid && h == 0 && finite_x) {
-                    const float thr = (K1 + tau) * (1.0f + 0x1p-16f);
-                    my_rq[qn + __builtin_amdgcn_mbcnt_hi((unsigned)(fin >> 32),
-                                 __builtin_amdgcn_mbcnt_lo((unsigned)fin, 0u))] =
-                        make_uint2((uint32_t)v | (any_lo ? 0x80000000u : 0u), __float_as_uint(thr));
+            unsigned long long need = __ballot(slow && valid[b] && h == 0);
+            bool deferred = false;
+            if (need) {
+                slow_count += __popcll(need);
+                // finite vectors go to the queue with their candidate window: every centroid
+                // that can be the fp32 argmin (or tie with it) screens below
+                // (K1 + tau)(1 + 2^-16) -- see pq_rerank_window; non-finite ones stay inline
+                const unsigned long long fin = need & __ballot(finite_x[b]);
+                const unsigned cnt = (unsigned)__popcll(fin);
+                if (my_rq && cnt && qn + cnt <= (unsigned)rq_seg) {
+                    if (slow && valid[b] && h == 0 && finite_x[b]) {
+                        const float thr = (K1 + tau) * (1.0f + 0x1p-16f);
+                        my_rq[qn + __builtin_amdgcn_mbcnt_hi((unsigned)(fin >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((unsigned)fin, 0u))] =
+                            make_uint2((uint32_t)v[b] | (any_lo[b] ? 0x80000000u : 0u),
+                                       __float_as_uint(thr));
+                    }
+                    qn += cnt;
+                    deferred = finite_x[b];
+                    need &= ~fin;
                 }
-                qn += cnt;
-                deferred = finite_x;
-                need &= ~fin;
-            }
-            unsigned long long todo = need;
-            while (todo) {
-                const int rs = __ffsll((long long)todo) - 1;
-                todo &= todo - 1;
-                float xv[D];
+                unsigned long long todo = need;
+                while (todo) {   // inline exact re-rank: non-finite x, or a full segment
+                    const int rs = __ffsll((long long)todo) - 1;
+                    todo &= todo - 1;
+                    float xv[D];
 #pragma unroll
-                for (int j = 0; j < D; ++j) {   // HALF: dims 8.. live in the partner lane
-                    const int src = HALF && j >= XD ? rs + 32 : rs;
-                    xv[j] = __int_as_float(__builtin_amdgcn_readlane(
-                        __float_as_int(xs[HALF && j >= XD ? j - XD : j]), src));
-                }
-                float best = INFINITY;
-                int bidx = 0x7FFFFFFF;
+                    for (int j = 0; j < D; ++j) {   // HALF: dims 8.. live in the partner lane
+                        const int src = HALF && j >= XD ? rs + 32 : rs;
+                        xv[j] = __int_as_float(__builtin_amdgcn_readlane(
+                            __float_as_int(xs[b][HALF && j >= XD ? j - XD : j]), src));
+                    }
+                    float best = INFINITY;
+                    int bidx = 0x7FFFFFFF;
 #pragma unroll 1
-                for (int q = 0; q < K / 64; ++q) {   // rare path: keep its registers few
-                    const int c = lane + 64 * q;
-                    float cv[D];
+                    for (int q = 0; q < K / 64; ++q) {   // rare path: keep its registers few
+                        const int c = lane + 64 * q;
+                        float cv[D];
 #pragma unroll
-                    for (int j = 0; j < D; ++j) cv[j] = cbase[(long long)c * D + j];
-                    const float dd = exact_dist<D>(xv, cv);
-                    if (dd < best) { best = dd; bidx = c; }
-                }
+                        for (int j = 0; j < D; ++j) cv[j] = cbase[(long long)c * D + j];
+                        const float dd = exact_dist<D>(xv, cv);
+                        if (dd < best) { best = dd; bidx = c; }
+                    }
 #pragma unroll
-                for (int off = 32; off >= 1; off >>= 1) {
-                    const float ob = __shfl_xor(best, off);
-                    const int oi = __shfl_xor(bidx, off);
-                    if (ob < best || (ob == best && oi < bidx)) { best = ob; bidx = oi; }
+                    for (int off = 32; off >= 1; off >>= 1) {
+                        const float ob = __shfl_xor(best, off);
+                        const int oi = __shfl_xor(bidx, off);
+                        if (ob < best || (ob == best && oi < bidx)) { best = ob; bidx = oi; }
+                    }
+                    if (lane == rs) code = bidx == 0x7FFFFFFF ? 0 : bidx;
                 }
-                if (lane == rs) code = bidx == 0x7FFFFFFF ? 0 : bidx;
             }
-        }
-        if (valid && h == 0 && !(deferred && slow)) {
-            codes[v * m_total + m] = (CodeT)code;
-            if (counts) atomicAdd(&hist[wave][code], 1u);
+            if (valid[b] && h == 0 && !(deferred && slow)) {
+                codes[v[b] * m_total + m] = (CodeT)code;
+                if (counts) atomicAdd(&hist[wave][code], 1u);
+            }
         }
     };
 
-    // Block schedule, two blocks (one chunk) per step.  Wave w of the subspace (w = bx
+    // Chunk schedule (a chunk = kNB blocks = one step).  Wave w of the subspace (w = bx
     // * kWavesPerWG + wave) starts on chunk w.  sched == nullptr: static stride over chunks.
     // Otherwise the remaining chunks are handed out by tickets, so waves that share their CU
     // with other work (a concurrent stream) simply take fewer chunks.  The dynamic region is
     // split into kXcds ranges with a head each; a wave drains the range of the XCD it runs on
     // first (XCC_ID; placement only affects speed), then moves on to the next range -- one
     // shared head per subspace saturated at a few dequeues per microsecond.  The ticket for
-    // the next chunk is requested a whole step ahead.
+    // the next chunk is requested a whole step ahead, and the next chunk's x is loaded
+    // during the current one.
     const long long wave_id = (long long)bx * kWavesPerWG + wave;   // within subspace
     const long long waves_m = (long long)gx * kWavesPerWG;
-    const long long nchunk = (nblk + 1) / 2;
+    const long long nchunk = (nblk + kNB - 1) / kNB;
     const long long R = nchunk > waves_m ? (nchunk - waves_m + kXcds - 1) / kXcds : 0;
     uint32_t* head = sched ? sched + (long long)m * kXcds * kSchedStride : nullptr;
     int xr = head ? (int)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & (kXcds - 1)) : 0;
@@ -453,31 +515,31 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         }
         return -1;
     };
-    long long blk = 2ll * wave_id;
-    float xn[XD];
-    load_x(blk, xn);
-    while (blk < nblk) {
-        float xa[XD];
+    long long ch = wave_id;
+    float xn[kNB][XD];
 #pragma unroll
-        for (int j = 0; j < XD; ++j) xa[j] = xn[j];
-        load_x(blk + 1, xn);   // the chunk's second block in flight during the first
-        body(blk, xa);
-#ifdef PQH_ASSIGN_STAMPS
-        nbdone += 2;
-#endif
-        if (blk + 1 >= nblk) break;
-        long long nb;
+    for (int b = 0; b < kNB; ++b) load_x(ch * kNB + b, xn[b]);
+    while (ch < nchunk) {
+        float xa[kNB][XD];
+#pragma unroll
+        for (int b = 0; b < kNB; ++b)
+#pragma unroll
+            for (int j = 0; j < XD; ++j) xa[b][j] = xn[b][j];
+        long long nc;
         if (!head) {
-            nb = blk + 2ll * waves_m;
+            nc = ch + waves_m;
         } else {
             const long long c = next_dyn();
-            nb = c < 0 ? nblk : 2ll * c;
+            nc = c < 0 ? nchunk : c;
         }
+        const long long pre = nc < nchunk ? nc : ch;   // branch-free: re-load at the end
 #pragma unroll
-        for (int j = 0; j < XD; ++j) xa[j] = xn[j];
-        load_x(nb, xn);        // the next chunk's first block in flight during the second
-        body(blk + 1, xa);
-        blk = nb;
+        for (int b = 0; b < kNB; ++b) load_x(pre * kNB + b, xn[b]);
+        body(ch * kNB, xa);
+#ifdef PQH_ASSIGN_STAMPS
+        nbdone += kNB;
+#endif
+        ch = nc;
     }
     if (rq && lane == 0) rq_cnt[seg_id] = qn;
 #ifdef PQH_ASSIGN_STAMPS
@@ -601,8 +663,7 @@ pq_rerank_window(const float* __restrict__ x, long long ldx, int m_total,
         bool lo;
         float xh[XD], xl[XD];
         split_x<D>(xs, X, lo, xh, xl);
-        float bv, tau;
-        screen_bound(X, true, e0_lo, cm, sc, bv, tau);
+        const float bv = screen_bias(X, true, cm);
         bf16x8 Bm[P::PM];
         bf16x8 Bl[P::PL];
         build_b<D>(xh, xl, bv, h, Bm, Bl);
@@ -853,7 +914,7 @@ int launch_mfma(pqh_pq* pq, const float* x, long long n, long long ldx, CodeT* c
                 hipSuccess || per_cu < 1)                                                   \
             per_cu = 1;                                                                     \
         long long gx = (long long)ctx->num_cus * per_cu / groups;                           \
-        gx = std::max(1ll, std::min(gx, ((nblk + 1) / 2 + kWavesPerWG - 1) / kWavesPerWG)); \
+        gx = std::max(1ll, std::min(gx, ((nblk + kNB - 1) / kNB + kWavesPerWG - 1) / kWavesPerWG)); \
         if (gx >= 16) gx &= ~7ll;   /* CU-uniform subspace placement (see the kernel) */   \
         const long long segs_m = gx * kWavesPerWG;                                          \
         const long long segs = segs_m * groups;                                             \
