@@ -64,14 +64,19 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--vectors", type=int, default=1_000_000, help="vectors per GPU")
     ap.add_argument("--mode", choices=["ctx", "noctx"], default="ctx")
-    ap.add_argument("--chunk", type=int, default=16)
+    ap.add_argument("--chunk", type=int, default=8,
+                    help="vectors per decode chunk (chunk-index sidecar granularity)")
     ap.add_argument("--cpu-sample", type=int, default=200_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-overlap", action="store_true",
                     help="serial schedule: no overlap of batch i's code tables with batch i+1")
-    ap.add_argument("--table-cus", type=int, default=64,
-                    help="compute units of the code-table streams in the overlapped schedule")
-    ap.add_argument("--depth", type=int, default=2,
+    ap.add_argument("--table-cus", type=int, default=256,
+                    help="compute units of the code-table streams in the overlapped schedule "
+                         "(>= the device's CU count: no CU mask)")
+    ap.add_argument("--exclusive", action="store_true",
+                    help="overlapped schedule: the other stages run on the CUs the code-table "
+                         "streams do not use (disjoint CU masks)")
+    ap.add_argument("--depth", type=int, default=3,
                     help="overlapped schedule: batches whose code tables are in flight at "
                          "once (one CU-limited stream each); batch i is encoded and decoded "
                          "after batch i+depth's assignment has been queued")
@@ -168,11 +173,15 @@ def main():
         dist.broadcast(ct, 0)
         cent = ct.cpu().numpy()
     overlap = not args.no_overlap
-    sA = torch.cuda.Stream(device=dev)
-    ctx = codec.Context(local, stream=sA)                 # assign/hist/encode/decode
-    # code tables: their own stream, limited to a quarter of the CUs, so batch i's tree
-    # build (latency-bound) runs beside batch i+1's assignment
-    # (latency-bound: consecutive batches' builds overlap each other on `depth` streams)
+    if overlap and args.exclusive:
+        ctx = codec.Context(local, cus=args.table_cus, complement=True)
+        sA = ctx.stream
+    else:
+        sA = torch.cuda.Stream(device=dev)
+        ctx = codec.Context(local, stream=sA)             # assign/hist/encode/decode
+    # code tables: their own streams (optionally CU-limited), so batch i's tree build
+    # (latency-bound) runs beside the assignment of the next batches and the builds of
+    # consecutive batches overlap each other on `depth` streams
     depth = max(1, args.depth) if overlap else 0
     ctxB = [codec.Context(local, cus=args.table_cus) for _ in range(depth)] or [ctx]
     pq = codec.PQ(ctx, cent)

@@ -50,6 +50,9 @@ int pqh_ctx_create(pqh_ctx_t** ctx, int device);
  * spread evenly over the device (hipExtStreamCreateWithCUMask) -- for running the
  * latency-bound code-table build beside the next batch's assignment. */
 int pqh_ctx_create_cu_limited(pqh_ctx_t** ctx, int device, int cus);
+/* As pqh_ctx_create_cu_limited; complement != 0 takes every compute unit the cus-subset does
+ * NOT use, so two contexts (cus, 0) and (cus, 1) run side by side on disjoint CUs. */
+int pqh_ctx_create_cu_split(pqh_ctx_t** ctx, int device, int cus, int complement);
 /* the context's current HIP stream (e.g. for torch.cuda.ExternalStream) */
 void* pqh_ctx_stream(const pqh_ctx_t* ctx);
 int pqh_ctx_destroy(pqh_ctx_t* ctx);

@@ -59,16 +59,17 @@ class Context:
 
     Default: torch's current stream, so torch's fills and copies are ordered with the pqh
     kernels.  cus > 0: the context keeps its own stream limited to that many compute units
-    (pqh_ctx_create_cu_limited); `stream` is then a torch.cuda.ExternalStream over it."""
+    (pqh_ctx_create_cu_split), or with complement=True to all the OTHER compute units;
+    `stream` is then a torch.cuda.ExternalStream over it."""
 
-    def __init__(self, device: int = 0, stream=None, cus: int = 0):
+    def __init__(self, device: int = 0, stream=None, cus: int = 0, complement: bool = False):
         torch = _torch()
         self.device = device
         torch.cuda.set_device(device)
         self.ptr = ctypes.c_void_p()
         if cus > 0:
-            check(lib().pqh_ctx_create_cu_limited(ctypes.byref(self.ptr), device, cus),
-                  "pqh_ctx_create_cu_limited")
+            check(lib().pqh_ctx_create_cu_split(ctypes.byref(self.ptr), device, cus,
+                                                int(complement)), "pqh_ctx_create_cu_split")
             self.stream = torch.cuda.ExternalStream(lib().pqh_ctx_stream(self.ptr), device=device)
             return
         self.stream = stream or torch.cuda.current_stream(device)

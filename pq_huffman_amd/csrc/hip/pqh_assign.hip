@@ -33,6 +33,7 @@
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
@@ -49,6 +50,7 @@ constexpr int kTiles = 8;        // K = 256 centroids = 8 tiles of 32 rows
 #ifndef PQH_ASSIGN_DEFER
 #define PQH_ASSIGN_DEFER 1
 #endif
+constexpr int kRqLds = 128;      // deferred re-rank queue entries per wave (LDS)
 #ifndef PQH_ASSIGN_RED
 #define PQH_ASSIGN_RED 0
 #endif
@@ -119,6 +121,12 @@ struct Slice {
     static constexpr int XD = HALF ? 8 : D;
 };
 
+// the value of lane l ^ 32 (a VALU lane swap, no LDS round trip)
+__device__ __forceinline__ unsigned partner32(unsigned v) {
+    const auto sw = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return (threadIdx.x & 32) ? sw[0] : sw[1];
+}
+
 // ||x||^2 (fp32 fma chain; HALF: plus the partner half-wave's), the bf16 split x = xh + xl
 // (+ r), and whether this lane's slice has any bf16 remainder.
 template <int D>
@@ -156,7 +164,8 @@ __device__ __forceinline__ float screen_bias(float X, bool finite_x, float cm) {
 // "pq_assign error bound"); when no x of the block has a bf16 remainder the split error is
 // 2^-15 P instead of 2^-13 P.  Returns the acceptance gap tau = 2.2 E0.
 __device__ __forceinline__ float screen_tau(float X, bool any_lo, float cm, float sc) {
-    const float Pm = sqrtf(X) * sc * 1.00001f;
+    // v_sqrt_f32 (1 ulp) instead of the correctly rounded expansion: the 1e-5 slack covers it
+    const float Pm = __builtin_amdgcn_sqrtf(X) * sc * 1.00001f;
     const float E0 = (any_lo ? 0x1p-13f : 0x1p-15f) * Pm + 0x1p-22f * cm +
                      0x1p-17f * (2.02f * Pm + 1.01f * cm + 1.05f * X);
     return 2.2f * E0 + 1e-30f;
@@ -239,14 +248,16 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
                const bf16x8* __restrict__ afrag, const float* __restrict__ cent,
                const float* __restrict__ cmax, const float* __restrict__ sqrt_cmax,
                CodeT* __restrict__ codes, uint32_t* __restrict__ counts,
-               unsigned long long* __restrict__ rerank, uint32_t* __restrict__ sched,
-               uint2* __restrict__ rq, int rq_seg, uint32_t* __restrict__ rq_cnt, int gx) {
+               unsigned long long* __restrict__ rerank, uint32_t* __restrict__ sched, int gx) {
     using P = Plan<D>;
     constexpr int K = kTiles * 32;
     __shared__ uint32_t hist[kWavesPerWG][K];
     // the subspace's A fragments, shared by the workgroup's waves (24 KB at D = 16): keeping
-    // them out of VGPRs is what lets 4 waves share each SIMD
+    // them out of VGPRs is what lets several waves share each SIMD
     __shared__ uint4 As[P::PA * kTiles * 64];
+    // each wave's re-rank queue (the LDS budget stays at 32 KB, so a workgroup still fits on
+    // a CU beside a code-table build's 112 KB)
+    __shared__ uint2 rqs[kWavesPerWG][kRqLds];
 
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -277,7 +288,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
 #endif
     const float cm = cmax[m];
     const float sc = sqrt_cmax[m];
-    const float* cbase = cent + (long long)m * K * D;
+    const float* cl = cent + (long long)m * K * D;   // fp32 centroids (L2-resident, 16 KB)
     const long long nblk = (n + 31) / 32;
     unsigned long long slow_count = 0;
 
@@ -298,7 +309,9 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         if constexpr (XD % 4 == 0) {
 #pragma unroll
             for (int j = 0; j < XD; j += 4) {
-                float4 q = *reinterpret_cast<const float4*>(xp + j);
+                // streamed once: non-temporal, so x does not evict the code tables that the
+                // stages around this one read from the Infinity Cache
+                const f32x4 q = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(xp + j));
                 dst[j] = q.x; dst[j + 1] = q.y; dst[j + 2] = q.z; dst[j + 3] = q.w;
             }
         } else {
@@ -307,10 +320,8 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         }
     };
     // Deferred re-rank: a vector whose screening gap is too small is appended to this wave's
-    // segment of the re-rank queue (no atomics: the segment is private) and finished by
-    // pq_rerank_fix; only when the segment is full does the wave re-rank inline.
-    const unsigned seg_id = (unsigned)((m * gx + bx) * kWavesPerWG + wave);
-    uint2* my_rq = rq ? rq + (long long)seg_id * rq_seg : nullptr;
+    // LDS queue and finished after the wave's last chunk (tail_rerank); only when the queue
+    // is full, or x is not finite, does the wave re-rank inline.
     unsigned qn = 0;
 
     // One step = a chunk of kNB consecutive 32-vector blocks, screened together: each tile's
@@ -403,8 +414,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
 #pragma unroll
         for (int b = 0; b < kNB; ++b) {
             // merge the two half-waves (lanes l and l^32 hold the same vector)
-            const unsigned o1 = __shfl_xor(m1[b], 32), o2 = __shfl_xor(m2[b], 32),
-                           ot = __shfl_xor(mt[b], 32);
+            const unsigned o1 = partner32(m1[b]), o2 = partner32(m2[b]), ot = partner32(mt[b]);
             const bool other = o1 < m1[b];
             const unsigned w_h = other ? (unsigned)(1 - h) : (unsigned)h;
             const unsigned w_t = other ? ot : mt[b];
@@ -424,13 +434,12 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
                 // (K1 + tau)(1 + 2^-16) -- see pq_rerank_window; non-finite ones stay inline
                 const unsigned long long fin = need & __ballot(finite_x[b]);
                 const unsigned cnt = (unsigned)__popcll(fin);
-                if (my_rq && cnt && qn + cnt <= (unsigned)rq_seg) {
+                if (PQH_ASSIGN_DEFER && cnt && qn + cnt <= (unsigned)kRqLds) {
                     if (slow && valid[b] && h == 0 && finite_x[b]) {
                         const float thr = (K1 + tau) * (1.0f + 0x1p-16f);
-                        my_rq[qn + __builtin_amdgcn_mbcnt_hi((unsigned)(fin >> 32),
-                                     __builtin_amdgcn_mbcnt_lo((unsigned)fin, 0u))] =
-                            make_uint2((uint32_t)v[b] | (any_lo[b] ? 0x80000000u : 0u),
-                                       __float_as_uint(thr));
+                        rqs[wave][qn + __builtin_amdgcn_mbcnt_hi((unsigned)(fin >> 32),
+                                      __builtin_amdgcn_mbcnt_lo((unsigned)fin, 0u))] =
+                            make_uint2((uint32_t)v[b], __float_as_uint(thr));
                     }
                     qn += cnt;
                     deferred = finite_x[b];
@@ -452,10 +461,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
 #pragma unroll 1
                     for (int q = 0; q < K / 64; ++q) {   // rare path: keep its registers few
                         const int c = lane + 64 * q;
-                        float cv[D];
-#pragma unroll
-                        for (int j = 0; j < D; ++j) cv[j] = cbase[(long long)c * D + j];
-                        const float dd = exact_dist<D>(xv, cv);
+                        const float dd = exact_dist<D>(xv, cl + c * D);
                         if (dd < best) { best = dd; bidx = c; }
                     }
 #pragma unroll
@@ -541,10 +547,86 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
 #endif
         ch = nc;
     }
-    if (rq && lane == 0) rq_cnt[seg_id] = qn;
+    // Tail: this wave's queued vectors, 32 at a time.  thr = (K1 + tau)(1 + 2^-16) bounds the
+    // screened score of every centroid whose fp32 direct-form distance can equal the minimum
+    // (S_k <= D_k + b + E0 <= D_min + b + E0 <= S_k1 + 2 E0 <= K1 (1 + 2^-19) + 2 E0 < thr):
+    // the vectors are re-screened with the main loop's own instruction sequence (bitwise the
+    // same scores: same bias, and a lo pass adds exact zeros for bf16-exact x), the centroids
+    // screening at or below thr are collected per lane, and only those few are evaluated in
+    // exact fp32 direct form (first index among equal distances) -- instead of all K.
+    // The workgroup's waves share their queues (they finish their chunks within about one
+    // chunk of each other): batch j of the concatenated queues goes to wave j % waves.
+    __shared__ unsigned qlen[kWavesPerWG];
+    if (lane == 0) qlen[wave] = qn;
+    __syncthreads();
+    unsigned qoff[kWavesPerWG + 1];
+    qoff[0] = 0;
+#pragma unroll
+    for (int w = 0; w < kWavesPerWG; ++w) qoff[w + 1] = qoff[w] + qlen[w];
+    const unsigned qtot = qoff[kWavesPerWG];
+    for (unsigned e0 = 32u * wave; e0 < qtot; e0 += 32u * kWavesPerWG) {
+        const unsigned e = e0 + (unsigned)r;
+        const bool valid = e < qtot;
+        int qw = 0;
+#pragma unroll
+        for (int w = 1; w < kWavesPerWG; ++w) qw += e >= qoff[w] ? 1 : 0;
+        const uint2 ent = valid ? rqs[qw][e - qoff[qw]] : make_uint2(0u, 0u);
+        const long long v = (long long)ent.x;
+        const float thr = __uint_as_float(ent.y);
+        float xv[D];
+        const float* xp = x + v * ldx + (long long)m * D;
+        if constexpr (D % 4 == 0) {
+#pragma unroll
+            for (int j = 0; j < D; j += 4) {
+                const float4 q = *reinterpret_cast<const float4*>(xp + j);
+                xv[j] = q.x; xv[j + 1] = q.y; xv[j + 2] = q.z; xv[j + 3] = q.w;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < D; ++j) xv[j] = xp[j];
+        }
+        float xs[XD];
+#pragma unroll
+        for (int j = 0; j < XD; ++j) xs[j] = valid ? xv[HALF ? (h ? 8 + j : j) : j] : 0.0f;
+        float X;
+        bool lo;
+        float xh[XD], xl[XD];
+        split_x<D>(xs, X, lo, xh, xl);
+        bf16x8 Bm[P::PM];
+        bf16x8 Bl[P::PL];
+        build_b<D>(xh, xl, screen_bias(X, true, cm), h, Bm, Bl);
+        const bool lo_pass = __any(lo);
+        float best = INFINITY;
+        int bidx = 0x7FFFFFFF;
+#pragma unroll 1
+        for (int t = 0; t < kTiles; ++t) {   // (rolled: the tail keeps its registers few)
+            const f32x16 acc = tile_scores<D>(As, lane, t, Bm, Bl, lo_pass);
+            uint32_t bits = 0;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) bits |= (acc[i] <= thr ? 1u : 0u) << i;
+            bits = valid ? bits : 0u;
+            while (__any(bits != 0)) {
+                if (bits) {
+                    const int i = __builtin_ctz(bits);
+                    bits &= bits - 1;
+                    const int k = tile_row(t, i, h);
+                    const float dd = exact_dist<D>(xv, cl + k * D);
+                    if (dd < best || (dd == best && k < bidx)) { best = dd; bidx = k; }
+                }
+            }
+        }
+        const float ob = __uint_as_float(partner32(__float_as_uint(best)));
+        const int oi = (int)partner32((unsigned)bidx);
+        if (ob < best || (ob == best && oi < bidx)) { best = ob; bidx = oi; }
+        if (valid && h == 0) {
+            const int code = bidx == 0x7FFFFFFF ? 0 : bidx;
+            codes[v * m_total + m] = (CodeT)code;
+            if (counts) atomicAdd(&hist[wave][code], 1u);
+        }
+    }
 #ifdef PQH_ASSIGN_STAMPS
     {
-        const unsigned gw = seg_id;
+        const unsigned gw = (unsigned)((m * gx + bx) * kWavesPerWG + wave);
         if (lane == 0 && gw < (unsigned)kStampWaves) {
             g_assign_stamps[gw][0] = rt0;   // 100 MHz, chip-wide
             g_assign_stamps[gw][1] = __builtin_amdgcn_s_memrealtime();
@@ -561,155 +643,6 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         }
     }
     if (lane == 0 && slow_count) atomicAdd(rerank, slow_count);
-}
-
-// Deferred re-rank (pq_assign_mfma's queue).  Entry = (vector | any_lo << 31, thr): the
-// vector's screening gap was too small, and thr = (K1 + tau)(1 + 2^-16) bounds the screened
-// score of every centroid whose fp32 direct-form distance can equal the minimum
-// (S_k <= D_k + b + E0 <= D_min + b + E0 <= S_k1 + 2 E0 <= K1 (1 + 2^-19) + 2 E0 < thr).
-// Vectors are re-screened 32 at a time with the main kernel's own instruction sequence
-// (bitwise the same scores; E0 with the main block's any_lo, carried in the entry), the
-// centroids screening below thr are collected per lane, and only those few are evaluated in
-// exact fp32 direct form (first index among equal distances) -- instead of all K.
-// grid (G, m): the workgroups of subspace m walk the concatenation of its waves' segments.
-template <int D, typename CodeT>
-__global__ void __launch_bounds__(256, 2)
-pq_rerank_window(const float* __restrict__ x, long long ldx, int m_total,
-                 const bf16x8* __restrict__ afrag, const float* __restrict__ cent,
-                 const float* __restrict__ cmax, const float* __restrict__ sqrt_cmax,
-                 const uint2* __restrict__ rq, int rq_seg, const uint32_t* __restrict__ rq_cnt,
-                 int segs_m, CodeT* __restrict__ codes, uint32_t* __restrict__ counts) {
-    using P = Plan<D>;
-    constexpr int K = kTiles * 32;
-    constexpr int XD = Slice<D>::XD;
-    extern __shared__ __attribute__((aligned(16))) char lds[];
-    uint4* As = reinterpret_cast<uint4*>(lds);
-    float* cl = reinterpret_cast<float*>(As + P::PA * kTiles * 64);   // [K][D]
-    uint32_t* scan = reinterpret_cast<uint32_t*>(cl + K * D);         // [segs_m + 1]
-    __shared__ uint32_t part[256];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int m = blockIdx.y, r = lane & 31, h = lane >> 5;
-    {
-        const uint4* src = reinterpret_cast<const uint4*>(afrag) + (long long)m * P::PA * kTiles * 64;
-        for (int i = tid; i < P::PA * kTiles * 64; i += 256) As[i] = src[i];
-        const float* cb = cent + (long long)m * K * D;
-        for (int i = tid; i < K * D; i += 256) cl[i] = cb[i];
-        // exclusive scan of the subspace's segment counts: per-thread runs, then the runs
-        const uint32_t* cnt = rq_cnt + (long long)m * segs_m;
-        const int run = (segs_m + 255) / 256, b0 = tid * run;
-        uint32_t sum = 0;
-        for (int i = 0; i < run; ++i) sum += b0 + i < segs_m ? cnt[b0 + i] : 0u;
-        part[tid] = sum;
-        __syncthreads();
-        if (tid < 64) {   // wave 0: scan of the 256 run sums, 4 per lane
-            uint32_t a0 = part[4 * tid], a1 = part[4 * tid + 1], a2 = part[4 * tid + 2],
-                     a3 = part[4 * tid + 3];
-            uint32_t tot = a0 + a1 + a2 + a3, inc = tot;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const uint32_t o = __shfl_up(inc, off);
-                if (lane >= off) inc += o;
-            }
-            uint32_t ex = inc - tot;
-            part[4 * tid] = ex;
-            part[4 * tid + 1] = ex + a0;
-            part[4 * tid + 2] = ex + a0 + a1;
-            part[4 * tid + 3] = ex + a0 + a1 + a2;
-        }
-        __syncthreads();
-        uint32_t acc = part[tid];
-        for (int i = 0; i < run; ++i)
-            if (b0 + i < segs_m) { scan[b0 + i] = acc; acc += cnt[b0 + i]; }
-        if (b0 < segs_m && b0 + run >= segs_m) scan[segs_m] = acc;   // total
-        __syncthreads();
-    }
-    const uint32_t total = scan[segs_m];
-    const float cm = cmax[m], sc = sqrt_cmax[m];
-    const long long nb = ((long long)total + 31) / 32;
-    const long long W = (long long)gridDim.x * 4;
-    for (long long b = (long long)blockIdx.x * 4 + wave; b < nb; b += W) {
-        const long long f = b * 32 + r;
-        const bool valid = f < (long long)total;
-        uint2 e = make_uint2(0u, 0u);
-        if (valid) {   // segment s with scan[s] <= f < scan[s + 1] (the last such s)
-            int lo = 0, hi = segs_m - 1;
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (scan[mid] <= (uint32_t)f) lo = mid; else hi = mid - 1;
-            }
-            e = rq[((long long)m * segs_m + lo) * rq_seg + ((uint32_t)f - scan[lo])];
-        }
-        const long long v = (long long)(e.x & 0x7FFFFFFFu);
-        const bool e0_lo = (e.x >> 31) != 0;
-        const float thr = __uint_as_float(e.y);
-        // the full sub-vector (exact distances) and this lane's screening slice
-        float xv[D];
-        const float* xp = x + v * ldx + (long long)m * D;
-        if constexpr (D % 4 == 0) {
-#pragma unroll
-            for (int j = 0; j < D; j += 4) {
-                const float4 q = *reinterpret_cast<const float4*>(xp + j);
-                xv[j] = q.x; xv[j + 1] = q.y; xv[j + 2] = q.z; xv[j + 3] = q.w;
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < D; ++j) xv[j] = xp[j];
-        }
-        float xs[XD];
-#pragma unroll
-        for (int j = 0; j < XD; ++j)
-            xs[j] = valid ? xv[Slice<D>::HALF ? (h ? 8 + j : j) : j] : 0.0f;
-        float X;
-        bool lo;
-        float xh[XD], xl[XD];
-        split_x<D>(xs, X, lo, xh, xl);
-        const float bv = screen_bias(X, true, cm);
-        bf16x8 Bm[P::PM];
-        bf16x8 Bl[P::PL];
-        build_b<D>(xh, xl, bv, h, Bm, Bl);
-        const bool lo_pass = __any(lo);
-        // candidates: bit (t & 1) * 16 + i of word t >> 1
-        uint32_t cw[kTiles / 2];
-#pragma unroll
-        for (int t = 0; t < kTiles; ++t) {
-            const f32x16 acc = tile_scores<D>(As, lane, t, Bm, Bl, lo_pass);
-            uint32_t bits = 0;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) bits |= (acc[i] <= thr ? 1u : 0u) << i;
-            if (t & 1) cw[t >> 1] |= bits << 16; else cw[t >> 1] = bits;
-        }
-        if (!valid) {
-#pragma unroll
-            for (int w = 0; w < kTiles / 2; ++w) cw[w] = 0;
-        }
-        float best = INFINITY;
-        int bidx = 0x7FFFFFFF;
-        while (true) {
-            const uint32_t any = cw[0] | cw[1] | cw[2] | cw[3];
-            if (!__any(any != 0)) break;
-            if (any) {
-                const int w = cw[0] ? 0 : cw[1] ? 1 : cw[2] ? 2 : 3;
-                const uint32_t word = w == 0 ? cw[0] : w == 1 ? cw[1] : w == 2 ? cw[2] : cw[3];
-                const int bit = __builtin_ctz(word);
-                const uint32_t rest = word & (word - 1);
-                cw[0] = w == 0 ? rest : cw[0];
-                cw[1] = w == 1 ? rest : cw[1];
-                cw[2] = w == 2 ? rest : cw[2];
-                cw[3] = w == 3 ? rest : cw[3];
-                const int k = tile_row(2 * w + (bit >> 4), bit & 15, h);
-                const float dd = exact_dist<D>(xv, cl + k * D);
-                if (dd < best || (dd == best && k < bidx)) { best = dd; bidx = k; }
-            }
-        }
-        const float ob = __shfl_xor(best, 32);
-        const int oi = __shfl_xor(bidx, 32);
-        if (ob < best || (ob == best && oi < bidx)) { best = ob; bidx = oi; }
-        if (valid && h == 0) {
-            const int code = bidx == 0x7FFFFFFF ? 0 : bidx;
-            codes[v * m_total + m] = (CodeT)code;
-            if (counts) atomicAdd(&counts[(long long)m * K + code], 1u);
-        }
-    }
 }
 
 // Exact VALU kernel: one thread per (vector, part); any K, any dsub.  Used for shapes the
@@ -887,23 +820,6 @@ int launch_mfma(pqh_pq* pq, const float* x, long long n, long long ldx, CodeT* c
 #else
     uint32_t* sched = pq->m <= kSchedMax ? ctx->d_sched : nullptr;
 #endif
-    // re-rank queue: one segment of kRqSeg entries per wave of the grid (sized below)
-    constexpr int kRqSeg = 1024;
-    auto rq_ensure = [&](long long segs) -> int {
-        if (segs <= ctx->rq_segs) return PQH_OK;
-        if (ctx->d_rq) PQH_HIP(ctx, hipFree(ctx->d_rq));
-        if (ctx->d_rq_cnt) PQH_HIP(ctx, hipFree(ctx->d_rq_cnt));
-        ctx->d_rq = nullptr;
-        ctx->d_rq_cnt = nullptr;
-        ctx->rq_segs = 0;
-        PQH_HIP(ctx, hipMalloc(&ctx->d_rq, (size_t)segs * kRqSeg * sizeof(uint2)));
-        PQH_HIP(ctx, hipMalloc(&ctx->d_rq_cnt, (size_t)segs * sizeof(uint32_t)));
-        ctx->rq_segs = segs;
-        return PQH_OK;
-    };
-    // entries carry the vector id in 31 bits; more segments than the window kernel's LDS
-    // scan holds (only with very small m on a large grid) fall back to inline re-ranking
-    const bool use_rq = PQH_ASSIGN_DEFER && n < 0x80000000ll;
     // grid = the workgroups that are resident at once (persistent, grid-stride over the
     // 32-vector blocks): more would only queue behind the first wave of workgroups
 #define PQH_CASE(DD)                                                                        \
@@ -916,36 +832,13 @@ int launch_mfma(pqh_pq* pq, const float* x, long long n, long long ldx, CodeT* c
         long long gx = (long long)ctx->num_cus * per_cu / groups;                           \
         gx = std::max(1ll, std::min(gx, ((nblk + kNB - 1) / kNB + kWavesPerWG - 1) / kWavesPerWG)); \
         if (gx >= 16) gx &= ~7ll;   /* CU-uniform subspace placement (see the kernel) */   \
-        const long long segs_m = gx * kWavesPerWG;                                          \
-        const long long segs = segs_m * groups;                                             \
-        const size_t fix_lds = (size_t)Plan<DD>::PA * kTiles * 64 * 16 +                    \
-                               (size_t)256 * DD * 4 + (size_t)(segs_m + 1) * 4;             \
-        const bool rq_on = use_rq && fix_lds <= 64 * 1024;                                  \
-        if (rq_on) {                                                                        \
-            int rc = rq_ensure(segs);                                                       \
-            if (rc) return rc;                                                              \
-        }                                                                                   \
         if (sched)                                                                          \
             PQH_HIP(ctx, hipMemsetAsync(sched, 0, (size_t)pq->m * kXcds * kSchedStride * 4,  \
                                         ctx->stream));                                      \
         hipLaunchKernelGGL((pq_assign_mfma<DD, CodeT>), dim3((unsigned)(gx * groups)), block, \
                            0, ctx->stream, x, n, ldx, pq->m, pq->d_afrag, pq->d_cent,       \
-                           pq->d_cmax, pq->d_sqc, codes, counts, rr, sched,                 \
-                           rq_on ? reinterpret_cast<uint2*>(ctx->d_rq) : nullptr, kRqSeg,   \
-                           ctx->d_rq_cnt, (int)gx);                                         \
+                           pq->d_cmax, pq->d_sqc, codes, counts, rr, sched, (int)gx);       \
         PQH_LAUNCH_CHECK(ctx);                                                              \
-        if (rq_on) {                                                                        \
-            /* ~2k waves in all: each takes a few 32-vector batches of the queue */         \
-            const unsigned gf = (unsigned)std::max(1ll, std::min(64ll, 512ll / groups + 1)); \
-            PQH_HIP(ctx, hipFuncSetAttribute((const void*)pq_rerank_window<DD, CodeT>,      \
-                                             hipFuncAttributeMaxDynamicSharedMemorySize,    \
-                                             (int)fix_lds));                                \
-            hipLaunchKernelGGL((pq_rerank_window<DD, CodeT>), dim3(gf, (unsigned)groups),   \
-                               dim3(256), fix_lds, ctx->stream, x, ldx, pq->m, pq->d_afrag, \
-                               pq->d_cent, pq->d_cmax, pq->d_sqc,                           \
-                               reinterpret_cast<const uint2*>(ctx->d_rq), kRqSeg,           \
-                               ctx->d_rq_cnt, (int)segs_m, codes, counts);                  \
-        }                                                                                   \
         break;                                                                              \
     }
     switch (pq->dsub) {

@@ -98,17 +98,20 @@ int pqh_ctx_create(pqh_ctx_t** out, int device) {
     return PQH_OK;
 }
 
-int pqh_ctx_create_cu_limited(pqh_ctx_t** out, int device, int cus) {
+int pqh_ctx_create_cu_split(pqh_ctx_t** out, int device, int cus, int complement) {
     int rc = pqh_ctx_create(out, device);
     if (rc) return rc;
     pqh_ctx* ctx = *out;
     if (cus <= 0 || cus >= ctx->num_cus) return PQH_OK;
-    // every (num_cus / cus)-th compute unit, so the subset spans all XCDs / shader engines
+    // every (num_cus / cus)-th compute unit, so the subset spans all XCDs / shader engines;
+    // complement: every other compute unit (a disjoint partner stream)
     std::vector<uint32_t> mask((ctx->num_cus + 31) / 32, 0u);
     const int stride = std::max(1, ctx->num_cus / cus);
+    std::vector<char> pick(ctx->num_cus, 0);
     int used = 0;
-    for (int cu = 0; cu < ctx->num_cus && used < cus; cu += stride, ++used)
-        mask[cu / 32] |= 1u << (cu % 32);
+    for (int cu = 0; cu < ctx->num_cus && used < cus; cu += stride, ++used) pick[cu] = 1;
+    for (int cu = 0; cu < ctx->num_cus; ++cu)
+        if ((pick[cu] != 0) != (complement != 0)) mask[cu / 32] |= 1u << (cu % 32);
     hipStream_t s = nullptr;
     if (hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
         pqh_ctx_destroy(ctx);
@@ -118,7 +121,14 @@ int pqh_ctx_create_cu_limited(pqh_ctx_t** out, int device, int cus) {
     (void)hipStreamDestroy(ctx->stream);
     ctx->stream = s;
     ctx->own_stream = true;
+    int n_on = 0;   // persistent grids are sized to the CUs this stream can use
+    for (uint32_t w : mask) n_on += __builtin_popcount(w);
+    ctx->num_cus = std::max(1, n_on);
     return PQH_OK;
+}
+
+int pqh_ctx_create_cu_limited(pqh_ctx_t** out, int device, int cus) {
+    return pqh_ctx_create_cu_split(out, device, cus, 0);
 }
 
 void* pqh_ctx_stream(const pqh_ctx_t* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
@@ -131,8 +141,6 @@ int pqh_ctx_destroy(pqh_ctx_t* ctx) {
     if (ctx->d_diag) (void)hipFree(ctx->d_diag);
     if (ctx->lb_state) (void)hipFree(ctx->lb_state);
     if (ctx->d_sched) (void)hipFree(ctx->d_sched);
-    if (ctx->d_rq) (void)hipFree(ctx->d_rq);
-    if (ctx->d_rq_cnt) (void)hipFree(ctx->d_rq_cnt);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return PQH_OK;

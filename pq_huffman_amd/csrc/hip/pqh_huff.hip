@@ -39,16 +39,37 @@ hist_ctx(const CodeT* __restrict__ codes, long long n, int m_total, int k,
     const int m = blockIdx.y;
     const int words = (k * k + 1) / 2;
     for (int w = threadIdx.x; w < words; w += blockDim.x) pairs[w] = 0;
+    constexpr int kRun = kHistChunk / 1024;   // consecutive vectors per thread
+    const long long v0 = (long long)blockIdx.x * kHistChunk + (long long)threadIdx.x * kRun;
+    // this thread's part-m codes of rows v0 - 1 .. v0 + kRun - 1, all loads issued before the
+    // first counter update (8-byte rows of u8 codes: whole rows, 16 B per load)
+    unsigned c[kRun + 1];
+    const bool wide = sizeof(CodeT) == 1 && m_total == 8 && v0 + kRun <= n;
+    if (wide) {
+        const uint4* rows = reinterpret_cast<const uint4*>(codes + v0 * 8);
+        uint4 q[kRun / 2];
+#pragma unroll
+        for (int u = 0; u < kRun / 2; ++u) q[u] = rows[u];
+        c[0] = v0 > 0 ? (unsigned)codes[(v0 - 1) * 8 + m] : (prev_row ? (unsigned)prev_row[m] : ~0u);
+        const int sh = 8 * (m & 3);
+#pragma unroll
+        for (int u = 0; u < kRun / 2; ++u) {
+            const unsigned a = m < 4 ? q[u].x : q[u].y, b = m < 4 ? q[u].z : q[u].w;
+            c[1 + 2 * u] = (a >> sh) & 0xFFu;
+            c[2 + 2 * u] = (b >> sh) & 0xFFu;
+        }
+    } else {
+        for (int u = 0; u <= kRun; ++u) {
+            const long long v = v0 - 1 + u;
+            c[u] = v < 0 ? (prev_row ? (unsigned)prev_row[m] : ~0u)
+                 : v < n ? ld_code(codes, v * m_total + m) : ~0u;
+        }
+    }
     __syncthreads();
-    const long long v0 = (long long)blockIdx.x * kHistChunk;
-    const long long v1 = min(n, v0 + kHistChunk);
-    for (long long v = v0 + threadIdx.x; v < v1; v += blockDim.x) {
-        unsigned prev;
-        if (v > 0) prev = ld_code(codes, (v - 1) * m_total + m);
-        else if (prev_row) prev = ld_code(prev_row, m);
-        else continue;
-        const unsigned cur = ld_code(codes, v * m_total + m);
-        if (prev >= (unsigned)k || cur >= (unsigned)k) continue;  // out-of-alphabet codes
+#pragma unroll
+    for (int u = 1; u <= kRun; ++u) {
+        const unsigned prev = c[u - 1], cur = c[u];
+        if (prev >= (unsigned)k || cur >= (unsigned)k) continue;  // absent / out of alphabet
         const unsigned bin = prev * (unsigned)k + cur;
         atomicAdd(&pairs[bin >> 1], 1u << ((bin & 1u) * 16));
     }

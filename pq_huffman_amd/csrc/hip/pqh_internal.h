@@ -30,10 +30,6 @@ struct pqh_ctx {
     // work-queue heads of the assignment kernel: kXcds per subspace, kSchedStride words
     // apart, zeroed before every launch
     uint32_t* d_sched = nullptr;
-    // deferred re-rank queue of the assignment kernel: rq_segs segments (one per wave)
-    void* d_rq = nullptr;          // uint2 entries (vector | any_lo << 31, threshold)
-    uint32_t* d_rq_cnt = nullptr;
-    long long rq_segs = 0;
 };
 constexpr int kSchedMax = 64;      // subspaces with a work queue (more: static schedule)
 constexpr int kXcds = 8;

@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "pqh_internal.h"
@@ -959,12 +960,26 @@ int pqh_tables_build(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts) 
     PQH_HIP(ctx, hipMemsetAsync(t->d_enc, 0, (size_t)t->m * t->items * 8, ctx->stream));
     const long long trees = t->tables;
     if (t->k <= 256) {
-        constexpr int TPW = 32;
-        const size_t lds = (size_t)TPW * (512 * 4 + 256 * 4 + 256 * 2);
-        PQH_HIP(ctx, hipFuncSetAttribute((const void*)huff_trees_small<TPW>,
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL((huff_trees_small<TPW>), dim3((unsigned)((trees + TPW - 1) / TPW)),
-                           dim3(64), lds, ctx->stream, d_counts, t->k, trees, t->d_enc, t->d_err);
+        // trees per workgroup: fewer = more, smaller workgroups (3.5 KB of LDS per tree), so
+        // the build spreads over more CUs and leaves each CU's LDS to concurrent kernels
+        static const int tpw_env = [] {
+            const char* e = std::getenv("PQH_TREE_TPW");
+            const int v = e ? std::atoi(e) : 0;
+            return v == 8 || v == 16 || v == 32 ? v : 32;
+        }();
+        auto launch = [&](auto tpw_c) -> int {
+            constexpr int TPW = decltype(tpw_c)::value;
+            const size_t lds = (size_t)TPW * (512 * 4 + 256 * 4 + 256 * 2);
+            PQH_HIP(ctx, hipFuncSetAttribute((const void*)huff_trees_small<TPW>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            hipLaunchKernelGGL((huff_trees_small<TPW>), dim3((unsigned)((trees + TPW - 1) / TPW)),
+                               dim3(64), lds, ctx->stream, d_counts, t->k, trees, t->d_enc, t->d_err);
+            return PQH_OK;
+        };
+        rc = tpw_env == 8 ? launch(std::integral_constant<int, 8>{})
+           : tpw_env == 32 ? launch(std::integral_constant<int, 32>{})
+                           : launch(std::integral_constant<int, 16>{});
+        if (rc) return rc;
     } else {
         constexpr int TPW = 1;
         const size_t lds = (size_t)4096 * TPW * (16 + 4 + 4 + 2);
