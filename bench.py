@@ -60,26 +60,23 @@ def pmc_traffic(kernel):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--vectors", type=int, default=1_000_000, help="vectors per GPU")
     ap.add_argument("--mode", choices=["ctx", "noctx"], default="ctx")
     ap.add_argument("--chunk", type=int, default=8,
                     help="vectors per decode chunk (chunk-index sidecar granularity)")
     ap.add_argument("--cpu-sample", type=int, default=200_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-overlap", action="store_true",
-                    help="serial schedule: no overlap of batch i's code tables with batch i+1")
-    ap.add_argument("--table-cus", type=int, default=256,
-                    help="compute units of the code-table streams in the overlapped schedule "
-                         "(>= the device's CU count: no CU mask)")
-    ap.add_argument("--exclusive", action="store_true",
-                    help="overlapped schedule: the other stages run on the CUs the code-table "
-                         "streams do not use (disjoint CU masks)")
-    ap.add_argument("--depth", type=int, default=3,
-                    help="overlapped schedule: batches whose code tables are in flight at "
-                         "once (one CU-limited stream each); batch i is encoded and decoded "
-                         "after batch i+depth's assignment has been queued")
+    ap.add_argument("--sched", choices=["lanes", "serial"], default="lanes",
+                    help="'lanes': assignment + histogram on one stream, each batch's code "
+                         "tables, encode and decode on one of --lanes streams (overlapped); "
+                         "'serial': every stage in order on one stream")
+    ap.add_argument("--no-overlap", action="store_true", help="same as --sched serial")
+    ap.add_argument("--lanes", type=int, default=3,
+                    help="streams taking batches round robin for tables + encode + decode")
+    ap.add_argument("--table-cus", type=int, default=0,
+                    help="limit each lane stream to this many CUs (0: no CU mask)")
     return ap.parse_args()
 
 
@@ -172,33 +169,39 @@ def main():
         ct = torch.from_numpy(cent).to(dev)
         dist.broadcast(ct, 0)
         cent = ct.cpu().numpy()
-    overlap = not args.no_overlap
-    if overlap and args.exclusive:
-        ctx = codec.Context(local, cus=args.table_cus, complement=True)
-        sA = ctx.stream
-    else:
-        sA = torch.cuda.Stream(device=dev)
-        ctx = codec.Context(local, stream=sA)             # assign/hist/encode/decode
-    # code tables: their own streams (optionally CU-limited), so batch i's tree build
-    # (latency-bound) runs beside the assignment of the next batches and the builds of
-    # consecutive batches overlap each other on `depth` streams
-    depth = max(1, args.depth) if overlap else 0
-    ctxB = [codec.Context(local, cus=args.table_cus) for _ in range(depth)] or [ctx]
+    # Streams.  A = torch's current (default) stream: assignment + histogram of every batch.
+    # `lanes` library streams (non-blocking): lane i % lanes builds batch i's code tables,
+    # encodes and decodes it, with its own tables and stream buffers.  So batch i's tree
+    # build (latency-bound) and encode/decode run beside the assignment of the batches after
+    # it, and consecutive batches' builds overlap each other.  1 + lanes = 4 streams: with 4
+    # hardware queues per process (GPU_MAX_HW_QUEUES, HIP's default) none share a queue.
+    # Serial: everything on A, in order.
+    serial = args.sched == "serial" or args.no_overlap
+    ctx = codec.Context(local)
+    sA = ctx.stream
+    nl = 1 if serial else max(1, args.lanes)
+    # (cus >= the device's CU count: a library stream of its own without a CU mask)
+    lanes = [ctx] if serial else [codec.Context(local, cus=args.table_cus or 1 << 20)
+                                  for _ in range(nl)]
     pq = codec.PQ(ctx, cent)
     items = k * k if ctxm else k
-    slots = depth + 1
+    slots = nl + 1            # codes / counts: the assignment runs ahead of the lanes
     codes = [torch.empty((n, m), dtype=torch.uint8, device=dev) for _ in range(slots)]
     counts = [torch.zeros((m, items), dtype=torch.int32, device=dev) for _ in range(slots)]
-    tabs = [codec.Tables(ctx, m, k, ctxm) for _ in range(slots)]
     halo = [None] * slots
     ev_hist = [torch.cuda.Event() for _ in range(slots)]
     ev_tab = [torch.cuda.Event() for _ in range(slots)]
-    dec = torch.empty_like(codes[0])
+    ev_enc = [torch.cuda.Event() for _ in range(slots)]
+    used = [False] * slots    # slot s has held a batch (its events were recorded)
     chunks = (n + args.chunk - 1) // args.chunk
-    coff = torch.empty(chunks, dtype=torch.int64, device=dev)
-    cprev = torch.empty((chunks, m), dtype=torch.uint8, device=dev) if ctxm else None
-    out = torch.zeros(n * m * 56 // 8 + 64, dtype=torch.uint8, device=dev)  # worst case
-    tot_dev = torch.zeros(1, dtype=torch.int64, device=dev)
+    tabs = [codec.Tables(c, m, k, ctxm) for c in lanes]
+    dec = [torch.empty((n, m), dtype=torch.uint8, device=dev) for _ in lanes]
+    coff = [torch.empty(chunks, dtype=torch.int64, device=dev) for _ in lanes]
+    cprev = [torch.empty((chunks, m), dtype=torch.uint8, device=dev) if ctxm else None
+             for _ in lanes]
+    out = [torch.zeros(n * m * 56 // 8 + 64, dtype=torch.uint8, device=dev)  # worst case
+           for _ in lanes]
+    tot_dev = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in lanes]
     raw_first = shard.raw_first(rank)
     stages = ("assign", "hist", "codebook", "encode", "decode")
     events = []          # (stage, start, end) of timed steps, read after the timed region
@@ -217,16 +220,22 @@ def main():
         if e1 is not None:
             e1.record(stream)
 
-    def front(i):
-        """batch i: assignment + histogram (stream A), then its code tables (stream B)"""
-        s = i % slots
+    def step(i):
+        """batch i: assignment + histogram on A, then tables, encode, decode on its lane"""
+        s, j = i % slots, i % nl
+        c = lanes[j]
+        sL = c.stream
         with torch.cuda.stream(sA):
+            if used[s]:              # the slot's previous batch: encoded (codes[s] free) ...
+                sA.wait_event(ev_enc[s])
             e = rec("assign", sA)
             pq.assign(x, codes[s])
             done(e, sA)
             tc = time.perf_counter()
             halo[s] = shard.exchange_halo(codes[s][-1], world, rank) if ctxm else None
             acc["collectives"] += time.perf_counter() - tc if state["timed"] else 0.0
+            if used[s]:              # ... and its tables built (counts[s] free)
+                sA.wait_event(ev_tab[s])
             e = rec("hist", sA)
             counts[s].zero_()
             codec.histogram(ctx, codes[s], k, ctxm, prev_row=halo[s], counts=counts[s])
@@ -235,51 +244,37 @@ def main():
             shard.reduce_counts(counts[s], world)
             acc["collectives"] += time.perf_counter() - tc if state["timed"] else 0.0
             ev_hist[s].record(sA)
-        cB = ctxB[i % len(ctxB)]
-        sB = cB.stream
-        sB.wait_event(ev_hist[s])
-        e = rec("codebook", sB)
-        tabs[s].build(counts[s], cB)              # GPU trees + lookup tables, no host trip
-        done(e, sB)
-        ev_tab[s].record(sB)
-
-    def back(i):
-        """batch i: encode + decode (stream A) once its tables are built"""
-        s = i % slots
-        with torch.cuda.stream(sA):
-            sA.wait_event(ev_tab[s])
-            e = rec("encode", sA)
+        used[s] = True
+        with torch.cuda.stream(sL):
+            sL.wait_event(ev_hist[s])
+            e = rec("codebook", sL)
+            tabs[j].build(counts[s], c)          # GPU trees + lookup tables, no host trip
+            done(e, sL)
+            ev_tab[s].record(sL)
+            e = rec("encode", sL)
             tc = time.perf_counter()
             if world > 1:   # place the shard in the global stream before writing it
-                total = codec.encode_size(ctx, tabs[s], codes[s], raw_first, halo[s])
+                total = codec.encode_size(c, tabs[j], codes[s], raw_first, halo[s])
                 goff, _ = shard.bit_offsets(total, world, rank)
                 bit_off = shard.local_bit_offset(goff)
-                out[:4].zero_()   # bits before bit_off belong to the previous shard
+                out[j][:4].zero_()   # bits before bit_off belong to the previous shard
             else:
                 bit_off = 0
             acc["collectives"] += time.perf_counter() - tc if state["timed"] else 0.0
             # one pass: look-back offsets, every word stored once (no zeroing of `out`)
-            codec.encode_write(ctx, tabs[s], codes[s], out, bit_off, raw_first, halo[s],
-                               args.chunk, coff, cprev, total=tot_dev)
-            done(e, sA)
-            enc = codec.Encoded(out, -1, args.chunk, coff, cprev, n, raw_first)
-            e = rec("decode", sA)
-            codec.decode(ctx, tabs[s], enc, out=dec)
-            done(e, sA)
-        state["last_slot"] = s
+            codec.encode_write(c, tabs[j], codes[s], out[j], bit_off, raw_first, halo[s],
+                               args.chunk, coff[j], cprev[j], total=tot_dev[j])
+            done(e, sL)
+            ev_enc[s].record(sL)
+            enc = codec.Encoded(out[j], -1, args.chunk, coff[j], cprev[j], n, raw_first)
+            e = rec("decode", sL)
+            codec.decode(c, tabs[j], enc, out=dec[j])
+            done(e, sL)
+        state["last"] = (s, j)
 
     def run(steps):
-        if overlap:      # software pipeline: batch i's tables overlap the assignment of
-            for i in range(steps):          # batches i+1 .. i+depth and each other
-                front(i)
-                if i >= depth:
-                    back(i - depth)
-            for i in range(max(0, steps - depth), steps):
-                back(i)
-        else:
-            for i in range(steps):
-                front(i)
-                back(i)
+        for i in range(steps):   # every dependency is an event: issue the batches in order
+            step(i)
 
     def barrier():
         torch.cuda.synchronize()
@@ -301,16 +296,16 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    s_last = state["last_slot"]
-    codes_last, tabs_last = codes[s_last], tabs[s_last]
+    s_last, j_last = state["last"]
 
-    # correctness after timing (not timed): exact round trip + oracle parity spot checks
-    codec.decode_status(ctx)
-    codec.encode_status(ctx)
-    assert torch.equal(dec, codes_last), "round trip mismatch"
+    # correctness after timing (not timed): exact round trip of the last batch, status words
+    for j, c in enumerate(lanes):
+        codec.decode_status(c)
+        codec.encode_status(c)
+        tabs[j].status()
+    assert torch.equal(dec[j_last], codes[s_last]), "round trip mismatch"
     rerank = pq.rerank_count()
-    tabs_last.status()
-    bits_per_vec = int(tot_dev.item()) / n
+    bits_per_vec = int(tot_dev[j_last].item()) / n
 
     if rank == 0:
         t_assign = acc["assign"] / args.steps
@@ -337,11 +332,12 @@ def main():
                                       "no sort" if ctxm else "non-context Huffman, no sort"),
                        "vectors_per_gpu": n, "m": m, "k": k, "mode": args.mode,
                        "chunk_vectors": args.chunk, "parallelism": f"dp{world} row shards",
-                       "schedule": ("pipelined: batch i's code tables (tree build, latency-bound) "
-                                    f"on one of {depth} {args.table_cus}-CU streams beside the "
-                                    f"assignment of batches i+1..i+{depth}; every timed step "
-                                    "runs all five stages, the pipeline fills and drains inside "
-                                    "the timed region" if overlap else "serial")},
+                       "schedule": ("serial" if serial else
+                                    f"lanes: assignment + histogram of every batch on one stream; "
+                                    f"batch i's code tables, encode and decode on lane stream "
+                                    f"i % {nl}, beside the assignment of the next batches; "
+                                    "every timed step runs all five stages and the pipeline "
+                                    "fills and drains inside the timed region")},
             "roofline": {"kernel": "pq_assign_mfma", "bound": "hbm",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -349,10 +345,15 @@ def main():
                          "bytes_per_vector": BYTES_PER_VEC_READ + BYTES_PER_VEC_WRITE,
                          "avg_ms": round(t_assign * 1e3, 4)},
             "stages_ms": {s: round(v / args.steps * 1e3, 4) for s, v in acc.items()},
-            "stages_note": ("per-stage HIP-event times; in the pipelined schedule 'codebook' "
-                            "overlaps the next batch's 'assign'" if overlap else "serial"),
-            # encode-side HBM-read roofline = 512 B/vec x N / t_encode / 8 TB/s
+            "stages_note": ("per-stage HIP-event times on their own streams" +
+                            ("" if serial else "; the stages of consecutive batches run "
+                             "concurrently, so they sum to more than ms_per_step")),
+            # encode-side HBM-read roofline = 512 B/vec x N / t_encode / 8 TB/s, with
+            # t_encode = the summed encode-side stage times of one batch (latency view) and,
+            # for the throughput view, the whole round-trip step time
             "encode_read_roofline_frac": round(BYTES_PER_VEC_READ * n / t_enc / 1e9 / HBM_PEAK_GBS, 4),
+            "roundtrip_read_roofline_frac": round(
+                BYTES_PER_VEC_READ * n * world * args.steps / elapsed / 1e9 / HBM_PEAK_GBS / world, 4),
             "bits_per_vector": round(bits_per_vec, 3),
             "rerank_fraction": round(rerank / (n * m), 6),
         }
