@@ -309,9 +309,9 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         if constexpr (XD % 4 == 0) {
 #pragma unroll
             for (int j = 0; j < XD; j += 4) {
-                // streamed once: non-temporal, so x does not evict the code tables that the
-                // stages around this one read from the Infinity Cache
-                const f32x4 q = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(xp + j));
+                // (plain loads: the 8 subspaces read the two 64-B halves of each row's lines,
+                // and non-temporal loads re-fetch the line per half -- 1.6x the HBM bytes)
+                const f32x4 q = *reinterpret_cast<const f32x4*>(xp + j);
                 dst[j] = q.x; dst[j + 1] = q.y; dst[j + 2] = q.z; dst[j + 3] = q.w;
             }
         } else {
