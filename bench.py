@@ -220,8 +220,8 @@ def main():
         if e1 is not None:
             e1.record(stream)
 
-    def step(i):
-        """batch i: assignment + histogram on A, then tables, encode, decode on its lane"""
+    def front(i):
+        """batch i: assignment + histogram on A, then its code tables on its lane"""
         s, j = i % slots, i % nl
         c = lanes[j]
         sL = c.stream
@@ -251,19 +251,27 @@ def main():
             tabs[j].build(counts[s], c)          # GPU trees + lookup tables, no host trip
             done(e, sL)
             ev_tab[s].record(sL)
+
+    def back(i):
+        """batch i: encode + decode on its lane (queued behind its tables)"""
+        s, j = i % slots, i % nl
+        c = lanes[j]
+        sL = c.stream
+        with torch.cuda.stream(sL):
             e = rec("encode", sL)
             tc = time.perf_counter()
-            if world > 1:   # place the shard in the global stream before writing it
+            if world > 1:   # place the shard in the global stream before writing it: sizes,
+                # all-gather + prefix sum on the device, offset read by the kernel (no host sync)
                 total = codec.encode_size(c, tabs[j], codes[s], raw_first, halo[s])
-                goff, _ = shard.bit_offsets(total, world, rank)
-                bit_off = shard.local_bit_offset(goff)
-                out[j][:4].zero_()   # bits before bit_off belong to the previous shard
+                goff, _ = shard.bit_offsets_device(total, world, rank)
+                out[j][:4].zero_()   # bits before the offset belong to the previous shard
+                acc["collectives"] += time.perf_counter() - tc if state["timed"] else 0.0
+                codec.encode_write_at(c, tabs[j], codes[s], out[j], goff, raw_first, halo[s],
+                                      args.chunk, coff[j], cprev[j], total=tot_dev[j])
             else:
-                bit_off = 0
-            acc["collectives"] += time.perf_counter() - tc if state["timed"] else 0.0
-            # one pass: look-back offsets, every word stored once (no zeroing of `out`)
-            codec.encode_write(c, tabs[j], codes[s], out[j], bit_off, raw_first, halo[s],
-                               args.chunk, coff[j], cprev[j], total=tot_dev[j])
+                # one pass: look-back offsets, every word stored once (no zeroing of `out`)
+                codec.encode_write(c, tabs[j], codes[s], out[j], 0, raw_first, halo[s],
+                                   args.chunk, coff[j], cprev[j], total=tot_dev[j])
             done(e, sL)
             ev_enc[s].record(sL)
             enc = codec.Encoded(out[j], -1, args.chunk, coff[j], cprev[j], n, raw_first)
@@ -272,9 +280,19 @@ def main():
             done(e, sL)
         state["last"] = (s, j)
 
+    # Every dependency is an event, so batches are issued in order.  With world > 1 the
+    # collectives of all streams run in issue order on the process group's one stream: batch
+    # i's bit-offset all-gather (which waits for its tables) is issued after the halo and
+    # histogram collectives of batch i + lag, so those never queue behind a table build.
+    lag = 0 if world == 1 or serial else nl - 1
+
     def run(steps):
-        for i in range(steps):   # every dependency is an event: issue the batches in order
-            step(i)
+        for i in range(steps):
+            front(i)
+            if i >= lag:
+                back(i - lag)
+        for i in range(max(0, steps - lag), steps):
+            back(i)
 
     def barrier():
         torch.cuda.synchronize()

@@ -157,6 +157,18 @@ int pqh_encode_write(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes,
                      unsigned long long* d_chunk_offsets, void* d_chunk_prev,
                      unsigned long long* d_total_bits);
 
+/* pqh_encode_write for one shard of a multi-GPU stream, with the shard's GLOBAL bit offset
+ * read from device memory (the exclusive scan of the shards' pqh_encode_size totals, e.g.
+ * an all-gather + prefix sum on the device): no host round trip.  The shard is written at
+ * bit (offset % 32) of d_out, whose word 0 is the global stream's word offset / 32, so the
+ * shards' buffers compose by OR-ing their boundary words. */
+int pqh_encode_write_at(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes, long long n,
+                        int raw_first, const void* d_prev_row,
+                        const unsigned long long* d_global_bit_offset, unsigned char* d_out,
+                        unsigned long long out_bytes, int chunk_vectors,
+                        unsigned long long* d_chunk_offsets, void* d_chunk_prev,
+                        unsigned long long* d_total_bits);
+
 /* Synchronises; PQH_ERR_CAPACITY if a pqh_encode_write since the last call had to drop
  * words because out_bytes was too small (nothing is written out of bounds). */
 int pqh_encode_status(pqh_ctx_t* ctx);

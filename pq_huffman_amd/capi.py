@@ -112,6 +112,7 @@ SIGNATURES = [
     ("pqh_codebooks_build", I, [P, I, I, I, P, I]),
     ("pqh_encode_size", I, [P, P, P, LL, I, P, P]),
     ("pqh_encode_write", I, [P, P, P, LL, I, P, ULL, P, ULL, I, P, P, P]),
+    ("pqh_encode_write_at", I, [P, P, P, LL, I, P, P, P, ULL, I, P, P, P]),
     ("pqh_decode", I, [P, P, P, ULL, LL, I, I, P, P, P]),
     ("pqh_decode_status", I, [P]), ("pqh_encode_status", I, [P]),
     ("pqh_chunk_index_host", I, [P, P, ULL, LL, I, I, P, P]),

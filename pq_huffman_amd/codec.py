@@ -357,6 +357,20 @@ def encode_write(ctx: Context, tables: Tables, codes, out, bit_offset: int = 0, 
     return total
 
 
+def encode_write_at(ctx: Context, tables: Tables, codes, out, global_bit_offset, raw_first: int = 1,
+                    prev_row=None, chunk_vectors: int = 64, chunk_offsets=None, chunk_prev=None,
+                    total=None):
+    """encode_write for one shard of a multi-GPU stream: the shard's global bit offset is a
+    device int64[1] (shard.bit_offsets_device), so no host round trip; the shard lands at
+    bit (offset % 32) of `out`."""
+    check(lib().pqh_encode_write_at(ctx.ptr, tables.ptr, _ptr(codes), codes.shape[0], raw_first,
+                                    _ptr(prev_row), _ptr(global_bit_offset), _ptr(out),
+                                    out.numel(), chunk_vectors, _ptr(chunk_offsets),
+                                    _ptr(chunk_prev), _ptr(total)),
+          "pqh_encode_write_at: " + ctx.last_error())
+    return total
+
+
 def encode(ctx: Context, tables: Tables, codes, chunk_vectors: int = 64, raw_first: int = 1,
            prev_row=None) -> Encoded:
     torch = _torch()

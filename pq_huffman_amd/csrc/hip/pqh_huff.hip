@@ -304,7 +304,9 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
             int raw_first, const CodeT* __restrict__ prev_row,
             const unsigned long long* __restrict__ enc, const uint32_t* __restrict__ enc32,
             long long items,
-            unsigned long long bit_offset, uint32_t* __restrict__ out_words, long long cap_words,
+            unsigned long long bit_offset_arg,
+            const unsigned long long* __restrict__ d_bit_offset,
+            uint32_t* __restrict__ out_words, long long cap_words,
             int chunk_vectors, unsigned long long* __restrict__ chunk_off,
             CodeT* __restrict__ chunk_prev, unsigned long long* __restrict__ err,
             unsigned long long* __restrict__ state, unsigned long long* __restrict__ tails,
@@ -316,6 +318,9 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
     __shared__ unsigned long long s_excl;
     __shared__ uint32_t s_head;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    // d_bit_offset: the shard's GLOBAL bit offset, produced on the device (multi-GPU, no host
+    // round trip); the shard's own buffer starts at its word, so only offset % 32 matters
+    const unsigned long long bit_offset = d_bit_offset ? (*d_bit_offset & 31ull) : bit_offset_arg;
     if (tid == 0) s_id = (long long)(atomicAdd(ticket, 1ull) - ticket_base);
     __syncthreads();
     const long long id = s_id;
@@ -571,11 +576,13 @@ int pqh_encode_size(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes, 
     return run_size(ctx, t, d_codes, n, raw_first, d_prev_row, d_total_bits);
 }
 
-int pqh_encode_write(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes, long long n,
-                     int raw_first, const void* d_prev_row, unsigned long long bit_offset,
-                     unsigned char* d_out, unsigned long long out_bytes, int chunk_vectors,
-                     unsigned long long* d_chunk_offsets, void* d_chunk_prev,
-                     unsigned long long* d_total_bits) {
+static int encode_write_impl(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes,
+                             long long n, int raw_first, const void* d_prev_row,
+                             unsigned long long bit_offset,
+                             const unsigned long long* d_bit_offset, unsigned char* d_out,
+                             unsigned long long out_bytes, int chunk_vectors,
+                             unsigned long long* d_chunk_offsets, void* d_chunk_prev,
+                             unsigned long long* d_total_bits) {
     if (!ctx || !t || n < 0 || (n > 0 && (!d_codes || !d_out))) return PQH_ERR_ARG;
     if ((reinterpret_cast<uintptr_t>(d_out) & 3u) || (out_bytes & 3u))
         return pqh_set_error(ctx, PQH_ERR_ARG, "stream buffer must be 4-byte aligned and sized");
@@ -619,7 +626,8 @@ int pqh_encode_write(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes,
         hipLaunchKernelGGL((enc_onepass<T, MAXM>), dim3((unsigned)nb), dim3(kEncBlock), lds,       \
                            ctx->stream, static_cast<const T*>(d_codes), n, t->m, t->k,            \
                            t->context, raw_first, static_cast<const T*>(d_prev_row), t->d_enc,    \
-                           t->d_enc32, t->items, bit_offset, words, (long long)(out_bytes / 4),               \
+                           t->d_enc32, t->items, bit_offset, d_bit_offset, words,                 \
+                           (long long)(out_bytes / 4),                                            \
                            chunk_vectors, d_chunk_offsets, static_cast<T*>(d_chunk_prev),         \
                            ctx->d_diag + 2, st, tails, ticket, ctx->lb_ticket_base,               \
                            (unsigned)ctx->lb_epoch, nb, total);                                   \
@@ -637,6 +645,28 @@ int pqh_encode_write(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes,
     PQH_LAUNCH_CHECK(ctx);
     ctx->lb_ticket_base += (unsigned long long)nb;
     return PQH_OK;
+}
+
+int pqh_encode_write(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes, long long n,
+                     int raw_first, const void* d_prev_row, unsigned long long bit_offset,
+                     unsigned char* d_out, unsigned long long out_bytes, int chunk_vectors,
+                     unsigned long long* d_chunk_offsets, void* d_chunk_prev,
+                     unsigned long long* d_total_bits) {
+    return encode_write_impl(ctx, t, d_codes, n, raw_first, d_prev_row, bit_offset, nullptr,
+                             d_out, out_bytes, chunk_vectors, d_chunk_offsets, d_chunk_prev,
+                             d_total_bits);
+}
+
+int pqh_encode_write_at(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes, long long n,
+                        int raw_first, const void* d_prev_row,
+                        const unsigned long long* d_global_bit_offset, unsigned char* d_out,
+                        unsigned long long out_bytes, int chunk_vectors,
+                        unsigned long long* d_chunk_offsets, void* d_chunk_prev,
+                        unsigned long long* d_total_bits) {
+    if (!d_global_bit_offset) return PQH_ERR_ARG;
+    return encode_write_impl(ctx, t, d_codes, n, raw_first, d_prev_row, 0, d_global_bit_offset,
+                             d_out, out_bytes, chunk_vectors, d_chunk_offsets, d_chunk_prev,
+                             d_total_bits);
 }
 
 // diagnostics only: phase stamps of the mid-grid workgroup of the last one-pass encode

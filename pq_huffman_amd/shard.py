@@ -65,6 +65,21 @@ def bit_offsets(total_bits, world: int, rank: int, group=None) -> Tuple[int, int
     return sum(host[:rank]), sum(host)
 
 
+def bit_offsets_device(total_bits, world: int, rank: int, group=None):
+    """bit_offsets without a host round trip: (this shard's global bit offset, the global
+    length) as (1,) int64 device tensors, from an all-gather of the shards' lengths and a
+    prefix sum on the device -- for pqh_encode_write_at."""
+    import torch
+    import torch.distributed as dist
+    t = total_bits.reshape(1).to(torch.int64)
+    if world == 1:
+        return torch.zeros_like(t), t.clone()
+    everyone = torch.empty(world, dtype=torch.int64, device=t.device)
+    dist.all_gather_into_tensor(everyone, t, group=group)
+    excl = torch.cumsum(everyone, 0) - everyone
+    return excl[rank:rank + 1].clone(), everyone.sum().reshape(1)
+
+
 def local_bit_offset(global_offset: int) -> int:
     """Bit offset inside the shard's own buffer, which starts at global word offset // 32."""
     return global_offset % 32

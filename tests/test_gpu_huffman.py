@@ -96,6 +96,50 @@ def test_sharded_encode_composes(gpu, oracle, ctxm):
     assert out[:len(stream)].cpu().numpy().tobytes() == stream
 
 
+@pytest.mark.parametrize("ctxm", [True, False])
+def test_sharded_encode_device_offsets(gpu, oracle, ctxm):
+    """Three shards, each written into a buffer of its own by pqh_encode_write_at with its
+    global bit offset in device memory (the multi-GPU path: no host round trip), stitched
+    by shard.stitch == the oracle's one-shot stream; each shard decodes from its own chunk
+    index."""
+    torch, codec, ctx = gpu
+    from pq_huffman_amd import shard
+    codes = datagen.skewed_codes(7001, 8, seed=41)
+    cd, cbs = _codebooks_from_gpu_hist(gpu, codes, 256, ctxm)
+    tabs = codec.Tables.from_codebooks(ctx, cbs)
+    cuts = [0, 2500, 4999, 7001]
+    totals, parts = [], []
+    for r in range(3):
+        piece = cd[cuts[r]:cuts[r + 1]]
+        prev = cd[cuts[r] - 1] if (ctxm and r > 0) else None
+        totals.append(codec.encode_size(ctx, tabs, piece, 1 if r == 0 else 0, prev))
+        parts.append((piece, prev))
+    offs = torch.cumsum(torch.cat(totals), 0) - torch.cat(totals)   # device prefix sum
+    shards = []
+    for r, (piece, prev) in enumerate(parts):
+        goff = offs[r:r + 1].clone()
+        out = torch.zeros(piece.shape[0] * 8 * 7 + 64, dtype=torch.uint8, device="cuda")
+        nch = (piece.shape[0] + 15) // 16
+        coff = torch.empty(nch, dtype=torch.int64, device="cuda")
+        cprev = torch.empty((nch, 8), dtype=torch.uint8, device="cuda") if ctxm else None
+        tot = torch.zeros(1, dtype=torch.int64, device="cuda")
+        codec.encode_write_at(ctx, tabs, piece, out, goff, 1 if r == 0 else 0, prev, 16,
+                              coff, cprev, total=tot)
+        codec.encode_status(ctx)
+        g = int(goff.item())
+        bits = int(tot.item())
+        assert bits == int(totals[r].item())
+        enc = codec.Encoded(out, -1, 16, coff, cprev, piece.shape[0], 1 if r == 0 else 0)
+        dec = codec.decode(ctx, tabs, enc)
+        codec.decode_status(ctx)
+        assert torch.equal(dec, piece), r
+        shards.append((out.cpu().numpy().tobytes(), g, bits))
+    total_bits = sum(s[2] for s in shards)
+    stream, obits = oracle.encode(codes, oracle.build_codebooks(codes, 256, ctxm))
+    assert obits == total_bits
+    assert shard.stitch(shards, total_bits)[:len(stream)] == stream
+
+
 def test_corrupt_stream_is_reported(gpu):
     torch, codec, ctx = gpu
     codes = np.zeros((100, 2), np.uint8)

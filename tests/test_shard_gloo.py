@@ -94,6 +94,10 @@ def _worker(rank, world, port, n, m, k, context, q):
         # exact bit length first (the size pass), then place the shard
         _, nbits = _pack(mine, cbs, shard.raw_first(rank), prev, 0)
         goff, total = shard.bit_offsets(torch.tensor([nbits], dtype=torch.int64), world, rank)
+        # the host-sync-free form the GPU bench feeds to pqh_encode_write_at
+        goff_d, total_d = shard.bit_offsets_device(torch.tensor([nbits], dtype=torch.int64),
+                                                   world, rank)
+        assert (int(goff_d.item()), int(total_d.item())) == (goff, total)
         buf, nb2 = _pack(mine, cbs, shard.raw_first(rank), prev, shard.local_bit_offset(goff))
         assert nb2 == nbits
         pieces = [None] * world
