@@ -225,25 +225,26 @@ def main():
         s, j = i % slots, i % nl
         c = lanes[j]
         sL = c.stream
-        with torch.cuda.stream(sA):
+        cF, sF = ctx, sA             # the stream of assignment + histogram
+        with torch.cuda.stream(sF):
             if used[s]:              # the slot's previous batch: encoded (codes[s] free) ...
-                sA.wait_event(ev_enc[s])
-            e = rec("assign", sA)
-            pq.assign(x, codes[s])
-            done(e, sA)
+                sF.wait_event(ev_enc[s])
+            e = rec("assign", sF)
+            pq.assign(x, codes[s], ctx=cF)
+            done(e, sF)
             tc = time.perf_counter()
             halo[s] = shard.exchange_halo(codes[s][-1], world, rank) if ctxm else None
             acc["collectives"] += time.perf_counter() - tc if state["timed"] else 0.0
             if used[s]:              # ... and its tables built (counts[s] free)
-                sA.wait_event(ev_tab[s])
-            e = rec("hist", sA)
+                sF.wait_event(ev_tab[s])
+            e = rec("hist", sF)
             counts[s].zero_()
-            codec.histogram(ctx, codes[s], k, ctxm, prev_row=halo[s], counts=counts[s])
-            done(e, sA)
+            codec.histogram(cF, codes[s], k, ctxm, prev_row=halo[s], counts=counts[s])
+            done(e, sF)
             tc = time.perf_counter()
             shard.reduce_counts(counts[s], world)
             acc["collectives"] += time.perf_counter() - tc if state["timed"] else 0.0
-            ev_hist[s].record(sA)
+            ev_hist[s].record(sF)
         used[s] = True
         with torch.cuda.stream(sL):
             sL.wait_event(ev_hist[s])
@@ -322,7 +323,7 @@ def main():
         codec.encode_status(c)
         tabs[j].status()
     assert torch.equal(dec[j_last], codes[s_last]), "round trip mismatch"
-    rerank = pq.rerank_count()
+    rerank = pq.rerank_count(ctx)
     bits_per_vec = int(tot_dev[j_last].item()) / n
 
     if rank == 0:

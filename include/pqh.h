@@ -76,7 +76,9 @@ int pqh_pq_destroy(pqh_pq_t* pq);
  * order, first minimum wins (oracle definition).  x rows are ld_x floats apart.
  * d_counts (optional, may be NULL): uint32 [m][k] non-context histogram accumulated
  * (+=) from the produced codes (huffman_encoder.c:139-164) -- fused in the kernel.
- * mode: 0 = MFMA screening + exact re-rank (default), 1 = exact VALU kernel only. */
+ * mode: 0 = MFMA screening + exact re-rank (default), 1 = exact VALU kernel only.
+ * ctx: any context of the codebook's device; the launch uses its stream and scratch, so
+ * contexts on different streams may assign concurrently. */
 int pqh_pq_assign(pqh_ctx_t* ctx, const pqh_pq_t* pq, const float* d_x, long long n,
                   long long ld_x, void* d_codes, uint32_t* d_counts, int mode);
 /* diagnostics of the last pqh_pq_assign (synchronises): vectors x parts re-ranked

@@ -117,18 +117,21 @@ class PQ:
         torch = _torch()
         return torch.uint8 if self.k <= 256 else torch.int16
 
-    def assign(self, x, codes=None, counts=None, mode: int = 0):
+    def assign(self, x, codes=None, counts=None, mode: int = 0, ctx: Context = None):
+        """codes (n, m) of x; on `ctx`'s stream (any context of the same device, default the
+        one the codebook was prepared with)."""
         torch = _torch()
         n = x.shape[0]
         if codes is None:
             codes = torch.empty((n, self.m), dtype=self.code_dtype, device=x.device)
-        check(lib().pqh_pq_assign(self.ctx.ptr, self.ptr, _ptr(x), n, x.stride(0), _ptr(codes),
+        c = ctx or self.ctx
+        check(lib().pqh_pq_assign(c.ptr, self.ptr, _ptr(x), n, x.stride(0), _ptr(codes),
                                   _ptr(counts), mode), "pqh_pq_assign")
         return codes
 
-    def rerank_count(self) -> int:
+    def rerank_count(self, ctx: Context = None) -> int:
         v = ctypes.c_ulonglong(0)
-        check(lib().pqh_pq_last_rerank_count(self.ctx.ptr, ctypes.byref(v)))
+        check(lib().pqh_pq_last_rerank_count((ctx or self.ctx).ptr, ctypes.byref(v)))
         return v.value
 
     def error(self, x, codes) -> float:

@@ -808,9 +808,8 @@ int plan_pa(int dsub) {
 }
 
 template <typename CodeT>
-int launch_mfma(pqh_pq* pq, const float* x, long long n, long long ldx, CodeT* codes,
-                uint32_t* counts) {
-    pqh_ctx* ctx = pq->ctx;
+int launch_mfma(pqh_ctx* ctx, pqh_pq* pq, const float* x, long long n, long long ldx,
+                CodeT* codes, uint32_t* counts) {
     const long long nblk = (n + 31) / 32;
     const int groups = pq->m;   // grid y: one subspace per workgroup
     dim3 block(64 * kWavesPerWG);
@@ -855,9 +854,8 @@ int launch_mfma(pqh_pq* pq, const float* x, long long n, long long ldx, CodeT* c
 }
 
 template <typename CodeT>
-int launch_exact(pqh_pq* pq, const float* x, long long n, long long ldx, CodeT* codes,
-                 uint32_t* counts) {
-    pqh_ctx* ctx = pq->ctx;
+int launch_exact(pqh_ctx* ctx, pqh_pq* pq, const float* x, long long n, long long ldx,
+                 CodeT* codes, uint32_t* counts) {
     const long long total = n * pq->m;
     if (total == 0) return PQH_OK;
     hipLaunchKernelGGL((pq_assign_exact<CodeT>), dim3((unsigned)((total + 255) / 256)), dim3(256),
@@ -934,7 +932,9 @@ int pqh_pq_destroy(pqh_pq_t* pq) {
 int pqh_pq_assign(pqh_ctx_t* ctx, const pqh_pq_t* cpq, const float* d_x, long long n,
                   long long ld_x, void* d_codes, uint32_t* d_counts, int mode) {
     pqh_pq* pq = const_cast<pqh_pq*>(cpq);
-    if (!ctx || !pq || pq->ctx != ctx || (n > 0 && (!d_x || !d_codes)) || n < 0 ||
+    // any context of the codebook's device may run the assignment (its stream, its
+    // work-queue heads and counters), so several streams can assign concurrently
+    if (!ctx || !pq || pq->ctx->device != ctx->device || (n > 0 && (!d_x || !d_codes)) || n < 0 ||
         ld_x < (long long)pq->m * pq->dsub)
         return PQH_ERR_ARG;
     int rc = pqh_use_device(ctx);
@@ -947,10 +947,10 @@ int pqh_pq_assign(pqh_ctx_t* ctx, const pqh_pq_t* cpq, const float* d_x, long lo
         mfma = false;  // vector loads need 16-byte aligned subspace slices
     if (pq->k <= 256) {
         uint8_t* c = static_cast<uint8_t*>(d_codes);
-        return mfma ? launch_mfma(pq, d_x, n, ld_x, c, d_counts)
-                    : launch_exact(pq, d_x, n, ld_x, c, d_counts);
+        return mfma ? launch_mfma(ctx, pq, d_x, n, ld_x, c, d_counts)
+                    : launch_exact(ctx, pq, d_x, n, ld_x, c, d_counts);
     }
-    return launch_exact(pq, d_x, n, ld_x, static_cast<uint16_t*>(d_codes), d_counts);
+    return launch_exact(ctx, pq, d_x, n, ld_x, static_cast<uint16_t*>(d_codes), d_counts);
 }
 
 // diagnostics: the per-wave stamps of the last assignment launch (PQH_ASSIGN_STAMPS builds;
