@@ -27,6 +27,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "pqh_internal.h"
@@ -51,9 +52,6 @@ constexpr int kTiles = 8;        // K = 256 centroids = 8 tiles of 32 rows
 #define PQH_ASSIGN_DEFER 1
 #endif
 constexpr int kRqLds = 128;      // deferred re-rank queue entries per wave (LDS)
-#ifndef PQH_ASSIGN_RED
-#define PQH_ASSIGN_RED 0
-#endif
 constexpr int kWavesPerWG = PQH_ASSIGN_WPG;   // subspace waves per workgroup
 constexpr int kNB = PQH_ASSIGN_NB;            // 32-vector blocks screened together per step
 
@@ -76,13 +74,6 @@ __device__ __forceinline__ unsigned min3u(unsigned a, unsigned b, unsigned c) {
     unsigned r;
     asm("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
-}
-
-__device__ __forceinline__ float bf16_up(float x) {
-    // smallest bf16 >= x for finite x >= 0
-    unsigned u = __float_as_uint(x);
-    if (u & 0xFFFFu) u = (u & 0xFFFF0000u) + 0x10000u;
-    return __uint_as_float(u);
 }
 
 // main-layout B slot value for vector-side quantities
@@ -127,27 +118,47 @@ __device__ __forceinline__ unsigned partner32(unsigned v) {
     return (threadIdx.x & 32) ? sw[0] : sw[1];
 }
 
-// ||x||^2 (fp32 fma chain; HALF: plus the partner half-wave's), the bf16 split x = xh + xl
-// (+ r), and whether this lane's slice has any bf16 remainder.
+// ||x||^2: fp32 fma chain over the lane's slice (HALF: plus the partner half-wave's, lower +
+// upper, so both halves round the same sum; a VALU lane swap, no LDS round trip).  The main
+// loop and the re-rank tail both use this, so their biases are bitwise the same.
+template <int D>
+__device__ __forceinline__ float norm_x(const float* xs) {
+    float X = 0.0f;
+#pragma unroll
+    for (int j = 0; j < Slice<D>::XD; ++j) X = fmaf(xs[j], xs[j], X);
+    if constexpr (Slice<D>::HALF) {
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(X), __float_as_uint(X),
+                                                         false, false);
+        X = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+    }
+    return X;
+}
+
+// whether some x of the lane's slice is not bf16-exact: a float whose low 16 bits are zero
+// converts to bf16 exactly (denormals are preserved, .amdhsa_float_denorm_mode_32 3), any
+// other leaves a non-zero remainder x - float(bf16(x))
+template <int D>
+__device__ __forceinline__ bool has_lo(const float* xs) {
+    unsigned o = 0;
+#pragma unroll
+    for (int j = 0; j < Slice<D>::XD; ++j) o |= __float_as_uint(xs[j]);
+    return (o & 0xFFFFu) != 0;
+}
+
+// ||x||^2, the bf16 split x = xh + xl (+ r), and whether this lane's slice has any bf16
+// remainder (the re-rank tail's form of the main loop's prologue).
 template <int D>
 __device__ __forceinline__ void split_x(const float* xs, float& X, bool& lo, float* xh, float* xl) {
     constexpr int XD = Slice<D>::XD;
-    X = 0.0f;
+    X = norm_x<D>(xs);
     lo = false;
 #pragma unroll
     for (int j = 0; j < XD; ++j) {
-        X = fmaf(xs[j], xs[j], X);
         __bf16 hb = (__bf16)xs[j];
         xh[j] = (float)hb;
         float rem = xs[j] - xh[j];
         xl[j] = (float)(__bf16)rem;
         lo |= rem != 0.0f;
-    }
-    if constexpr (Slice<D>::HALF) {   // + the other half-wave's 8 dims (lower + upper, so
-        // both halves round the same sum); a VALU lane swap, no LDS round trip
-        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(X), __float_as_uint(X),
-                                                         false, false);
-        X = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
     }
 }
 
@@ -156,19 +167,35 @@ __device__ __forceinline__ void split_x(const float* xs, float& X, bool& lo, flo
 // E0 (below) <= 7.7e-5 (X + Cmax), so X + 2^-10 (X + Cmax) suffices -- no square root on
 // the way to the first MFMA.  b_v <= 1.0078 X + 0.001 Cmax stays inside the accumulation
 // term of E0 (1.05 X + 1.01 Cmax).
-__device__ __forceinline__ float screen_bias(float X, bool finite_x, float cm) {
-    return finite_x ? bf16_up(X + 0x1p-10f * (X + cm) + 1e-30f) : 0.0f;
+// cmb = 2^-10 Cmax + 1e-30 (per subspace): b_v = bf16_up(X (1 + 2^-10) + cmb), where
+// bf16_up of a finite x >= 0 is (bits + 0xFFFF) & 0xFFFF0000.
+__device__ __forceinline__ float screen_bias(float X, bool finite_x, float cmb) {
+    const unsigned u = __float_as_uint(fmaf(X, 1.0f + 0x1p-10f, cmb));
+    return finite_x ? __uint_as_float((u + 0xFFFFu) & 0xFFFF0000u) : 0.0f;
 }
 
-// error bound E0 of the screening score against the fp32 direct-form distance (DESIGN.md
-// "pq_assign error bound"); when no x of the block has a bf16 remainder the split error is
-// 2^-15 P instead of 2^-13 P.  Returns the acceptance gap tau = 2.2 E0.
-__device__ __forceinline__ float screen_tau(float X, bool any_lo, float cm, float sc) {
-    // v_sqrt_f32 (1 ulp) instead of the correctly rounded expansion: the 1e-5 slack covers it
-    const float Pm = __builtin_amdgcn_sqrtf(X) * sc * 1.00001f;
-    const float E0 = (any_lo ? 0x1p-13f : 0x1p-15f) * Pm + 0x1p-22f * cm +
-                     0x1p-17f * (2.02f * Pm + 1.01f * cm + 1.05f * X);
-    return 2.2f * E0 + 1e-30f;
+// Error bound E0 of the screening score against the fp32 direct-form distance (DESIGN.md
+// "pq_assign error bound"), P = sqrt(X) sqrt(Cmax):
+//   E0 = c_lo P + 2^-22 Cmax + 2^-17 (2.02 P + 1.01 Cmax + 1.05 X),
+// c_lo = 2^-13 when some x of the block has a bf16 remainder, else 2^-15.  The acceptance
+// gap tau = 2.2 E0 is evaluated as a1 sqrt(X) + (c X + b) with per-subspace coefficients
+// (TauCoef); every term is positive, so inflating each coefficient by 2^-20 covers the
+// rounding of the coefficients and of the two fmas, and the 1e-5 on sqrt(Cmax) covers
+// v_sqrt_f32 (1 ulp) against the correctly rounded root.
+struct TauCoef {
+    float a_nolo, a_lo, b, c;
+};
+
+__device__ __forceinline__ TauCoef tau_coef(float cm, float sc) {
+    constexpr float up = 1.0f + 0x1p-20f;
+    const float s = 2.2f * 1.00001f * sc;
+    return {s * (0x1p-15f + 2.02f * 0x1p-17f) * up, s * (0x1p-13f + 2.02f * 0x1p-17f) * up,
+            2.2f * cm * (0x1p-22f + 1.01f * 0x1p-17f) * up + 1e-30f,
+            2.2f * 1.05f * 0x1p-17f * up};
+}
+
+__device__ __forceinline__ float screen_tau(float X, bool any_lo, const TauCoef& q) {
+    return fmaf(any_lo ? q.a_lo : q.a_nolo, __builtin_amdgcn_sqrtf(X), fmaf(q.c, X, q.b));
 }
 
 template <int D>
@@ -204,6 +231,38 @@ __device__ __forceinline__ void build_b(const float* xh, const float* xl, float 
                 float v1 = s1 < D ? xl[s1 < D ? s1 : 0] : 0.0f;
                 Bl[p][j] = (__bf16)(h ? v1 : v0);
             }
+    }
+}
+
+// The main loop's B operands, straight from x: the same bf16 values as split_x + build_b
+// (xh = bf16(x), xl = bf16(x - xh)), with packed conversions; xl only when LO.
+template <int D, bool LO>
+__device__ __forceinline__ void make_b(const float* xs, float bv, int h, bf16x8* Bm, bf16x8* Bl) {
+    if constexpr (Slice<D>::HALF) {
+        typedef float f32x8 __attribute__((ext_vector_type(8)));
+        f32x8 xv;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xv[j] = xs[j];
+        Bm[0] = __builtin_convertvector(xv, bf16x8);
+        Bm[1] = Bm[0];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            Bm[2][j] = (__bf16)(h ? 0.0f : (j < 3 ? 1.0f : (j == 3 ? bv : 0.0f)));
+        if constexpr (LO) {
+            f32x8 rem;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) rem[j] = xs[j] - (float)Bm[0][j];
+            Bl[0] = __builtin_convertvector(rem, bf16x8);
+        }
+    } else {
+        constexpr int XD = Slice<D>::XD;
+        float xh[XD], xl[XD];
+#pragma unroll
+        for (int j = 0; j < XD; ++j) {
+            xh[j] = (float)(__bf16)xs[j];
+            xl[j] = LO ? (float)(__bf16)(xs[j] - xh[j]) : 0.0f;
+        }
+        build_b<D>(xh, xl, bv, h, Bm, Bl);
     }
 }
 
@@ -288,6 +347,8 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
 #endif
     const float cm = cmax[m];
     const float sc = sqrt_cmax[m];
+    const float cmb = fmaf(cm, 0x1p-10f, 1e-30f);   // see screen_bias
+    const TauCoef tq = tau_coef(cm, sc);
     const float* cl = cent + (long long)m * K * D;   // fp32 centroids (L2-resident, 16 KB)
     const long long nblk = (n + 31) / 32;
     unsigned long long slow_count = 0;
@@ -326,104 +387,107 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
 
     // One step = a chunk of kNB consecutive 32-vector blocks, screened together: each tile's
     // A fragments are read from LDS once for all kNB blocks, and the kNB independent MFMA
-    // chains and key reductions give the SIMD work to overlap.
-    auto body = [&](long long blk0, float (*xin)[XD]) {
+    // chains and key reductions give the SIMD work to overlap.  The kernel is VALU-issue
+    // bound (a wave64 VALU instruction takes ~4 cycles of its SIMD), so the per-block work
+    // outside the key reduction is kept to a few dozen instructions: the B operands come
+    // straight from x by packed conversions, the lo pass is decided once per chunk (a lo pass
+    // over bf16-exact x adds exact zeros, so the blocks without a remainder keep their exact
+    // scores and their tighter bound), and the winner's tile rides in its key.
+    auto body = [&](auto lo_c, long long blk0, float (*xs)[XD], const float* X,
+                    const bool* any_lo, const bool* finite_x) {
+        constexpr bool LO = decltype(lo_c)::value;
         long long v[kNB];
-        bool valid[kNB], any_lo[kNB], finite_x[kNB];
-        float xs[kNB][XD], X[kNB];
+        bool valid[kNB];
         bf16x8 Bm[kNB][P::PM], Bl[kNB][P::PL];
 #pragma unroll
         for (int b = 0; b < kNB; ++b) {
             v[b] = (blk0 + b) * 32 + r;
-            valid[b] = v[b] < n;
-#pragma unroll
-            for (int j = 0; j < XD; ++j) xs[b][j] = valid[b] ? xin[b][j] : 0.0f;
+            valid[b] = v[b] < n;   // rows past n hold row n - 1 (clamped loads), never stored
+            make_b<D, LO>(xs[b], screen_bias(X[b], finite_x[b], cmb), h, Bm[b], Bl[b]);
         }
-#ifdef PQH_ASSIGN_NOCOMPUTE   // diagnostic: the kernel's memory traffic alone
+        // Keys: float bits with the low 6 mantissa bits replaced by (t mod 4, accumulator
+        // register i); tiles 0-3 and 4-7 keep separate running (min, second-min) pairs, so a
+        // key names its centroid.  (The and-mask sits in an SGPR and the or-value is an
+        // inline constant below 64: one v_and_or_b32 per value.)  Values go in groups of
+        // three: the group's top two by min3/med3, then (m1, m2) <- (min(m1, g1), med3(m1,
+        // g1, min(m2, g2))).
+        unsigned m1[kNB][2], m2[kNB][2];
 #pragma unroll
-        for (int b = 0; b < kNB; ++b) {
-            float q = 0.0f;
+        for (int b = 0; b < kNB; ++b)
 #pragma unroll
-            for (int j = 0; j < XD; ++j) q += xs[b][j];
-            if (valid[b] && h == 0) codes[v[b] * m_total + m] = (CodeT)(int)q;
-        }
-        return;
-#endif
-#pragma unroll
-        for (int b = 0; b < kNB; ++b) {
-            bool lo;
-            float xh[XD], xl[XD];
-            split_x<D>(xs[b], X[b], lo, xh, xl);
-            any_lo[b] = __any(lo);
-            finite_x[b] = isfinite(X[b]);
-            build_b<D>(xh, xl, screen_bias(X[b], finite_x[b], cm), h, Bm[b], Bl[b]);
-        }
-        // Keys: float bits with the low 4 mantissa bits replaced by the accumulator register
-        // i.  One running (min, second-min) per block over the lane's 128 values; values go
-        // in groups of three: the group's top two by min3/med3, then (m1, m2) <- (min(m1, g1),
-        // med3(m1, g1, min(m2, g2))).  The winner's tile is the last tile that lowered m1.
-        unsigned m1[kNB], m2[kNB], mt[kNB];
-#pragma unroll
-        for (int b = 0; b < kNB; ++b) { m1[b] = 0xFFFFFFFFu; m2[b] = 0xFFFFFFFFu; mt[b] = 0; }
-#pragma unroll
-        for (int t = 0; t < kTiles; ++t) {
-            bf16x8 a[P::PA];
+            for (int g = 0; g < 2; ++g) { m1[b][g] = 0xFFFFFFFFu; m2[b][g] = 0xFFFFFFFFu; }
+        auto load_a = [&](int t, bf16x8* a) {
 #pragma unroll
             for (int p = 0; p < P::PA; ++p)
                 a[p] = *reinterpret_cast<const bf16x8*>(&As[(p * kTiles + t) * 64 + lane]);
-            f32x16 acc[kNB];
-#ifdef PQH_ASSIGN_NOMFMA   // diagnostic timing only: no matrix work, scores from the B data
+        };
+        // A tile's 16 keys by a two-level tournament of triples (36 VALU instead of 43):
+        //   level 1: five triples -> (g1, g2) = (min3, med3); G2 = the smallest g2;
+        //   level 2: the five g1 and key 15 as two triples -> (h1a, h2a), (h1b, h2b);
+        //   then m1' = min3(m1, h1a, h1b) and m2' = min3(m2, min3(G2, h2a, h2b),
+        //   med3(m1, h1a, h1b)).  Every key but the overall minimum is >= one of the
+        //   candidates of m2' (a key is a triple's minimum or >= its triple's second), and
+        //   every candidate is a key other than the minimum, so m2' is the exact second
+        //   smallest key.
+        auto reduce = [&](const f32x16& acc, int t, int b) {
+            const int g = t >> 2;
+            unsigned kk[16];
 #pragma unroll
-            for (int b = 0; b < kNB; ++b)
+            for (int i = 0; i < 16; ++i)
+                kk[i] = (__float_as_uint(acc[i]) & ~63u) | (unsigned)(((t & 3) << 4) | i);
+            unsigned g1[5], g2[5];
+            auto tri = [&](int q) {
+                g1[q] = min3u(kk[3 * q], kk[3 * q + 1], kk[3 * q + 2]);
+                g2[q] = med3u(kk[3 * q], kk[3 * q + 1], kk[3 * q + 2]);
+            };
+            // (in this order, so few partial results are live at once)
+            tri(0); tri(1); tri(2);
+            const unsigned G2a = min3u(g2[0], g2[1], g2[2]);
+            const unsigned h1a = min3u(g1[0], g1[1], g1[2]), h2a = med3u(g1[0], g1[1], g1[2]);
+            tri(3); tri(4);
+            const unsigned G2 = min3u(G2a, g2[3], g2[4]);
+            const unsigned h1b = min3u(g1[3], g1[4], kk[15]), h2b = med3u(g1[3], g1[4], kk[15]);
+            const unsigned s = med3u(m1[b][g], h1a, h1b);
+            m1[b][g] = min3u(m1[b][g], h1a, h1b);
+            m2[b][g] = min3u(m2[b][g], min3u(G2, h2a, h2b), s);
+        };
+        // Software pipeline over the tiles: block b's MFMA chain for tile t + 1 is issued
+        // right after its tile-t keys are reduced, so it runs while the other block's keys
+        // are (the scheduling barriers keep the compiler from sinking the chain behind them).
+        bf16x8 a[P::PA];
+        load_a(0, a);
+        f32x16 acc[kNB];
 #pragma unroll
-                for (int i = 0; i < 16; ++i)
-                    acc[b][i] = (float)Bm[b][i & 7][i >> 3] + (float)a[0][i & 7] * (float)(t + 1);
-#else
+        for (int b = 0; b < kNB; ++b) acc[b] = tile_scores_a<D>(a, Bm[b], Bl[b], LO);
 #pragma unroll
-            for (int b = 0; b < kNB; ++b) acc[b] = tile_scores_a<D>(a, Bm[b], Bl[b], any_lo[b]);
-#endif
+        for (int t = 0; t < kTiles; ++t) {
+            if (t + 1 < kTiles) load_a(t + 1, a);
 #pragma unroll
             for (int b = 0; b < kNB; ++b) {
-                unsigned kk[16];
-#pragma unroll
-                for (int i = 0; i < 16; ++i)
-                    kk[i] = (__float_as_uint(acc[b][i]) & ~15u) | (unsigned)i;
-                const unsigned prev = m1[b];
-#if PQH_ASSIGN_RED == 3   // diagnostic timing only: MFMA + overhead, no key reduction
-                m1[b] = min3u(m1[b], __float_as_uint(acc[b][0]), __float_as_uint(acc[b][15]));
-                m2[b] = m1[b] + 100000;
-#elif PQH_ASSIGN_RED == 2   // diagnostic timing only (wrong codes): min over raw bits
-#pragma unroll
-                for (int q = 0; q < 8; ++q) m1[b] = min3u(m1[b], kk[2 * q], kk[2 * q + 1]);
-                m2[b] = m1[b] + 100000;
-#else
-#pragma unroll
-                for (int g = 0; g < 5; ++g) {
-                    const unsigned a0 = kk[3 * g], a1 = kk[3 * g + 1], a2 = kk[3 * g + 2];
-                    const unsigned g1 = min3u(a0, a1, a2);
-                    const unsigned g2 = med3u(a0, a1, a2);
-                    m2[b] = med3u(m1[b], g1, min(m2[b], g2));
-                    m1[b] = min(m1[b], g1);
-                }
-                m2[b] = med3u(m1[b], m2[b], kk[15]);
-                m1[b] = min(m1[b], kk[15]);
-#endif
-                mt[b] = m1[b] != prev ? (unsigned)t : mt[b];
+                reduce(acc[b], t, b);
+                if (t + 1 < kTiles) acc[b] = tile_scores_a<D>(a, Bm[b], Bl[b], LO);
+                __builtin_amdgcn_sched_barrier(0);
             }
         }
 #pragma unroll
         for (int b = 0; b < kNB; ++b) {
-            // merge the two half-waves (lanes l and l^32 hold the same vector)
-            const unsigned o1 = partner32(m1[b]), o2 = partner32(m2[b]), ot = partner32(mt[b]);
-            const bool other = o1 < m1[b];
-            const unsigned w_h = other ? (unsigned)(1 - h) : (unsigned)h;
-            const unsigned w_t = other ? ot : mt[b];
-            const unsigned b2 = min(min(m2[b], o2), max(m1[b], o1));
-            const unsigned b1 = min(m1[b], o1);
-            int code = tile_row((int)w_t, (int)(b1 & 15u), (int)w_h);
-            const float tau = screen_tau(X[b], any_lo[b], cm, sc);
-            const float K1 = __uint_as_float(b1 & ~15u), K2 = __uint_as_float(b2 & ~15u);
-            const bool slow = !(K2 - K1 > tau + 0x1p-15f * K2) || !finite_x[b];
+            // the lane's 128 centroids: merge the two tile groups ...
+            const unsigned a1 = m1[b][0], c1 = m1[b][1];
+            const unsigned own1 = min(a1, c1);
+            const unsigned own2 = min(min(m2[b][0], m2[b][1]), max(a1, c1));
+            const int wt = (c1 < a1 ? 4 : 0) | (int)((own1 >> 4) & 3u);
+            // ... then the two half-waves (lanes l and l^32 hold the same vector): after the
+            // swap, s[0] holds the lower half's value and s[1] the upper half's, in every lane
+            const auto s1 = __builtin_amdgcn_permlane32_swap(own1, own1, false, false);
+            const auto s2 = __builtin_amdgcn_permlane32_swap(own2, own2, false, false);
+            const unsigned b1 = min((unsigned)s1[0], (unsigned)s1[1]);
+            const unsigned b2 = min(min((unsigned)s2[0], (unsigned)s2[1]),
+                                    max((unsigned)s1[0], (unsigned)s1[1]));
+            const bool mine = own1 == b1;   // this half holds the winner (both: a tie -> slow)
+            int code = tile_row(wt, (int)(own1 & 15u), h);
+            const float tau = screen_tau(X[b], any_lo[b], tq);
+            const float K1 = __uint_as_float(b1 & ~63u), K2 = __uint_as_float(b2 & ~63u);
+            const bool slow = !(K2 - K1 > fmaf(0x1p-15f, K2, tau)) || !finite_x[b];
 
             unsigned long long need = __ballot(slow && valid[b] && h == 0);
             bool deferred = false;
@@ -431,7 +495,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
                 slow_count += __popcll(need);
                 // finite vectors go to the queue with their candidate window: every centroid
                 // that can be the fp32 argmin (or tie with it) screens below
-                // (K1 + tau)(1 + 2^-16) -- see pq_rerank_window; non-finite ones stay inline
+                // (K1 + tau)(1 + 2^-16) -- see the tail; non-finite ones stay inline
                 const unsigned long long fin = need & __ballot(finite_x[b]);
                 const unsigned cnt = (unsigned)__popcll(fin);
                 if (PQH_ASSIGN_DEFER && cnt && qn + cnt <= (unsigned)kRqLds) {
@@ -473,11 +537,42 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
                     if (lane == rs) code = bidx == 0x7FFFFFFF ? 0 : bidx;
                 }
             }
-            if (valid[b] && h == 0 && !(deferred && slow)) {
+            // fast path: the winner's half stores; slow path: the lower half (inline code),
+            // unless the vector waits in the queue
+            if (valid[b] && (slow ? (h == 0 && !deferred) : mine)) {
                 codes[v[b] * m_total + m] = (CodeT)code;
                 if (counts) atomicAdd(&hist[wave][code], 1u);
             }
         }
+    };
+    // per chunk: ||x||^2, finiteness and bf16 remainders of its blocks, then the tile loop
+    // with or without the lo pass
+    auto step = [&](long long blk0, float (*xs)[XD]) {
+#ifdef PQH_ASSIGN_NOCOMPUTE   // diagnostic: the kernel's memory traffic alone
+#pragma unroll
+        for (int b = 0; b < kNB; ++b) {
+            const long long vv = (blk0 + b) * 32 + r;
+            float q = 0.0f;
+#pragma unroll
+            for (int j = 0; j < XD; ++j) q += xs[b][j];
+            if (vv < n && h == 0) codes[vv * m_total + m] = (CodeT)(int)q;
+        }
+        return;
+#endif
+        float X[kNB];
+        bool any_lo[kNB], finite_x[kNB];
+        bool chunk_lo = false;
+#pragma unroll
+        for (int b = 0; b < kNB; ++b) {
+            X[b] = norm_x<D>(xs[b]);
+            any_lo[b] = __any(has_lo<D>(xs[b]));
+            finite_x[b] = isfinite(X[b]);
+            chunk_lo |= any_lo[b];
+        }
+        if (chunk_lo)
+            body(std::true_type{}, blk0, xs, X, any_lo, finite_x);
+        else
+            body(std::false_type{}, blk0, xs, X, any_lo, finite_x);
     };
 
     // Chunk schedule (a chunk = kNB blocks = one step).  Wave w of the subspace (w = bx
@@ -541,7 +636,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         const long long pre = nc < nchunk ? nc : ch;   // branch-free: re-load at the end
 #pragma unroll
         for (int b = 0; b < kNB; ++b) load_x(pre * kNB + b, xn[b]);
-        body(ch * kNB, xa);
+        step(ch * kNB, xa);
 #ifdef PQH_ASSIGN_STAMPS
         nbdone += kNB;
 #endif
@@ -594,7 +689,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         split_x<D>(xs, X, lo, xh, xl);
         bf16x8 Bm[P::PM];
         bf16x8 Bl[P::PL];
-        build_b<D>(xh, xl, screen_bias(X, true, cm), h, Bm, Bl);
+        build_b<D>(xh, xl, screen_bias(X, true, cmb), h, Bm, Bl);
         const bool lo_pass = __any(lo);
         float best = INFINITY;
         int bidx = 0x7FFFFFFF;
