@@ -139,9 +139,13 @@ __device__ __forceinline__ float norm_x(const float* xs) {
 // other leaves a non-zero remainder x - float(bf16(x))
 template <int D>
 __device__ __forceinline__ bool has_lo(const float* xs) {
-    unsigned o = 0;
-#pragma unroll
-    for (int j = 0; j < Slice<D>::XD; ++j) o |= __float_as_uint(xs[j]);
+    constexpr int XD = Slice<D>::XD;
+    unsigned o = __float_as_uint(xs[0]);
+    int j = 1;
+    for (; j + 1 < XD; j += 2)   // v_or3_b32: two values per instruction
+        asm("v_or3_b32 %0, %1, %2, %3"
+            : "=v"(o) : "v"(o), "v"(__float_as_uint(xs[j])), "v"(__float_as_uint(xs[j + 1])));
+    for (; j < XD; ++j) o |= __float_as_uint(xs[j]);
     return (o & 0xFFFFu) != 0;
 }
 
@@ -360,13 +364,18 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     constexpr int XD = Slice<D>::XD;
     // Branch-free loads (the row index is clamped; the block's validity is applied when
     // the slice is used), so the prefetch stays in flight across a whole block.
+    // The lane's slice of row r of block 0; a block's rows are a uniform offset away.  Only
+    // the last, partial block clamps its rows (to n - 1), on a wave-uniform branch.
+    const float* const xlane = x + (long long)r * ldx + (long long)m * D + (HALF ? 8 * h : 0);
     auto load_x = [&](long long b, float* dst) {
-        long long vv = b * 32 + r;
-        vv = vv < n ? vv : n - 1;
-#ifdef PQH_ASSIGN_L2X   // diagnostic: compute-bound time, x re-read from an L2-resident 64 KB
-        vv &= 1023;
-#endif
-        const float* xp = x + vv * ldx + (long long)m * D + (HALF ? 8 * h : 0);
+        const float* xp;
+        if (b * 32 + 32 <= n) {
+            xp = xlane + b * 32 * ldx;
+        } else {
+            long long vv = b * 32 + r;
+            vv = vv < n ? vv : n - 1;
+            xp = x + vv * ldx + (long long)m * D + (HALF ? 8 * h : 0);
+        }
         if constexpr (XD % 4 == 0) {
 #pragma unroll
             for (int j = 0; j < XD; j += 4) {
@@ -513,13 +522,10 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
                 while (todo) {   // inline exact re-rank: non-finite x, or a full segment
                     const int rs = __ffsll((long long)todo) - 1;
                     todo &= todo - 1;
-                    float xv[D];
+                    float xv[D];   // the vector's slice, re-read (a uniform address)
+                    const float* xr = x + ((blk0 + b) * 32 + rs) * ldx + (long long)m * D;
 #pragma unroll
-                    for (int j = 0; j < D; ++j) {   // HALF: dims 8.. live in the partner lane
-                        const int src = HALF && j >= XD ? rs + 32 : rs;
-                        xv[j] = __int_as_float(__builtin_amdgcn_readlane(
-                            __float_as_int(xs[b][HALF && j >= XD ? j - XD : j]), src));
-                    }
+                    for (int j = 0; j < D; ++j) xv[j] = xr[j];
                     float best = INFINITY;
                     int bidx = 0x7FFFFFFF;
 #pragma unroll 1
