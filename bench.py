@@ -53,8 +53,8 @@ def pmc_traffic(kernel):
             continue
         for name, e in ks.items():
             if name.startswith(kernel) and "hbm_bytes" in e:
-                return e["hbm_bytes"], os.path.relpath(f, ROOT)
-    return None, None
+                return e["hbm_bytes"], os.path.relpath(f, ROOT), e.get("avg_us")
+    return None, None, None
 
 
 def parse():
@@ -329,7 +329,7 @@ def main():
     if rank == 0:
         t_assign = acc["assign"] / args.steps
         achieved = (BYTES_PER_VEC_READ + BYTES_PER_VEC_WRITE) * n / t_assign / 1e9
-        traffic, traffic_src = pmc_traffic("pq_assign_mfma")
+        traffic, traffic_src, prof_avg_us = pmc_traffic("pq_assign_mfma")
         t_enc = (acc["assign"] + acc["hist"] + acc["codebook"] + acc["encode"]) / args.steps
         res = {
             "metric": METRIC,
@@ -362,7 +362,12 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "traffic_source": traffic_src,
                          "bytes_per_vector": BYTES_PER_VEC_READ + BYTES_PER_VEC_WRITE,
-                         "avg_ms": round(t_assign * 1e3, 4)},
+                         "avg_ms": round(t_assign * 1e3, 4),
+                         # rocprofv3 kernel-trace average of this bench command (dispatch
+                         # begin -> end); avg_ms above is HIP events around the launch on its
+                         # stream, which also count the wait for CUs held by the lanes
+                         "profile_avg_ms": (round(prof_avg_us / 1e3, 4)
+                                            if prof_avg_us is not None else None)},
             "stages_ms": {s: round(v / args.steps * 1e3, 4) for s, v in acc.items()},
             "stages_note": ("per-stage HIP-event times on their own streams" +
                             ("" if serial else "; the stages of consecutive batches run "
