@@ -127,3 +127,135 @@ def stitch_np(shards: Sequence[Tuple["object", int, int]], total_bits: int):
 def raw_first(rank: int) -> int:
     """Context mode writes global row 0 raw; only rank 0 holds it."""
     return 1 if rank == 0 else 0
+
+
+# ---- sort mode across ranks (SURVEY.md 8e: "sort mode is not embarrassingly parallel") ----
+#
+# The reference's default mode sorts all rows (huffman_encoder.c:301-317: qsort + strncmp) --
+# a stable sort by key(row) = the row with every byte after its first 0 zeroed.  Across
+# ranks it is a sample sort: every rank sorts its shard (stable), all-gathers a few sample
+# keys, picks world - 1 splitters, and all-to-alls each row to the rank whose key range holds
+# it.  A row goes to rank d = #{splitters < key}, so all rows with one key land on one rank;
+# they arrive in source-rank order (= global row order) and each source's run is already in
+# stable order, so a final stable local sort yields the rank's slice of the global order.
+# The slices concatenated in rank order are the reference's sorted rows; some slices may be
+# empty (heavy keys), which `halo_ragged` handles.
+
+
+def sort_key_words(codes):
+    """(n, ceil(m/8)) int64 words that order like the strncmp key: the row's bytes with every
+    byte after its first 0 zeroed, big-endian, sign bit flipped so that signed int64
+    comparison is unsigned comparison."""
+    import torch
+    n, m = codes.shape
+    c = codes.to(torch.int64)
+    ones = torch.ones((n, 1), dtype=torch.int64, device=c.device)
+    alive = torch.cumprod(torch.cat([ones, (c[:, :-1] != 0).to(torch.int64)], 1), 1)
+    kb = c * alive
+    w = (m + 7) // 8
+    if w * 8 != m:
+        kb = torch.cat([kb, torch.zeros((n, w * 8 - m), dtype=torch.int64, device=c.device)], 1)
+    shifts = torch.arange(56, -1, -8, dtype=torch.int64, device=c.device)
+    words = (kb.view(n, w, 8) << shifts).sum(-1)          # disjoint fields: sum == or
+    return words ^ torch.tensor(-(1 << 63), dtype=torch.int64, device=c.device)
+
+
+def _count_le(words, key):
+    """#rows of the lexicographically sorted (n, W) `words` that are <= `key` (W ints)."""
+    import torch
+    lo, hi = 0, words.shape[0]
+    for j, kv in enumerate(key):
+        col = words[lo:hi, j].contiguous()
+        t = torch.tensor([kv], dtype=torch.int64, device=words.device)
+        a = int(torch.searchsorted(col, t).item())
+        b = int(torch.searchsorted(col, t, right=True).item())
+        if j == len(key) - 1:
+            return lo + b
+        lo, hi = lo + a, lo + b     # rows before lo are smaller; [lo, hi) tie on word j
+        if lo == hi:
+            break
+    return lo
+
+
+def sort_rows_distributed(codes, world: int, rank: int, local_sort, group=None,
+                          samples: int = 256):
+    """This rank's slice of the stable strncmp-key sort of all ranks' rows.
+
+    codes: (n_r, m) uint8 tensor, the rank's contiguous row shard (rank order = row order).
+    local_sort(t) -> t sorted (stable, strncmp key): the GPU library's pqh_sort_rows
+    (`codec.sort_rows`) on the GPU; the CPU tests pass the oracle's.  Returns a new
+    (n'_r, m) tensor on the same device."""
+    import torch
+    import torch.distributed as dist
+    srt = local_sort(codes) if codes.shape[0] else codes
+    if world == 1:
+        return srt
+    n, m = srt.shape
+    dev = srt.device
+    words = sort_key_words(srt)
+    nw = words.shape[1]
+    # samples: evenly spaced keys of the sorted shard (an empty shard sends none)
+    s = min(samples, n)
+    idx = (torch.arange(s, device=dev) * n) // max(s, 1) if s else torch.zeros(0, dtype=torch.long,
+                                                                               device=dev)
+    mine = torch.full((samples, nw + 1), 0, dtype=torch.int64, device=dev)
+    if s:
+        mine[:s, :nw] = words[idx]
+        mine[:s, nw] = 1                                        # valid flag
+    allsamp = torch.empty((world * samples, nw + 1), dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(allsamp, mine, group=group)
+    keys = sorted(tuple(r[:nw]) for r in allsamp.cpu().tolist() if r[nw])
+    splitters = [keys[(j + 1) * len(keys) // world - 1] for j in range(world - 1)] if keys else []
+    # rows to rank d: #splitters < key, i.e. the boundaries are #rows <= splitter_j
+    bounds = [0] + [_count_le(words, sp) for sp in splitters] + [n] * (world - len(splitters))
+    send = torch.tensor([bounds[d + 1] - bounds[d] for d in range(world)], dtype=torch.int64)
+    recv = torch.empty_like(send)
+    sd, rd = send.to(dev), recv.to(dev)
+    dist.all_to_all_single(rd, sd, group=group)
+    recv = rd.cpu()
+    out = torch.empty((int(recv.sum()), m), dtype=srt.dtype, device=dev)
+    dist.all_to_all_single(out.view(-1), srt.reshape(-1),
+                           output_split_sizes=[int(v) * m for v in recv.tolist()],
+                           input_split_sizes=[int(v) * m for v in send.tolist()], group=group)
+    return local_sort(out) if out.shape[0] else out
+
+
+def library_sort(ctx):
+    """local_sort for sort_rows_distributed on the GPU: the library's stable radix sort
+    (pqh_sort_rows, in place) on the context's stream."""
+    from . import codec
+
+    def run(t):
+        t = t.contiguous()
+        codec.sort_rows(ctx, t)
+        return t
+    return run
+
+
+def halo_ragged(last_row, world: int, rank: int, group=None):
+    """exchange_halo for shards that may be empty (sorted slices): `last_row` is the (m,)
+    last row or None.  Returns (halo, raw_first): the last row of the nearest non-empty
+    predecessor (None if there is none) and whether this rank holds global row 0, which
+    context mode writes raw (huffman_encoder.c:234)."""
+    import torch
+    import torch.distributed as dist
+    if world == 1:
+        return None, 1
+    m = last_row.numel() if last_row is not None else None
+    # everyone needs m: share it with the non-empty flag
+    info = torch.tensor([1 if last_row is not None else 0, m or 0], dtype=torch.int64)
+    dev = last_row.device if last_row is not None else None
+    allinfo = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(allinfo, info, group=group)
+    mm = max(int(t[1]) for t in allinfo)
+    row = (last_row.reshape(-1).to(torch.int64).cpu() if last_row is not None
+           else torch.zeros(mm, dtype=torch.int64))
+    rows = [torch.zeros(mm, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(rows, row, group=group)
+    has = [int(t[0]) for t in allinfo]
+    prev = next((r for r in range(rank - 1, -1, -1) if has[r]), None)
+    first = next((r for r in range(world) if has[r]), None)
+    halo = rows[prev] if prev is not None else None
+    if halo is not None and dev is not None:
+        halo = halo.to(dev)
+    return halo, 1 if first == rank else 0

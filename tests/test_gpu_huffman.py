@@ -311,3 +311,22 @@ def test_sort_ctx_mode_vs_reference_files(gpu, name):
     tabs = codec.Tables.from_codebooks(ctx, cbs)
     enc = codec.encode(ctx, tabs, cd, chunk_vectors=16)
     assert codec.indices_file_bytes(enc) == g["sort_ctx__indices"].tobytes()
+
+
+def test_gpu_sort_key_words_and_local_sort(gpu, oracle):
+    """The pieces of the multi-GPU sort mode that run on the GPU: sort_key_words on device
+    tensors orders rows like the oracle, and sort_rows_distributed with the library sort
+    (one rank) is the oracle's stable strncmp sort.  The multi-rank protocol itself is
+    covered by the gloo tests (test_shard_gloo.py)."""
+    torch, codec, ctx = gpu
+    from pq_huffman_amd import shard
+    for n, m in ((1000, 8), (777, 3), (513, 16)):
+        a = _zero_heavy_rows(n, m, 3)
+        w = shard.sort_key_words(torch.from_numpy(a).cuda()).cpu().numpy()
+        np.testing.assert_array_equal(w, shard.sort_key_words(torch.from_numpy(a)).numpy())
+        order = np.lexsort(tuple(w[:, j] for j in range(w.shape[1] - 1, -1, -1)))
+        assert np.array_equal(a[order], oracle.sort_rows(a))
+        out = shard.sort_rows_distributed(torch.from_numpy(a).cuda(), 1, 0,
+                                          shard.library_sort(ctx))
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), oracle.sort_rows(a))

@@ -155,3 +155,91 @@ def test_stitch_word_alignment():
         if bit:
             ref[j // 8] |= 1 << (7 - j % 8)
     assert out == ref.tobytes()
+
+
+# ---- sort mode across ranks: sample sort + ragged halo (shard.sort_rows_distributed) -----
+
+def _sort_codes(kind, n, m, k):
+    codes = skewed_codes(n, m, k, seed=5)
+    if kind == "zeros":      # many 0 bytes: long runs of equal strncmp keys, ties everywhere
+        rng = np.random.default_rng(6)
+        codes[rng.random(codes.shape) < 0.3] = 0
+    elif kind == "onekey":   # every row starts with 0: one key, all rows land on one rank
+        codes[:, 0] = 0
+    return codes
+
+
+def _local_sort(t):
+    return torch.from_numpy(orc.sort_rows(t.numpy())) if t.shape[0] else t
+
+
+def _sort_worker(rank, world, port, kind, n, m, k, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        codes = _sort_codes(kind, n, m, k)
+        b, e = shard.row_range(n, world, rank)
+        mine = shard.sort_rows_distributed(torch.from_numpy(codes[b:e]), world, rank,
+                                           _local_sort, samples=16).numpy()
+        # the context-mode encode protocol on the (possibly empty) sorted slices
+        last = torch.from_numpy(mine[-1].astype(np.int64)) if len(mine) else None
+        halo, raw = shard.halo_ragged(last, world, rank)
+        prev = halo.numpy() if halo is not None else None
+        counts = torch.from_numpy(_local_hist(mine, k, True, prev))
+        shard.reduce_counts(counts, world)
+        cnt = counts.numpy().astype(np.float64)
+        lens = np.zeros((m, k * k), np.int32)
+        cds = np.zeros((m, k * k, 8), np.uint8)
+        for i in range(m):
+            lens[i], cds[i] = orc.codebook(k, cnt[i], True, 8)
+        cbs = orc.Codebooks(k, True, lens, cds, 8)
+        _, nbits = _pack(mine, cbs, raw, prev, 0)
+        goff, total = shard.bit_offsets(torch.tensor([nbits], dtype=torch.int64), world, rank)
+        buf, _ = _pack(mine, cbs, raw, prev, shard.local_bit_offset(goff))
+        pieces = [None] * world
+        dist.all_gather_object(pieces, (buf, goff, nbits))
+        slices = [None] * world
+        dist.all_gather_object(slices, mine)
+        if rank == 0:
+            q.put((np.concatenate(slices), shard.stitch(pieces, total), [len(s) for s in slices]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,kind,m", [(2, "skewed", 8), (3, "zeros", 8), (3, "zeros", 16),
+                                          (2, "onekey", 4), (3, "skewed", 3)])
+def test_distributed_sort_mode_matches_single_process(world, kind, m):
+    """Sample sort across gloo ranks, then the sort+context encode on the sorted slices:
+    the concatenated slices equal the oracle's stable strncmp-key sort of all rows, and the
+    stitched stream equals the oracle's single-process sort+context stream
+    (huffman_encoder.c:301-317, :220-238)."""
+    n, k = 400, 256
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sort_worker, args=(r, world, port, kind, n, m, k, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    rows, stream, sizes = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = orc.sort_rows(_sort_codes(kind, n, m, k))
+    np.testing.assert_array_equal(rows, want)
+    assert sum(sizes) == n
+    if kind == "onekey":
+        assert sorted(sizes)[:-1] == [0] * (world - 1)    # the empty-slice path ran
+    cbs = orc.build_codebooks(want, k, True)
+    ref, _ = orc.encode(want, cbs)
+    assert stream == ref
+
+
+def test_sort_key_words_order():
+    """sort_key_words orders rows like the stable strncmp comparator of the oracle."""
+    for m in (3, 8, 12):
+        codes = _sort_codes("zeros", 500, m, 256)
+        w = shard.sort_key_words(torch.from_numpy(codes)).numpy()
+        order = np.lexsort(tuple(w[:, j] for j in range(w.shape[1] - 1, -1, -1)), axis=0)
+        np.testing.assert_array_equal(codes[order], orc.sort_rows(codes))
