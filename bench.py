@@ -60,8 +60,10 @@ def pmc_traffic(kernel):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
-    ap.add_argument("--warmup", type=int, default=5)
+    # 200 steps = 200 M vectors, ~0.1 s: the lanes pipeline fills and drains inside the timed
+    # region, and at 30 steps that costs ~7 % of the steady-state rate
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--vectors", type=int, default=1_000_000, help="vectors per GPU")
     ap.add_argument("--mode", choices=["ctx", "noctx"], default="ctx")
     ap.add_argument("--chunk", type=int, default=8,

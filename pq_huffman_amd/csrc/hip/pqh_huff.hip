@@ -28,16 +28,22 @@ template <typename CodeT>
 __device__ __forceinline__ unsigned ld_code(const CodeT* c, long long i) { return (unsigned)c[i]; }
 
 // ---------------------------------------------------------------- histograms
-// Context histogram, pass 1: workgroup (chunk of kHistChunk vectors, part) counts its
-// (prev, cur) pairs in LDS as u16 pairs (a chunk cannot overflow 16 bits) and stores the
-// packed counters as its private partial -- plain coalesced stores, no global atomics.
+// Context histogram, pass 1: workgroup (chunk of kHistChunk vectors, part, prev-range z)
+// counts its (prev, cur) pairs with prev in [z k / split, (z + 1) k / split) in LDS as u16
+// pairs (a chunk cannot overflow 16 bits) and stores the packed counters as its slice of
+// the chunk's private partial -- plain coalesced stores, no global atomics.  split = 2
+// halves the LDS (64 KB at K = 256), so a workgroup fits on a CU beside the assignment's and
+// the code-table builds' workgroups; every split re-reads the chunk's rows (L2 hits).
 template <typename CodeT>
 __global__ void __launch_bounds__(1024)
 hist_ctx(const CodeT* __restrict__ codes, long long n, int m_total, int k,
-         const CodeT* __restrict__ prev_row, uint32_t* __restrict__ partial) {
-    extern __shared__ uint32_t pairs[];   // k*k u16 counters packed two per word
+         const CodeT* __restrict__ prev_row, uint32_t* __restrict__ partial, int split) {
+    extern __shared__ uint32_t pairs[];   // (k / split) * k u16 counters packed two per word
     const int m = blockIdx.y;
-    const int words = (k * k + 1) / 2;
+    const int prows = k / split;
+    const unsigned plo = (unsigned)(blockIdx.z * prows);
+    const int all_words = (k * k + 1) / 2;
+    const int words = split == 1 ? all_words : prows * k / 2;
     for (int w = threadIdx.x; w < words; w += blockDim.x) pairs[w] = 0;
     constexpr int kRun = kHistChunk / 1024;   // consecutive vectors per thread
     const long long v0 = (long long)blockIdx.x * kHistChunk + (long long)threadIdx.x * kRun;
@@ -70,11 +76,14 @@ hist_ctx(const CodeT* __restrict__ codes, long long n, int m_total, int k,
     for (int u = 1; u <= kRun; ++u) {
         const unsigned prev = c[u - 1], cur = c[u];
         if (prev >= (unsigned)k || cur >= (unsigned)k) continue;  // absent / out of alphabet
-        const unsigned bin = prev * (unsigned)k + cur;
+        const unsigned pr = prev - plo;
+        if (pr >= (unsigned)prows) continue;                      // another split's range
+        const unsigned bin = pr * (unsigned)k + cur;
         atomicAdd(&pairs[bin >> 1], 1u << ((bin & 1u) * 16));
     }
     __syncthreads();
-    uint32_t* out = partial + ((long long)m * gridDim.x + blockIdx.x) * words;
+    uint32_t* out = partial + ((long long)m * gridDim.x + blockIdx.x) * all_words +
+                    (long long)blockIdx.z * words;
     if ((words & 3) == 0) {
         const uint4* src = reinterpret_cast<const uint4*>(pairs);
         uint4* dst = reinterpret_cast<uint4*>(out);
@@ -507,15 +516,22 @@ int pqh_histogram(pqh_ctx_t* ctx, const void* d_codes, long long n, int m, int k
     if (context) {
         const unsigned chunks = (unsigned)((n + kHistChunk - 1) / kHistChunk);
         const int words = (k * k + 1) / 2;
-        const size_t lds = (size_t)words * 4;
+        // prev-range splits per chunk (PQH_HIST_SPLIT = 1, 2 or 4; default 2 for even k)
+        static const int split_env = [] {
+            const char* e = std::getenv("PQH_HIST_SPLIT");
+            const int v = e ? std::atoi(e) : 2;
+            return v == 1 || v == 4 ? v : 2;
+        }();
+        const int split = k % (2 * split_env) == 0 ? split_env : (k % 4 == 0 ? 2 : 1);
+        const size_t lds = (size_t)(split == 1 ? words : (k / split) * k / 2) * 4;
         rc = pqh_ensure_ws(ctx, (size_t)m * chunks * words * 4);
         if (rc) return rc;
         uint32_t* partial = static_cast<uint32_t*>(ctx->ws);
         PQH_HIP(ctx, hipFuncSetAttribute((const void*)hist_ctx<uint8_t>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL(hist_ctx<uint8_t>, dim3(chunks, m), dim3(1024), lds, ctx->stream,
-                           static_cast<const uint8_t*>(d_codes), n, m, k,
-                           static_cast<const uint8_t*>(d_prev_row), partial);
+        hipLaunchKernelGGL(hist_ctx<uint8_t>, dim3(chunks, m, split), dim3(1024), lds,
+                           ctx->stream, static_cast<const uint8_t*>(d_codes), n, m, k,
+                           static_cast<const uint8_t*>(d_prev_row), partial, split);
         PQH_LAUNCH_CHECK(ctx);
         hipLaunchKernelGGL(hist_ctx_reduce, dim3((unsigned)((words + 255) / 256), m), dim3(256), 0,
                            ctx->stream, partial, (int)chunks, words, (long long)k * k, d_counts);

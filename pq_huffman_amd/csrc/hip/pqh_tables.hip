@@ -962,10 +962,11 @@ int pqh_tables_build(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts) 
     if (t->k <= 256) {
         // trees per workgroup: fewer = more, smaller workgroups (3.5 KB of LDS per tree), so
         // the build spreads over more CUs and leaves each CU's LDS to concurrent kernels
+        // (16 = 56 KB: beside three assignment workgroups; PQH_TREE_TPW = 8 / 16 / 32)
         static const int tpw_env = [] {
             const char* e = std::getenv("PQH_TREE_TPW");
             const int v = e ? std::atoi(e) : 0;
-            return v == 8 || v == 16 || v == 32 ? v : 32;
+            return v == 8 || v == 16 || v == 32 ? v : 16;
         }();
         auto launch = [&](auto tpw_c) -> int {
             constexpr int TPW = decltype(tpw_c)::value;
