@@ -77,6 +77,9 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true", help="same as --sched serial")
     ap.add_argument("--lanes", type=int, default=3,
                     help="streams taking batches round robin for tables + encode + decode")
+    ap.add_argument("--hist-on", choices=["assign", "lanes"], default="assign",
+                    help="stream of the context histogram: the assignment's, or the batch's "
+                         "lane (before its code tables)")
     ap.add_argument("--table-cus", type=int, default=0,
                     help="limit each lane stream to this many CUs (0: no CU mask)")
     return ap.parse_args()
@@ -222,6 +225,20 @@ def main():
         if e1 is not None:
             e1.record(stream)
 
+    hist_on_lane = args.hist_on == "lanes" and not serial
+
+    def hist(s, c, st):
+        """batch s's symbol histogram on stream st (context c), then its all-reduce"""
+        if used[s]:                  # the slot's previous batch: tables built (counts free)
+            st.wait_event(ev_tab[s])
+        e = rec("hist", st)
+        counts[s].zero_()
+        codec.histogram(c, codes[s], k, ctxm, prev_row=halo[s], counts=counts[s])
+        done(e, st)
+        tc = time.perf_counter()
+        shard.reduce_counts(counts[s], world)
+        acc["collectives"] += time.perf_counter() - tc if state["timed"] else 0.0
+
     def front(i):
         """batch i: assignment + histogram on A, then its code tables on its lane"""
         s, j = i % slots, i % nl
@@ -237,19 +254,15 @@ def main():
             tc = time.perf_counter()
             halo[s] = shard.exchange_halo(codes[s][-1], world, rank) if ctxm else None
             acc["collectives"] += time.perf_counter() - tc if state["timed"] else 0.0
-            if used[s]:              # ... and its tables built (counts[s] free)
-                sF.wait_event(ev_tab[s])
-            e = rec("hist", sF)
-            counts[s].zero_()
-            codec.histogram(cF, codes[s], k, ctxm, prev_row=halo[s], counts=counts[s])
-            done(e, sF)
-            tc = time.perf_counter()
-            shard.reduce_counts(counts[s], world)
-            acc["collectives"] += time.perf_counter() - tc if state["timed"] else 0.0
+            if not hist_on_lane:
+                hist(s, cF, sF)
             ev_hist[s].record(sF)
-        used[s] = True
         with torch.cuda.stream(sL):
             sL.wait_event(ev_hist[s])
+            if hist_on_lane:
+                hist(s, c, sL)
+        used[s] = True
+        with torch.cuda.stream(sL):
             e = rec("codebook", sL)
             tabs[j].build(counts[s], c)          # GPU trees + lookup tables, no host trip
             done(e, sL)
