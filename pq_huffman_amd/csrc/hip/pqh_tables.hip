@@ -532,26 +532,35 @@ lut_fill(const unsigned long long* __restrict__ enc, uint32_t* __restrict__ enc3
     const long long l2base = (long long)(mt >> 9);
     uint16_t* L1 = lut1 + (t << kL1Max);
     block_w2max(e, k, w1, l2_bits, w2max);
-    // subtable ids in prefix order: per-thread chunk counts, then a serial scan of 256
+    // subtable ids in prefix order: per-thread chunk counts, then a block-wide exclusive
+    // scan (wave scans + the four wave totals; 256 threads)
     const int np = 1 << w1;
     const int per = (np + blockDim.x - 1) / blockDim.x;
     const int p0 = threadIdx.x * per, p1 = min(np, p0 + per);
     uint32_t c_id = 0;
     for (int p = p0; p < p1; ++p) c_id += w2max[p] ? 1u : 0u;
-    part[threadIdx.x] = c_id;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t a = 0;
-        for (int q = 0; q < (int)blockDim.x; ++q) {
-            const uint32_t x = part[q];
-            part[q] = a;
-            a += x;
+    {
+        const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+        uint32_t incl = c_id;
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(incl, off);
+            if (lane >= off) incl += y;
         }
-        nsub = a;
-        nlong = 0;
+        if (lane == 63) part[wid] = incl;
+        __syncthreads();
+        uint32_t before = 0, all = 0;
+        for (int w = 0; w < (int)blockDim.x / 64; ++w) {
+            const uint32_t x = part[w];
+            before += w < wid ? x : 0u;
+            all += x;
+        }
+        if (threadIdx.x == 0) {
+            nsub = all;
+            nlong = 0;
+        }
+        c_id = before + incl - c_id;
     }
     __syncthreads();
-    c_id = part[threadIdx.x];
     for (int p = p0; p < p1; ++p)
         if (w2max[p]) sub_id[p] = c_id++;
     for (int i = threadIdx.x; i < np; i += blockDim.x) L1[i] = 0;
