@@ -75,11 +75,23 @@ def parse():
                          "tables, encode and decode on one of --lanes streams (overlapped); "
                          "'serial': every stage in order on one stream")
     ap.add_argument("--no-overlap", action="store_true", help="same as --sched serial")
-    ap.add_argument("--lanes", type=int, default=3,
+    ap.add_argument("--lanes", type=int, default=2,
                     help="streams taking batches round robin for tables + encode + decode")
+    ap.add_argument("--elanes", type=int, default=1,
+                    help="> 0: encode + decode on this many streams of their own; the --lanes "
+                         "streams then build code tables only")
     ap.add_argument("--hist-on", choices=["assign", "lanes"], default="assign",
                     help="stream of the context histogram: the assignment's, or the batch's "
                          "lane (before its code tables)")
+    ap.add_argument("--tbufs", type=int, default=2,
+                    help="code-table sets per table lane when --elanes > 0")
+    ap.add_argument("--extra-slots", type=int, default=3,
+                    help="code/count buffers beyond one per lane")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="process-group backend (nccl = RCCL; gloo only to rehearse the "
+                         "multi-rank schedule with every rank on one GPU, --one-device)")
+    ap.add_argument("--one-device", action="store_true",
+                    help="every rank uses GPU 0 (schedule rehearsal on a one-GPU box)")
     ap.add_argument("--table-cus", type=int, default=0,
                     help="limit each lane stream to this many CUs (0: no CU mask)")
     return ap.parse_args()
@@ -158,10 +170,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.one_device:
+        local = 0
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.dist_backend)
     else:
         torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -188,9 +205,17 @@ def main():
     # (cus >= the device's CU count: a library stream of its own without a CU mask)
     lanes = [ctx] if serial else [codec.Context(local, cus=args.table_cus or 1 << 20)
                                   for _ in range(nl)]
+    # encode + decode streams: the table lanes themselves, or --elanes streams of their own
+    # (then batch i's tables are built on lane i % lanes while the encode/decode streams
+    # work on earlier batches, and a table lane rebuilds only after the decode that read it)
+    elanes = lanes if serial or args.elanes <= 0 else [codec.Context(local, cus=1 << 20)
+                                                       for _ in range(args.elanes)]
+    ne = len(elanes)
     pq = codec.PQ(ctx, cent)
     items = k * k if ctxm else k
-    slots = nl + 1            # codes / counts: the assignment runs ahead of the lanes
+    # codes / counts buffers: the assignment runs up to `slots` batches ahead of the oldest
+    # batch not yet encoded
+    slots = nl + max(1, args.extra_slots)
     codes = [torch.empty((n, m), dtype=torch.uint8, device=dev) for _ in range(slots)]
     counts = [torch.zeros((m, items), dtype=torch.int32, device=dev) for _ in range(slots)]
     halo = [None] * slots
@@ -199,14 +224,21 @@ def main():
     ev_enc = [torch.cuda.Event() for _ in range(slots)]
     used = [False] * slots    # slot s has held a batch (its events were recorded)
     chunks = (n + args.chunk - 1) // args.chunk
-    tabs = [codec.Tables(c, m, k, ctxm) for c in lanes]
-    dec = [torch.empty((n, m), dtype=torch.uint8, device=dev) for _ in lanes]
-    coff = [torch.empty(chunks, dtype=torch.int64, device=dev) for _ in lanes]
+    # code tables: one set per lane; two per table lane when encode/decode have streams of
+    # their own, so a lane builds batch i + lanes's tables while batch i's are still read
+    nbuf = 1 if elanes is lanes else max(1, args.tbufs)
+    tabs = [codec.Tables(c, m, k, ctxm) for c in lanes for _ in range(nbuf)]
+    ev_dec = [torch.cuda.Event() for _ in tabs]    # last decode that read tabs[t]
+
+    def tab_index(i):
+        return (i % nl) * nbuf + (i // nl) % nbuf
+    dec = [torch.empty((n, m), dtype=torch.uint8, device=dev) for _ in elanes]
+    coff = [torch.empty(chunks, dtype=torch.int64, device=dev) for _ in elanes]
     cprev = [torch.empty((chunks, m), dtype=torch.uint8, device=dev) if ctxm else None
-             for _ in lanes]
+             for _ in elanes]
     out = [torch.zeros(n * m * 56 // 8 + 64, dtype=torch.uint8, device=dev)  # worst case
-           for _ in lanes]
-    tot_dev = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in lanes]
+           for _ in elanes]
+    tot_dev = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in elanes]
     raw_first = shard.raw_first(rank)
     stages = ("assign", "hist", "codebook", "encode", "decode")
     events = []          # (stage, start, end) of timed steps, read after the timed region
@@ -263,44 +295,54 @@ def main():
                 hist(s, c, sL)
         used[s] = True
         with torch.cuda.stream(sL):
+            ti = tab_index(i)
+            if elanes is not lanes:              # tabs[ti] free: its last decode is done
+                sL.wait_event(ev_dec[ti])
             e = rec("codebook", sL)
-            tabs[j].build(counts[s], c)          # GPU trees + lookup tables, no host trip
+            tabs[ti].build(counts[s], c)         # GPU trees + lookup tables, no host trip
             done(e, sL)
             ev_tab[s].record(sL)
 
     def back(i):
-        """batch i: encode + decode on its lane (queued behind its tables)"""
-        s, j = i % slots, i % nl
-        c = lanes[j]
+        """batch i: encode + decode on its lane (queued behind its tables) or on its
+        encode/decode stream (after an event wait for its tables)"""
+        s, jt = i % slots, tab_index(i)
+        j = i % ne
+        c = elanes[j]
         sL = c.stream
+        tj = tabs[jt]
         with torch.cuda.stream(sL):
+            if elanes is not lanes:
+                sL.wait_event(ev_tab[s])
             e = rec("encode", sL)
             tc = time.perf_counter()
             if world > 1:   # place the shard in the global stream before writing it: sizes,
                 # all-gather + prefix sum on the device, offset read by the kernel (no host sync)
-                total = codec.encode_size(c, tabs[j], codes[s], raw_first, halo[s])
+                total = codec.encode_size(c, tj, codes[s], raw_first, halo[s])
                 goff, _ = shard.bit_offsets_device(total, world, rank)
                 out[j][:4].zero_()   # bits before the offset belong to the previous shard
                 acc["collectives"] += time.perf_counter() - tc if state["timed"] else 0.0
-                codec.encode_write_at(c, tabs[j], codes[s], out[j], goff, raw_first, halo[s],
+                codec.encode_write_at(c, tj, codes[s], out[j], goff, raw_first, halo[s],
                                       args.chunk, coff[j], cprev[j], total=tot_dev[j])
             else:
                 # one pass: look-back offsets, every word stored once (no zeroing of `out`)
-                codec.encode_write(c, tabs[j], codes[s], out[j], 0, raw_first, halo[s],
+                codec.encode_write(c, tj, codes[s], out[j], 0, raw_first, halo[s],
                                    args.chunk, coff[j], cprev[j], total=tot_dev[j])
             done(e, sL)
             ev_enc[s].record(sL)
             enc = codec.Encoded(out[j], -1, args.chunk, coff[j], cprev[j], n, raw_first)
             e = rec("decode", sL)
-            codec.decode(c, tabs[j], enc, out=dec[j])
+            codec.decode(c, tj, enc, out=dec[j])
             done(e, sL)
+            ev_dec[jt].record(sL)
         state["last"] = (s, j)
 
     # Every dependency is an event, so batches are issued in order.  With world > 1 the
     # collectives of all streams run in issue order on the process group's one stream: batch
     # i's bit-offset all-gather (which waits for its tables) is issued after the halo and
     # histogram collectives of batch i + lag, so those never queue behind a table build.
-    lag = 0 if world == 1 or serial else nl - 1
+    # (back(i) must be issued before front(i + lanes * nbuf) waits for its decode)
+    lag = 0 if world == 1 or serial else nl * nbuf - 1
 
     def run(steps):
         for i in range(steps):
@@ -333,10 +375,11 @@ def main():
     s_last, j_last = state["last"]
 
     # correctness after timing (not timed): exact round trip of the last batch, status words
-    for j, c in enumerate(lanes):
+    for t in tabs:
+        t.status()
+    for c in elanes:
         codec.decode_status(c)
         codec.encode_status(c)
-        tabs[j].status()
     assert torch.equal(dec[j_last], codes[s_last]), "round trip mismatch"
     rerank = pq.rerank_count(ctx)
     bits_per_vec = int(tot_dev[j_last].item()) / n
