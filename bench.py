@@ -363,6 +363,7 @@ def main():
     state["timed"] = True
     t0 = time.perf_counter()
     run(args.steps)
+    t_issue = time.perf_counter() - t0          # host time to issue the K steps
     barrier()
     elapsed = time.perf_counter() - t0
     state["timed"] = False
@@ -436,6 +437,7 @@ def main():
             "encode_read_roofline_frac": round(BYTES_PER_VEC_READ * n / t_enc / 1e9 / HBM_PEAK_GBS, 4),
             "roundtrip_read_roofline_frac": round(
                 BYTES_PER_VEC_READ * n * world * args.steps / elapsed / 1e9 / HBM_PEAK_GBS / world, 4),
+            "host_issue_ms_per_step": round(t_issue / args.steps * 1e3, 3),
             "bits_per_vector": round(bits_per_vec, 3),
             "rerank_fraction": round(rerank / (n * m), 6),
         }
