@@ -22,7 +22,7 @@ namespace {
 
 constexpr int kEncBlock = 512;   // vectors per encode workgroup (one thread each)
 constexpr int kMaxCodeLen = 56;
-constexpr int kHistChunk = 32768; // vectors per context-histogram workgroup (< 65536)
+constexpr int kHistChunk = 61440; // vectors per context-histogram workgroup (< 65536)
 
 template <typename CodeT>
 __device__ __forceinline__ unsigned ld_code(const CodeT* c, long long i) { return (unsigned)c[i]; }
@@ -46,40 +46,45 @@ hist_ctx(const CodeT* __restrict__ codes, long long n, int m_total, int k,
     const int words = split == 1 ? all_words : prows * k / 2;
     for (int w = threadIdx.x; w < words; w += blockDim.x) pairs[w] = 0;
     constexpr int kRun = kHistChunk / 1024;   // consecutive vectors per thread
+    constexpr int kSub = 20;                  // ... taken kSub at a time (registers)
+    static_assert(kRun % kSub == 0 && kSub % 2 == 0, "whole 16-byte row pairs per group");
     const long long v0 = (long long)blockIdx.x * kHistChunk + (long long)threadIdx.x * kRun;
-    // this thread's part-m codes of rows v0 - 1 .. v0 + kRun - 1, all loads issued before the
-    // first counter update (8-byte rows of u8 codes: whole rows, 16 B per load)
-    unsigned c[kRun + 1];
-    const bool wide = sizeof(CodeT) == 1 && m_total == 8 && v0 + kRun <= n;
-    if (wide) {
-        const uint4* rows = reinterpret_cast<const uint4*>(codes + v0 * 8);
-        uint4 q[kRun / 2];
-#pragma unroll
-        for (int u = 0; u < kRun / 2; ++u) q[u] = rows[u];
-        c[0] = v0 > 0 ? (unsigned)codes[(v0 - 1) * 8 + m] : (prev_row ? (unsigned)prev_row[m] : ~0u);
-        const int sh = 8 * (m & 3);
-#pragma unroll
-        for (int u = 0; u < kRun / 2; ++u) {
-            const unsigned a = m < 4 ? q[u].x : q[u].y, b = m < 4 ? q[u].z : q[u].w;
-            c[1 + 2 * u] = (a >> sh) & 0xFFu;
-            c[2 + 2 * u] = (b >> sh) & 0xFFu;
-        }
-    } else {
-        for (int u = 0; u <= kRun; ++u) {
-            const long long v = v0 - 1 + u;
-            c[u] = v < 0 ? (prev_row ? (unsigned)prev_row[m] : ~0u)
-                 : v < n ? ld_code(codes, v * m_total + m) : ~0u;
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int u = 1; u <= kRun; ++u) {
-        const unsigned prev = c[u - 1], cur = c[u];
-        if (prev >= (unsigned)k || cur >= (unsigned)k) continue;  // absent / out of alphabet
+    auto count = [&](unsigned prev, unsigned cur) {
+        if (prev >= (unsigned)k || cur >= (unsigned)k) return;   // absent / out of alphabet
         const unsigned pr = prev - plo;
-        if (pr >= (unsigned)prows) continue;                      // another split's range
+        if (pr >= (unsigned)prows) return;                       // another split's range
         const unsigned bin = pr * (unsigned)k + cur;
         atomicAdd(&pairs[bin >> 1], 1u << ((bin & 1u) * 16));
+    };
+    unsigned prevc = v0 > 0 ? (v0 - 1 < n ? ld_code(codes, (v0 - 1) * m_total + m) : ~0u)
+                            : (prev_row ? (unsigned)prev_row[m] : ~0u);
+    const bool wide = sizeof(CodeT) == 1 && m_total == 8 && v0 + kRun <= n;
+    __syncthreads();   // the counters are zeroed (one barrier on every path: `wide` varies)
+    if (wide) {
+        // this thread's part-m codes of kSub consecutive rows per group, all of a group's
+        // loads issued before its counter updates (8-byte rows of u8 codes: 16 B per load)
+        const uint4* rows = reinterpret_cast<const uint4*>(codes + v0 * 8);
+        const int sh = 8 * (m & 3);
+        for (int g = 0; g < kRun / kSub; ++g) {
+            uint4 q[kSub / 2];
+#pragma unroll
+            for (int u = 0; u < kSub / 2; ++u) q[u] = rows[g * (kSub / 2) + u];
+#pragma unroll
+            for (int u = 0; u < kSub / 2; ++u) {
+                const unsigned a = m < 4 ? q[u].x : q[u].y, b = m < 4 ? q[u].z : q[u].w;
+                const unsigned ca = (a >> sh) & 0xFFu, cb = (b >> sh) & 0xFFu;
+                count(prevc, ca);
+                count(ca, cb);
+                prevc = cb;
+            }
+        }
+    } else {
+        for (int u = 0; u < kRun; ++u) {
+            const long long v = v0 + u;
+            const unsigned cur = v < n ? ld_code(codes, v * m_total + m) : ~0u;
+            count(prevc, cur);
+            prevc = cur;
+        }
     }
     __syncthreads();
     uint32_t* out = partial + ((long long)m * gridDim.x + blockIdx.x) * all_words +
