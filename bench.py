@@ -264,8 +264,8 @@ def main():
         if used[s]:                  # the slot's previous batch: tables built (counts free)
             st.wait_event(ev_tab[s])
         e = rec("hist", st)
-        counts[s].zero_()
-        codec.histogram(c, codes[s], k, ctxm, prev_row=halo[s], counts=counts[s])
+        codec.histogram(c, codes[s], k, ctxm, prev_row=halo[s], counts=counts[s],
+                        accumulate=False)            # overwrites: no zeroing pass
         done(e, st)
         tc = time.perf_counter()
         shard.reduce_counts(counts[s], world)

@@ -107,6 +107,9 @@ int pqh_kmeans_train(pqh_ctx_t* ctx, const float* d_x, long long n, long long ld
  * shard boundary).  d_counts must be zeroed by the caller before the first call. */
 int pqh_histogram(pqh_ctx_t* ctx, const void* d_codes, long long n, int m, int k, int context,
                   const void* d_prev_row, uint32_t* d_counts);
+/* counts = histogram of codes (overwrites; no zeroing by the caller).  Same arguments. */
+int pqh_histogram_set(pqh_ctx_t* ctx, const void* d_codes, long long n, int m, int k,
+                      int context, const void* d_prev_row, uint32_t* d_counts);
 
 /* ---- code tables ------------------------------------------------------------------ */
 /* Device-resident Huffman code tables of m parts: encode entries + decode lookup tables. */

@@ -105,6 +105,7 @@ SIGNATURES = [
     ("pqh_pq_reconstruct", I, [P, P, P, LL, P, LL]),
     ("pqh_kmeans_train", I, [P, P, LL, LL, I, I, I, I, P]),
     ("pqh_histogram", I, [P, P, LL, I, I, I, P, P]),
+    ("pqh_histogram_set", I, [P, P, LL, I, I, I, P, P]),
     ("pqh_tables_create", I, [P, P, I, P]), ("pqh_tables_destroy", I, [P]),
     ("pqh_tables_alloc", I, [P, I, I, I, P]), ("pqh_tables_build", I, [P, P, P]),
     ("pqh_tables_upload", I, [P, P, P]), ("pqh_tables_status", I, [P, P]),

@@ -299,14 +299,19 @@ class Tables:
             pass
 
 
-def histogram(ctx: Context, codes, k: int, context: bool, prev_row=None, counts=None):
+def histogram(ctx: Context, codes, k: int, context: bool, prev_row=None, counts=None,
+              accumulate: bool = True):
+    """counts (+)= the symbol histogram of codes (huffman_encoder.c:139-205);
+    accumulate=False overwrites `counts` (pqh_histogram_set: no zeroing pass)."""
     torch = _torch()
     n, m = codes.shape
     items = k * k if context else k
     if counts is None:
-        counts = torch.zeros((m, items), dtype=torch.int32, device=codes.device)
-    check(lib().pqh_histogram(ctx.ptr, _ptr(codes), n, m, k, int(context), _ptr(prev_row),
-                              _ptr(counts)), "pqh_histogram")
+        counts = torch.empty((m, items), dtype=torch.int32, device=codes.device)
+        accumulate = False
+    fn = lib().pqh_histogram if accumulate else lib().pqh_histogram_set
+    check(fn(ctx.ptr, _ptr(codes), n, m, k, int(context), _ptr(prev_row), _ptr(counts)),
+          "pqh_histogram")
     return counts
 
 

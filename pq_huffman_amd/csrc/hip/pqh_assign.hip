@@ -311,7 +311,8 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
                const bf16x8* __restrict__ afrag, const float* __restrict__ cent,
                const float* __restrict__ cmax, const float* __restrict__ sqrt_cmax,
                CodeT* __restrict__ codes, uint32_t* __restrict__ counts,
-               unsigned long long* __restrict__ rerank, uint32_t* __restrict__ sched, int gx) {
+               unsigned long long* __restrict__ rerank, uint32_t* __restrict__ sched, int gx,
+               unsigned long long* __restrict__ rerank_next, uint32_t* __restrict__ sched_next) {
     using P = Plan<D>;
     constexpr int K = kTiles * 32;
     __shared__ uint32_t hist[kWavesPerWG][K];
@@ -337,6 +338,15 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     const int bx = inter ? (L / (8 * m_total)) * 8 + (L & 7) : L % gx;
     const int r = lane & 31;
     const int h = lane >> 5;
+    if (L == 0 && wave == 0) {   // the next launch's queue heads and re-rank counter
+        // (agent-scope stores: written through to where the next launch's atomics act)
+        if (sched_next)
+            for (int q = lane; q < m_total * kXcds; q += 64)
+                __hip_atomic_store(sched_next + q * kSchedStride, 0u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0)
+            __hip_atomic_store(rerank_next, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     {
         const uint4* src = reinterpret_cast<const uint4*>(afrag) + (long long)m * P::PA * kTiles * 64;
         for (int i = threadIdx.x; i < P::PA * kTiles * 64; i += blockDim.x) As[i] = src[i];
@@ -914,11 +924,16 @@ int launch_mfma(pqh_ctx* ctx, pqh_pq* pq, const float* x, long long n, long long
     const long long nblk = (n + 31) / 32;
     const int groups = pq->m;   // grid y: one subspace per workgroup
     dim3 block(64 * kWavesPerWG);
-    unsigned long long* rr = ctx->d_diag;
+    // alternate launches use alternate queue-head sets and re-rank counters; each zeroes the
+    // other's for the next launch (the stream orders the launches)
+    const int ring = (int)(ctx->assign_launches++ & 1);
+    unsigned long long* rr = ctx->d_diag + (ring ? 4 : 0);
+    unsigned long long* rr_next = ctx->d_diag + (ring ? 0 : 4);
+    ctx->rerank_slot = ring ? 4 : 0;
 #ifdef PQH_ASSIGN_STATIC   // diagnostic: static chunk stride, no work queues
     uint32_t* sched = nullptr;
 #else
-    uint32_t* sched = pq->m <= kSchedMax ? ctx->d_sched : nullptr;
+    uint32_t* sched = pq->m <= kSchedMax ? ctx->d_sched + ring * kSchedSet : nullptr;
 #endif
     // grid = the workgroups that are resident at once (persistent, grid-stride over the
     // 32-vector blocks): more would only queue behind the first wave of workgroups
@@ -932,12 +947,10 @@ int launch_mfma(pqh_ctx* ctx, pqh_pq* pq, const float* x, long long n, long long
         long long gx = (long long)ctx->num_cus * per_cu / groups;                           \
         gx = std::max(1ll, std::min(gx, ((nblk + kNB - 1) / kNB + kWavesPerWG - 1) / kWavesPerWG)); \
         if (gx >= 16) gx &= ~7ll;   /* CU-uniform subspace placement (see the kernel) */   \
-        if (sched)                                                                          \
-            PQH_HIP(ctx, hipMemsetAsync(sched, 0, (size_t)pq->m * kXcds * kSchedStride * 4,  \
-                                        ctx->stream));                                      \
         hipLaunchKernelGGL((pq_assign_mfma<DD, CodeT>), dim3((unsigned)(gx * groups)), block, \
                            0, ctx->stream, x, n, ldx, pq->m, pq->d_afrag, pq->d_cent,       \
-                           pq->d_cmax, pq->d_sqc, codes, counts, rr, sched, (int)gx);       \
+                           pq->d_cmax, pq->d_sqc, codes, counts, rr, sched, (int)gx,         \
+                           rr_next, sched ? ctx->d_sched + (1 - ring) * kSchedSet : nullptr); \
         PQH_LAUNCH_CHECK(ctx);                                                              \
         break;                                                                              \
     }
@@ -1040,12 +1053,16 @@ int pqh_pq_assign(pqh_ctx_t* ctx, const pqh_pq_t* cpq, const float* d_x, long lo
         return PQH_ERR_ARG;
     int rc = pqh_use_device(ctx);
     if (rc) return rc;
-    PQH_HIP(ctx, hipMemsetAsync(ctx->d_diag, 0, sizeof(unsigned long long), ctx->stream));
-    if (n == 0) return PQH_OK;
-    bool mfma = mode == 0 && pq->mfma_ok;
+    bool mfma = mode == 0 && pq->mfma_ok && n > 0;
     if (mfma && pq->dsub % 4 == 0 &&
         ((ld_x % 4) != 0 || (reinterpret_cast<uintptr_t>(d_x) & 15u) != 0))
         mfma = false;  // vector loads need 16-byte aligned subspace slices
+    // the other paths re-rank nothing: their count is d_diag[6] = 0
+    if (!mfma) {
+        ctx->rerank_slot = 6;
+        PQH_HIP(ctx, hipMemsetAsync(ctx->d_diag + 6, 0, sizeof(unsigned long long), ctx->stream));
+    }
+    if (n == 0) return PQH_OK;
     if (pq->k <= 256) {
         uint8_t* c = static_cast<uint8_t*>(d_codes);
         return mfma ? launch_mfma(ctx, pq, d_x, n, ld_x, c, d_counts)
@@ -1066,7 +1083,7 @@ int pqh_debug_assign_stamps(pqh_ctx_t* ctx, unsigned long long* out, int max_wav
 
 int pqh_pq_last_rerank_count(pqh_ctx_t* ctx, unsigned long long* count) {
     if (!ctx || !count) return PQH_ERR_ARG;
-    PQH_HIP(ctx, hipMemcpyAsync(count, ctx->d_diag, sizeof(unsigned long long),
+    PQH_HIP(ctx, hipMemcpyAsync(count, ctx->d_diag + ctx->rerank_slot, sizeof(unsigned long long),
                                 hipMemcpyDeviceToHost, ctx->stream));
     PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return PQH_OK;

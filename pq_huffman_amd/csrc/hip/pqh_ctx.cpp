@@ -86,8 +86,8 @@ int pqh_ctx_create(pqh_ctx_t** out, int device) {
     ctx->own_stream = true;
     if (hipMalloc(&ctx->d_diag, 8 * sizeof(unsigned long long)) != hipSuccess ||
         hipMemset(ctx->d_diag, 0, 8 * sizeof(unsigned long long)) != hipSuccess ||
-        hipMalloc(&ctx->d_sched, (size_t)kSchedMax * kXcds * kSchedStride * sizeof(uint32_t)) != hipSuccess ||
-        hipMemset(ctx->d_sched, 0, (size_t)kSchedMax * kXcds * kSchedStride * sizeof(uint32_t)) != hipSuccess) {
+        hipMalloc(&ctx->d_sched, (size_t)2 * kSchedSet * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(ctx->d_sched, 0, (size_t)2 * kSchedSet * sizeof(uint32_t)) != hipSuccess) {
         if (ctx->d_diag) (void)hipFree(ctx->d_diag);
         if (ctx->d_sched) (void)hipFree(ctx->d_sched);
         (void)hipStreamDestroy(ctx->stream);

@@ -102,7 +102,7 @@ hist_ctx(const CodeT* __restrict__ codes, long long n, int m_total, int k,
 // packed word, so every counter has a single writer)
 __global__ void __launch_bounds__(256)
 hist_ctx_reduce(const uint32_t* __restrict__ partial, int chunks, int words, long long items,
-                uint32_t* __restrict__ counts) {
+                uint32_t* __restrict__ counts, int set) {
     const int m = blockIdx.y;
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= words) return;
@@ -114,8 +114,13 @@ hist_ctx_reduce(const uint32_t* __restrict__ partial, int chunks, int words, lon
         hi += x >> 16;
     }
     uint32_t* out = counts + (long long)m * items;
-    if (lo) out[2 * w] += lo;
-    if (hi && 2 * w + 1 < items) out[2 * w + 1] += hi;
+    if (set) {   // every counter has exactly one writer: a plain store overwrites
+        out[2 * w] = lo;
+        if (2 * w + 1 < items) out[2 * w + 1] = hi;
+    } else {
+        if (lo) out[2 * w] += lo;
+        if (hi && 2 * w + 1 < items) out[2 * w + 1] += hi;
+    }
 }
 
 template <typename CodeT>
@@ -511,12 +516,15 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
 
 extern "C" {
 
-int pqh_histogram(pqh_ctx_t* ctx, const void* d_codes, long long n, int m, int k, int context,
-                  const void* d_prev_row, uint32_t* d_counts) {
+static int histogram_impl(pqh_ctx_t* ctx, const void* d_codes, long long n, int m, int k,
+                          int context, const void* d_prev_row, uint32_t* d_counts, int set) {
     if (!ctx || m <= 0 || k <= 0 || n < 0 || !d_counts || (n > 0 && !d_codes)) return PQH_ERR_ARG;
     if (context && k > 256) return PQH_ERR_UNSUPPORTED;
     int rc = pqh_use_device(ctx);
     if (rc) return rc;
+    const long long items = context ? (long long)k * k : k;
+    if (set && (n == 0 || !context))   // the plain kernel and an empty input only add
+        PQH_HIP(ctx, hipMemsetAsync(d_counts, 0, (size_t)m * items * 4, ctx->stream));
     if (n == 0) return PQH_OK;
     if (context) {
         const unsigned chunks = (unsigned)((n + kHistChunk - 1) / kHistChunk);
@@ -539,7 +547,8 @@ int pqh_histogram(pqh_ctx_t* ctx, const void* d_codes, long long n, int m, int k
                            static_cast<const uint8_t*>(d_prev_row), partial, split);
         PQH_LAUNCH_CHECK(ctx);
         hipLaunchKernelGGL(hist_ctx_reduce, dim3((unsigned)((words + 255) / 256), m), dim3(256), 0,
-                           ctx->stream, partial, (int)chunks, words, (long long)k * k, d_counts);
+                           ctx->stream, partial, (int)chunks, words, (long long)k * k, d_counts,
+                           set);
     } else {
         const unsigned blocks = (unsigned)std::min<long long>((n + 4095) / 4096, 512);
         if (k <= 256)
@@ -551,6 +560,16 @@ int pqh_histogram(pqh_ctx_t* ctx, const void* d_codes, long long n, int m, int k
     }
     PQH_LAUNCH_CHECK(ctx);
     return PQH_OK;
+}
+
+int pqh_histogram(pqh_ctx_t* ctx, const void* d_codes, long long n, int m, int k, int context,
+                  const void* d_prev_row, uint32_t* d_counts) {
+    return histogram_impl(ctx, d_codes, n, m, k, context, d_prev_row, d_counts, 0);
+}
+
+int pqh_histogram_set(pqh_ctx_t* ctx, const void* d_codes, long long n, int m, int k,
+                      int context, const void* d_prev_row, uint32_t* d_counts) {
+    return histogram_impl(ctx, d_codes, n, m, k, context, d_prev_row, d_counts, 1);
 }
 
 // workspace layout for encode: [block_bits u32 nb][pad][block_off u64 nb]

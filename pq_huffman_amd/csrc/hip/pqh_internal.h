@@ -20,7 +20,8 @@ struct pqh_ctx {
     // grow-only scratch (stream ordered use, allocated outside timed regions)
     void* ws = nullptr;
     size_t ws_bytes = 0;
-    // [0] rerank count, [1] decode error, [2] encode capacity error, [3] scratch total bits
+    // [0] / [4] re-rank counters of alternate assignment launches, [1] decode error,
+    // [2] encode capacity error, [3] scratch total bits, [6] re-rank count of the exact path
     unsigned long long* d_diag = nullptr;
     // one-pass encoder look-back state: [lb_cap] block states, [lb_cap] tails, ticket
     unsigned long long* lb_state = nullptr;
@@ -28,12 +29,16 @@ struct pqh_ctx {
     unsigned lb_epoch = 0;
     unsigned long long lb_ticket_base = 0;
     // work-queue heads of the assignment kernel: kXcds per subspace, kSchedStride words
-    // apart, zeroed before every launch
+    // apart; two sets used by alternate launches, each launch zeroing the other set (and the
+    // other re-rank counter, d_diag[0] / d_diag[4]) for the next one -- no memset dispatches
     uint32_t* d_sched = nullptr;
+    unsigned long long assign_launches = 0;
+    int rerank_slot = 0;              // d_diag slot of the last assignment's re-rank count
 };
 constexpr int kSchedMax = 64;      // subspaces with a work queue (more: static schedule)
 constexpr int kXcds = 8;
 constexpr int kSchedStride = 64;   // u32 words = 256 B
+constexpr long long kSchedSet = (long long)kSchedMax * kXcds * kSchedStride;   // words per set
 
 int pqh_set_error(pqh_ctx* ctx, int code, const char* fmt, ...);
 int pqh_ensure_ws(pqh_ctx* ctx, size_t bytes);

@@ -61,6 +61,21 @@ def test_k4096_noctx_vs_reference(gpu):
 
 
 @pytest.mark.parametrize("ctxm", [True, False])
+def test_histogram_set_overwrites(gpu, oracle, ctxm):
+    """pqh_histogram_set: counts = histogram, whatever the buffer held (the bench's form);
+    n = 0 gives zeros.  Sizes span several 61,440-vector chunks plus a partial one."""
+    torch, codec, ctx = gpu
+    for n in (130001, 5, 0):
+        codes = datagen.skewed_codes(max(n, 1), 8, seed=9)[:n]
+        cd = torch.from_numpy(np.ascontiguousarray(codes)).cuda().reshape(n, 8)
+        items = 256 * 256 if ctxm else 256
+        junk = torch.full((8, items), 12345, dtype=torch.int32, device="cuda")
+        codec.histogram(ctx, cd, 256, ctxm, counts=junk, accumulate=False)
+        want = (oracle.histogram(codes, 256, ctxm) if n else np.zeros((8, items), np.int64))
+        assert np.array_equal(codec.counts_to_host(junk), want)
+
+
+@pytest.mark.parametrize("ctxm", [True, False])
 def test_histogram_vs_oracle_with_halo(gpu, oracle, ctxm):
     torch, codec, ctx = gpu
     codes = datagen.skewed_codes(70001, 8, seed=8)
