@@ -262,6 +262,8 @@ def main():
             e1.record(stream)
 
     hist_on_lane = args.hist_on == "lanes" and not serial
+    parts = torch.arange(m, device=dev)
+    ones_m = torch.ones(m, dtype=torch.int32, device=dev)
 
     def hist(s, c, st):
         """batch s's symbol histogram on stream st (context c)"""
@@ -292,16 +294,24 @@ def main():
             e = rec("assign", sF)
             pq.assign(x, codes[s], ctx=cF)
             done(e, sF)
-            tc = time.perf_counter()
-            halo[s] = shard.exchange_halo(codes[s][-1], world, rank) if ctxm else None
-            acc["collectives"] += time.perf_counter() - tc if state["timed"] else 0.0
-            if not hist_on_lane:
+            halo[s] = None
+            if not hist_on_lane:     # (the shard-boundary pair is added on the lane)
                 hist(s, cF, sF)
             ev_hist[s].record(sF)
         with torch.cuda.stream(sL):
             sL.wait_event(ev_hist[s])
+            # the one-row halo all-gather on the lane too, so the assignment stream never
+            # waits for RCCL; the pair (previous shard's last row, first row) is one more
+            # count per part, exactly what pqh_histogram's prev_row adds
+            tc = time.perf_counter()
+            halo[s] = shard.exchange_halo(codes[s][-1], world, rank) if ctxm else None
+            acc["collectives"] += time.perf_counter() - tc if state["timed"] else 0.0
             if hist_on_lane:
                 hist(s, c, sL)
+            elif halo[s] is not None:
+                cs = counts[s]
+                cs.index_put_((parts, halo[s].long() * k + codes[s][0].long()), ones_m,
+                              accumulate=True)
             reduce(s)
         used[s] = True
         with torch.cuda.stream(sL):
@@ -324,6 +334,8 @@ def main():
         with torch.cuda.stream(sL):
             if elanes is not lanes:
                 sL.wait_event(ev_tab[s])
+            if halo[s] is not None:   # made on the table lane: keep it until this stream's use
+                halo[s].record_stream(sL)
             e = rec("encode", sL)
             tc = time.perf_counter()
             if world > 1:   # place the shard in the global stream before writing it: sizes,
@@ -457,9 +469,22 @@ def main():
             res["cpu_baseline"]["host_cpu"] = _cpu_name()
             res["cpu_baseline"]["nproc"] = os.cpu_count()
         print(json.dumps(res), flush=True)
+    # teardown in a fixed order while HIP is alive (tables, codebook, contexts), rather than
+    # in whatever order the interpreter's exit happens to collect them
+    torch.cuda.synchronize()
+    for t in tabs:
+        t.close()
+    pq.close()
+    for c in {id(c): c for c in list(lanes) + list(elanes) + [ctx]}.values():
+        c.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+        # (a rank once died with SIGSEGV in the interpreter's exit after the last barrier in
+        # a gloo rehearsal; the results are out, so leave without further teardown)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
 
 
 def _cpu_name():
