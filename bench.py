@@ -85,6 +85,8 @@ def parse():
                          "lane (before its code tables)")
     ap.add_argument("--tbufs", type=int, default=2,
                     help="code-table sets per table lane when --elanes > 0")
+    ap.add_argument("--a-priority", action="store_true",
+                    help="run the assignment stream at high priority")
     ap.add_argument("--extra-slots", type=int, default=3,
                     help="code/count buffers beyond one per lane")
     ap.add_argument("--dist-backend", default="nccl",
@@ -203,7 +205,9 @@ def main():
     # hardware queues per process (GPU_MAX_HW_QUEUES, HIP's default) none share a queue.
     # Serial: everything on A, in order.
     serial = args.sched == "serial" or args.no_overlap
-    ctx = codec.Context(local)
+    # stream A: torch's default stream, or (--a-priority) a high-priority stream of its own
+    ctx = (codec.Context(local, stream=torch.cuda.Stream(device=dev, priority=-1))
+           if args.a_priority else codec.Context(local))
     sA = ctx.stream
     nl = 1 if serial else max(1, args.lanes)
     # (cus >= the device's CU count: a library stream of its own without a CU mask)

@@ -338,6 +338,9 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     const int bx = inter ? (L / (8 * m_total)) * 8 + (L & 7) : L % gx;
     const int r = lane & 31;
     const int h = lane >> 5;
+#ifdef PQH_ASSIGN_PRIO   // (experiment) wave issue priority against concurrent kernels
+    __builtin_amdgcn_s_setprio(PQH_ASSIGN_PRIO);
+#endif
     if (L == 0 && wave == 0) {   // the next launch's queue heads and re-rank counter
         // (agent-scope stores: written through to where the next launch's atomics act)
         if (sched_next)
