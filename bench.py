@@ -443,6 +443,10 @@ def main():
                                     "every timed step runs all five stages and the pipeline "
                                     "fills and drains inside the timed region")},
             "roofline": {"kernel": "pq_assign_mfma", "bound": "hbm",
+                         # what actually limits the kernel (PMC): the
+                         # wave64 VALU issue of the top-2 key reduction, ~4 cycles each
+                         "limiter": "VALU issue (top-2 key reduction), not HBM",
+                         "mfma_tflops_algorithmic": round(65536 * n / t_assign / 1e12, 1),
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "traffic_source": traffic_src,

@@ -245,6 +245,9 @@ huff_trees_small(const uint32_t* __restrict__ counts, int k, long long trees,
     const uint32_t* cnt = counts + tree * k;
     unsigned long long* out = enc + tree * k;
     const bool stamp = tree == 0;
+#ifdef PQH_LAT_PRIO   // (experiment) latency-bound waves first in issue arbitration
+    __builtin_amdgcn_s_setprio(PQH_LAT_PRIO);
+#endif
     if (stamp) g_tree_stamps[0] = __builtin_amdgcn_s_memtime();
     uint32_t* kid = kid_all + t;
     uint32_t* lcnt = kid;                      // leaf counts until the first merge
@@ -835,6 +838,9 @@ dec_chunks(const uint32_t* __restrict__ words, long long nwords, long long n, in
     CodeT* stage = reinterpret_cast<CodeT*>(lds + meta_b + l1_b + ((long long)win_words + 4) * 4);
     const int lane = threadIdx.x;
     const bool stamp = blockIdx.x == 0 && lane == 0;
+#ifdef PQH_LAT_PRIO   // (experiment) latency-bound waves first in issue arbitration
+    __builtin_amdgcn_s_setprio(PQH_LAT_PRIO);
+#endif
     if (stamp) g_tree_stamps[8] = __builtin_amdgcn_s_memtime();
     for (long long t = lane; t < tables; t += 64) meta[t] = meta_g[t];
     if constexpr (L1_IN_LDS) {
