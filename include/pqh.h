@@ -201,6 +201,36 @@ int pqh_chunk_index_host(const pqh_tables_t* t, const unsigned char* stream,
  * (strncmp order), uint8 codes only.  d_tmp: n*m bytes scratch. */
 int pqh_sort_rows(pqh_ctx_t* ctx, void* d_codes, long long n, int m, void* d_tmp);
 
+/* ---- tree-ordered context coding (huffman_encoder.c --tree: :240-286, :321-375) ---- */
+/* DFS order of a stored forest (mst.tree: tree_load_file, mst.c:273-288 -- num_edges
+ * u32 targets grouped by source, children_counts[v] of them per vertex) exactly as
+ * tree_collect_vertices_dfs (mst.c:290-364), plus each stream row's coding context, the
+ * traverser's active parent (mst.c:366-405): parents[p] = the parent's vertex id, or -1 for
+ * a root.  Host; returns num_roots (>= 1 when num_vertices > 0) or PQH_ERR_ARG.
+ * parents may be NULL. */
+int pqh_tree_order(long long num_vertices, long long num_edges, const uint32_t* edge_targets,
+                   const int* children_counts, uint32_t* vertices, int* num_children,
+                   long long* parents);
+/* d_rows[p] = d_codes[d_vertices[p]] (stream order) and d_tree_prev[p][i] =
+ * d_codes[d_parents[p]][i], 0xFFFF for a root.  Ids outside [0, n) are reported by
+ * pqh_tree_status (nothing is read for them). */
+int pqh_tree_gather(pqh_ctx_t* ctx, const void* d_codes, long long n, int m, int k,
+                    const uint32_t* d_vertices, const long long* d_parents, void* d_rows,
+                    uint16_t* d_tree_prev);
+/* Synchronises; PQH_ERR_ARG if the last pqh_tree_gather met an id outside the rows. */
+int pqh_tree_status(pqh_ctx_t* ctx);
+/* counts[i][prev][cur] += pairs (d_tree_prev[p][i], d_rows[p][i]) of the non-root rows
+ * (tree_collect_indices_stats, mst.c:442-490); K = 256, u8 rows. */
+int pqh_histogram_tree(pqh_ctx_t* ctx, const void* d_rows, const uint16_t* d_tree_prev,
+                       long long n, int m, int k, uint32_t* d_counts);
+/* encode_tree_data (huffman_encoder.c:240-286): context tables, each row coded in its
+ * d_tree_prev context, roots raw 8 bits per part.  Same buffer rules as pqh_encode_write
+ * (no chunk index: decoding a tree stream needs the children stream). */
+int pqh_encode_tree_write(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_rows,
+                          const uint16_t* d_tree_prev, long long n,
+                          unsigned long long bit_offset, unsigned char* d_out,
+                          unsigned long long out_bytes, unsigned long long* d_total_bits);
+
 /* ---- whole-file host helpers used by the CLI tools ------------------------------- */
 typedef struct {
     int context;           /* order-1 context coding (default 1) */

@@ -188,6 +188,27 @@ def huffman_mode_fixtures(lib, tmp, n, m, seed, name, full=True):
     return summary
 
 
+def tree_fixtures(tmp, n=1000, m=8, seed=21, roots=3, name="tree_m8_n1000"):
+    """Tree mode (huffman_encoder --tree mst.tree, huffman_decoder --tree) on a seeded
+    forest in the reference's mst.tree layout, with and without the default sort."""
+    codes = datagen.skewed_codes(n, m, 256, seed=seed)
+    targets, counts = datagen.random_forest(n, roots=roots, seed=seed)
+    tree = os.path.join(tmp, name + ".tree")
+    datagen.write_tree(tree, n, targets, counts)
+    arrays = {"input": codes, "targets": targets, "counts": counts}
+    for mode, flags in (("tree_nosort", ["--no-sort"]), ("tree_sort", [])):
+        out, _ = run_cli_encode(codes, flags + ["--tree", tree], tmp, f"{name}_{mode}")
+        outf = os.path.join(tmp, f"{name}_{mode}_decoded.bin")
+        r = subprocess.run([os.path.join(REF, "huffman_decoder"), out, "--output-file", outf,
+                            "--tree"], capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr
+        arrays[mode + "__decoded"] = np.fromfile(outf, np.uint8).reshape(n, m)
+        for f in ("huffman_codebooks.bin", "huffman_indices.bin",
+                  "huffman_children_codebooks.bin", "huffman_children.bin"):
+            arrays[mode + "__" + f.split(".")[0]] = np.frombuffer(read(out + f), np.uint8)
+    np.savez_compressed(os.path.join(GOLD, f"huff_{name}.npz"), **arrays)
+
+
 def k4096_fixture(lib, tmp):
     n, m = 2000, 8
     codes = datagen.skewed_codes(n, m, 4096, seed=11, p=0.004)
@@ -242,6 +263,15 @@ def pq_fixtures():
 
 def main():
     build()
+    if sys.argv[1:] == ["tree"]:   # only the tree-mode fixtures
+        tmp = tempfile.mkdtemp(prefix="pqh_golden_")
+        try:
+            tree_fixtures(tmp)
+            tree_fixtures(tmp, n=300, m=16, seed=22, roots=1, name="tree_m16_n300")
+            tree_fixtures(tmp, n=64, m=8, seed=23, roots=16, name="tree_m8_n64_forest")
+        finally:
+            shutil.rmtree(tmp, ignore_errors=True)
+        return
     os.makedirs(GOLD, exist_ok=True)
     lib = reflib()
     tmp = tempfile.mkdtemp(prefix="pqh_golden_")

@@ -49,6 +49,12 @@ def lib():
         L.orc_stats_json.argtypes = [LL, I, I, I, P, ctypes.c_char_p, I]
         L.orc_stats_json.restype = I
         L.orc_bitstream_write.argtypes = [P, P, I, P, LL]
+        L.orc_decode_tree.argtypes = [P, LL, LL, I, I, P, P, I, P, P]
+        L.orc_tree_order.argtypes = [LL, LL, P, P, P, P]
+        L.orc_tree_parents.argtypes = [LL, P, P, P]
+        L.orc_tree_histogram.argtypes = [P, LL, I, I, P, P, P]
+        L.orc_tree_encode.argtypes = [P, LL, I, I, P, P, P, P, I, P, LL]
+        L.orc_tree_encode.restype = LL
         L.orc_bitstream_write.restype = LL
         _lib = L
     return _lib
@@ -203,3 +209,79 @@ def estimate_parts(cbs: Codebooks, counts: np.ndarray) -> np.ndarray:
     return np.array([lib().orc_estimate_size(_p(np.ascontiguousarray(cbs.lens[i])),
                                              _p(np.ascontiguousarray(counts[i])), cbs.items)
                      for i in range(cbs.lens.shape[0])])
+
+
+# ---- tree mode (huffman_encoder.c --tree; mst.c:290-490) --------------------------------
+def tree_order(n: int, targets: np.ndarray, counts: np.ndarray):
+    """(vertices u32, num_children i32, num_roots) -- tree_collect_vertices_dfs."""
+    targets = np.ascontiguousarray(targets, np.uint32)
+    counts = np.ascontiguousarray(counts, np.int32)
+    vert = np.zeros(max(n, 1), np.uint32)
+    nch = np.zeros(max(n, 1), np.int32)
+    roots = lib().orc_tree_order(n, len(targets), _p(targets), _p(counts), _p(vert), _p(nch))
+    assert roots >= 0
+    return vert[:n], nch[:n], roots
+
+
+def tree_parents(num_children: np.ndarray, ids=None) -> np.ndarray:
+    """Active traverser parent per stream row (ids=None: stream positions, the decoder's)."""
+    nch = np.ascontiguousarray(num_children, np.int32)
+    n = len(nch)
+    out = np.zeros(max(n, 1), np.int64)
+    idp = None if ids is None else np.ascontiguousarray(ids, np.uint32)
+    lib().orc_tree_parents(n, None if idp is None else _p(idp), _p(nch), _p(out))
+    return out[:n]
+
+
+def tree_histogram(codes: np.ndarray, vertices, parents, k: int = 256) -> np.ndarray:
+    codes = np.ascontiguousarray(codes, np.uint8)
+    n, m = codes.shape
+    out = np.zeros(m * k * k, np.float64)
+    v = np.ascontiguousarray(vertices, np.uint32)
+    par = np.ascontiguousarray(parents, np.int64)
+    lib().orc_tree_histogram(_p(codes), n, m, k, _p(v), _p(par), _p(out))
+    return out.reshape(m, k * k)
+
+
+def tree_codebooks(codes: np.ndarray, vertices, parents, stride: int = 8) -> Codebooks:
+    counts = tree_histogram(codes, vertices, parents)
+    m = codes.shape[1]
+    lens = np.zeros((m, 256 * 256), np.int32)
+    cds = np.zeros((m, 256 * 256, stride), np.uint8)
+    for i in range(m):
+        lens[i], cds[i] = codebook(256, counts[i], True, stride)
+    return Codebooks(256, True, lens, cds, stride)
+
+
+def tree_encode(codes: np.ndarray, vertices, parents, cbs: Codebooks) -> tuple[bytes, int]:
+    codes = np.ascontiguousarray(codes, np.uint8)
+    n, m = codes.shape
+    cap = int(cbs.lens.max(initial=8) + 8) * n * m // 8 + 64
+    out = np.zeros(cap, np.uint8)
+    v = np.ascontiguousarray(vertices, np.uint32)
+    par = np.ascontiguousarray(parents, np.int64)
+    bits = lib().orc_tree_encode(_p(codes), n, m, 256, _p(v), _p(par), _p(cbs.lens),
+                                 _p(cbs.codes), cbs.stride, _p(out), cap)
+    assert bits >= 0
+    return out[:(bits + 7) // 8].tobytes(), bits
+
+
+def tree_decode(stream: bytes, n: int, m: int, cbs: Codebooks, num_children) -> np.ndarray:
+    """Rows in stream (DFS) order, contexts from the children counts."""
+    pos = tree_parents(num_children)
+    buf = np.frombuffer(stream, np.uint8).copy() if len(stream) else np.zeros(1, np.uint8)
+    out = np.zeros((n, m), np.uint8)
+    rc = lib().orc_decode_tree(_p(buf), len(stream), n, m, 256, _p(cbs.lens), _p(cbs.codes),
+                               cbs.stride, _p(out), _p(pos))
+    if rc != 0:
+        raise ValueError(f"oracle tree decode failed rc={rc}")
+    return out
+
+
+def children_codebook(num_children) -> tuple[np.ndarray, Codebooks]:
+    """tree_collect_num_children_stats (mst.c:407-440) + its non-context codebook."""
+    nch = np.asarray(num_children, np.int64)
+    alphabet = int(nch.max(initial=0)) + 1
+    counts = np.bincount(nch, minlength=alphabet).astype(np.float64)
+    lens, cds = codebook(alphabet, counts, False)
+    return counts, Codebooks(alphabet, False, lens[None], cds[None], cds.shape[1])

@@ -294,9 +294,32 @@ static int orc_trie_node(orc_trie_t* t) {
     return t->nodes++;
 }
 
+static int orc_decode_impl(const unsigned char* stream, long long stream_bytes, long long n,
+                           int m, int k, int context, const int* lens,
+                           const unsigned char* codetab, int stride, void* out, int esize,
+                           const long long* parent_pos);
+
 int orc_decode(const unsigned char* stream, long long stream_bytes, long long n, int m, int k,
                int context, const int* lens, const unsigned char* codetab, int stride,
                void* out, int esize) {
+    return orc_decode_impl(stream, stream_bytes, n, m, k, context, lens, codetab, stride, out,
+                           esize, NULL);
+}
+
+/* Tree-mode decode (huffman_decoder.c:214-247 with --tree): row v's context is the decoded
+ * row at stream position parent_pos[v] (the traverser driven by the children stream), a
+ * root (-1) restarts every part with HUFFMAN_NO_SYMBOL, i.e. the raw warm-up bits. */
+int orc_decode_tree(const unsigned char* stream, long long stream_bytes, long long n, int m,
+                    int k, const int* lens, const unsigned char* codetab, int stride,
+                    void* out, const long long* parent_pos) {
+    return orc_decode_impl(stream, stream_bytes, n, m, k, 1, lens, codetab, stride, out, 1,
+                           parent_pos);
+}
+
+static int orc_decode_impl(const unsigned char* stream, long long stream_bytes, long long n,
+                           int m, int k, int context, const int* lens,
+                           const unsigned char* codetab, int stride, void* out, int esize,
+                           const long long* parent_pos) {
     long long per = context ? (long long)k * k : k;
     int roots_per_part = context ? k : 1;
     orc_trie_t trie = {0};
@@ -330,6 +353,9 @@ int orc_decode(const unsigned char* stream, long long stream_bytes, long long n,
     long long pos = 0, total = stream_bytes * 8;
     int rc = 0;
     for (long long v = 0; v < n && !rc; ++v) {
+        if (parent_pos)
+            for (int i = 0; i < m; ++i)
+                prev[i] = parent_pos[v] < 0 ? -1 : ((unsigned char*)out)[parent_pos[v] * m + i];
         for (int i = 0; i < m; ++i) {
             int s;
             if (context && prev[i] < 0) {
@@ -542,4 +568,88 @@ long long orc_bitstream_write(const unsigned char* data, const long long* lens, 
         p += (lens[i] + 7) / 8;
     }
     return w.overflow ? -1 : (w.bits + 7) / 8;
+}
+
+/* ------------------------------------------------------------------------------------
+ * Tree mode (huffman_encoder.c --tree <mst.tree>).
+ * orc_tree_order: tree_collect_vertices_dfs (mst.c:290-364) over the loaded forest
+ * (tree_load_file + restore_tree_edges_pointers, mst.c:52-61,273-288): adjacency of vertex
+ * v = targets[sum(counts[<v]) ...][counts[v]]; returns num_roots.
+ * orc_tree_parents: the tree_traverser (mst.c:366-405) replayed over num_children; ids[p]
+ * is what gets pushed (vertex ids for the encoder, NULL = stream positions for the decoder,
+ * huffman_decoder.c:245).  out[p] = the active parent before row p, -1 if none.
+ * ---------------------------------------------------------------------------------- */
+int orc_tree_order(long long nv, long long ne, const unsigned* targets, const int* counts,
+                   unsigned* vertices, int* num_children) {
+    long long* first = malloc(sizeof(long long) * (nv + 1));
+    unsigned* stack = malloc(sizeof(unsigned) * (nv ? nv : 1));
+    char* seen = calloc(nv ? nv : 1, 1);
+    first[0] = 0;
+    for (long long v = 0; v < nv; ++v) first[v + 1] = first[v] + counts[v];
+    if (first[nv] != ne) { free(first); free(stack); free(seen); return -1; }
+    long long done = 0, sp = 0;
+    unsigned root = 0;
+    int roots = 0;
+    while (done < nv) {
+        if (sp == 0) {
+            while (root < nv && seen[root]) ++root;
+            stack[sp++] = root;
+            seen[root] = 1;
+            ++roots;
+        }
+        unsigned cur = stack[--sp];
+        vertices[done] = cur;
+        int c = 0;
+        for (long long e = first[cur]; e < first[cur + 1]; ++e) c += !seen[targets[e]];
+        num_children[done++] = c;
+        for (long long e = first[cur]; e < first[cur + 1]; ++e)
+            if (!seen[targets[e]]) { seen[targets[e]] = 1; stack[sp++] = targets[e]; }
+    }
+    free(first); free(stack); free(seen);
+    return roots;
+}
+
+void orc_tree_parents(long long n, const unsigned* ids, const int* num_children,
+                      long long* out) {
+    long long* sv = malloc(sizeof(long long) * (n ? n : 1));
+    int* sc = malloc(sizeof(int) * (n ? n : 1));
+    long long sp = 0;
+    for (long long p = 0; p < n; ++p) {
+        out[p] = sp ? sv[sp - 1] : -1;
+        if (sp && --sc[sp - 1] == 0) --sp;
+        if (num_children[p]) { sv[sp] = ids ? ids[p] : p; sc[sp] = num_children[p]; ++sp; }
+    }
+    free(sv); free(sc);
+}
+
+/* tree_collect_indices_stats (mst.c:442-490): pairs (codes[parent], codes[vertex]). */
+void orc_tree_histogram(const unsigned char* codes, long long n, int m, int k,
+                        const unsigned* vertices, const long long* parents, double* counts) {
+    long long per = (long long)k * k;
+    memset(counts, 0, sizeof(double) * per * m);
+    for (long long p = 0; p < n; ++p) {
+        if (parents[p] < 0) continue;
+        for (int i = 0; i < m; ++i)
+            counts[i * per + (long long)codes[parents[p] * m + i] * k + codes[(long long)vertices[p] * m + i]] += 1;
+    }
+}
+
+/* encode_tree_data (huffman_encoder.c:240-286): rows in DFS order, context = parent's code,
+ * roots raw 8 bits per part.  Returns total bits or -1 on overflow. */
+long long orc_tree_encode(const unsigned char* codes, long long n, int m, int k,
+                          const unsigned* vertices, const long long* parents, const int* lens,
+                          const unsigned char* codetab, int stride, unsigned char* out,
+                          long long cap) {
+    long long per = (long long)k * k;
+    orc_bw_t w = {out, cap, 0, 0};
+    memset(out, 0, cap);
+    for (long long p = 0; p < n; ++p) {
+        const unsigned char* cur = codes + (long long)vertices[p] * m;
+        for (int i = 0; i < m; ++i) {
+            if (parents[p] < 0) { orc_bw_put(&w, cur + i, 8); continue; }
+            long long item = i * per + (long long)codes[parents[p] * m + i] * k + cur[i];
+            orc_bw_put(&w, codetab + item * stride, lens[item]);
+        }
+    }
+    return w.overflow ? -1 : w.bits;
 }

@@ -118,6 +118,11 @@ SIGNATURES = [
     ("pqh_decode_status", I, [P]), ("pqh_encode_status", I, [P]),
     ("pqh_chunk_index_host", I, [P, P, ULL, LL, I, I, P, P]),
     ("pqh_sort_rows", I, [P, P, LL, I, P]),
+    ("pqh_tree_order", I, [LL, LL, P, P, P, P, P]),
+    ("pqh_tree_gather", I, [P, P, LL, I, I, P, P, P, P]),
+    ("pqh_tree_status", I, [P]),
+    ("pqh_histogram_tree", I, [P, P, P, LL, I, I, P]),
+    ("pqh_encode_tree_write", I, [P, P, P, P, LL, ULL, P, ULL, P]),
     ("pqh_encode_files", I, [P, LL, I, P, S]),
     ("pqh_decode_files", I, [S, P, P, P]),
 ]

@@ -423,3 +423,109 @@ def indices_file_bytes(enc: Encoded) -> bytes:
     """huffman_indices.bin content: u64 N + stream bytes."""
     body = enc.stream[:enc.nbytes].cpu().numpy().tobytes()
     return np.uint64(enc.n).tobytes() + body
+
+
+# ---- tree-ordered context coding (huffman_encoder.c --tree; mst.c:253-490) ---------------
+def load_tree(path: str):
+    """mst.tree (tree_save_file, mst.c:253-265): i64 N, i64 E, u32 targets[E], i32 counts[N].
+    Returns (n, targets, counts)."""
+    with open(path, "rb") as fh:
+        raw = fh.read()
+    n, e = (int(v) for v in np.frombuffer(raw[:16], np.int64))
+    if len(raw) < 16 + 4 * e + 4 * n:
+        raise ValueError(f"{path}: truncated tree file")
+    targets = np.frombuffer(raw[16:16 + 4 * e], np.uint32).copy()
+    counts = np.frombuffer(raw[16 + 4 * e:16 + 4 * e + 4 * n], np.int32).copy()
+    return n, targets, counts
+
+
+def tree_order(targets, counts):
+    """DFS order of the forest (tree_collect_vertices_dfs, mst.c:290-364) and each stream
+    row's coding context (tree_traverser, mst.c:366-405), by the library's host walk.
+    Returns (vertices u32[n], num_children i32[n], parents i64[n] (-1: root), num_roots)."""
+    targets = np.ascontiguousarray(targets, np.uint32)
+    counts = np.ascontiguousarray(counts, np.int32)
+    n = len(counts)
+    vert = np.zeros(max(n, 1), np.uint32)
+    nch = np.zeros(max(n, 1), np.int32)
+    par = np.zeros(max(n, 1), np.int64)
+    roots = lib().pqh_tree_order(n, len(targets), _ptr(targets), _ptr(counts), _ptr(vert),
+                                 _ptr(nch), _ptr(par))
+    if roots < 0:
+        raise PqhError(roots, "pqh_tree_order: malformed forest")
+    return vert[:n], nch[:n], par[:n], roots
+
+
+@dataclass
+class TreeEncoded:
+    stream: object             # device uint8 (huffman_indices.bin payload), padded to 4 B
+    bits: int
+    n: int
+    num_roots: int
+    tables: object             # Tables (context, m parts)
+    vertices: np.ndarray       # stream row p is input row vertices[p]
+    num_children: np.ndarray
+    children_codebook: object  # Codebooks (one non-context book, alphabet max + 1)
+    children: object           # Encoded: the children stream (huffman_children.bin)
+
+    @property
+    def nbytes(self) -> int:
+        return (self.bits + 7) // 8
+
+
+def tree_encode(ctx: Context, codes, targets, counts) -> TreeEncoded:
+    """Tree mode of huffman_encoder (huffman_encoder.c:321-375, encode_tree_data :240-286)
+    on device uint8 codes [n, m]: host DFS order -> device gather of the rows in stream order
+    beside their parents' codes -> parent/child pair histogram -> GPU code tables -> one-pass
+    encode with explicit contexts; plus the children-count stream (non-context code book of
+    tree_collect_num_children_stats, mst.c:407-440, coded by the GPU encoder)."""
+    torch = _torch()
+    n, m = codes.shape
+    if len(counts) != n:
+        raise ValueError(f"tree has {len(counts)} vertices for {n} rows")
+    vert, nch, par, roots = tree_order(targets, counts)
+    dev = codes.device
+    d_vert = torch.from_numpy(vert.astype(np.int32)).to(dev)
+    d_par = torch.from_numpy(par).to(dev)
+    rows = torch.empty((n, m), dtype=torch.uint8, device=dev)
+    prev = torch.empty((n, m), dtype=torch.int16, device=dev)
+    check(lib().pqh_tree_gather(ctx.ptr, _ptr(codes), n, m, 256, _ptr(d_vert), _ptr(d_par),
+                                _ptr(rows), _ptr(prev)), "pqh_tree_gather")
+    check(lib().pqh_tree_status(ctx.ptr), "pqh_tree_gather: " + ctx.last_error())
+    cnt = torch.zeros((m, 256 * 256), dtype=torch.int32, device=dev)
+    check(lib().pqh_histogram_tree(ctx.ptr, _ptr(rows), _ptr(prev), n, m, 256, _ptr(cnt)),
+          "pqh_histogram_tree")
+    tables = Tables(ctx, m, 256, True).build(cnt)
+    tables.status()
+    words = (n * m * 56 + 31) // 32 + 2          # 56-bit codes at most
+    out = torch.zeros(words * 4, dtype=torch.uint8, device=dev)
+    total = torch.zeros(1, dtype=torch.int64, device=dev)
+    check(lib().pqh_encode_tree_write(ctx.ptr, tables.ptr, _ptr(rows), _ptr(prev), n, 0,
+                                      _ptr(out), out.numel(), _ptr(total)),
+          "pqh_encode_tree_write: " + ctx.last_error())
+    encode_status(ctx)
+    bits = int(total.item())
+    # children stream: one non-context part over the child counts
+    alphabet = int(nch.max(initial=0)) + 1
+    if alphabet > 4096:
+        raise PqhError(-4, f"tree_encode: {alphabet - 1} children at one vertex (max 4095)")
+    ccounts = np.bincount(nch, minlength=alphabet).astype(np.float64)[None]
+    cbook = Codebooks(ccounts, alphabet, False)
+    ctab = Tables.from_codebooks(ctx, cbook)
+    cdt = torch.uint8 if alphabet <= 256 else torch.int16
+    ccodes = torch.from_numpy(nch.astype(np.uint8 if alphabet <= 256 else np.int16)
+                              .reshape(n, 1)).to(dev)
+    assert ccodes.dtype == cdt
+    children = encode(ctx, ctab, ccodes, chunk_vectors=64, raw_first=1)
+    return TreeEncoded(out, bits, n, roots, tables, vert, nch, cbook, children)
+
+
+def tree_files(enc: TreeEncoded) -> dict:
+    """The reference's tree-mode output files (huffman_encoder.c:343-375, :398-428)."""
+    cb = enc.tables.codebooks()
+    stream = enc.stream[:enc.nbytes].cpu().numpy().tobytes()
+    cstream = enc.children.stream[:enc.children.nbytes].cpu().numpy().tobytes()
+    return {"huffman_codebooks.bin": cb.file_bytes(),
+            "huffman_indices.bin": np.uint64(enc.n).tobytes() + stream,
+            "huffman_children_codebooks.bin": enc.children_codebook.file_bytes()[4:],
+            "huffman_children.bin": cstream}

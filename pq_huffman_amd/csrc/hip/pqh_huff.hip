@@ -149,12 +149,16 @@ __device__ __forceinline__ unsigned long long sym_entry(const CodeT* codes, long
                                                         int m_total, int k, int context,
                                                         int raw_first, const CodeT* prev_row,
                                                         const unsigned long long* enc,
-                                                        long long items) {
+                                                        long long items,
+                                                        const uint16_t* tree_prev) {
     const unsigned s = ld_code(codes, v * m_total + i);
     if (s >= (unsigned)k) return 0;  // out-of-alphabet symbol: no code (length 0)
     if (!context) return enc[(long long)i * items + s];
     unsigned prev;
-    if (v > 0) {
+    if (tree_prev) {   // tree order: the row's context is its parent's code (0xFFFF: root)
+        prev = tree_prev[v * m_total + i];
+        if (prev == 0xFFFFu) return (8ull << 56) | (s & 0xFFu);
+    } else if (v > 0) {
         prev = ld_code(codes, (v - 1) * m_total + i);
     } else if (!raw_first && prev_row) {
         prev = ld_code(prev_row, i);
@@ -169,14 +173,15 @@ template <typename CodeT>
 __global__ void __launch_bounds__(kEncBlock)
 enc_size(const CodeT* __restrict__ codes, long long n, int m_total, int k, int context,
          int raw_first, const CodeT* __restrict__ prev_row, const unsigned long long* __restrict__ enc,
-         long long items, uint32_t* __restrict__ block_bits) {
+         long long items, uint32_t* __restrict__ block_bits,
+         const uint16_t* __restrict__ tree_prev) {
     __shared__ uint32_t red[kEncBlock / 64];
     const long long v = (long long)blockIdx.x * kEncBlock + threadIdx.x;
     uint32_t bits = 0;
     if (v < n)
         for (int i = 0; i < m_total; ++i)
             bits += (uint32_t)(sym_entry(codes, v, i, m_total, k, context, raw_first, prev_row,
-                                         enc, items) >> 56);
+                                         enc, items, tree_prev) >> 56);
     for (int off = 32; off >= 1; off >>= 1) bits += __shfl_xor(bits, off);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = bits;
     __syncthreads();
@@ -274,11 +279,15 @@ __device__ __forceinline__ void gather_entries(const CodeT* __restrict__ codes, 
                                                const CodeT* __restrict__ prev_row,
                                                const unsigned long long* __restrict__ enc,
                                                const uint32_t* __restrict__ enc32,
-                                               long long items, unsigned long long (&ent)[MAXM]) {
+                                               long long items, unsigned long long (&ent)[MAXM],
+                                               const uint16_t* __restrict__ tree_prev) {
     unsigned cur[MAXM], prv[MAXM];
     load_row<CodeT, MAXM>(codes, v, m, cur);
-    const bool raw = context && v == 0 && (raw_first || !prev_row);
-    if (context && v > 0) {
+    bool raw = context && v == 0 && (raw_first || !prev_row);
+    if (tree_prev) {   // tree order: explicit parent row (0xFFFF in part 0: a root, raw)
+        load_row<uint16_t, MAXM>(tree_prev, v, m, prv);
+        raw = prv[0] == 0xFFFFu;
+    } else if (context && v > 0) {
         load_row<CodeT, MAXM>(codes, v - 1, m, prv);
     } else {
 #pragma unroll
@@ -330,7 +339,8 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
             CodeT* __restrict__ chunk_prev, unsigned long long* __restrict__ err,
             unsigned long long* __restrict__ state, unsigned long long* __restrict__ tails,
             unsigned long long* __restrict__ ticket, unsigned long long ticket_base,
-            unsigned epoch, long long nb, unsigned long long* __restrict__ total_out) {
+            unsigned epoch, long long nb, unsigned long long* __restrict__ total_out,
+            const uint16_t* __restrict__ tree_prev) {
     extern __shared__ uint32_t img[];   // LDS image of this block's bit range
     __shared__ uint32_t wsum[kEncBlock / 64];
     __shared__ long long s_id;
@@ -353,13 +363,13 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
     if (v < n) {
         if constexpr (MAXM > 0) {
             gather_entries<CodeT, MAXM>(codes, v, m_total, k, context, raw_first, prev_row, enc,
-                                        enc32, items, ent);
+                                        enc32, items, ent, tree_prev);
 #pragma unroll
             for (int i = 0; i < MAXM; ++i) bits += (uint32_t)(ent[i] >> 56);
         } else {
             for (int i = 0; i < m_total; ++i)
                 bits += (uint32_t)(sym_entry(codes, v, i, m_total, k, context, raw_first,
-                                             prev_row, enc, items) >> 56);
+                                             prev_row, enc, items, tree_prev) >> 56);
         }
     }
     uint32_t incl = bits;
@@ -466,7 +476,8 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
             for (int i = 0; i < MAXM; ++i) put(ent[i]);   // length 0 past m_total
         } else {
             for (int i = 0; i < m_total; ++i)
-                put(sym_entry(codes, v, i, m_total, k, context, raw_first, prev_row, enc, items));
+                put(sym_entry(codes, v, i, m_total, k, context, raw_first, prev_row, enc, items,
+                              tree_prev));
         }
         if (nacc > 0) atomicOr(&img[w], (uint32_t)(acc << (32 - nacc)));
         pos += bits;
@@ -593,11 +604,13 @@ static int run_size(pqh_ctx* ctx, const pqh_tables* t, const void* d_codes, long
     if (t->k <= 256)
         hipLaunchKernelGGL(enc_size<uint8_t>, dim3((unsigned)nb), dim3(kEncBlock), 0, ctx->stream,
                            static_cast<const uint8_t*>(d_codes), n, t->m, t->k, t->context,
-                           raw_first, static_cast<const uint8_t*>(d_prev_row), t->d_enc, t->items, bb);
+                           raw_first, static_cast<const uint8_t*>(d_prev_row), t->d_enc, t->items, bb,
+                           nullptr);
     else
         hipLaunchKernelGGL(enc_size<uint16_t>, dim3((unsigned)nb), dim3(kEncBlock), 0, ctx->stream,
                            static_cast<const uint16_t*>(d_codes), n, t->m, t->k, t->context,
-                           raw_first, static_cast<const uint16_t*>(d_prev_row), t->d_enc, t->items, bb);
+                           raw_first, static_cast<const uint16_t*>(d_prev_row), t->d_enc, t->items, bb,
+                           nullptr);
     PQH_LAUNCH_CHECK(ctx);
     hipLaunchKernelGGL(scan_blocks, dim3(1), dim3(1024), 0, ctx->stream, bb, nb, bo, d_total);
     PQH_LAUNCH_CHECK(ctx);
@@ -622,7 +635,8 @@ static int encode_write_impl(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* 
                              const unsigned long long* d_bit_offset, unsigned char* d_out,
                              unsigned long long out_bytes, int chunk_vectors,
                              unsigned long long* d_chunk_offsets, void* d_chunk_prev,
-                             unsigned long long* d_total_bits) {
+                             unsigned long long* d_total_bits,
+                             const uint16_t* tree_prev = nullptr) {
     if (!ctx || !t || n < 0 || (n > 0 && (!d_codes || !d_out))) return PQH_ERR_ARG;
     if ((reinterpret_cast<uintptr_t>(d_out) & 3u) || (out_bytes & 3u))
         return pqh_set_error(ctx, PQH_ERR_ARG, "stream buffer must be 4-byte aligned and sized");
@@ -670,7 +684,7 @@ static int encode_write_impl(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* 
                            (long long)(out_bytes / 4),                                            \
                            chunk_vectors, d_chunk_offsets, static_cast<T*>(d_chunk_prev),         \
                            ctx->d_diag + 2, st, tails, ticket, ctx->lb_ticket_base,               \
-                           (unsigned)ctx->lb_epoch, nb, total);                                   \
+                           (unsigned)ctx->lb_epoch, nb, total, tree_prev);                        \
     } while (0)
     if (t->k <= 256) {
         if (t->m <= 8) PQH_ENC(uint8_t, 8);
@@ -748,3 +762,121 @@ int pqh_codebooks_build(const double* counts, int m, int k, int context,
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- tree-ordered coding
+// Tree mode (huffman_encoder.c:240-286 + mst.c:407-490): the stream walks the rows in the DFS
+// order of a spanning forest and codes each row in the context of its forest parent.  The
+// order and parents come from pqh_tree_order (host); the device gathers the rows into stream
+// order with their parents' codes beside them (tree_prev, 0xFFFF for a root), after which
+// the histogram and the encoder are the context-mode ones with an explicit context row.
+namespace {
+
+constexpr int kTreeChunk = 61440;   // vectors per tree-histogram workgroup (< 65536: u16)
+
+template <typename CodeT>
+__global__ void __launch_bounds__(256)
+tree_gather(const CodeT* __restrict__ codes, long long n, int m,
+            const uint32_t* __restrict__ vertices, const long long* __restrict__ parents,
+            CodeT* __restrict__ rows, uint16_t* __restrict__ tree_prev,
+            unsigned long long* __restrict__ err) {
+    const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const long long v = vertices[p];
+    const long long par = parents[p];
+    const bool bad = v >= n || par >= n;
+    if (bad) atomicOr(err, 1ull);   // an id outside the rows: reported, nothing read
+    for (int i = 0; i < m; ++i) {
+        rows[p * m + i] = bad ? CodeT(0) : codes[v * m + i];
+        tree_prev[p * m + i] = (bad || par < 0) ? uint16_t(0xFFFF) : uint16_t(codes[par * m + i]);
+    }
+}
+
+// (parent code, code) pair counts of one part over a chunk of stream rows, as packed u16
+// counters in LDS (k * k / 2 words; 128 KB at K = 256), flushed with one global atomic per
+// non-zero counter (tree_collect_indices_stats, mst.c:442-490; roots are not counted).
+template <typename CodeT>
+__global__ void __launch_bounds__(1024)
+hist_tree(const CodeT* __restrict__ rows, const uint16_t* __restrict__ tree_prev, long long n,
+          int m_total, int k, uint32_t* __restrict__ counts) {
+    extern __shared__ uint32_t pairs[];
+    const int m = blockIdx.y;
+    const int words = (k * k + 1) / 2;
+    for (int w = threadIdx.x; w < words; w += blockDim.x) pairs[w] = 0;
+    __syncthreads();
+    const long long p0 = (long long)blockIdx.x * kTreeChunk;
+    const long long p1 = p0 + kTreeChunk < n ? p0 + kTreeChunk : n;
+    for (long long p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
+        const unsigned prev = tree_prev[p * m_total + m];
+        const unsigned cur = (unsigned)rows[p * m_total + m];
+        if (prev >= (unsigned)k || cur >= (unsigned)k) continue;   // root / out of alphabet
+        const unsigned bin = prev * (unsigned)k + cur;
+        atomicAdd(&pairs[bin >> 1], 1u << ((bin & 1u) * 16));
+    }
+    __syncthreads();
+    uint32_t* out = counts + (long long)m * k * k;
+    for (int w = threadIdx.x; w < words; w += blockDim.x) {
+        const uint32_t c = pairs[w];
+        if (c & 0xFFFFu) atomicAdd(&out[2 * w], c & 0xFFFFu);
+        if ((c >> 16) && 2 * w + 1 < k * k) atomicAdd(&out[2 * w + 1], c >> 16);
+    }
+}
+
+}  // namespace
+
+int pqh_tree_gather(pqh_ctx_t* ctx, const void* d_codes, long long n, int m, int k,
+                    const uint32_t* d_vertices, const long long* d_parents, void* d_rows,
+                    uint16_t* d_tree_prev) {
+    if (!ctx || n < 0 || m <= 0 || k <= 0 || k > 4096) return PQH_ERR_ARG;
+    if (n > 0 && (!d_codes || !d_vertices || !d_parents || !d_rows || !d_tree_prev))
+        return PQH_ERR_ARG;
+    int rc = pqh_use_device(ctx);
+    if (rc) return rc;
+    if (n == 0) return PQH_OK;
+    const unsigned blocks = (unsigned)((n + 255) / 256);
+    if (k <= 256)
+        hipLaunchKernelGGL(tree_gather<uint8_t>, dim3(blocks), dim3(256), 0, ctx->stream,
+                           static_cast<const uint8_t*>(d_codes), n, m, d_vertices, d_parents,
+                           static_cast<uint8_t*>(d_rows), d_tree_prev, ctx->d_diag + 7);
+    else
+        hipLaunchKernelGGL(tree_gather<uint16_t>, dim3(blocks), dim3(256), 0, ctx->stream,
+                           static_cast<const uint16_t*>(d_codes), n, m, d_vertices, d_parents,
+                           static_cast<uint16_t*>(d_rows), d_tree_prev, ctx->d_diag + 7);
+    PQH_LAUNCH_CHECK(ctx);
+    return PQH_OK;
+}
+
+int pqh_tree_status(pqh_ctx_t* ctx) {
+    if (!ctx) return PQH_ERR_ARG;
+    unsigned long long e = 0;
+    PQH_HIP(ctx, hipMemcpyAsync(&e, ctx->d_diag + 7, 8, hipMemcpyDeviceToHost, ctx->stream));
+    PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    PQH_HIP(ctx, hipMemsetAsync(ctx->d_diag + 7, 0, 8, ctx->stream));
+    return e ? pqh_set_error(ctx, PQH_ERR_ARG, "tree order names a row outside the input") : PQH_OK;
+}
+
+int pqh_histogram_tree(pqh_ctx_t* ctx, const void* d_rows, const uint16_t* d_tree_prev,
+                       long long n, int m, int k, uint32_t* d_counts) {
+    if (!ctx || n < 0 || m <= 0 || k <= 0 || !d_counts) return PQH_ERR_ARG;
+    if (k > 256) return PQH_ERR_UNSUPPORTED;   // context alphabets are K = 256 (mst.c:440)
+    if (n > 0 && (!d_rows || !d_tree_prev)) return PQH_ERR_ARG;
+    int rc = pqh_use_device(ctx);
+    if (rc) return rc;
+    if (n == 0) return PQH_OK;
+    const unsigned chunks = (unsigned)((n + kTreeChunk - 1) / kTreeChunk);
+    const size_t lds = (size_t)((k * k + 1) / 2) * 4;
+    PQH_HIP(ctx, hipFuncSetAttribute((const void*)hist_tree<uint8_t>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(hist_tree<uint8_t>, dim3(chunks, m), dim3(1024), lds, ctx->stream,
+                       static_cast<const uint8_t*>(d_rows), d_tree_prev, n, m, k, d_counts);
+    PQH_LAUNCH_CHECK(ctx);
+    return PQH_OK;
+}
+
+int pqh_encode_tree_write(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_rows,
+                          const uint16_t* d_tree_prev, long long n,
+                          unsigned long long bit_offset, unsigned char* d_out,
+                          unsigned long long out_bytes, unsigned long long* d_total_bits) {
+    if (!ctx || !t || !t->context || t->k > 256 || (n > 0 && !d_tree_prev)) return PQH_ERR_ARG;
+    return encode_write_impl(ctx, t, d_rows, n, 1, nullptr, bit_offset, nullptr, d_out,
+                             out_bytes, 0, nullptr, nullptr, d_total_bits, d_tree_prev);
+}

@@ -21,7 +21,8 @@ struct pqh_ctx {
     void* ws = nullptr;
     size_t ws_bytes = 0;
     // [0] / [4] re-rank counters of alternate assignment launches, [1] decode error,
-    // [2] encode capacity error, [3] scratch total bits, [6] re-rank count of the exact path
+    // [2] encode capacity error, [3] scratch total bits, [6] re-rank count of the exact path,
+    // [7] tree-order id error
     unsigned long long* d_diag = nullptr;
     // one-pass encoder look-back state: [lb_cap] block states, [lb_cap] tails, ticket
     unsigned long long* lb_state = nullptr;

@@ -1,0 +1,74 @@
+// pqh_tree.cpp -- host side of tree-ordered context coding.
+//
+// The DFS order of a stored spanning forest (mst.c:290-364, tree_collect_vertices_dfs) and
+// each row's coding context -- the vertex on top of the traverser stack when the row is
+// coded (mst.c:366-405, tree_traverser_*; driven by huffman_encoder.c:240-286).  Both are a
+// sequential stack walk over the forest's adjacency lists, O(N) host work like the code-book
+// heaps; the rows themselves are gathered, counted and coded on the GPU (pqh_huff.hip).
+#include <cstdint>
+#include <vector>
+
+#include "pqh_internal.h"
+
+int pqh_tree_order(long long num_vertices, long long num_edges, const uint32_t* edge_targets,
+                   const int* children_counts, uint32_t* vertices, int* num_children,
+                   long long* parents) {
+    if (num_vertices < 0 || num_edges < 0 || (num_vertices > 0 && !children_counts) ||
+        (num_edges > 0 && !edge_targets) || (num_vertices > 0 && (!vertices || !num_children)))
+        return PQH_ERR_ARG;
+    if (num_vertices == 0) return 0;
+    // adjacency list of vertex i = edge_targets[first[i], first[i] + children_counts[i])
+    // (restore_tree_edges_pointers, mst.c:52-61)
+    std::vector<long long> first((size_t)num_vertices + 1, 0);
+    for (long long i = 0; i < num_vertices; ++i) {
+        if (children_counts[i] < 0) return PQH_ERR_ARG;
+        first[i + 1] = first[i] + children_counts[i];
+    }
+    if (first[num_vertices] != num_edges) return PQH_ERR_ARG;
+    for (long long e = 0; e < num_edges; ++e)
+        if ((long long)edge_targets[e] >= num_vertices) return PQH_ERR_ARG;
+
+    // DFS with marking on push; roots are the lowest unvisited ids (mst.c:303-353)
+    std::vector<uint32_t> stack((size_t)num_vertices);
+    std::vector<char> visited((size_t)num_vertices, 0);
+    long long processed = 0, stack_size = 0, children_sum = 0;
+    uint32_t next_root = 0;
+    int num_roots = 0;
+    while (processed < num_vertices) {
+        if (stack_size == 0) {
+            while ((long long)next_root < num_vertices && visited[next_root]) ++next_root;
+            stack[stack_size++] = next_root;
+            visited[next_root] = 1;
+            ++num_roots;
+        }
+        const uint32_t cur = stack[--stack_size];
+        vertices[processed] = cur;
+        int kids = 0;   // unvisited neighbours counted before any of them is pushed (:322-333)
+        for (long long e = first[cur]; e < first[cur + 1]; ++e) kids += !visited[edge_targets[e]];
+        num_children[processed] = kids;
+        children_sum += kids;
+        ++processed;
+        for (long long e = first[cur]; e < first[cur + 1]; ++e) {
+            const uint32_t t = edge_targets[e];
+            if (!visited[t]) {
+                visited[t] = 1;
+                stack[stack_size++] = t;
+            }
+        }
+    }
+    // the reference asserts this (mst.c:357): a duplicated edge breaks the child counts
+    if (children_sum != num_vertices - num_roots) return PQH_ERR_ARG;
+
+    // coding context of each stream row: the traverser's active parent (mst.c:383-405)
+    if (parents) {
+        struct item { uint32_t vertex; int left; };
+        std::vector<item> tstack;
+        tstack.reserve((size_t)num_vertices);
+        for (long long p = 0; p < num_vertices; ++p) {
+            parents[p] = tstack.empty() ? -1 : (long long)tstack.back().vertex;
+            if (!tstack.empty() && --tstack.back().left == 0) tstack.pop_back();
+            if (num_children[p]) tstack.push_back({vertices[p], num_children[p]});
+        }
+    }
+    return num_roots;
+}

@@ -87,3 +87,41 @@ def write_vecsl(path, a: np.ndarray) -> None:
     with open(path, "wb") as f:
         np.array([n, d], np.uint32).tofile(f)
         np.ascontiguousarray(a).tofile(f)
+
+
+def random_forest(n: int, roots: int = 3, seed: int = 9, max_fan: int = 6):
+    """A spanning forest of n vertices in the reference's mst.tree layout (mst.c:173-236):
+    every edge stored in both directions, grouped by source vertex (order within a source
+    arbitrary).  Returns (targets u32 [2(n - roots)], counts i32 [n])."""
+    rng = np.random.default_rng(seed)
+    perm = rng.permutation(n)
+    adj = [[] for _ in range(n)]
+    roots = max(1, min(roots, n)) if n else 0
+    for j in range(roots, n):          # attach perm[j] below a recent earlier vertex
+        lo = max(0, j - max_fan * 4)
+        par = perm[int(rng.integers(lo, j))] if j > lo else perm[0]
+        adj[par].append(perm[j])
+        adj[perm[j]].append(par)
+    for a in adj:
+        rng.shuffle(a)
+    counts = np.array([len(a) for a in adj], np.int32)
+    targets = np.array([t for a in adj for t in a], np.uint32)
+    return targets, counts
+
+
+def write_tree(path, n: int, targets: np.ndarray, counts: np.ndarray) -> None:
+    """tree_save_file (mst.c:253-265): i64 N, i64 E, u32 targets[E], i32 counts[N]."""
+    with open(path, "wb") as f:
+        f.write(np.int64(n).tobytes())
+        f.write(np.int64(len(targets)).tobytes())
+        f.write(np.ascontiguousarray(targets, np.uint32).tobytes())
+        f.write(np.ascontiguousarray(counts, np.int32).tobytes())
+
+
+def read_tree(path):
+    """tree_load_file (mst.c:273-288) -> (n, targets, counts)."""
+    raw = open(path, "rb").read()
+    n, e = np.frombuffer(raw[:16], np.int64)
+    targets = np.frombuffer(raw[16:16 + 4 * e], np.uint32).copy()
+    counts = np.frombuffer(raw[16 + 4 * e:16 + 4 * e + 4 * n], np.int32).copy()
+    return int(n), targets, counts

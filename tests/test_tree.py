@@ -1,0 +1,156 @@
+"""Tree-ordered context coding (huffman_encoder --tree mst.tree; huffman_encoder.c:240-286,
+:321-375; mst.c:253-490).
+
+CPU: the oracle against the fixtures the reference's own binaries produced
+(oracle/gen_golden.py tree: huffman_encoder --tree / huffman_decoder --tree on seeded
+forests in the mst.tree layout), and the library's host DFS/traverser walk against the
+oracle.  GPU: pqh_tree_gather + pqh_histogram_tree + GPU code tables + pqh_encode_tree_write
+byte-identical to the reference files, and at larger sizes to the oracle (plus an oracle
+decode round trip)."""
+import numpy as np
+import pytest
+
+from conftest import golden
+import datagen
+
+CASES = ["tree_m8_n1000", "tree_m16_n300", "tree_m8_n64_forest"]
+FILES = ["huffman_codebooks", "huffman_indices", "huffman_children_codebooks",
+         "huffman_children"]
+
+
+def _oracle_files(oracle, codes, targets, counts):
+    vert, nch, _ = oracle.tree_order(len(counts), targets, counts)
+    par = oracle.tree_parents(nch, vert)
+    cbs = oracle.tree_codebooks(codes, vert, par)
+    stream, bits = oracle.tree_encode(codes, vert, par, cbs)
+    _, ccb = oracle.children_codebook(nch)
+    return vert, nch, par, cbs, stream, ccb
+
+
+def _children_stream(oracle, ccb, nch):
+    codes = np.ascontiguousarray(nch.reshape(-1, 1).astype(np.uint16 if ccb.k > 256 else np.uint8))
+    return oracle.encode(codes, ccb)[0]
+
+
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("mode", ["tree_nosort", "tree_sort"])
+def test_oracle_tree_vs_reference_files(oracle, case, mode):
+    g = golden(f"huff_{case}.npz")
+    codes = g["input"]
+    if mode == "tree_sort":          # the CLI sorts first by default (huffman_encoder.c:313)
+        codes = oracle.sort_rows(codes)
+    vert, nch, par, cbs, stream, ccb = _oracle_files(oracle, codes, g["targets"], g["counts"])
+    assert oracle.codebooks_file(cbs) == g[mode + "__huffman_codebooks"].tobytes()
+    assert np.uint64(len(codes)).tobytes() + stream == g[mode + "__huffman_indices"].tobytes()
+    assert oracle.serialize(ccb.k, False, ccb.lens[0], ccb.codes[0]) == \
+        g[mode + "__huffman_children_codebooks"].tobytes()
+    assert _children_stream(oracle, ccb, nch) == g[mode + "__huffman_children"].tobytes()
+    # the reference decoder emits rows in stream (DFS) order
+    np.testing.assert_array_equal(g[mode + "__decoded"], codes[vert])
+    np.testing.assert_array_equal(oracle.tree_decode(stream, len(codes), codes.shape[1], cbs, nch),
+                                  codes[vert])
+
+
+@pytest.mark.parametrize("n,roots,seed", [(1, 1, 1), (2, 1, 2), (1000, 3, 3), (5000, 40, 4),
+                                          (64, 64, 5), (20000, 1, 6)])
+def test_library_tree_order_vs_oracle(oracle, n, roots, seed):
+    from pq_huffman_amd import codec
+    targets, counts = datagen.random_forest(n, roots=roots, seed=seed)
+    vert, nch, par, nroots = codec.tree_order(targets, counts)
+    ov, onch, oroots = oracle.tree_order(n, targets, counts)
+    np.testing.assert_array_equal(vert, ov)
+    np.testing.assert_array_equal(nch, onch)
+    assert nroots == oroots == roots
+    np.testing.assert_array_equal(par, oracle.tree_parents(onch, ov))
+    assert sorted(vert.tolist()) == list(range(n))
+    assert (par < 0).sum() == roots
+
+
+def test_library_tree_order_rejects_malformed():
+    from pq_huffman_amd import codec
+    from pq_huffman_amd.capi import PqhError
+    targets, counts = datagen.random_forest(50, roots=2, seed=7)
+    with pytest.raises(PqhError):             # edge count disagrees with the adjacency sizes
+        codec.tree_order(targets[:-1], counts)
+    bad = targets.copy()
+    bad[0] = 50                               # target outside the vertices
+    with pytest.raises(PqhError):
+        codec.tree_order(bad, counts)
+
+
+def test_tree_file_roundtrip(tmp_path):
+    from pq_huffman_amd import codec
+    targets, counts = datagen.random_forest(300, roots=4, seed=8)
+    p = str(tmp_path / "mst.tree")
+    datagen.write_tree(p, 300, targets, counts)
+    n, t2, c2 = codec.load_tree(p)
+    assert n == 300
+    np.testing.assert_array_equal(t2, targets)
+    np.testing.assert_array_equal(c2, counts)
+
+
+# ---------------------------------------------------------------- GPU
+@pytest.fixture(scope="module")
+def gpu():
+    import torch
+    from pq_huffman_amd import codec
+    assert torch.cuda.is_available(), "GPU tests need the MI355X (no fallback path)"
+    ctx = codec.Context(0)
+    yield ctx
+    ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("mode", ["tree_nosort", "tree_sort"])
+def test_gpu_tree_encode_vs_reference_files(gpu, oracle, case, mode):
+    import torch
+    from pq_huffman_amd import codec
+    g = golden(f"huff_{case}.npz")
+    codes = g["input"]
+    d = torch.from_numpy(codes).cuda()
+    if mode == "tree_sort":
+        codec.sort_rows(gpu, d)
+    enc = codec.tree_encode(gpu, d, g["targets"], g["counts"])
+    files = codec.tree_files(enc)
+    for f in FILES:
+        assert files[f + ".bin"] == g[mode + "__" + f].tobytes(), f
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,m,roots", [(200_000, 8, 17), (50_000, 16, 1), (1_000_000, 8, 1000)])
+def test_gpu_tree_encode_vs_oracle_roundtrip(gpu, oracle, n, m, roots):
+    import torch
+    from pq_huffman_amd import codec
+    codes = datagen.skewed_codes(n, m, 256, seed=n + m)
+    targets, counts = datagen.random_forest(n, roots=roots, seed=roots)
+    enc = codec.tree_encode(gpu, torch.from_numpy(codes).cuda(), targets, counts)
+    vert, nch, _ = oracle.tree_order(n, targets, counts)
+    par = oracle.tree_parents(nch, vert)
+    cbs = oracle.tree_codebooks(codes, vert, par)
+    stream, bits = oracle.tree_encode(codes, vert, par, cbs)
+    assert enc.bits == bits
+    got = enc.stream[:enc.nbytes].cpu().numpy().tobytes()
+    assert got == stream
+    np.testing.assert_array_equal(oracle.tree_decode(got, n, m, cbs, enc.num_children),
+                                  codes[enc.vertices])
+    assert enc.children.stream[:enc.children.nbytes].cpu().numpy().tobytes() == \
+        _children_stream(oracle, oracle.children_codebook(nch)[1], nch)
+
+
+@pytest.mark.gpu
+def test_gpu_tree_gather_reports_bad_ids(gpu):
+    import torch
+    from pq_huffman_amd import codec
+    from pq_huffman_amd.capi import lib
+    n, m = 1000, 8
+    codes = torch.zeros((n, m), dtype=torch.uint8, device="cuda")
+    vert = torch.arange(n, dtype=torch.int32, device="cuda")
+    vert[5] = n + 3
+    par = torch.full((n,), -1, dtype=torch.int64, device="cuda")
+    rows = torch.empty_like(codes)
+    prev = torch.empty((n, m), dtype=torch.int16, device="cuda")
+    assert lib().pqh_tree_gather(gpu.ptr, codes.data_ptr(), n, m, 256, vert.data_ptr(),
+                                 par.data_ptr(), rows.data_ptr(), prev.data_ptr()) == 0
+    assert lib().pqh_tree_status(gpu.ptr) != 0
+    assert lib().pqh_tree_status(gpu.ptr) == 0      # the flag is cleared after a report
