@@ -224,12 +224,29 @@ int pqh_tree_status(pqh_ctx_t* ctx);
 int pqh_histogram_tree(pqh_ctx_t* ctx, const void* d_rows, const uint16_t* d_tree_prev,
                        long long n, int m, int k, uint32_t* d_counts);
 /* encode_tree_data (huffman_encoder.c:240-286): context tables, each row coded in its
- * d_tree_prev context, roots raw 8 bits per part.  Same buffer rules as pqh_encode_write
- * (no chunk index: decoding a tree stream needs the children stream). */
+ * d_tree_prev context, roots raw 8 bits per part.  Same buffer rules as pqh_encode_write;
+ * chunk_vectors > 0 emits the chunk bit offsets (the tree decoder's index). */
 int pqh_encode_tree_write(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_rows,
                           const uint16_t* d_tree_prev, long long n,
                           unsigned long long bit_offset, unsigned char* d_out,
-                          unsigned long long out_bytes, unsigned long long* d_total_bits);
+                          unsigned long long out_bytes, int chunk_vectors,
+                          unsigned long long* d_chunk_offsets, unsigned long long* d_total_bits);
+/* Decode-side index from the child counts (decoded children stream): parent_pos[p] = the
+ * stream position of row p's context (-1: root; huffman_decoder.c:214-247), and per chunk
+ * of C rows the rows whose context precedes the chunk: ext_offsets[chunks + 1] into
+ * ext_positions (may be NULL to count).  Host; returns the ext count or PQH_ERR_ARG. */
+long long pqh_tree_ext_index(long long n, const int* num_children, int chunk_vectors,
+                             long long* parent_pos, long long* ext_offsets,
+                             long long* ext_positions);
+/* huffman_decoder --tree on the GPU: rows in stream order.  One lane per chunk (offsets
+ * from pqh_encode_tree_write); a context inside the chunk is read from the chunk's own
+ * decoded rows, one before it from d_ext_rows[d_ext_offsets[j]...] (m codes each, the rows
+ * at ext_positions).  Errors are reported by pqh_decode_status. */
+int pqh_decode_tree(pqh_ctx_t* ctx, const pqh_tables_t* t, const unsigned char* d_stream,
+                    unsigned long long stream_bytes, long long n, int chunk_vectors,
+                    const unsigned long long* d_chunk_offsets, const long long* d_parent_pos,
+                    const long long* d_ext_offsets, const unsigned char* d_ext_rows,
+                    void* d_rows);
 
 /* ---- whole-file host helpers used by the CLI tools ------------------------------- */
 typedef struct {

@@ -467,13 +467,32 @@ class TreeEncoded:
     num_children: np.ndarray
     children_codebook: object  # Codebooks (one non-context book, alphabet max + 1)
     children: object           # Encoded: the children stream (huffman_children.bin)
+    chunk_vectors: int = 0     # decode sidecar: chunk bit offsets (device int64 [chunks])
+    chunk_offsets: object = None
+    ext_rows: object = None    # device uint8 [ext, m]: contexts that precede their chunk
 
     @property
     def nbytes(self) -> int:
         return (self.bits + 7) // 8
 
 
-def tree_encode(ctx: Context, codes, targets, counts) -> TreeEncoded:
+def tree_ext_index(num_children, chunk_vectors: int):
+    """(parent_pos i64[n], ext_offsets i64[chunks + 1], ext_positions i64[ext]) -- the
+    decode-side index of a tree stream (pqh_tree_ext_index)."""
+    nch = np.ascontiguousarray(num_children, np.int32)
+    n = len(nch)
+    chunks = (n + chunk_vectors - 1) // chunk_vectors
+    pp = np.zeros(max(n, 1), np.int64)
+    eo = np.zeros(chunks + 1, np.int64)
+    cnt = lib().pqh_tree_ext_index(n, _ptr(nch), chunk_vectors, _ptr(pp), _ptr(eo), None)
+    if cnt < 0:
+        raise PqhError(int(cnt), "pqh_tree_ext_index")
+    ep = np.zeros(max(cnt, 1), np.int64)
+    lib().pqh_tree_ext_index(n, _ptr(nch), chunk_vectors, _ptr(pp), _ptr(eo), _ptr(ep))
+    return pp[:n], eo, ep[:cnt]
+
+
+def tree_encode(ctx: Context, codes, targets, counts, chunk_vectors: int = 64) -> TreeEncoded:
     """Tree mode of huffman_encoder (huffman_encoder.c:321-375, encode_tree_data :240-286)
     on device uint8 codes [n, m]: host DFS order -> device gather of the rows in stream order
     beside their parents' codes -> parent/child pair histogram -> GPU code tables -> one-pass
@@ -500,9 +519,15 @@ def tree_encode(ctx: Context, codes, targets, counts) -> TreeEncoded:
     words = (n * m * 56 + 31) // 32 + 2          # 56-bit codes at most
     out = torch.zeros(words * 4, dtype=torch.uint8, device=dev)
     total = torch.zeros(1, dtype=torch.int64, device=dev)
+    chunks = (n + chunk_vectors - 1) // chunk_vectors
+    coff = torch.empty(max(chunks, 1), dtype=torch.int64, device=dev)
     check(lib().pqh_encode_tree_write(ctx.ptr, tables.ptr, _ptr(rows), _ptr(prev), n, 0,
-                                      _ptr(out), out.numel(), _ptr(total)),
+                                      _ptr(out), out.numel(), chunk_vectors, _ptr(coff),
+                                      _ptr(total)),
           "pqh_encode_tree_write: " + ctx.last_error())
+    # decode sidecar: the contexts each chunk needs from before it (the encoder has them)
+    _, _, ext_pos = tree_ext_index(nch, chunk_vectors)
+    ext_rows = rows.index_select(0, torch.from_numpy(ext_pos).to(dev))
     encode_status(ctx)
     bits = int(total.item())
     # children stream: one non-context part over the child counts
@@ -517,7 +542,32 @@ def tree_encode(ctx: Context, codes, targets, counts) -> TreeEncoded:
                               .reshape(n, 1)).to(dev)
     assert ccodes.dtype == cdt
     children = encode(ctx, ctab, ccodes, chunk_vectors=64, raw_first=1)
-    return TreeEncoded(out, bits, n, roots, tables, vert, nch, cbook, children)
+    return TreeEncoded(out, bits, n, roots, tables, vert, nch, cbook, children, chunk_vectors,
+                       coff, ext_rows)
+
+
+def tree_decode(ctx: Context, enc: TreeEncoded, tables: Tables = None, out=None):
+    """huffman_decoder --tree on the GPU (huffman_decoder.c:214-247): the children stream
+    first (GPU decode of its non-context book), then the host traverser over the decoded
+    child counts, then one lane per chunk with the encoder's sidecar.  Rows come back in
+    stream (DFS) order, as the reference decoder writes them."""
+    torch = _torch()
+    t = tables or enc.tables
+    ctab = Tables.from_codebooks(ctx, enc.children_codebook)
+    nch = decode(ctx, ctab, enc.children)
+    decode_status(ctx)
+    nch = nch.cpu().numpy().reshape(-1).view(np.uint8 if ctab.k <= 256 else np.int16)
+    pp, eo, _ = tree_ext_index(nch.astype(np.int32), enc.chunk_vectors)
+    dev = enc.stream.device
+    if out is None:
+        out = torch.empty((enc.n, t.m), dtype=torch.uint8, device=dev)
+    d_pp = torch.from_numpy(pp).to(dev)
+    d_eo = torch.from_numpy(eo).to(dev)
+    check(lib().pqh_decode_tree(ctx.ptr, t.ptr, _ptr(enc.stream), enc.stream.numel(), enc.n,
+                                enc.chunk_vectors, _ptr(enc.chunk_offsets), _ptr(d_pp),
+                                _ptr(d_eo), _ptr(enc.ext_rows), _ptr(out)), "pqh_decode_tree")
+    decode_status(ctx)
+    return out
 
 
 def tree_files(enc: TreeEncoded) -> dict:

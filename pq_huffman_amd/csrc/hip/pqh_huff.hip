@@ -875,8 +875,10 @@ int pqh_histogram_tree(pqh_ctx_t* ctx, const void* d_rows, const uint16_t* d_tre
 int pqh_encode_tree_write(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_rows,
                           const uint16_t* d_tree_prev, long long n,
                           unsigned long long bit_offset, unsigned char* d_out,
-                          unsigned long long out_bytes, unsigned long long* d_total_bits) {
+                          unsigned long long out_bytes, int chunk_vectors,
+                          unsigned long long* d_chunk_offsets, unsigned long long* d_total_bits) {
     if (!ctx || !t || !t->context || t->k > 256 || (n > 0 && !d_tree_prev)) return PQH_ERR_ARG;
     return encode_write_impl(ctx, t, d_rows, n, 1, nullptr, bit_offset, nullptr, d_out,
-                             out_bytes, 0, nullptr, nullptr, d_total_bits, d_tree_prev);
+                             out_bytes, chunk_vectors, d_chunk_offsets, nullptr, d_total_bits,
+                             d_tree_prev);
 }

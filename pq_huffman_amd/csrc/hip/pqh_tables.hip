@@ -1249,3 +1249,94 @@ int pqh_chunk_index_host(const pqh_tables_t* t, const unsigned char* stream,
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- tree-mode decode
+// huffman_decoder --tree (huffman_decoder.c:214-247): row p is decoded in the context of the
+// row at stream position parent_pos[p] (the traverser replayed over the children stream),
+// a root starting every part with the raw warm-up bits.  One lane per chunk of C rows from
+// the encoder's chunk index; the chunk's rows are staged in LDS, so a parent inside the
+// chunk is read back from there, and the parents that lie before the chunk come from the
+// ext sidecar (ext_rows[ext_off[j] ...], in row order) -- every chunk decodes independently.
+namespace {
+__global__ void __launch_bounds__(64)
+dec_tree(const uint32_t* __restrict__ words, long long nwords, long long n, int m, int k,
+         int chunk_vectors, const unsigned long long* __restrict__ chunk_off,
+         const long long* __restrict__ parent_pos, const long long* __restrict__ ext_off,
+         const uint8_t* __restrict__ ext_rows, const uint16_t* __restrict__ lut1,
+         const uint16_t* __restrict__ lut2, const uint32_t* __restrict__ meta, int w1,
+         long long lut2_cap, const pqh_long_code* __restrict__ longs,
+         const uint32_t* __restrict__ long_cnt, uint8_t* __restrict__ out,
+         unsigned long long* __restrict__ err) {
+    extern __shared__ uint8_t tstage[];   // [64 lanes][C rows][m]
+    const long long chunks = (n + chunk_vectors - 1) / chunk_vectors;
+    const long long j = (long long)blockIdx.x * 64 + threadIdx.x;
+    if (j >= chunks) return;               // no barriers below: lanes are independent
+    const long long v0 = j * chunk_vectors;
+    const long long v1 = min(n, v0 + chunk_vectors);
+    uint8_t* st = tstage + (long long)threadIdx.x * chunk_vectors * m;
+    DecTables T{meta, lut1, lut2, lut2_cap, longs, long_cnt, k, w1};
+    BitReader br;
+    br.init(words, nwords - 1, chunk_off[j]);
+    long long e = ext_off[j];
+    const long long e_end = ext_off[j + 1];
+    int warm_bits = 1;
+    while ((1 << warm_bits) < k) ++warm_bits;
+    bool ok = true;
+    for (long long p = v0; p < v1 && ok; ++p) {
+        const long long pp = parent_pos[p];
+        const uint8_t* prow = nullptr;
+        if (pp >= v0 && pp < p) {
+            prow = st + (pp - v0) * m;
+        } else if (pp >= 0) {
+            if (pp >= p || e >= e_end) { ok = false; break; }   // inconsistent sidecar
+            prow = ext_rows + e * m;
+            ++e;
+        }
+        uint8_t* o = st + (p - v0) * m;
+        for (int i = 0; i < m; ++i) {
+            unsigned sym;
+            if (!prow) {
+                sym = br.peek(warm_bits);
+                br.skip(warm_bits);
+            } else if (!dec_symbol(br, T, (long long)i * k + prow[i], sym)) {
+                ok = false;
+                break;
+            }
+            o[i] = (uint8_t)sym;
+        }
+    }
+    const long long nb = (v1 - v0) * m;
+    uint8_t* dst = out + v0 * m;
+    for (long long q = 0; q < nb; ++q) dst[q] = st[q];
+    if (!ok) atomicOr(err, 1ull);
+}
+}  // namespace
+
+int pqh_decode_tree(pqh_ctx_t* ctx, const pqh_tables_t* t, const unsigned char* d_stream,
+                    unsigned long long stream_bytes, long long n, int chunk_vectors,
+                    const unsigned long long* d_chunk_offsets, const long long* d_parent_pos,
+                    const long long* d_ext_offsets, const unsigned char* d_ext_rows,
+                    void* d_rows) {
+    if (!ctx || !t || !t->context || t->k > 256 || n < 0 || chunk_vectors <= 0 ||
+        (n > 0 && (!d_stream || !d_chunk_offsets || !d_parent_pos || !d_ext_offsets || !d_rows)))
+        return PQH_ERR_ARG;
+    if (reinterpret_cast<uintptr_t>(d_stream) & 3u) return PQH_ERR_ARG;
+    const size_t lds = (size_t)64 * chunk_vectors * t->m;
+    if (lds > 160 * 1024) return PQH_ERR_UNSUPPORTED;
+    int rc = pqh_use_device(ctx);
+    if (rc) return rc;
+    if (n == 0) return PQH_OK;
+    PQH_HIP(ctx, hipMemsetAsync(ctx->d_diag + 1, 0, 8, ctx->stream));
+    const long long chunks = (n + chunk_vectors - 1) / chunk_vectors;
+    if (lds > 64 * 1024)
+        PQH_HIP(ctx, hipFuncSetAttribute((const void*)dec_tree,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(dec_tree, dim3((unsigned)((chunks + 63) / 64)), dim3(64), lds, ctx->stream,
+                       reinterpret_cast<const uint32_t*>(d_stream), (long long)(stream_bytes / 4),
+                       n, t->m, t->k, chunk_vectors, d_chunk_offsets, d_parent_pos,
+                       d_ext_offsets, d_ext_rows, t->d_lut1, t->d_lut2, t->d_meta, t->l1_bits,
+                       t->lut2_cap, t->d_long, t->d_long_cnt, static_cast<uint8_t*>(d_rows),
+                       ctx->d_diag + 1);
+    PQH_LAUNCH_CHECK(ctx);
+    return PQH_OK;
+}

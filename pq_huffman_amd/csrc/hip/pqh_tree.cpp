@@ -72,3 +72,31 @@ int pqh_tree_order(long long num_vertices, long long num_edges, const uint32_t* 
     }
     return num_roots;
 }
+
+// Decode-side index of a tree stream: the stream position of each row's context
+// (the traverser of huffman_decoder.c:214-247, pushing positions), and per chunk of C rows
+// the rows whose context lies before the chunk -- ext_offsets[j] .. ext_offsets[j + 1] index
+// ext_positions, the context positions in row order.  Returns the ext count.
+long long pqh_tree_ext_index(long long n, const int* num_children, int chunk_vectors,
+                             long long* parent_pos, long long* ext_offsets,
+                             long long* ext_positions) {
+    if (n < 0 || chunk_vectors <= 0 || (n > 0 && (!num_children || !parent_pos || !ext_offsets)))
+        return PQH_ERR_ARG;
+    struct item { long long pos; int left; };
+    std::vector<item> tstack;
+    long long ext = 0;
+    for (long long p = 0; p < n; ++p) {
+        if (p % chunk_vectors == 0) ext_offsets[p / chunk_vectors] = ext;
+        const long long pp = tstack.empty() ? -1 : tstack.back().pos;
+        parent_pos[p] = pp;
+        if (pp >= 0 && pp < p - p % chunk_vectors) {
+            if (ext_positions) ext_positions[ext] = pp;
+            ++ext;
+        }
+        if (!tstack.empty() && --tstack.back().left == 0) tstack.pop_back();
+        if (num_children[p] < 0) return PQH_ERR_ARG;
+        if (num_children[p]) tstack.push_back({p, num_children[p]});
+    }
+    if (n > 0) ext_offsets[(n + chunk_vectors - 1) / chunk_vectors] = ext;
+    return ext;
+}

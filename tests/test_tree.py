@@ -115,6 +115,8 @@ def test_gpu_tree_encode_vs_reference_files(gpu, oracle, case, mode):
     files = codec.tree_files(enc)
     for f in FILES:
         assert files[f + ".bin"] == g[mode + "__" + f].tobytes(), f
+    np.testing.assert_array_equal(codec.tree_decode(gpu, enc).cpu().numpy(),
+                                  g[mode + "__decoded"])
 
 
 @pytest.mark.gpu
@@ -136,6 +138,12 @@ def test_gpu_tree_encode_vs_oracle_roundtrip(gpu, oracle, n, m, roots):
                                   codes[enc.vertices])
     assert enc.children.stream[:enc.children.nbytes].cpu().numpy().tobytes() == \
         _children_stream(oracle, oracle.children_codebook(nch)[1], nch)
+    # GPU tree decode (chunked, with the encoder's sidecar) returns the stream-order rows
+    for c in (64, 7):
+        e2 = enc if c == 64 else codec.tree_encode(gpu, torch.from_numpy(codes).cuda(), targets,
+                                                   counts, chunk_vectors=c)
+        dec = codec.tree_decode(gpu, e2).cpu().numpy()
+        np.testing.assert_array_equal(dec, codes[enc.vertices])
 
 
 @pytest.mark.gpu
@@ -154,3 +162,19 @@ def test_gpu_tree_gather_reports_bad_ids(gpu):
                                  par.data_ptr(), rows.data_ptr(), prev.data_ptr()) == 0
     assert lib().pqh_tree_status(gpu.ptr) != 0
     assert lib().pqh_tree_status(gpu.ptr) == 0      # the flag is cleared after a report
+
+
+@pytest.mark.parametrize("n,roots,c", [(1000, 3, 64), (5000, 40, 7), (20000, 1, 64), (1, 1, 4)])
+def test_tree_ext_index_vs_oracle(oracle, n, roots, c):
+    """The decode sidecar index: parent positions equal the oracle traverser's, and the ext
+    list is exactly the rows whose context precedes their chunk, in row order."""
+    from pq_huffman_amd import codec
+    targets, counts = datagen.random_forest(n, roots=roots, seed=n + c)
+    _, nch, _ = oracle.tree_order(n, targets, counts)
+    pp, eo, ep = codec.tree_ext_index(nch, c)
+    np.testing.assert_array_equal(pp, oracle.tree_parents(nch))
+    rows = np.arange(n)
+    ext = (pp >= 0) & (pp < rows - rows % c)
+    np.testing.assert_array_equal(ep, pp[ext])
+    np.testing.assert_array_equal(eo[:-1], np.concatenate([[0], np.cumsum(ext)])[rows[::c]])
+    assert eo[-1] == ext.sum()
