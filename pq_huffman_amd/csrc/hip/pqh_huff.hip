@@ -785,6 +785,28 @@ tree_gather(const CodeT* __restrict__ codes, long long n, int m,
     const long long par = parents[p];
     const bool bad = v >= n || par >= n;
     if (bad) atomicOr(err, 1ull);   // an id outside the rows: reported, nothing read
+    if (sizeof(CodeT) == 1 && (m & 7) == 0) {   // whole 8-byte groups: wide loads and stores
+        for (int q = 0; q < m / 8; ++q) {
+            const unsigned long long c =
+                bad ? 0ull : reinterpret_cast<const unsigned long long*>(codes + v * m)[q];
+            const unsigned long long pc =
+                (bad || par < 0) ? 0ull : reinterpret_cast<const unsigned long long*>(codes + par * m)[q];
+            reinterpret_cast<unsigned long long*>(rows + p * m)[q] = c;
+            unsigned long long w[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                w[h] = 0;
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    w[h] |= (unsigned long long)((bad || par < 0) ? 0xFFFFu
+                                                 : (unsigned)((pc >> (8 * (4 * h + b))) & 0xFFu))
+                            << (16 * b);
+            }
+            reinterpret_cast<unsigned long long*>(tree_prev + p * m)[2 * q] = w[0];
+            reinterpret_cast<unsigned long long*>(tree_prev + p * m)[2 * q + 1] = w[1];
+        }
+        return;
+    }
     for (int i = 0; i < m; ++i) {
         rows[p * m + i] = bad ? CodeT(0) : codes[v * m + i];
         tree_prev[p * m + i] = (bad || par < 0) ? uint16_t(0xFFFF) : uint16_t(codes[par * m + i]);

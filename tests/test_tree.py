@@ -139,8 +139,8 @@ def test_gpu_tree_encode_vs_oracle_roundtrip(gpu, oracle, n, m, roots):
     assert enc.children.stream[:enc.children.nbytes].cpu().numpy().tobytes() == \
         _children_stream(oracle, oracle.children_codebook(nch)[1], nch)
     # GPU tree decode (chunked, with the encoder's sidecar) returns the stream-order rows
-    for c in (64, 7):
-        e2 = enc if c == 64 else codec.tree_encode(gpu, torch.from_numpy(codes).cuda(), targets,
+    for c in (16, 7, 64):
+        e2 = enc if c == 16 else codec.tree_encode(gpu, torch.from_numpy(codes).cuda(), targets,
                                                    counts, chunk_vectors=c)
         dec = codec.tree_decode(gpu, e2).cpu().numpy()
         np.testing.assert_array_equal(dec, codes[enc.vertices])
