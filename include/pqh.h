@@ -261,6 +261,13 @@ typedef struct {
  * huffman_stats.txt (appended), and the decode sidecar huffman_chunks.bin. */
 int pqh_encode_files(const unsigned char* codes, long long n, int m,
                      const pqh_encode_options_t* options, const char* out_prefix);
+/* huffman_encoder --tree <tree_path>: tree-ordered context coding of host codes (n x m,
+ * K = 256) over the forest stored in mst.tree (sorted first when sort != 0, as the CLI
+ * does).  Writes the reference's tree-mode files under out_prefix: huffman_codebooks.bin,
+ * huffman_indices.bin, huffman_stats.txt, huffman_children_codebooks.bin,
+ * huffman_children.bin, huffman_children_stats.txt. */
+int pqh_encode_tree_files(const unsigned char* codes, long long n, int m, int sort,
+                          const char* tree_path, const char* out_prefix);
 /* Decodes huffman_indices.bin (+ sidecar when present) under in_prefix into codes
  * (n x m host buffer, n from the file header). */
 int pqh_decode_files(const char* in_prefix, unsigned char** codes_out, long long* n_out,

@@ -204,7 +204,8 @@ def tree_fixtures(tmp, n=1000, m=8, seed=21, roots=3, name="tree_m8_n1000"):
         assert r.returncode == 0, r.stderr
         arrays[mode + "__decoded"] = np.fromfile(outf, np.uint8).reshape(n, m)
         for f in ("huffman_codebooks.bin", "huffman_indices.bin",
-                  "huffman_children_codebooks.bin", "huffman_children.bin"):
+                  "huffman_children_codebooks.bin", "huffman_children.bin",
+                  "huffman_stats.txt", "huffman_children_stats.txt"):
             arrays[mode + "__" + f.split(".")[0]] = np.frombuffer(read(out + f), np.uint8)
     np.savez_compressed(os.path.join(GOLD, f"huff_{name}.npz"), **arrays)
 

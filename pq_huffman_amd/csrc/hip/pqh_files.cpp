@@ -262,3 +262,182 @@ extern "C" int pqh_decode_files(const char* in_prefix, unsigned char** codes_out
     *m_out = (int)m;
     return PQH_OK;
 }
+
+// huffman_encoder --tree <mst.tree> (huffman_encoder.c:321-375, :398-428): tree order and
+// contexts on the host (pqh_tree_order), rows gathered, counted and coded on the GPU, the
+// children stream coded by the GPU encoder with the host-built children code book.
+// Writes huffman_codebooks.bin, huffman_indices.bin, huffman_stats.txt (appended),
+// huffman_children_codebooks.bin, huffman_children.bin, huffman_children_stats.txt.
+extern "C" int pqh_encode_tree_files(const unsigned char* codes, long long n, int m, int sort,
+                                     const char* tree_path, const char* out_prefix) {
+    const int k = 256;
+    if (!codes || n <= 0 || m <= 0 || m > 16 || !tree_path || !out_prefix) return PQH_ERR_ARG;
+    // tree_load_file (mst.c:273-288): i64 N, i64 E, u32 targets[E], i32 counts[N]
+    FILE* tf = fopen(tree_path, "rb");
+    if (!tf) return PQH_ERR_ARG;
+    long long nv = 0, ne = 0;
+    bool ok = fread(&nv, 8, 1, tf) == 1 && fread(&ne, 8, 1, tf) == 1 && nv == n && ne >= 0;
+    std::vector<uint32_t> targets(ok ? (size_t)ne : 0);
+    std::vector<int> adj(ok ? (size_t)nv : 0);
+    ok = ok && fread(targets.data(), 4, (size_t)ne, tf) == (size_t)ne &&
+         fread(adj.data(), 4, (size_t)nv, tf) == (size_t)nv;
+    fclose(tf);
+    if (!ok) return PQH_ERR_ARG;
+    std::vector<uint32_t> vert(n);
+    std::vector<int> nch(n);
+    std::vector<long long> par(n);
+    const int roots = pqh_tree_order(n, ne, targets.data(), adj.data(), vert.data(), nch.data(),
+                                     par.data());
+    if (roots < 0) return roots;
+
+    CtxGuard g;
+    int rc = pqh_ctx_create(&g.ctx, 0);
+    if (rc) return rc;
+    pqh_ctx* ctx = g.ctx;
+    const long long items = (long long)k * k;
+    DevBuf<unsigned char> d_codes, d_rows;
+    DevBuf<uint16_t> d_prev;
+    DevBuf<uint32_t> d_vert, d_counts;
+    DevBuf<long long> d_par;
+    if ((rc = d_codes.alloc(ctx, (size_t)n * m)) || (rc = d_rows.alloc(ctx, (size_t)n * m)) ||
+        (rc = d_prev.alloc(ctx, (size_t)n * m)) || (rc = d_vert.alloc(ctx, n)) ||
+        (rc = d_par.alloc(ctx, n)) || (rc = d_counts.alloc(ctx, (size_t)m * items)))
+        return rc;
+    PQH_HIP(ctx, hipMemcpyAsync(d_codes.p, codes, (size_t)n * m, hipMemcpyHostToDevice, ctx->stream));
+    PQH_HIP(ctx, hipMemcpyAsync(d_vert.p, vert.data(), (size_t)n * 4, hipMemcpyHostToDevice, ctx->stream));
+    PQH_HIP(ctx, hipMemcpyAsync(d_par.p, par.data(), (size_t)n * 8, hipMemcpyHostToDevice, ctx->stream));
+    if (sort) {   // the CLI sorts before applying the tree (huffman_encoder.c:313-325)
+        DevBuf<unsigned char> tmp;
+        if ((rc = tmp.alloc(ctx, (size_t)n * m))) return rc;
+        if ((rc = pqh_sort_rows(ctx, d_codes.p, n, m, tmp.p))) return rc;
+    }
+    if ((rc = pqh_tree_gather(ctx, d_codes.p, n, m, k, d_vert.p, d_par.p, d_rows.p, d_prev.p)) ||
+        (rc = pqh_tree_status(ctx)))
+        return rc;
+    PQH_HIP(ctx, hipMemsetAsync(d_counts.p, 0, (size_t)m * items * 4, ctx->stream));
+    if ((rc = pqh_histogram_tree(ctx, d_rows.p, d_prev.p, n, m, k, d_counts.p))) return rc;
+    pqh_tables_t* tab = nullptr;
+    if ((rc = pqh_tables_alloc(ctx, m, k, 1, &tab))) return rc;
+    rc = pqh_tables_build(ctx, tab, d_counts.p);
+    std::vector<huffman_codebook_t> cbs(m);
+    if (!rc) rc = pqh_tables_codebooks(ctx, tab, cbs.data());
+    if (rc) {
+        pqh_tables_destroy(tab);
+        return rc;
+    }
+    std::vector<uint32_t> hc((size_t)m * items);
+    PQH_HIP(ctx, hipMemcpyAsync(hc.data(), d_counts.p, hc.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
+    PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    std::vector<double> counts(hc.begin(), hc.end());
+
+    // children code book + stream (huffman_encoder.c:343-375)
+    int alphabet = 0;
+    for (long long p = 0; p < n; ++p) alphabet = nch[p] > alphabet ? nch[p] : alphabet;
+    ++alphabet;
+    printf("Max num children: %d\n", alphabet);
+    if (alphabet > 4096) {
+        for (auto& cb : cbs) huffman_codebook_destroy(&cb);
+        pqh_tables_destroy(tab);
+        return pqh_set_error(ctx, PQH_ERR_UNSUPPORTED, "more than 4095 children at one vertex");
+    }
+    std::vector<double> ccounts(alphabet, 0.0);
+    for (long long p = 0; p < n; ++p) ccounts[nch[p]] += 1.0;
+    huffman_codebook_t ccb;
+    huffman_codebook_encode_init(&ccb, alphabet, ccounts.data());
+    {
+        FILE* f = fopen(path_of(out_prefix, "huffman_children_codebooks.bin").c_str(), "wb");
+        if (f) {
+            huffman_codebook_save(&ccb, f);
+            fclose(f);
+        }
+        huffman_stats_t cst;
+        huffman_stats_init(&cst, n, 1, k);
+        huffman_stats_push(&cst, 0, huffman_estimate_size(&ccb, ccounts.data()));
+        huffman_stats_print_filename(&cst, path_of(out_prefix, "huffman_children_stats.txt").c_str());
+        huffman_stats_destroy(&cst);
+    }
+
+    huffman_stats_t st;
+    huffman_stats_init(&st, n, m, k);
+    st.num_roots = roots;
+    double total_bits = 8.0 * m * roots;
+    for (int i = 0; i < m; ++i) {
+        const double e = huffman_estimate_size(&cbs[i], counts.data() + i * items);
+        huffman_stats_push(&st, i, e);
+        total_bits += e;
+    }
+    huffman_stats_print(&st);
+    huffman_stats_print_filename(&st, path_of(out_prefix, "huffman_stats.txt").c_str());
+    huffman_stats_destroy(&st);
+    FILE* cf = fopen(path_of(out_prefix, "huffman_codebooks.bin").c_str(), "wb");
+    if (cf) {
+        uint32_t mu = (uint32_t)m;
+        fwrite(&mu, 4, 1, cf);
+        for (int i = 0; i < m; ++i) huffman_codebook_save(&cbs[i], cf);
+        fclose(cf);
+    }
+    for (auto& cb : cbs) huffman_codebook_destroy(&cb);
+
+    // the row stream (encode_tree_data, huffman_encoder.c:240-286)
+    const unsigned long long cap = ((unsigned long long)total_bits + 31) / 32 * 4 + 64;
+    DevBuf<unsigned char> d_out;
+    DevBuf<unsigned long long> d_total;
+    unsigned long long bits = 0;
+    if (!(rc = d_out.alloc(ctx, cap)) && !(rc = d_total.alloc(ctx, 1)))
+        rc = pqh_encode_tree_write(ctx, tab, d_rows.p, d_prev.p, n, 0, d_out.p, cap, 0, nullptr,
+                                   d_total.p);
+    if (!rc) rc = pqh_encode_status(ctx);
+    pqh_tables_destroy(tab);
+    std::vector<unsigned char> stream;
+    if (!rc) {
+        PQH_HIP(ctx, hipMemcpyAsync(&bits, d_total.p, 8, hipMemcpyDeviceToHost, ctx->stream));
+        PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        stream.resize((bits + 7) / 8 + 1);
+        PQH_HIP(ctx, hipMemcpyAsync(stream.data(), d_out.p, (bits + 7) / 8, hipMemcpyDeviceToHost,
+                                    ctx->stream));
+    }
+    // the children stream: one non-context part, u8 or u16 symbols
+    pqh_tables_t* ctab = nullptr;
+    const size_t esz = alphabet <= 256 ? 1 : 2;
+    DevBuf<unsigned char> d_cc, d_cout;
+    std::vector<unsigned char> cstream;
+    unsigned long long cbits = 0;
+    if (!rc) rc = pqh_tables_create(ctx, &ccb, 1, &ctab);
+    if (!rc) {
+        std::vector<unsigned char> cc((size_t)n * esz);
+        for (long long p = 0; p < n; ++p) {
+            if (esz == 1) cc[p] = (unsigned char)nch[p];
+            else reinterpret_cast<uint16_t*>(cc.data())[p] = (uint16_t)nch[p];
+        }
+        double cb_bits = huffman_estimate_size(&ccb, ccounts.data());
+        const unsigned long long ccap = ((unsigned long long)cb_bits + 31) / 32 * 4 + 64;
+        if (!(rc = d_cc.alloc(ctx, cc.size())) && !(rc = d_cout.alloc(ctx, ccap))) {
+            PQH_HIP(ctx, hipMemcpyAsync(d_cc.p, cc.data(), cc.size(), hipMemcpyHostToDevice, ctx->stream));
+            rc = pqh_encode_write(ctx, ctab, d_cc.p, n, 1, nullptr, 0, d_cout.p, ccap, 0, nullptr,
+                                  nullptr, d_total.p);
+        }
+        if (!rc) rc = pqh_encode_status(ctx);
+        if (!rc) {
+            PQH_HIP(ctx, hipMemcpyAsync(&cbits, d_total.p, 8, hipMemcpyDeviceToHost, ctx->stream));
+            PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            cstream.resize((cbits + 7) / 8 + 1);
+            PQH_HIP(ctx, hipMemcpyAsync(cstream.data(), d_cout.p, (cbits + 7) / 8,
+                                        hipMemcpyDeviceToHost, ctx->stream));
+            PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        }
+    }
+    if (ctab) pqh_tables_destroy(ctab);
+    huffman_codebook_destroy(&ccb);
+    if (rc) return rc;
+    FILE* ef = fopen(path_of(out_prefix, "huffman_indices.bin").c_str(), "wb");
+    if (!ef) return pqh_set_error(ctx, PQH_ERR_ARG, "cannot write indices");
+    unsigned long long nn = (unsigned long long)n;
+    fwrite(&nn, 8, 1, ef);
+    fwrite(stream.data(), 1, (bits + 7) / 8, ef);
+    fclose(ef);
+    FILE* chf = fopen(path_of(out_prefix, "huffman_children.bin").c_str(), "wb");
+    if (!chf) return pqh_set_error(ctx, PQH_ERR_ARG, "cannot write children stream");
+    fwrite(cstream.data(), 1, (cbits + 7) / 8, chf);
+    fclose(chf);
+    return PQH_OK;
+}

@@ -178,3 +178,26 @@ def test_tree_ext_index_vs_oracle(oracle, n, roots, c):
     np.testing.assert_array_equal(ep, pp[ext])
     np.testing.assert_array_equal(eo[:-1], np.concatenate([[0], np.cumsum(ext)])[rows[::c]])
     assert eo[-1] == ext.sum()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,flags", [("tree_nosort", ["--no-sort"]), ("tree_sort", [])])
+def test_cli_encoder_tree_matches_reference_files(tmp_path, mode, flags):
+    """huffman_encoder --tree (pqh_encode_tree_files) writes the reference's six files."""
+    import os
+    import subprocess
+    from conftest import ROOT
+    g = golden("huff_tree_m8_n1000.npz")
+    pqdir, out = tmp_path / "pq", tmp_path / "out"
+    pqdir.mkdir()
+    out.mkdir()
+    datagen.write_vecsl(str(pqdir / "pq_indices.bvecsl"), g["input"])
+    tree = tmp_path / "mst.tree"
+    datagen.write_tree(str(tree), 1000, g["targets"], g["counts"])
+    r = subprocess.run([os.path.join(ROOT, "pq_huffman_amd", "bin", "huffman_encoder"),
+                        str(pqdir) + "/", str(out) + "/", "8", "--tree", str(tree)] + flags,
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    for f in FILES + ["huffman_stats", "huffman_children_stats"]:
+        ext = ".txt" if f.endswith("stats") else ".bin"
+        assert (out / (f + ext)).read_bytes() == g[mode + "__" + f].tobytes(), f
