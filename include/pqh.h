@@ -265,9 +265,15 @@ int pqh_encode_files(const unsigned char* codes, long long n, int m,
  * K = 256) over the forest stored in mst.tree (sorted first when sort != 0, as the CLI
  * does).  Writes the reference's tree-mode files under out_prefix: huffman_codebooks.bin,
  * huffman_indices.bin, huffman_stats.txt, huffman_children_codebooks.bin,
- * huffman_children.bin, huffman_children_stats.txt. */
+ * huffman_children.bin, huffman_children_stats.txt, plus the decode sidecar
+ * huffman_tree_chunks.bin (pqh extension: chunk bit offsets + ext context rows). */
 int pqh_encode_tree_files(const unsigned char* codes, long long n, int m, int sort,
                           const char* tree_path, const char* out_prefix);
+/* huffman_decoder --tree: decodes the tree-mode files under in_prefix into rows in stream
+ * (DFS) order, as the reference decoder writes them.  Needs the decode sidecar
+ * huffman_tree_chunks.bin that pqh_encode_tree_files writes (PQH_ERR_ARG without it). */
+int pqh_decode_tree_files(const char* in_prefix, unsigned char** codes_out, long long* n_out,
+                          int* m_out);
 /* Decodes huffman_indices.bin (+ sidecar when present) under in_prefix into codes
  * (n x m host buffer, n from the file header). */
 int pqh_decode_files(const char* in_prefix, unsigned char** codes_out, long long* n_out,

@@ -126,6 +126,7 @@ SIGNATURES = [
     ("pqh_tree_ext_index", LL, [LL, P, I, P, P, P]),
     ("pqh_decode_tree", I, [P, P, P, ULL, LL, I, P, P, P, P, P]),
     ("pqh_encode_tree_files", I, [P, LL, I, I, S, S]),
+    ("pqh_decode_tree_files", I, [S, P, P, P]),
     ("pqh_encode_files", I, [P, LL, I, P, S]),
     ("pqh_decode_files", I, [S, P, P, P]),
 ]

@@ -20,6 +20,15 @@ struct Sidecar {
     uint64_t n, chunks;
 };
 
+// huffman_tree_chunks.bin: the tree decoder's index (pqh extension) -- chunk bit offsets
+// and the context rows that precede each chunk (pqh_tree_ext_index order)
+struct TreeSidecar {
+    char magic[4];
+    uint32_t version, m, chunk_vectors;
+    uint64_t n, chunks, ext;
+};
+constexpr int kTreeFileChunk = 16;
+
 struct CtxGuard {
     pqh_ctx_t* ctx = nullptr;
     ~CtxGuard() { pqh_ctx_destroy(ctx); }
@@ -381,11 +390,17 @@ extern "C" int pqh_encode_tree_files(const unsigned char* codes, long long n, in
     // the row stream (encode_tree_data, huffman_encoder.c:240-286)
     const unsigned long long cap = ((unsigned long long)total_bits + 31) / 32 * 4 + 64;
     DevBuf<unsigned char> d_out;
-    DevBuf<unsigned long long> d_total;
+    DevBuf<unsigned long long> d_total, d_coff;
     unsigned long long bits = 0;
+    const long long chunks = (n + kTreeFileChunk - 1) / kTreeFileChunk;
+    if ((rc = d_coff.alloc(ctx, chunks + 1))) {
+        pqh_tables_destroy(tab);
+        huffman_codebook_destroy(&ccb);
+        return rc;
+    }
     if (!(rc = d_out.alloc(ctx, cap)) && !(rc = d_total.alloc(ctx, 1)))
-        rc = pqh_encode_tree_write(ctx, tab, d_rows.p, d_prev.p, n, 0, d_out.p, cap, 0, nullptr,
-                                   d_total.p);
+        rc = pqh_encode_tree_write(ctx, tab, d_rows.p, d_prev.p, n, 0, d_out.p, cap,
+                                   kTreeFileChunk, d_coff.p, d_total.p);
     if (!rc) rc = pqh_encode_status(ctx);
     pqh_tables_destroy(tab);
     std::vector<unsigned char> stream;
@@ -429,6 +444,33 @@ extern "C" int pqh_encode_tree_files(const unsigned char* codes, long long n, in
     if (ctab) pqh_tables_destroy(ctab);
     huffman_codebook_destroy(&ccb);
     if (rc) return rc;
+    // decode sidecar: chunk offsets + the context rows that precede each chunk
+    std::vector<unsigned long long> coff(chunks);
+    std::vector<unsigned char> rows((size_t)n * m);
+    PQH_HIP(ctx, hipMemcpyAsync(coff.data(), d_coff.p, chunks * 8, hipMemcpyDeviceToHost, ctx->stream));
+    PQH_HIP(ctx, hipMemcpyAsync(rows.data(), d_rows.p, rows.size(), hipMemcpyDeviceToHost, ctx->stream));
+    PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    std::vector<long long> pp(n), eo(chunks + 1);
+    const long long ext = pqh_tree_ext_index(n, nch.data(), kTreeFileChunk, pp.data(), eo.data(),
+                                             nullptr);
+    if (ext < 0) return (int)ext;
+    std::vector<long long> ep(ext + 1);
+    pqh_tree_ext_index(n, nch.data(), kTreeFileChunk, pp.data(), eo.data(), ep.data());
+    FILE* tsf = fopen(path_of(out_prefix, "huffman_tree_chunks.bin").c_str(), "wb");
+    if (tsf) {
+        TreeSidecar h;
+        memcpy(h.magic, "PQHT", 4);
+        h.version = 1;
+        h.m = m;
+        h.chunk_vectors = kTreeFileChunk;
+        h.n = n;
+        h.chunks = chunks;
+        h.ext = ext;
+        fwrite(&h, sizeof(h), 1, tsf);
+        fwrite(coff.data(), 8, chunks, tsf);
+        for (long long e = 0; e < ext; ++e) fwrite(rows.data() + ep[e] * m, 1, m, tsf);
+        fclose(tsf);
+    }
     FILE* ef = fopen(path_of(out_prefix, "huffman_indices.bin").c_str(), "wb");
     if (!ef) return pqh_set_error(ctx, PQH_ERR_ARG, "cannot write indices");
     unsigned long long nn = (unsigned long long)n;
@@ -439,5 +481,132 @@ extern "C" int pqh_encode_tree_files(const unsigned char* codes, long long n, in
     if (!chf) return pqh_set_error(ctx, PQH_ERR_ARG, "cannot write children stream");
     fwrite(cstream.data(), 1, (cbits + 7) / 8, chf);
     fclose(chf);
+    return PQH_OK;
+}
+
+// huffman_decoder --tree (huffman_decoder.c:174-247) on the GPU: the children stream first
+// (GPU decode; its chunk index from a host walk of the table), the traverser index on the
+// host, then dec_tree with the encoder's sidecar huffman_tree_chunks.bin (required: a tree
+// stream cannot be split into independent chunks without it).  Rows in stream order.
+extern "C" int pqh_decode_tree_files(const char* in_prefix, unsigned char** codes_out,
+                                     long long* n_out, int* m_out) {
+    if (!in_prefix || !codes_out || !n_out || !m_out) return PQH_ERR_ARG;
+    *codes_out = nullptr;
+    auto slurp = [&](const char* name, long long skip, std::vector<unsigned char>& buf,
+                     unsigned long long& bytes) {
+        FILE* f = fopen(path_of(in_prefix, name).c_str(), "rb");
+        if (!f) return false;
+        fseek(f, 0, SEEK_END);
+        const long long size = ftell(f);
+        fseek(f, skip, SEEK_SET);
+        bytes = size > skip ? (unsigned long long)(size - skip) : 0;
+        buf.assign(((bytes + 3) / 4) * 4 + 8, 0);
+        const bool ok = !bytes || fread(buf.data(), 1, bytes, f) == bytes;
+        fclose(f);
+        return ok;
+    };
+    FILE* cf = fopen(path_of(in_prefix, "huffman_codebooks.bin").c_str(), "rb");
+    if (!cf) return PQH_ERR_ARG;
+    uint32_t m = 0;
+    if (fread(&m, 4, 1, cf) != 1 || m == 0 || m > 16) {
+        fclose(cf);
+        return PQH_ERR_CORRUPT;
+    }
+    std::vector<huffman_codebook_t> cbs(m);
+    for (uint32_t i = 0; i < m; ++i) huffman_codebook_load(&cbs[i], cf);
+    fclose(cf);
+    huffman_codebook_t ccb;
+    FILE* ccf = fopen(path_of(in_prefix, "huffman_children_codebooks.bin").c_str(), "rb");
+    if (!ccf) {
+        for (auto& cb : cbs) huffman_codebook_destroy(&cb);
+        return PQH_ERR_ARG;
+    }
+    huffman_codebook_load(&ccb, ccf);
+    fclose(ccf);
+    unsigned long long n = 0;
+    {
+        FILE* ef = fopen(path_of(in_prefix, "huffman_indices.bin").c_str(), "rb");
+        if (!ef || fread(&n, 8, 1, ef) != 1) n = 0;
+        if (ef) fclose(ef);
+    }
+    std::vector<unsigned char> stream, cstream, side;
+    unsigned long long bytes = 0, cbytes = 0, sbytes = 0;
+    bool ok = n > 0 && slurp("huffman_indices.bin", 8, stream, bytes) &&
+              slurp("huffman_children.bin", 0, cstream, cbytes) &&
+              slurp("huffman_tree_chunks.bin", 0, side, sbytes) && sbytes >= sizeof(TreeSidecar);
+    TreeSidecar h{};
+    if (ok) {
+        memcpy(&h, side.data(), sizeof(h));
+        ok = !memcmp(h.magic, "PQHT", 4) && h.n == n && h.m == m && h.chunk_vectors > 0 &&
+             h.chunks == (n + h.chunk_vectors - 1) / h.chunk_vectors &&
+             sbytes >= sizeof(h) + h.chunks * 8 + h.ext * m;
+    }
+    CtxGuard g;
+    int rc = ok ? pqh_ctx_create(&g.ctx, 0) : PQH_ERR_ARG;
+    pqh_tables_t *tab = nullptr, *ctab = nullptr;
+    if (!rc) rc = pqh_tables_create(g.ctx, cbs.data(), (int)m, &tab);
+    if (!rc) rc = pqh_tables_create(g.ctx, &ccb, 1, &ctab);
+    const int calpha = ccb.alphabet_size;
+    for (auto& cb : cbs) huffman_codebook_destroy(&cb);
+    huffman_codebook_destroy(&ccb);
+    auto fail = [&](int r) {
+        if (tab) pqh_tables_destroy(tab);
+        if (ctab) pqh_tables_destroy(ctab);
+        return r;
+    };
+    if (rc) return fail(rc);
+    pqh_ctx* ctx = g.ctx;
+    // children stream -> child counts
+    const int CC = 64;
+    const long long cchunks = ((long long)n + CC - 1) / CC;
+    const size_t cesz = calpha <= 256 ? 1 : 2;
+    std::vector<unsigned long long> ccoff(cchunks + 1);
+    std::vector<unsigned char> ccprev((cchunks + 1) * cesz);
+    if ((rc = pqh_chunk_index_host(ctab, cstream.data(), cbytes, (long long)n, 1, CC, ccoff.data(),
+                                   ccprev.data())))
+        return fail(rc);
+    DevBuf<unsigned char> d_cstream, d_cc, d_stream, d_ext, d_rows;
+    DevBuf<unsigned long long> d_ccoff, d_coff;
+    DevBuf<long long> d_pp, d_eo;
+    if ((rc = d_cstream.alloc(ctx, cstream.size())) || (rc = d_ccoff.alloc(ctx, cchunks + 1)) ||
+        (rc = d_cc.alloc(ctx, n * cesz)))
+        return fail(rc);
+    PQH_HIP(ctx, hipMemcpyAsync(d_cstream.p, cstream.data(), cstream.size(), hipMemcpyHostToDevice, ctx->stream));
+    PQH_HIP(ctx, hipMemcpyAsync(d_ccoff.p, ccoff.data(), (cchunks + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+    rc = pqh_decode(ctx, ctab, d_cstream.p, cstream.size(), (long long)n, 1, CC, d_ccoff.p, nullptr,
+                    d_cc.p);
+    if (!rc) rc = pqh_decode_status(ctx);
+    if (rc) return fail(rc);
+    std::vector<unsigned char> ccodes(n * cesz);
+    PQH_HIP(ctx, hipMemcpy(ccodes.data(), d_cc.p, ccodes.size(), hipMemcpyDeviceToHost));
+    std::vector<int> nch(n);
+    for (unsigned long long p = 0; p < n; ++p)
+        nch[p] = cesz == 1 ? ccodes[p] : reinterpret_cast<const uint16_t*>(ccodes.data())[p];
+    // traverser index; its ext count must agree with the sidecar's
+    const int C = (int)h.chunk_vectors;
+    std::vector<long long> pp(n), eo(h.chunks + 1);
+    const long long ext = pqh_tree_ext_index((long long)n, nch.data(), C, pp.data(), eo.data(), nullptr);
+    if (ext < 0 || (unsigned long long)ext != h.ext) return fail(PQH_ERR_CORRUPT);
+    if ((rc = d_stream.alloc(ctx, stream.size())) || (rc = d_coff.alloc(ctx, h.chunks + 1)) ||
+        (rc = d_pp.alloc(ctx, n)) || (rc = d_eo.alloc(ctx, h.chunks + 1)) ||
+        (rc = d_ext.alloc(ctx, h.ext * m + 1)) || (rc = d_rows.alloc(ctx, n * m)))
+        return fail(rc);
+    const unsigned char* sp = side.data() + sizeof(h);
+    PQH_HIP(ctx, hipMemcpyAsync(d_stream.p, stream.data(), stream.size(), hipMemcpyHostToDevice, ctx->stream));
+    PQH_HIP(ctx, hipMemcpyAsync(d_coff.p, sp, h.chunks * 8, hipMemcpyHostToDevice, ctx->stream));
+    if (h.ext)
+        PQH_HIP(ctx, hipMemcpyAsync(d_ext.p, sp + h.chunks * 8, h.ext * m, hipMemcpyHostToDevice, ctx->stream));
+    PQH_HIP(ctx, hipMemcpyAsync(d_pp.p, pp.data(), n * 8, hipMemcpyHostToDevice, ctx->stream));
+    PQH_HIP(ctx, hipMemcpyAsync(d_eo.p, eo.data(), (h.chunks + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+    rc = pqh_decode_tree(ctx, tab, d_stream.p, stream.size(), (long long)n, C, d_coff.p, d_pp.p,
+                         d_eo.p, d_ext.p, d_rows.p);
+    if (!rc) rc = pqh_decode_status(ctx);
+    if (rc) return fail(rc);
+    fail(0);
+    unsigned char* out = (unsigned char*)malloc(n * m + 1);
+    PQH_HIP(ctx, hipMemcpy(out, d_rows.p, n * m, hipMemcpyDeviceToHost));
+    *codes_out = out;
+    *n_out = (long long)n;
+    *m_out = (int)m;
     return PQH_OK;
 }

@@ -32,13 +32,12 @@ int main(int argc, const char* argv[]) {
     }
     const char* out_file = NULL;
     const char* check = NULL;
+    int tree = 0;
     for (int i = 2; i < argc; ++i) {
         if (!strcmp(argv[i], "--output-file") && i + 1 < argc) out_file = argv[++i];
         else if (!strcmp(argv[i], "--check-file") && i + 1 < argc) check = argv[++i];
-        else if (!strcmp(argv[i], "--tree")) {
-            fprintf(stderr, "--tree: not supported by this build\n");
-            return 1;
-        } else {
+        else if (!strcmp(argv[i], "--tree")) tree = 1;
+        else {
             fprintf(stderr, "Unknown arg: %s\n", argv[i]);
             return 1;
         }
@@ -46,7 +45,9 @@ int main(int argc, const char* argv[]) {
     unsigned char* codes = NULL;
     long long n = 0;
     int m = 0;
-    int rc = pqh_decode_files(argv[1], &codes, &n, &m);
+    /* --tree: rows come back in the stream's DFS order (huffman_decoder.c:214-247) */
+    int rc = tree ? pqh_decode_tree_files(argv[1], &codes, &n, &m)
+                  : pqh_decode_files(argv[1], &codes, &n, &m);
     if (rc) {
         fprintf(stderr, "huffman_decoder: %s\n", pqh_status_string(rc));
         return 1;

@@ -201,3 +201,15 @@ def test_cli_encoder_tree_matches_reference_files(tmp_path, mode, flags):
     for f in FILES + ["huffman_stats", "huffman_children_stats"]:
         ext = ".txt" if f.endswith("stats") else ".bin"
         assert (out / (f + ext)).read_bytes() == g[mode + "__" + f].tobytes(), f
+    # huffman_decoder --tree: the GPU decode (with the sidecar) gives the reference's rows
+    dec = tmp_path / "dec.bin"
+    r = subprocess.run([os.path.join(ROOT, "pq_huffman_amd", "bin", "huffman_decoder"),
+                        str(out) + "/", "--tree", "--output-file", str(dec), "--check-file",
+                        str(pqdir / "pq_indices.bvecsl")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert dec.read_bytes() == g[mode + "__decoded"].tobytes()
+    (out / "huffman_tree_chunks.bin").unlink()      # no sidecar: refused, not mis-decoded
+    r = subprocess.run([os.path.join(ROOT, "pq_huffman_amd", "bin", "huffman_decoder"),
+                        str(out) + "/", "--tree", "--output-file", str(dec)],
+                       capture_output=True, text=True)
+    assert r.returncode != 0
