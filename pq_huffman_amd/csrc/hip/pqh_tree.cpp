@@ -19,42 +19,55 @@ int pqh_tree_order(long long num_vertices, long long num_edges, const uint32_t* 
     if (num_vertices == 0) return 0;
     // adjacency list of vertex i = edge_targets[first[i], first[i] + children_counts[i])
     // (restore_tree_edges_pointers, mst.c:52-61)
-    std::vector<long long> first((size_t)num_vertices + 1, 0);
+    // (a forest has < 2^32 edges: 32-bit offsets halve the walk's random-access footprint)
+    if (num_edges >= (1LL << 32) || num_vertices >= (1LL << 32) - 1) return PQH_ERR_ARG;
+    std::vector<uint32_t> first((size_t)num_vertices + 1, 0);
+    long long total = 0;
     for (long long i = 0; i < num_vertices; ++i) {
         if (children_counts[i] < 0) return PQH_ERR_ARG;
-        first[i + 1] = first[i] + children_counts[i];
+        total += children_counts[i];
+        if (total > num_edges) return PQH_ERR_ARG;
+        first[i + 1] = (uint32_t)total;
     }
-    if (first[num_vertices] != num_edges) return PQH_ERR_ARG;
+    if (total != num_edges) return PQH_ERR_ARG;
     for (long long e = 0; e < num_edges; ++e)
         if ((long long)edge_targets[e] >= num_vertices) return PQH_ERR_ARG;
 
-    // DFS with marking on push; roots are the lowest unvisited ids (mst.c:303-353)
+    // DFS with marking on push; roots are the lowest unvisited ids (mst.c:303-353).
+    // mark[v] = 0 unvisited, else 1 + the DFS position of the vertex that pushed it, so one
+    // pass over the adjacency list both pushes and counts: the reference counts unvisited
+    // neighbours before pushing any (:322-333), so a target repeated in one list counts once
+    // per repeat -- a repeat is a target already marked by this same vertex.
     std::vector<uint32_t> stack((size_t)num_vertices);
-    std::vector<char> visited((size_t)num_vertices, 0);
+    std::vector<uint32_t> mark((size_t)num_vertices, 0);
     long long processed = 0, stack_size = 0, children_sum = 0;
     uint32_t next_root = 0;
     int num_roots = 0;
     while (processed < num_vertices) {
         if (stack_size == 0) {
-            while ((long long)next_root < num_vertices && visited[next_root]) ++next_root;
+            while ((long long)next_root < num_vertices && mark[next_root]) ++next_root;
             stack[stack_size++] = next_root;
-            visited[next_root] = 1;
+            mark[next_root] = UINT32_MAX;   // pushed by no vertex
             ++num_roots;
         }
         const uint32_t cur = stack[--stack_size];
+        const uint32_t stamp = (uint32_t)processed + 1;
         vertices[processed] = cur;
-        int kids = 0;   // unvisited neighbours counted before any of them is pushed (:322-333)
-        for (long long e = first[cur]; e < first[cur + 1]; ++e) kids += !visited[edge_targets[e]];
+        int kids = 0;
+        for (uint32_t e = first[cur]; e < first[cur + 1]; ++e) {
+            const uint32_t t = edge_targets[e];
+            const uint32_t mt = mark[t];
+            if (!mt) {
+                mark[t] = stamp;
+                stack[stack_size++] = t;
+                ++kids;
+            } else if (mt == stamp) {
+                ++kids;
+            }
+        }
         num_children[processed] = kids;
         children_sum += kids;
         ++processed;
-        for (long long e = first[cur]; e < first[cur + 1]; ++e) {
-            const uint32_t t = edge_targets[e];
-            if (!visited[t]) {
-                visited[t] = 1;
-                stack[stack_size++] = t;
-            }
-        }
     }
     // the reference asserts this (mst.c:357): a duplicated edge breaks the child counts
     if (children_sum != num_vertices - num_roots) return PQH_ERR_ARG;

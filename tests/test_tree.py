@@ -76,6 +76,25 @@ def test_library_tree_order_rejects_malformed():
     bad[0] = 50                               # target outside the vertices
     with pytest.raises(PqhError):
         codec.tree_order(bad, counts)
+    # a target repeated in one list counts twice before the push (mst.c:322-333), so the
+    # child sum breaks the reference's assert (mst.c:357)
+    with pytest.raises(PqhError):
+        codec.tree_order(np.array([1, 1], np.uint32), np.array([2, 0, 0], np.int32))
+
+
+@pytest.mark.parametrize("targets,counts", [
+    ([1, 2, 0, 2, 0, 1], [2, 2, 2]),          # both directions and a cycle: back edges skipped
+    ([0, 1, 1, 0], [2, 1, 1]),                # self loops on a root and on a child
+    ([3, 2, 1, 0], [1, 1, 1, 1]),             # two trees whose second root is not the lowest id
+])
+def test_library_tree_order_back_edges_vs_oracle(oracle, targets, counts):
+    from pq_huffman_amd import codec
+    t, c = np.array(targets, np.uint32), np.array(counts, np.int32)
+    vert, nch, par, nroots = codec.tree_order(t, c)
+    ov, onch, oroots = oracle.tree_order(len(c), t, c)
+    np.testing.assert_array_equal(vert, ov)
+    np.testing.assert_array_equal(nch, onch)
+    assert nroots == oroots
 
 
 def test_tree_file_roundtrip(tmp_path):
