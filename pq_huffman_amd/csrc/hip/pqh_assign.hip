@@ -17,9 +17,10 @@
 //       [xh . ch | xh . cl | 1,1,1,b_v . n1,n2,n3,1]  (+ xl . ch only if the block has
 //    any x that is not bf16-exact -- SIFT-like integer data skips that pass);
 //    x = xh + xl + r, c = ch + cl + r', ||c||^2 = n1 + n2 + n3 (bf16 splits).
-//  * Scores become packed uint keys (float bits, low 4 bits = accumulator register) and
-//    each lane keeps the smallest and second smallest key over its 128 centroids; the
-//    two half-waves merge.  If the runner-up is further than a rigorous error bound tau
+//  * Each lane's 128 scores (8 tiles x 16 accumulator registers) are reduced over two
+//    partitions of that grid on the raw score bits (P: tile halves, Q: register pairs);
+//    their group minima give the smallest and second smallest score and the winner's
+//    cell (see `reduce`), and the two half-waves merge.  If the runner-up is further than a rigorous error bound tau
 //    from the winner the winner IS the fp32 direct-form argmin; otherwise (and for any
 //    non-finite input) the wave re-ranks all K centroids of that vector with the exact
 //    fp32 direct form and first-index tie break.
@@ -70,10 +71,33 @@ __device__ __forceinline__ unsigned med3u(unsigned a, unsigned b, unsigned c) {
     return r;
 }
 
+// v_min3_u32 of MFMA results.  The compiler's hazard recognizer does not look into inline
+// asm, so an asm read of an accumulator gets none of the wait states an MFMA result needs
+// (it would read stale values).  `after` is a compiler-generated value computed from the
+// same accumulator (its read got the wait states); as an extra operand it keeps this asm
+// behind that read, when the whole result is available.
+__device__ __forceinline__ unsigned min3d(unsigned a, unsigned b, unsigned c, unsigned after) {
+    unsigned r;
+    asm("v_min3_u32 %0, %1, %2, %3 ; after %4" : "=v"(r) : "v"(a), "v"(b), "v"(c), "v"(after));
+    return r;
+}
+
 __device__ __forceinline__ unsigned min3u(unsigned a, unsigned b, unsigned c) {
     unsigned r;
     asm("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
+}
+
+// Smallest and second smallest of 8 distinct keys (10 VALU): two triples and a pair give
+// their (min, second); every key but the overall minimum is >= one of the three seconds or
+// is the second smallest of the three minima, and each of those is a key other than the
+// minimum, so their minimum is the second key.
+__device__ __forceinline__ void top2_8(const unsigned* k, unsigned& m1, unsigned& m2) {
+    const unsigned a1 = min3u(k[0], k[1], k[2]), a2 = med3u(k[0], k[1], k[2]);
+    const unsigned b1 = min3u(k[3], k[4], k[5]), b2 = med3u(k[3], k[4], k[5]);
+    const unsigned c1 = min(k[6], k[7]), c2 = max(k[6], k[7]);
+    m1 = min3u(a1, b1, c1);
+    m2 = min(min3u(a2, b2, c2), med3u(a1, b1, c1));
 }
 
 // main-layout B slot value for vector-side quantities
@@ -381,6 +405,9 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     // the last, partial block clamps its rows (to n - 1), on a wave-uniform branch.
     const float* const xlane = x + (long long)r * ldx + (long long)m * D + (HALF ? 8 * h : 0);
     auto load_x = [&](long long b, float* dst) {
+#ifdef PQH_ASSIGN_NOMEM   // diagnostic: every chunk re-reads the first 64 blocks (cache hits)
+        b &= 63;
+#endif
         const float* xp;
         if (b * 32 + 32 <= n) {
             xp = xlane + b * 32 * ldx;
@@ -427,51 +454,52 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
             valid[b] = v[b] < n;   // rows past n hold row n - 1 (clamped loads), never stored
             make_b<D, LO>(xs[b], screen_bias(X[b], finite_x[b], cmb), h, Bm[b], Bl[b]);
         }
-        // Keys: float bits with the low 6 mantissa bits replaced by (t mod 4, accumulator
-        // register i); tiles 0-3 and 4-7 keep separate running (min, second-min) pairs, so a
-        // key names its centroid.  (The and-mask sits in an SGPR and the or-value is an
-        // inline constant below 64: one v_and_or_b32 per value.)  Values go in groups of
-        // three: the group's top two by min3/med3, then (m1, m2) <- (min(m1, g1), med3(m1,
-        // g1, min(m2, g2))).
-        unsigned m1[kNB][2], m2[kNB][2];
-#pragma unroll
-        for (int b = 0; b < kNB; ++b)
-#pragma unroll
-            for (int g = 0; g < 2; ++g) { m1[b][g] = 0xFFFFFFFFu; m2[b][g] = 0xFFFFFFFFu; }
+        // The lane's 128 scores of a block form an 8 x 16 grid: tile t (row) x accumulator
+        // register i (column).  Instead of ranking every score with its index attached, two
+        // partitions of the grid are reduced on the raw score bits:
+        //   P-groups (t, g): the 8 registers i in [8g, 8g + 8) of tile t -- 16 minima;
+        //   Q-groups j:      registers j and j + 8 of every tile        -- 8 running minima.
+        // A P-group and a Q-group share exactly one cell, so the smallest and second
+        // smallest score of the lane are
+        //   S1 = min P = min Q,   S2 = min(second min P, second min Q)
+        // (if the runner-up shares the winner's P-group it lies in another Q-group, and vice
+        // versa), and the winner's cell is (argmin P, argmin Q).  A score is touched by one
+        // min3 of each partition -- 1 VALU per score instead of 2.25 for keys + tournament --
+        // and only the 24 group minima get index bits (the winner's P-group in the low 4
+        // bits, its Q-group in the low 3).
+        unsigned pm1[kNB], pm2[kNB], qg[kNB][8];
         auto load_a = [&](int t, bf16x8* a) {
 #pragma unroll
             for (int p = 0; p < P::PA; ++p)
                 a[p] = *reinterpret_cast<const bf16x8*>(&As[(p * kTiles + t) * 64 + lane]);
         };
-        // A tile's 16 keys by a two-level tournament of triples (36 VALU instead of 43):
-        //   level 1: five triples -> (g1, g2) = (min3, med3); G2 = the smallest g2;
-        //   level 2: the five g1 and key 15 as two triples -> (h1a, h2a), (h1b, h2b);
-        //   then m1' = min3(m1, h1a, h1b) and m2' = min3(m2, min3(G2, h2a, h2b),
-        //   med3(m1, h1a, h1b)).  Every key but the overall minimum is >= one of the
-        //   candidates of m2' (a key is a triple's minimum or >= its triple's second), and
-        //   every candidate is a key other than the minimum, so m2' is the exact second
-        //   smallest key.
         auto reduce = [&](const f32x16& acc, int t, int b) {
-            const int g = t >> 2;
-            unsigned kk[16];
+            unsigned a[16];
 #pragma unroll
-            for (int i = 0; i < 16; ++i)
-                kk[i] = (__float_as_uint(acc[i]) & ~63u) | (unsigned)(((t & 3) << 4) | i);
-            unsigned g1[5], g2[5];
-            auto tri = [&](int q) {
-                g1[q] = min3u(kk[3 * q], kk[3 * q + 1], kk[3 * q + 2]);
-                g2[q] = med3u(kk[3 * q], kk[3 * q + 1], kk[3 * q + 2]);
-            };
-            // (in this order, so few partial results are live at once)
-            tri(0); tri(1); tri(2);
-            const unsigned G2a = min3u(g2[0], g2[1], g2[2]);
-            const unsigned h1a = min3u(g1[0], g1[1], g1[2]), h2a = med3u(g1[0], g1[1], g1[2]);
-            tri(3); tri(4);
-            const unsigned G2 = min3u(G2a, g2[3], g2[4]);
-            const unsigned h1b = min3u(g1[3], g1[4], kk[15]), h2b = med3u(g1[3], g1[4], kk[15]);
-            const unsigned s = med3u(m1[b][g], h1a, h1b);
-            m1[b][g] = min3u(m1[b][g], h1a, h1b);
-            m2[b][g] = min3u(m2[b][g], min3u(G2, h2a, h2b), s);
+            for (int i = 0; i < 16; ++i) a[i] = __float_as_uint(acc[i]);
+            // P: the tile's two group minima, keyed (P-group index 2t + g in the low 4 bits)
+            // and folded into the running top two of the P keys
+            // (e0, e1: the compiler-generated first reads of the tile's results, see min3d)
+            const unsigned e0 = min(a[6], a[7]), e1 = min(a[14], a[15]);
+            const unsigned k0 =
+                (min3u(min3d(a[0], a[1], a[2], e0), min3d(a[3], a[4], a[5], e0), e0) & ~15u) |
+                (unsigned)(2 * t);
+            const unsigned k1 =
+                (min3u(min3d(a[8], a[9], a[10], e1), min3d(a[11], a[12], a[13], e1), e1) & ~15u) |
+                (unsigned)(2 * t + 1);
+            if (t == 0) {
+                pm1[b] = min(k0, k1);
+                pm2[b] = max(k0, k1);
+            } else {
+                pm2[b] = med3u(pm1[b], pm2[b], k0);
+                pm1[b] = min(pm1[b], k0);
+                pm2[b] = med3u(pm1[b], pm2[b], k1);
+                pm1[b] = min(pm1[b], k1);
+            }
+            // Q: running minima of the register pairs (j, j + 8)
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                qg[b][j] = t == 0 ? min(a[j], a[j + 8]) : min3d(qg[b][j], a[j], a[j + 8], e1);
         };
         // Software pipeline over the tiles: block b's MFMA chain for tile t + 1 is issued
         // right after its tile-t keys are reduced, so it runs while the other block's keys
@@ -493,11 +521,17 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         }
 #pragma unroll
         for (int b = 0; b < kNB; ++b) {
-            // the lane's 128 centroids: merge the two tile groups ...
-            const unsigned a1 = m1[b][0], c1 = m1[b][1];
-            const unsigned own1 = min(a1, c1);
-            const unsigned own2 = min(min(m2[b][0], m2[b][1]), max(a1, c1));
-            const int wt = (c1 < a1 ? 4 : 0) | (int)((own1 >> 4) & 3u);
+            // the lane's 128 centroids: keyed group minima, top two of each partition ...
+            unsigned qk[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) qk[j] = (qg[b][j] & ~7u) | (unsigned)j;
+            const unsigned p1 = pm1[b], p2 = pm2[b];
+            unsigned q1, q2;
+            top2_8(qk, q1, q2);
+            const unsigned own1 = p1;
+            const unsigned own2 = min(p2, q2);
+            const int wt = (int)((p1 & 15u) >> 1);
+            const int wi = (int)(q1 & 7u) + 8 * (int)(p1 & 1u);
             // ... then the two half-waves (lanes l and l^32 hold the same vector): after the
             // swap, s[0] holds the lower half's value and s[1] the upper half's, in every lane
             const auto s1 = __builtin_amdgcn_permlane32_swap(own1, own1, false, false);
@@ -506,10 +540,12 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
             const unsigned b2 = min(min((unsigned)s2[0], (unsigned)s2[1]),
                                     max((unsigned)s1[0], (unsigned)s1[1]));
             const bool mine = own1 == b1;   // this half holds the winner (both: a tie -> slow)
-            int code = tile_row(wt, (int)(own1 & 15u), h);
+            int code = tile_row(wt, wi, h);
             const float tau = screen_tau(X[b], any_lo[b], tq);
-            const float K1 = __uint_as_float(b1 & ~63u), K2 = __uint_as_float(b2 & ~63u);
-            const bool slow = !(K2 - K1 > fmaf(0x1p-15f, K2, tau)) || !finite_x[b];
+            // a key differs from its score by less than 16 ulp (2^-19 relative): 2^-17 K2
+            // covers both keys of the gap
+            const float K1 = __uint_as_float(b1), K2 = __uint_as_float(b2);
+            const bool slow = !(K2 - K1 > fmaf(0x1p-17f, K2, tau)) || !finite_x[b];
 
             unsigned long long need = __ballot(slow && valid[b] && h == 0);
             bool deferred = false;
