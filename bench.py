@@ -94,15 +94,22 @@ def parse():
                          "multi-rank schedule with every rank on one GPU, --one-device)")
     ap.add_argument("--one-device", action="store_true",
                     help="every rank uses GPU 0 (schedule rehearsal on a one-GPU box)")
+    ap.add_argument("--dump", default="",
+                    help="write the last batch's stitched stream and all ranks' codes to this "
+                         ".npz on rank 0 (parity tests)")
     ap.add_argument("--table-cus", type=int, default=0,
                     help="limit each lane stream to this many CUs (0: no CU mask)")
     return ap.parse_args()
 
 
+GEN_CHUNK = 4_000_000   # rows generated at a time (a 125M-row shard is 64 GB)
+
+
 def make_data(torch, n, d, seed, rank, device):
     """SIFT-like synthetic shard generated on the device: integer-valued floats in [0,255]
     from a Gaussian mixture with Zipf(1.1) weights.  Mixture centres
-    come from `seed` (shared by all ranks), rows from (seed, rank)."""
+    come from `seed` (shared by all ranks), rows from (seed, rank) in chunks of GEN_CHUNK
+    rows (chunk c > 0 reseeded with c), so a shard of any size is generated in place."""
     g = torch.Generator(device=device)
     g.manual_seed(seed)
     centers = 1024
@@ -111,10 +118,15 @@ def make_data(torch, n, d, seed, rank, device):
     mu = mu.to(device)
     w = 1.0 / torch.arange(1, centers + 1, dtype=torch.float64) ** 1.1
     w = (w / w.sum()).to(device)
-    g.manual_seed(seed * 1000003 + rank)
-    lab = torch.multinomial(w, n, replacement=True, generator=g)
-    x = mu[lab] + 12.0 * torch.randn((n, d), generator=g, device=device)
-    return torch.clamp(torch.round(x), 0, 255).contiguous()
+    x = torch.empty((n, d), dtype=torch.float32, device=device)
+    for c, r0 in enumerate(range(0, n, GEN_CHUNK)):
+        r1 = min(n, r0 + GEN_CHUNK)
+        g.manual_seed(seed * 1000003 + rank + c * 7919 * 1000003)
+        lab = torch.multinomial(w, r1 - r0, replacement=True, generator=g)
+        xc = mu[lab] + 12.0 * torch.randn((r1 - r0, d), generator=g, device=device)
+        x[r0:r1] = torch.clamp(torch.round(xc), 0, 255)
+        del lab, xc
+    return x
 
 
 def train_centroids(torch, x, m, k, iters=4, sample=50_000, seed=7):
@@ -141,12 +153,11 @@ def train_centroids(torch, x, m, k, iters=4, sample=50_000, seed=7):
     return out.numpy()
 
 
-def cpu_baseline(x_host, cent, ctxm, sample):
-    """The reference CPU path (oracle restatement, single thread) on a bounded sample."""
-    from oracle import oracle_ctypes as orc
-    xs = np.ascontiguousarray(x_host[:sample])
+def cpu_leg(orc, xs, cent, ctxm, threads):
+    """One timed pass of the CPU path on xs: assign (threads) + histogram + codebooks +
+    bit-serial encode + trie decode (single thread, as the reference's Huffman half)."""
     t0 = time.perf_counter()
-    codes, _ = orc.pq_assign(xs, cent, threads=1)
+    codes, _ = orc.pq_assign(xs, cent, threads=threads)
     t1 = time.perf_counter()
     cbs = orc.build_codebooks(codes, 256, ctxm)
     stream, bits = orc.encode(codes, cbs)
@@ -154,13 +165,62 @@ def cpu_baseline(x_host, cent, ctxm, sample):
     dec = orc.decode(stream, len(codes), codes.shape[1], cbs)
     t3 = time.perf_counter()
     assert np.array_equal(dec, codes)
-    return {"value": round(sample / (t3 - t0) / 1e6, 4), "unit": "Mvec/s", "cores": 1,
-            "kind": "port",
-            "sample": f"{sample} vectors of the rank-0 shard, M=8 K=256 "
-                      f"{'context' if ctxm else 'non-context'}: oracle assign + histogram + "
-                      f"codebooks + bit-serial encode + trie decode, single thread -O2",
+    return {"value": round(len(xs) / (t3 - t0) / 1e6, 4),
             "stages_s": {"assign": round(t1 - t0, 3), "encode": round(t2 - t1, 3),
                          "decode": round(t3 - t2, 3)}}
+
+
+def cpu_baseline(x_host, cent, ctxm, sample):
+    """The reference CPU path (the oracle: a byte-exact restatement of the reference) on
+    bounded samples of the shard, on this host:
+      1 thread -O2 (the headline `value`), all granted threads -O2 (OpenMP over rows for the
+      assignment; the Huffman half stays single-threaded like the reference's), and 1 thread
+      at the reference's as-shipped -O0 -g (src/Makefile:9) on a quarter of the sample."""
+    from oracle import oracle_ctypes as orc
+    xs = np.ascontiguousarray(x_host[:sample])
+    # the host cores this process may use (the GPU box grants a share of the machine and
+    # sets OMP_NUM_THREADS to it)
+    threads = int(os.environ.get("OMP_NUM_THREADS") or len(os.sched_getaffinity(0)))
+    orc.use_build("O2")
+    one = cpu_leg(orc, xs, cent, ctxm, 1)
+    allc = cpu_leg(orc, xs, cent, ctxm, threads)
+    q = max(1, sample // 4)
+    orc.use_build("O0")
+    o0 = cpu_leg(orc, np.ascontiguousarray(xs[:q]), cent, ctxm, 1)
+    orc.use_build("O2")
+    mode = "context" if ctxm else "non-context"
+    return {"value": one["value"], "unit": "Mvec/s", "cores": 1, "kind": "port",
+            "sample": f"{sample} vectors of the rank-0 shard, M=8 K=256 {mode}: oracle assign "
+                      f"+ histogram + codebooks + bit-serial encode + trie decode, single "
+                      f"thread -O2",
+            "stages_s": one["stages_s"],
+            "legs": [
+                dict(one, cores=1, build="-O2", sample=sample),
+                dict(allc, cores=threads, build="-O2", sample=sample,
+                     note="OpenMP assignment over rows; Huffman half single-threaded"),
+                dict(o0, cores=1, build="-O0 -g (as shipped)", sample=q)]}
+
+
+def pcie_ms(torch, x, codes, stream_bytes):
+    """PCIe-inclusive costs reported beside `value` (never part of it): pinned H2D of the
+    vectors, D2H of their codes and of their stream bytes, for a 1M-row
+    slice of the shard (the whole SIFT1M-shaped shard)."""
+    hx = torch.empty(x.shape, dtype=x.dtype, pin_memory=True)
+    hc = torch.empty(codes.shape, dtype=codes.dtype, pin_memory=True)
+    hs = torch.empty(int(stream_bytes), dtype=torch.uint8, pin_memory=True)
+    dsb = torch.empty(int(stream_bytes), dtype=torch.uint8, device=x.device)
+    out = {}
+    for name, fn in (("h2d_vectors", lambda: x.copy_(hx, non_blocking=True)),
+                     ("d2h_codes", lambda: hc.copy_(codes, non_blocking=True)),
+                     ("d2h_stream", lambda: hs.copy_(dsb, non_blocking=True))):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        out[name] = round((time.perf_counter() - t0) / 3 * 1e3, 3)
+    return out
 
 
 def main():
@@ -210,7 +270,10 @@ def main():
            if args.a_priority else codec.Context(local))
     sA = ctx.stream
     nl = 1 if serial else max(1, args.lanes)
-    # (cus >= the device's CU count: a library stream of its own without a CU mask)
+    # Lane streams are the library's own (pqh_ctx_create_cu_split; cus >= the device's CU
+    # count: no CU mask).  (torch.cuda.Stream lanes measured 1,107 vs 2,250 Mvec/s: torch's
+    # stream pool maps them onto the hardware queues of its other streams.)  Tensors used on
+    # them are released before the contexts destroy them (teardown below).
     lanes = [ctx] if serial else [codec.Context(local, cus=args.table_cus or 1 << 20)
                                   for _ in range(nl)]
     # encode + decode streams: the table lanes themselves, or --elanes streams of their own
@@ -346,6 +409,7 @@ def main():
                 # all-gather + prefix sum on the device, offset read by the kernel (no host sync)
                 total = codec.encode_size(c, tj, codes[s], raw_first, halo[s])
                 goff, _ = shard.bit_offsets_device(total, world, rank)
+                state["goff"] = goff
                 out[j][:4].zero_()   # bits before the offset belong to the previous shard
                 acc["collectives"] += time.perf_counter() - tc if state["timed"] else 0.0
                 codec.encode_write_at(c, tj, codes[s], out[j], goff, raw_first, halo[s],
@@ -411,6 +475,22 @@ def main():
     rerank = pq.rerank_count(ctx)
     bits_per_vec = int(tot_dev[j_last].item()) / n
 
+    if args.dump:   # the last batch's shard stream + codes, gathered to rank 0 (tests)
+        nb = (int(tot_dev[j_last].item()) + 7) // 8 + 8
+        goff = int(state["goff"].item()) if world > 1 else 0
+        mine = {"codes": codes[s_last].cpu().numpy(), "bits": int(tot_dev[j_last].item()),
+                "goff": goff, "buf": out[j_last][:nb].cpu().numpy()}
+        allp = [None] * world
+        if world > 1:
+            dist.all_gather_object(allp, mine)
+        else:
+            allp = [mine]
+        if rank == 0:
+            total = sum(p["bits"] for p in allp)
+            stitched = shard.stitch_np([(p["buf"], p["goff"], p["bits"]) for p in allp], total)
+            np.savez(args.dump, stream=stitched, bits=np.int64(total),
+                     codes=np.concatenate([p["codes"] for p in allp]))
+
     if rank == 0:
         t_assign = acc["assign"] / args.steps
         achieved = (BYTES_PER_VEC_READ + BYTES_PER_VEC_WRITE) * n / t_assign / 1e9
@@ -471,15 +551,25 @@ def main():
             "bits_per_vector": round(bits_per_vec, 3),
             "rerank_fraction": round(rerank / (n * m), 6),
         }
+        if world == 1:
+            # (after the timed region, on a scratch copy of a 1M-row slice)
+            r1 = min(n, 1_000_000)
+            res["pcie_ms"] = pcie_ms(torch, x[:r1].clone(), codes[s_last][:r1],
+                                     (bits_per_vec * r1 + 7) // 8)
+            res["pcie_ms"]["rows"] = r1
         if not args.no_cpu_baseline and world == 1:
             xh = x[:args.cpu_sample].cpu().numpy()
             res["cpu_baseline"] = cpu_baseline(xh, cent, ctxm, args.cpu_sample)
             res["cpu_baseline"]["host_cpu"] = _cpu_name()
             res["cpu_baseline"]["nproc"] = os.cpu_count()
         print(json.dumps(res), flush=True)
-    # teardown in a fixed order while HIP is alive (tables, codebook, contexts), rather than
-    # in whatever order the interpreter's exit happens to collect them
+    # Teardown in a fixed order while HIP is alive.  The halo rows were used on the lane
+    # streams (record_stream): torch's allocator records an event on those streams when such
+    # a tensor is freed, so they are freed -- and the allocator's events drained -- while the
+    # streams exist; then tables, codebook and contexts (which destroy the lane streams).
+    halo[:] = [None] * slots
     torch.cuda.synchronize()
+    torch.cuda.empty_cache()
     for t in tabs:
         t.close()
     pq.close()
@@ -488,11 +578,6 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-        # (a rank once died with SIGSEGV in the interpreter's exit after the last barrier in
-        # a gloo rehearsal; the results are out, so leave without further teardown)
-        sys.stdout.flush()
-        sys.stderr.flush()
-        os._exit(0)
 
 
 def _cpu_name():

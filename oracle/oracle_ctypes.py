@@ -13,7 +13,9 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _ROOT = os.path.dirname(_HERE)
 _LIB = os.path.join(_HERE, "_build", "liboracle.so")
+_LIB_O0 = os.path.join(_HERE, "_build", "liboracle_O0.so")   # -O0 -g (the reference's build)
 _lib = None
+_libs = {}
 
 P, I, LL = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong
 
@@ -25,9 +27,24 @@ def build() -> None:
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(_LIB):
+        _lib = _load(_LIB)
+    return _lib
+
+
+def use_build(opt: str) -> None:
+    """Route this module's functions to the -O2 (default) or the -O0 -g build."""
+    global _lib
+    path = _LIB_O0 if opt == "O0" else _LIB
+    if path not in _libs:
+        _libs[path] = _load(path)
+    _lib = _libs[path]
+
+
+def _load(path):
+    if True:
+        if not os.path.exists(path):
             build()
-        L = ctypes.CDLL(_LIB)
+        L = ctypes.CDLL(path)
         L.orc_codebook.argtypes = [I, I, P, P, P, I]
         L.orc_codebook.restype = I
         L.orc_codebook_serialize.argtypes = [I, I, P, P, I, P, LL]
@@ -56,8 +73,8 @@ def lib():
         L.orc_tree_encode.argtypes = [P, LL, I, I, P, P, P, P, I, P, LL]
         L.orc_tree_encode.restype = LL
         L.orc_bitstream_write.restype = LL
-        _lib = L
-    return _lib
+        _libs[path] = L
+        return L
 
 
 def bitstream_write(data: np.ndarray, lens: np.ndarray) -> bytes:

@@ -1,0 +1,129 @@
+"""Full-size parity of the exact path behind the bench line, and configs[2]'s per-rank
+shard on one GPU.
+
+The bench step (bench.py) is pq_assign (MFMA screen + exact re-rank) -> pqh_histogram_set
+-> pqh_tables_build (GPU heap simulation) -> pqh_encode_write (one pass, chunk index) ->
+pqh_decode (chunked).  Here the same calls, on the bench's own data generator and
+centroids, are compared with the CPU oracle on every row:
+  * all 1,000,000 PQ codes (oracle: fp32 direct form, first minimum -- SURVEY.md 8c),
+  * the codebook file bytes and the stream bytes (huffman_encoder.c:398-428),
+  * decode == codes (huffman_decoder.c:211-255),
+for SIFT-like integer data (bf16-exact: no lo pass) and for Deep-like unit-norm data (every
+x has a bf16 remainder: the lo pass and its tighter bound are active).
+
+configs[2] (1B rows over 8 GPUs) is a 125M-row, 64 GB shard per rank: the shard is run on
+one GPU through the same calls; the round trip must be exact, the stream length must equal
+the codebook estimate, the GPU histogram and codebooks must equal the oracle's, and the PQ
+codes must equal the oracle's on sampled windows of rows."""
+import numpy as np
+import pytest
+
+import datagen
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    import torch
+    from pq_huffman_amd import codec
+    assert torch.cuda.is_available()
+    return torch, codec, codec.Context(0)
+
+
+def _bench_path(gpu, x, cent, chunk=8):
+    """the bench's per-batch calls, in its order, on one stream"""
+    torch, codec, ctx = gpu
+    n = x.shape[0]
+    m, k, _ = cent.shape
+    pq = codec.PQ(ctx, cent)
+    codes = torch.empty((n, m), dtype=torch.uint8, device=x.device)
+    pq.assign(x, codes)
+    counts = torch.empty((m, k * k), dtype=torch.int32, device=x.device)
+    codec.histogram(ctx, codes, k, True, counts=counts, accumulate=False)
+    tabs = codec.Tables(ctx, m, k, True).build(counts)
+    chunks = (n + chunk - 1) // chunk
+    out = torch.empty(n * m * 56 // 8 + 64, dtype=torch.uint8, device=x.device)
+    coff = torch.empty(chunks, dtype=torch.int64, device=x.device)
+    cprev = torch.empty((chunks, m), dtype=torch.uint8, device=x.device)
+    tot = torch.zeros(1, dtype=torch.int64, device=x.device)
+    codec.encode_write(ctx, tabs, codes, out, 0, 1, None, chunk, coff, cprev, total=tot)
+    codec.encode_status(ctx)
+    enc = codec.Encoded(out, int(tot.item()), chunk, coff, cprev, n, 1)
+    dec = codec.decode(ctx, tabs, enc)
+    codec.decode_status(ctx)
+    tabs.status()
+    return pq, codes, counts, tabs, enc, dec
+
+
+def _check_against_oracle(gpu, oracle, xh, cent, codes, tabs, enc, dec):
+    torch, codec, ctx = gpu
+    assert torch.equal(dec, codes)
+    hc = codes.cpu().numpy()
+    want, _ = oracle.pq_assign(xh, cent, threads=0)
+    bad = int((hc != want).sum())
+    assert bad == 0, f"{bad} PQ codes differ from the oracle"
+    ocb = oracle.build_codebooks(want, cent.shape[1], True)
+    assert tabs.codebooks().file_bytes() == oracle.codebooks_file(ocb)
+    stream, bits = oracle.encode(want, ocb)
+    assert enc.bits == bits
+    assert enc.stream[:len(stream)].cpu().numpy().tobytes() == stream
+
+
+def test_bench_path_sift1m_all_rows(gpu, oracle):
+    import bench
+    torch, codec, ctx = gpu
+    dev = torch.device("cuda", 0)
+    x = bench.make_data(torch, 1_000_000, 128, 0x5EED, 0, dev)
+    cent = bench.train_centroids(torch, bench.make_data(torch, 200_000, 128, 0x5EED, 0, dev),
+                                 8, 256)
+    pq, codes, counts, tabs, enc, dec = _bench_path(gpu, x, cent)
+    assert pq.rerank_count() > 0
+    _check_against_oracle(gpu, oracle, x.cpu().numpy(), cent, codes, tabs, enc, dec)
+
+
+def test_bench_path_deep1m_all_rows(gpu, oracle):
+    """configs[3] shape (96-d, M = 16, dsub = 6) on 1M non-integer rows: the lo pass."""
+    torch, codec, ctx = gpu
+    xh = datagen.deep_like(1_000_000, 96, seed=31)
+    assert (xh.view(np.uint32) & 0xFFFF).any(axis=1).all()   # every row has a remainder
+    cent = datagen.lloyd_centroids(xh, 16, 256, iters=2, sample=30000, seed=5)
+    x = torch.from_numpy(xh).cuda()
+    pq, codes, counts, tabs, enc, dec = _bench_path(gpu, x, cent)
+    _check_against_oracle(gpu, oracle, xh, cent, codes, tabs, enc, dec)
+
+
+def test_configs2_shard_125m_rows(gpu, oracle):
+    """BASELINE.json configs[2]: the per-rank shard (1e9 / 8 = 125M rows x 128-d, 64 GB)."""
+    import bench
+    torch, codec, ctx = gpu
+    dev = torch.device("cuda", 0)
+    n = 125_000_000
+    x = bench.make_data(torch, n, 128, 0x5EED, 3, dev)
+    cent = bench.train_centroids(torch, bench.make_data(torch, 200_000, 128, 0x5EED, 0, dev),
+                                 8, 256)
+    pq, codes, counts, tabs, enc, dec = _bench_path(gpu, x, cent, chunk=64)
+    assert torch.equal(dec, codes)
+    hc = codes.cpu().numpy()
+    ch = codec.counts_to_host(counts)
+    assert np.array_equal(ch, oracle.histogram(hc, 256, True).reshape(ch.shape))
+    cbs = tabs.codebooks(ch)
+    assert int(cbs.estimate().sum()) + 8 * 8 == enc.bits        # + row 0 raw
+    ocb = oracle.build_codebooks(hc, 256, True)
+    assert cbs.file_bytes() == oracle.codebooks_file(ocb)
+    # PQ codes on windows: the first rows, rows around 2^26 and 2^31 / 32 blocks, the last
+    for lo in (0, (1 << 26) - 50_000, 67_108_864 - 7, n - 100_000):
+        w = slice(lo, lo + 100_000)
+        want, _ = oracle.pq_assign(x[w].cpu().numpy(), cent, threads=0)
+        assert np.array_equal(hc[w], want), lo
+    # stream bits on a window: the oracle encodes rows [a - 1, b) -- row a - 1 raw, rows
+    # [a, b) in context -- and the chunk index places rows [a, b) in the GPU stream
+    a = (n // 2) // 64 * 64
+    b = a + 200_000
+    start = int(enc.chunk_offsets[a // 64].item())
+    stop = int(enc.chunk_offsets[b // 64].item())
+    ostream, obits = oracle.encode(np.ascontiguousarray(hc[a - 1:b]), ocb)
+    assert obits - 8 * 8 == stop - start
+    gbytes = enc.stream[start // 8:(stop + 7) // 8 + 1].cpu().numpy()
+    gbits = np.unpackbits(gbytes)[start % 8:start % 8 + (stop - start)]
+    assert np.array_equal(gbits, np.unpackbits(np.frombuffer(ostream, np.uint8))[64:obits])
