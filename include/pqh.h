@@ -241,7 +241,9 @@ long long pqh_tree_ext_index(long long n, const int* num_children, int chunk_vec
 /* huffman_decoder --tree on the GPU: rows in stream order.  One lane per chunk (offsets
  * from pqh_encode_tree_write); a context inside the chunk is read from the chunk's own
  * decoded rows, one before it from d_ext_rows[d_ext_offsets[j]...] (m codes each, the rows
- * at ext_positions).  Errors are reported by pqh_decode_status. */
+ * at ext_positions).  stream_bytes is the stream's exact length (d_stream readable up to the
+ * next multiple of 4 bytes); a chunk whose offset or symbols pass stream_bytes * 8 bits (a
+ * truncated file, a stale sidecar) is an error.  Errors are reported by pqh_decode_status. */
 int pqh_decode_tree(pqh_ctx_t* ctx, const pqh_tables_t* t, const unsigned char* d_stream,
                     unsigned long long stream_bytes, long long n, int chunk_vectors,
                     const unsigned long long* d_chunk_offsets, const long long* d_parent_pos,

@@ -230,7 +230,7 @@ def bitstream_fixture(lib, tmp):
     """Reference writer with tiny buffers (mid-stream flush path) on random writes."""
     rng = np.random.default_rng(5)
     arrays = {}
-    for buf in (2, 3, 64):  # 1-byte buffers loop forever in the reference (bitstream.c:355-358)
+    for buf in (2, 3, 64):  # 1-byte buffers loop forever in the reference (bitstream.c:131-147)
         lens = rng.integers(0, 40, 300).astype(np.int64)
         data = b"".join(bytes(rng.integers(0, 256, (int(L) + 7) // 8, dtype=np.uint8)) for L in lens)
         dbuf = np.frombuffer(data, np.uint8).copy()

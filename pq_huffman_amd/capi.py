@@ -47,6 +47,12 @@ class HuffmanStats(ctypes.Structure):             # stats.h huffman_stats_t
                 ("partial_lengths", ctypes.POINTER(D)), ("num_roots", I)]
 
 
+class Block(ctypes.Structure):                    # fast_nn_block.h block_t
+    _fields_ = [("id", ctypes.c_longlong), ("num_dimensions", ctypes.c_int),
+                ("capacity", ctypes.c_longlong), ("indices", ctypes.POINTER(ctypes.c_longlong)),
+                ("data", ctypes.POINTER(ctypes.c_float)), ("size", ctypes.c_longlong)]
+
+
 class EncodeOptions(ctypes.Structure):            # pqh.h pqh_encode_options_t
     _fields_ = [("context", I), ("sort", I), ("chunk_vectors", I), ("only_estimate", I)]
 

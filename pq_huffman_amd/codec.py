@@ -547,11 +547,14 @@ def tree_encode(ctx: Context, codes, targets, counts, chunk_vectors: int = 16) -
                        coff, ext_rows)
 
 
-def tree_decode(ctx: Context, enc: TreeEncoded, tables: Tables = None, out=None):
+def tree_decode(ctx: Context, enc: TreeEncoded, tables: Tables = None, out=None,
+                stream_bytes: int = None):
     """huffman_decoder --tree on the GPU (huffman_decoder.c:214-247): the children stream
     first (GPU decode of its non-context book), then the host traverser over the decoded
     child counts, then one lane per chunk with the encoder's sidecar.  Rows come back in
-    stream (DFS) order, as the reference decoder writes them."""
+    stream (DFS) order, as the reference decoder writes them.  stream_bytes (default: the
+    encoded length) bounds the bits the decoder may consume: a stream shorter than its
+    sidecar says raises PqhError (PQH_ERR_CORRUPT)."""
     torch = _torch()
     t = tables or enc.tables
     ctab = Tables.from_codebooks(ctx, enc.children_codebook)
@@ -564,7 +567,8 @@ def tree_decode(ctx: Context, enc: TreeEncoded, tables: Tables = None, out=None)
         out = torch.empty((enc.n, t.m), dtype=torch.uint8, device=dev)
     d_pp = torch.from_numpy(pp).to(dev)
     d_eo = torch.from_numpy(eo).to(dev)
-    check(lib().pqh_decode_tree(ctx.ptr, t.ptr, _ptr(enc.stream), enc.stream.numel(), enc.n,
+    nb = enc.nbytes if stream_bytes is None else stream_bytes
+    check(lib().pqh_decode_tree(ctx.ptr, t.ptr, _ptr(enc.stream), nb, enc.n,
                                 enc.chunk_vectors, _ptr(enc.chunk_offsets), _ptr(d_pp),
                                 _ptr(d_eo), _ptr(enc.ext_rows), _ptr(out)), "pqh_decode_tree")
     decode_status(ctx)

@@ -355,9 +355,17 @@ extern "C" int pqh_encode_tree_files(const unsigned char* codes, long long n, in
     huffman_codebook_encode_init(&ccb, alphabet, ccounts.data());
     {
         FILE* f = fopen(path_of(out_prefix, "huffman_children_codebooks.bin").c_str(), "wb");
+        bool ok = f != nullptr;
         if (f) {
             huffman_codebook_save(&ccb, f);
-            fclose(f);
+            ok = !ferror(f);
+            ok = fclose(f) == 0 && ok;
+        }
+        if (!ok) {
+            for (auto& cb : cbs) huffman_codebook_destroy(&cb);
+            huffman_codebook_destroy(&ccb);
+            pqh_tables_destroy(tab);
+            return pqh_set_error(ctx, PQH_ERR_ARG, "cannot write huffman_children_codebooks.bin");
         }
         huffman_stats_t cst;
         huffman_stats_init(&cst, n, 1, k);
@@ -379,13 +387,20 @@ extern "C" int pqh_encode_tree_files(const unsigned char* codes, long long n, in
     huffman_stats_print_filename(&st, path_of(out_prefix, "huffman_stats.txt").c_str());
     huffman_stats_destroy(&st);
     FILE* cf = fopen(path_of(out_prefix, "huffman_codebooks.bin").c_str(), "wb");
+    bool cf_ok = cf != nullptr;
     if (cf) {
         uint32_t mu = (uint32_t)m;
-        fwrite(&mu, 4, 1, cf);
+        cf_ok = fwrite(&mu, 4, 1, cf) == 1;
         for (int i = 0; i < m; ++i) huffman_codebook_save(&cbs[i], cf);
-        fclose(cf);
+        cf_ok = !ferror(cf) && cf_ok;
+        cf_ok = fclose(cf) == 0 && cf_ok;
     }
     for (auto& cb : cbs) huffman_codebook_destroy(&cb);
+    if (!cf_ok) {
+        huffman_codebook_destroy(&ccb);
+        pqh_tables_destroy(tab);
+        return pqh_set_error(ctx, PQH_ERR_ARG, "cannot write huffman_codebooks.bin");
+    }
 
     // the row stream (encode_tree_data, huffman_encoder.c:240-286)
     const unsigned long long cap = ((unsigned long long)total_bits + 31) / 32 * 4 + 64;
@@ -457,7 +472,8 @@ extern "C" int pqh_encode_tree_files(const unsigned char* codes, long long n, in
     std::vector<long long> ep(ext + 1);
     pqh_tree_ext_index(n, nch.data(), kTreeFileChunk, pp.data(), eo.data(), ep.data());
     FILE* tsf = fopen(path_of(out_prefix, "huffman_tree_chunks.bin").c_str(), "wb");
-    if (tsf) {
+    if (!tsf) return pqh_set_error(ctx, PQH_ERR_ARG, "cannot write huffman_tree_chunks.bin");
+    {
         TreeSidecar h;
         memcpy(h.magic, "PQHT", 4);
         h.version = 1;
@@ -466,21 +482,25 @@ extern "C" int pqh_encode_tree_files(const unsigned char* codes, long long n, in
         h.n = n;
         h.chunks = chunks;
         h.ext = ext;
-        fwrite(&h, sizeof(h), 1, tsf);
-        fwrite(coff.data(), 8, chunks, tsf);
-        for (long long e = 0; e < ext; ++e) fwrite(rows.data() + ep[e] * m, 1, m, tsf);
-        fclose(tsf);
+        bool ok = fwrite(&h, sizeof(h), 1, tsf) == 1;
+        ok = (long long)fwrite(coff.data(), 8, chunks, tsf) == chunks && ok;
+        for (long long e = 0; e < ext && ok; ++e)
+            ok = fwrite(rows.data() + ep[e] * m, 1, m, tsf) == (size_t)m;
+        ok = fclose(tsf) == 0 && ok;
+        if (!ok) return pqh_set_error(ctx, PQH_ERR_ARG, "cannot write huffman_tree_chunks.bin");
     }
     FILE* ef = fopen(path_of(out_prefix, "huffman_indices.bin").c_str(), "wb");
     if (!ef) return pqh_set_error(ctx, PQH_ERR_ARG, "cannot write indices");
     unsigned long long nn = (unsigned long long)n;
-    fwrite(&nn, 8, 1, ef);
-    fwrite(stream.data(), 1, (bits + 7) / 8, ef);
-    fclose(ef);
+    bool wok = fwrite(&nn, 8, 1, ef) == 1;
+    wok = fwrite(stream.data(), 1, (bits + 7) / 8, ef) == (bits + 7) / 8 && wok;
+    wok = fclose(ef) == 0 && wok;
+    if (!wok) return pqh_set_error(ctx, PQH_ERR_ARG, "cannot write indices");
     FILE* chf = fopen(path_of(out_prefix, "huffman_children.bin").c_str(), "wb");
     if (!chf) return pqh_set_error(ctx, PQH_ERR_ARG, "cannot write children stream");
-    fwrite(cstream.data(), 1, (cbits + 7) / 8, chf);
-    fclose(chf);
+    wok = fwrite(cstream.data(), 1, (cbits + 7) / 8, chf) == (cbits + 7) / 8;
+    wok = fclose(chf) == 0 && wok;
+    if (!wok) return pqh_set_error(ctx, PQH_ERR_ARG, "cannot write children stream");
     return PQH_OK;
 }
 
@@ -598,7 +618,7 @@ extern "C" int pqh_decode_tree_files(const char* in_prefix, unsigned char** code
         PQH_HIP(ctx, hipMemcpyAsync(d_ext.p, sp + h.chunks * 8, h.ext * m, hipMemcpyHostToDevice, ctx->stream));
     PQH_HIP(ctx, hipMemcpyAsync(d_pp.p, pp.data(), n * 8, hipMemcpyHostToDevice, ctx->stream));
     PQH_HIP(ctx, hipMemcpyAsync(d_eo.p, eo.data(), (h.chunks + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
-    rc = pqh_decode_tree(ctx, tab, d_stream.p, stream.size(), (long long)n, C, d_coff.p, d_pp.p,
+    rc = pqh_decode_tree(ctx, tab, d_stream.p, bytes, (long long)n, C, d_coff.p, d_pp.p,
                          d_eo.p, d_ext.p, d_rows.p);
     if (!rc) rc = pqh_decode_status(ctx);
     if (rc) return fail(rc);

@@ -1266,7 +1266,7 @@ dec_tree(const uint32_t* __restrict__ words, long long nwords, long long n, int 
          const uint16_t* __restrict__ lut2, const uint32_t* __restrict__ meta, int w1,
          long long lut2_cap, const pqh_long_code* __restrict__ longs,
          const uint32_t* __restrict__ long_cnt, uint8_t* __restrict__ out,
-         unsigned long long* __restrict__ err) {
+         unsigned long long* __restrict__ err, unsigned long long total_bits) {
     extern __shared__ uint8_t tstage[];   // [64 lanes][C rows][m]
     const long long chunks = (n + chunk_vectors - 1) / chunk_vectors;
     const long long j = (long long)blockIdx.x * 64 + threadIdx.x;
@@ -1281,7 +1281,9 @@ dec_tree(const uint32_t* __restrict__ words, long long nwords, long long n, int 
     const long long e_end = ext_off[j + 1];
     int warm_bits = 1;
     while ((1 << warm_bits) < k) ++warm_bits;
-    bool ok = true;
+    // a chunk that starts past the stream's end (a truncated file or a stale sidecar) reads
+    // nothing; one whose symbols run past it is reported below -- never decoded silently
+    bool ok = chunk_off[j] <= total_bits;
     for (long long p = v0; p < v1 && ok; ++p) {
         const long long pp = parent_pos[p];
         const uint8_t* prow = nullptr;
@@ -1305,9 +1307,10 @@ dec_tree(const uint32_t* __restrict__ words, long long nwords, long long n, int 
             o[i] = (uint8_t)sym;
         }
     }
+    if (br.pos() > total_bits) ok = false;
     const long long nb = (v1 - v0) * m;
     uint8_t* dst = out + v0 * m;
-    for (long long q = 0; q < nb; ++q) dst[q] = st[q];
+    for (long long q = 0; q < nb; ++q) dst[q] = ok ? st[q] : 0;
     if (!ok) atomicOr(err, 1ull);
 }
 }  // namespace
@@ -1332,11 +1335,11 @@ int pqh_decode_tree(pqh_ctx_t* ctx, const pqh_tables_t* t, const unsigned char* 
         PQH_HIP(ctx, hipFuncSetAttribute((const void*)dec_tree,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(dec_tree, dim3((unsigned)((chunks + 63) / 64)), dim3(64), lds, ctx->stream,
-                       reinterpret_cast<const uint32_t*>(d_stream), (long long)(stream_bytes / 4),
+                       reinterpret_cast<const uint32_t*>(d_stream), (long long)((stream_bytes + 3) / 4),
                        n, t->m, t->k, chunk_vectors, d_chunk_offsets, d_parent_pos,
                        d_ext_offsets, d_ext_rows, t->d_lut1, t->d_lut2, t->d_meta, t->l1_bits,
                        t->lut2_cap, t->d_long, t->d_long_cnt, static_cast<uint8_t*>(d_rows),
-                       ctx->d_diag + 1);
+                       ctx->d_diag + 1, stream_bytes * 8ull);
     PQH_LAUNCH_CHECK(ctx);
     return PQH_OK;
 }

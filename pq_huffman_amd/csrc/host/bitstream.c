@@ -5,7 +5,7 @@
  * destroyed, read streams seek the file back over unread whole bytes on destroy, and
  * reading past the end prints "bit_stream: eof" and exits(1) (bitstream.c:159-162).
  * Writes move whole bytes with shifts instead of one bit per iteration
- * (bitstream.c:80-98); a 1-byte buffer no longer spins forever (bitstream.c:355-358
+ * (bitstream.c:80-98); a 1-byte buffer no longer spins forever (bitstream.c:131-147
  * computes a zero batch length there).
  */
 #include "bitstream.h"

@@ -1,6 +1,6 @@
 /* fast_nn_block.c -- drop-in for the reference's src/fast_nn_block.c:6-71 (block_t).
- * Difference: initial_capacity is honoured (the reference always starts at 100,
- * fast_nn_block.c:11); growth is (capacity + 1) * 2 as in :41-44. */
+ * Same observable behaviour: initial_capacity is ignored and every block starts with room
+ * for 100 rows (fast_nn_block.c:11); growth is (capacity + 1) * 2 (:41-44). */
 #include "fast_nn_block.h"
 
 #include <stdlib.h>
@@ -10,7 +10,8 @@ void block_init(block_t* block, long long block_id, int num_dimensions, long lon
                 int init_flags) {
     block->id = block_id;
     block->num_dimensions = num_dimensions;
-    block->capacity = initial_capacity > 0 ? initial_capacity : 100;
+    (void)initial_capacity;   /* ignored, as in the reference */
+    block->capacity = 100;
     block->size = 0;
     block->data = (init_flags & BLOCK_INIT_WITH_DATA)
                       ? (float*)malloc(sizeof(float) * num_dimensions * block->capacity)

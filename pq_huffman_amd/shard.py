@@ -232,30 +232,43 @@ def library_sort(ctx):
     return run
 
 
-def halo_ragged(last_row, world: int, rank: int, group=None):
+def halo_ragged(last_row, world: int, rank: int, group=None, device=None, dtype=None):
     """exchange_halo for shards that may be empty (sorted slices): `last_row` is the (m,)
     last row or None.  Returns (halo, raw_first): the last row of the nearest non-empty
-    predecessor (None if there is none) and whether this rank holds global row 0, which
-    context mode writes raw (huffman_encoder.c:234)."""
+    predecessor (None if there is none), in last_row's dtype (`dtype` on an empty rank,
+    uint8 by default) on the group's device, and whether this rank holds global row 0,
+    which context mode writes raw (huffman_encoder.c:234).
+
+    Everything moves as device tensors through all_gather_into_tensor, so the same call runs
+    on an RCCL group (device = this rank's GPU) and a gloo one (CPU tensors).  `device` is
+    needed only on a rank whose slice is empty; it defaults to the current GPU when the
+    group's backend is nccl, else the CPU."""
     import torch
     import torch.distributed as dist
     if world == 1:
         return None, 1
-    m = last_row.numel() if last_row is not None else None
+    if last_row is not None:
+        dev, dt = last_row.device, last_row.dtype
+    else:
+        nccl = dist.get_backend(group) == "nccl"
+        dev = device if device is not None else (
+            torch.device("cuda", torch.cuda.current_device()) if nccl else torch.device("cpu"))
+        dt = dtype if dtype is not None else torch.uint8
     # everyone needs m: share it with the non-empty flag
-    info = torch.tensor([1 if last_row is not None else 0, m or 0], dtype=torch.int64)
-    dev = last_row.device if last_row is not None else None
-    allinfo = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
-    dist.all_gather(allinfo, info, group=group)
-    mm = max(int(t[1]) for t in allinfo)
-    row = (last_row.reshape(-1).to(torch.int64).cpu() if last_row is not None
-           else torch.zeros(mm, dtype=torch.int64))
-    rows = [torch.zeros(mm, dtype=torch.int64) for _ in range(world)]
-    dist.all_gather(rows, row, group=group)
-    has = [int(t[0]) for t in allinfo]
+    info = torch.tensor([1 if last_row is not None else 0,
+                         last_row.numel() if last_row is not None else 0],
+                        dtype=torch.int64, device=dev)
+    allinfo = torch.empty(world * 2, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(allinfo, info, group=group)
+    allinfo = allinfo.view(world, 2).cpu().tolist()
+    mm = max(r[1] for r in allinfo)
+    row = torch.zeros(mm, dtype=torch.int64, device=dev)
+    if last_row is not None:
+        row[:last_row.numel()] = last_row.reshape(-1).to(torch.int64)
+    rows = torch.empty(world * mm, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(rows, row, group=group)
+    has = [r[0] for r in allinfo]
     prev = next((r for r in range(rank - 1, -1, -1) if has[r]), None)
     first = next((r for r in range(world) if has[r]), None)
-    halo = rows[prev] if prev is not None else None
-    if halo is not None and dev is not None:
-        halo = halo.to(dev)
+    halo = rows.view(world, mm)[prev].to(dt).contiguous() if prev is not None else None
     return halo, 1 if first == rank else 0

@@ -100,7 +100,7 @@ def test_bitstream_writer_matches_reference(buf, tmp_path):
 
 
 def test_bitstream_one_byte_buffer_terminates(tmp_path):
-    """The reference loops forever here (bitstream.c:355-358); the drop-in must not."""
+    """The reference loops forever here (bitstream.c:131-147); the drop-in must not."""
     path = str(tmp_path / "bs1.bin").encode()
     f = _libc.fopen(path, b"wb")
     s = lib().bit_stream_create_from_file_buffered(ctypes.c_void_p(f), 1)
@@ -219,3 +219,32 @@ def test_fvecs_and_centroids_io(tmp_path):
     got = np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ctypes.c_float)), (9 * 12,))
     assert (n.value, d.value) == (9, 12)
     assert np.array_equal(got.reshape(9, 12), x)
+
+
+def test_block_matches_reference_behaviour():
+    """block_t (fast_nn_block.c:6-71): capacity starts at 100 whatever initial_capacity says
+    (:11), grows to (capacity + 1) * 2 on a full push (:42-44), keeps rows and global ids in
+    push order; set_id empties the block (:68-71); destroy resets every field (:24-39)."""
+    from pq_huffman_amd.capi import Block
+    b = Block()
+    lib().block_init(ctypes.byref(b), 7, 3, 5000, 0xFF)
+    assert (b.id, b.num_dimensions, b.capacity, b.size) == (7, 3, 100, 0)
+    rows = np.arange(3 * 250, dtype=np.float32).reshape(250, 3)
+    caps = []
+    for i in range(250):
+        lib().block_push(ctypes.byref(b), 1000 + i, rows[i].ctypes.data_as(ctypes.c_void_p))
+        caps.append(b.capacity)
+    assert sorted(set(caps)) == [100, 202, 406]
+    assert caps.index(202) == 100 and caps.index(406) == 202
+    data = np.ctypeslib.as_array(b.data, (250 * 3,)).reshape(250, 3)
+    ids = np.ctypeslib.as_array(b.indices, (250,))
+    assert np.array_equal(data, rows) and np.array_equal(ids, np.arange(1000, 1250))
+    lib().block_set_id(ctypes.byref(b), 9)
+    assert (b.id, b.size, b.capacity) == (9, 0, 406)
+    lib().block_destroy(ctypes.byref(b))
+    assert (b.id, b.num_dimensions, b.capacity, b.size) == (-1, 0, 0, 0)
+    assert not b.data and not b.indices
+    # data-only block: no index array, rows still stored
+    lib().block_init(ctypes.byref(b), 0, 2, 0, 0x01)
+    assert not b.indices and b.data
+    lib().block_destroy(ctypes.byref(b))

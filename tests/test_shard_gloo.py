@@ -183,8 +183,10 @@ def _sort_worker(rank, world, port, kind, n, m, k, q):
         mine = shard.sort_rows_distributed(torch.from_numpy(codes[b:e]), world, rank,
                                            _local_sort, samples=16).numpy()
         # the context-mode encode protocol on the (possibly empty) sorted slices
-        last = torch.from_numpy(mine[-1].astype(np.int64)) if len(mine) else None
+        last = torch.from_numpy(mine[-1].copy()) if len(mine) else None
         halo, raw = shard.halo_ragged(last, world, rank)
+        # the halo keeps the codes' dtype: the library reads prev_row as m code bytes
+        assert halo is None or (halo.dtype == torch.uint8 and halo.shape == (m,))
         prev = halo.numpy() if halo is not None else None
         counts = torch.from_numpy(_local_hist(mine, k, True, prev))
         shard.reduce_counts(counts, world)

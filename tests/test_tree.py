@@ -166,6 +166,26 @@ def test_gpu_tree_encode_vs_oracle_roundtrip(gpu, oracle, n, m, roots):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cut", [1, 4, 1000])
+def test_gpu_tree_decode_rejects_truncated_stream(gpu, cut):
+    """A stream shorter than the encoder's sidecar says (a truncated huffman_indices.bin)
+    is reported as corrupt, never decoded into garbage rows."""
+    import torch
+    from pq_huffman_amd import codec
+    from pq_huffman_amd.capi import PqhError
+    n, m = 20_000, 8
+    codes = datagen.skewed_codes(n, m, 256, seed=3)
+    targets, counts = datagen.random_forest(n, roots=5, seed=4)
+    enc = codec.tree_encode(gpu, torch.from_numpy(codes).cuda(), targets, counts)
+    dec = codec.tree_decode(gpu, enc).cpu().numpy()          # exact length: fine
+    np.testing.assert_array_equal(dec, codes[enc.vertices])
+    with pytest.raises(PqhError):
+        codec.tree_decode(gpu, enc, stream_bytes=enc.nbytes - cut)
+    dec = codec.tree_decode(gpu, enc).cpu().numpy()          # the next decode is clean
+    np.testing.assert_array_equal(dec, codes[enc.vertices])
+
+
+@pytest.mark.gpu
 def test_gpu_tree_gather_reports_bad_ids(gpu):
     import torch
     from pq_huffman_amd import codec
