@@ -12,11 +12,12 @@
 //  * One wave per subspace, its centroid sub-codebook resident in VGPRs as MFMA A
 //    fragments; a workgroup = up to 8 subspace waves over the same 32-vector block, so
 //    every input row is read from HBM once per workgroup (512 B per SIFT vector).
-//  * Screening score S_k = ||c_k||^2 - 2 x.c_k + b_v computed exactly-as-bounded by
-//    v_mfma_f32_32x32x16_bf16 over an augmented K dimension:
-//       [xh . ch | xh . cl | 1,1,1,b_v . n1,n2,n3,1]  (+ xl . ch only if the block has
-//    any x that is not bf16-exact -- SIFT-like integer data skips that pass);
-//    x = xh + xl + r, c = ch + cl + r', ||c||^2 = n1 + n2 + n3 (bf16 splits).
+//  * Screening score S_k = ||c_k||^2 - 2 x.c_k computed exactly-as-bounded by
+//    v_mfma_f32_32x32x16_bf16: the accumulator starts at ||c_k||^2 (fp32, the C operand,
+//    read from LDS) and the K dimension is [xh . ch | xh . cl]  (+ xl . ch only if the
+//    block has any x that is not bf16-exact -- SIFT-like integer data skips that pass);
+//    x = xh + xl + r, c = ch + cl + r' (bf16 splits).  Scores are signed and ordered as
+//    floats (v_min3_f32 / v_med3_f32).
 //  * Each lane's 128 scores (8 tiles x 16 accumulator registers) are reduced over two
 //    partitions of that grid on the raw score bits (P: tile halves, Q: register pairs);
 //    their group minima give the smallest and second smallest score and the winner's
@@ -58,33 +59,66 @@ constexpr int kNB = PQH_ASSIGN_NB;            // 32-vector blocks screened toget
 
 template <int D>
 struct Plan {
-    static constexpr int MAIN = 2 * D + 4;            // xh.ch | xh.cl | aux
+    static constexpr int MAIN = 2 * D;                // xh.ch | xh.cl (||c||^2: the C operand)
     static constexpr int PM = (MAIN + 15) / 16;       // main MFMA passes
     static constexpr int PL = (D + 15) / 16;          // lo passes (xl . ch)
-    static constexpr bool REUSE = (D == 16);          // lo pass A == main pass 0 A
-    static constexpr int PA = PM + (REUSE ? 0 : PL);  // distinct A fragments per tile
+    // The lo pass reuses the main passes' A fragments: main slots [0, D) hold ch, and the lo
+    // B operand is xl in slots [0, D) and zero elsewhere, so A pass p gives xl . ch over
+    // dims [16p, 16p + 16) and the cl slots meet zeros.
+    static constexpr int PA = PM;                     // distinct A fragments per tile
 };
 
+// Scores and keys are fp32 values carried as their bit patterns (unsigned) and ordered as
+// floats: a key is a score with its low mantissa bits replaced by an index, which keeps the
+// order of scores whose truncations differ (truncation moves a positive value down and a
+// negative one up, monotonically) and makes every key distinct.  The min/med instructions
+// are written in asm so the compiler neither canonicalises nor reorders them.
 __device__ __forceinline__ unsigned med3u(unsigned a, unsigned b, unsigned c) {
     unsigned r;
-    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    asm("v_med3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
 }
 
-// v_min3_u32 of MFMA results.  The compiler's hazard recognizer does not look into inline
+// v_min3_f32 of MFMA results.  The compiler's hazard recognizer does not look into inline
 // asm, so an asm read of an accumulator gets none of the wait states an MFMA result needs
 // (it would read stale values).  `after` is a compiler-generated value computed from the
 // same accumulator (its read got the wait states); as an extra operand it keeps this asm
 // behind that read, when the whole result is available.
 __device__ __forceinline__ unsigned min3d(unsigned a, unsigned b, unsigned c, unsigned after) {
     unsigned r;
-    asm("v_min3_u32 %0, %1, %2, %3 ; after %4" : "=v"(r) : "v"(a), "v"(b), "v"(c), "v"(after));
+    asm("v_min3_f32 %0, %1, %2, %3 ; after %4" : "=v"(r) : "v"(a), "v"(b), "v"(c), "v"(after));
     return r;
 }
 
 __device__ __forceinline__ unsigned min3u(unsigned a, unsigned b, unsigned c) {
     unsigned r;
-    asm("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+__device__ __forceinline__ unsigned minu(unsigned a, unsigned b) {
+    unsigned r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+__device__ __forceinline__ unsigned maxu(unsigned a, unsigned b) {
+    unsigned r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+// min(a, b) of two accumulator values as a compiler-generated instruction (v_med3_f32
+// with -inf: the compiler inserts the MFMA wait states before it) -- the anchor of min3d.
+// `ninf` holds -inf in a register the compiler cannot see into (an asm v_mov), so the
+// med3 is not rewritten into a min with canonicalising maxes.
+__device__ __forceinline__ unsigned anchor_min(unsigned a, unsigned b, float ninf) {
+    return __float_as_uint(__builtin_amdgcn_fmed3f(__uint_as_float(a), __uint_as_float(b), ninf));
+}
+
+__device__ __forceinline__ float opaque_ninf() {
+    float r;
+    asm volatile("v_mov_b32 %0, 0xff800000" : "=v"(r));
     return r;
 }
 
@@ -95,18 +129,16 @@ __device__ __forceinline__ unsigned min3u(unsigned a, unsigned b, unsigned c) {
 __device__ __forceinline__ void top2_8(const unsigned* k, unsigned& m1, unsigned& m2) {
     const unsigned a1 = min3u(k[0], k[1], k[2]), a2 = med3u(k[0], k[1], k[2]);
     const unsigned b1 = min3u(k[3], k[4], k[5]), b2 = med3u(k[3], k[4], k[5]);
-    const unsigned c1 = min(k[6], k[7]), c2 = max(k[6], k[7]);
+    const unsigned c1 = minu(k[6], k[7]), c2 = maxu(k[6], k[7]);
     m1 = min3u(a1, b1, c1);
-    m2 = min(min3u(a2, b2, c2), med3u(a1, b1, c1));
+    m2 = minu(min3u(a2, b2, c2), med3u(a1, b1, c1));
 }
 
 // main-layout B slot value for vector-side quantities
 template <int D>
-__device__ __forceinline__ float main_slot(int s, const float* xh, float bv) {
+__device__ __forceinline__ float main_slot(int s, const float* xh) {
     if (s < D) return xh[s];
     if (s < 2 * D) return xh[s - D];
-    if (s < 2 * D + 3) return 1.0f;
-    if (s == 2 * D + 3) return bv;
     return 0.0f;
 }
 
@@ -190,20 +222,8 @@ __device__ __forceinline__ void split_x(const float* xs, float& X, bool& lo, flo
     }
 }
 
-// Per-vector bias b_v of the screening score: keeps every score positive, so scores order
-// as unsigned integers.  Needs b_v >= X + 3 E0; with P = sqrt(X Cmax) <= (X + Cmax) / 2,
-// E0 (below) <= 7.7e-5 (X + Cmax), so X + 2^-10 (X + Cmax) suffices -- no square root on
-// the way to the first MFMA.  b_v <= 1.0078 X + 0.001 Cmax stays inside the accumulation
-// term of E0 (1.05 X + 1.01 Cmax).
-// cmb = 2^-10 Cmax + 1e-30 (per subspace): b_v = bf16_up(X (1 + 2^-10) + cmb), where
-// bf16_up of a finite x >= 0 is (bits + 0xFFFF) & 0xFFFF0000.
-__device__ __forceinline__ float screen_bias(float X, bool finite_x, float cmb) {
-    const unsigned u = __float_as_uint(fmaf(X, 1.0f + 0x1p-10f, cmb));
-    return finite_x ? __uint_as_float((u + 0xFFFFu) & 0xFFFF0000u) : 0.0f;
-}
-
-// Error bound E0 of the screening score against the fp32 direct-form distance (DESIGN.md
-// "pq_assign error bound"), P = sqrt(X) sqrt(Cmax):
+// Error bound E0 of the screening score S_k = D_k - X against the fp32 direct-form
+// distance D_k (DESIGN.md "pq_assign error bound"), P = sqrt(X) sqrt(Cmax):
 //   E0 = c_lo P + 2^-22 Cmax + 2^-17 (2.02 P + 1.01 Cmax + 1.05 X),
 // c_lo = 2^-13 when some x of the block has a bf16 remainder, else 2^-15.  The acceptance
 // gap tau = 2.2 E0 is evaluated as a1 sqrt(X) + (c X + b) with per-subspace coefficients
@@ -227,27 +247,24 @@ __device__ __forceinline__ float screen_tau(float X, bool any_lo, const TauCoef&
 }
 
 template <int D>
-__device__ __forceinline__ void build_b(const float* xh, const float* xl, float bv, int h,
+__device__ __forceinline__ void build_b(const float* xh, const float* xl, int h,
                                         bf16x8* Bm, bf16x8* Bl) {
     using P = Plan<D>;
     if constexpr (Slice<D>::HALF) {
-        // slots 16p + 8h + j: p = 0, 1 -> xh[8h + j]; p = 2 -> aux (h = 0) / zero (h = 1)
+        // slots 16p + 8h + j: p = 0, 1 -> xh[8h + j]
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             Bm[0][j] = (__bf16)xh[j];
             Bl[0][j] = (__bf16)xl[j];
         }
         Bm[1] = Bm[0];
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-            Bm[2][j] = (__bf16)(h ? 0.0f : (j < 3 ? 1.0f : (j == 3 ? bv : 0.0f)));
     } else {
 #pragma unroll
         for (int p = 0; p < P::PM; ++p)
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                float v0 = main_slot<D>(16 * p + j, xh, bv);
-                float v1 = main_slot<D>(16 * p + 8 + j, xh, bv);
+                float v0 = main_slot<D>(16 * p + j, xh);
+                float v1 = main_slot<D>(16 * p + 8 + j, xh);
                 Bm[p][j] = (__bf16)(h ? v1 : v0);
             }
 #pragma unroll
@@ -265,7 +282,7 @@ __device__ __forceinline__ void build_b(const float* xh, const float* xl, float 
 // The main loop's B operands, straight from x: the same bf16 values as split_x + build_b
 // (xh = bf16(x), xl = bf16(x - xh)), with packed conversions; xl only when LO.
 template <int D, bool LO>
-__device__ __forceinline__ void make_b(const float* xs, float bv, int h, bf16x8* Bm, bf16x8* Bl) {
+__device__ __forceinline__ void make_b(const float* xs, int h, bf16x8* Bm, bf16x8* Bl) {
     if constexpr (Slice<D>::HALF) {
         typedef float f32x8 __attribute__((ext_vector_type(8)));
         f32x8 xv;
@@ -273,9 +290,6 @@ __device__ __forceinline__ void make_b(const float* xs, float bv, int h, bf16x8*
         for (int j = 0; j < 8; ++j) xv[j] = xs[j];
         Bm[0] = __builtin_convertvector(xv, bf16x8);
         Bm[1] = Bm[0];
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-            Bm[2][j] = (__bf16)(h ? 0.0f : (j < 3 ? 1.0f : (j == 3 ? bv : 0.0f)));
         if constexpr (LO) {
             f32x8 rem;
 #pragma unroll
@@ -290,38 +304,44 @@ __device__ __forceinline__ void make_b(const float* xs, float bv, int h, bf16x8*
             xh[j] = (float)(__bf16)xs[j];
             xl[j] = LO ? (float)(__bf16)(xs[j] - xh[j]) : 0.0f;
         }
-        build_b<D>(xh, xl, bv, h, Bm, Bl);
+        build_b<D>(xh, xl, h, Bm, Bl);
     }
 }
 
-// the 32 x 32 score tile: centroid rows (A fragments a[0 .. PA)) x the block's vectors (B)
+// the 32 x 32 score tile: centroid rows (A fragments a[0 .. PA)) x the block's vectors (B),
+// accumulated onto the rows' ||c||^2 (cn: this lane's 16 rows of the tile)
 template <int D>
 __device__ __forceinline__ f32x16 tile_scores_a(const bf16x8* a, const bf16x8* Bm,
-                                                const bf16x8* Bl, bool lo_pass) {
+                                                const bf16x8* Bl, bool lo_pass, const f32x16& cn) {
     using P = Plan<D>;
-    f32x16 acc = {0};
+    f32x16 acc = cn;
 #pragma unroll
     for (int p = 0; p < P::PM; ++p)
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[p], Bm[p], acc, 0, 0, 0);
     if (lo_pass) {
 #pragma unroll
         for (int p = 0; p < P::PL; ++p)
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[P::REUSE ? 0 : P::PM + p], Bl[p],
-                                                          acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[p], Bl[p], acc, 0, 0, 0);
     }
     return acc;
 }
 
+// this lane's 16 rows of ||c||^2 for tile t (LDS image [tile][half][16]: every lane of a
+// half-wave reads the same 64 bytes, a broadcast)
+__device__ __forceinline__ f32x16 tile_norms(const float* Cn, int t, int h) {
+    return *reinterpret_cast<const f32x16*>(Cn + (t * 2 + h) * 16);
+}
+
 // tile t with its A fragments read from the LDS copy
 template <int D>
-__device__ __forceinline__ f32x16 tile_scores(const uint4* As, int lane, int t, const bf16x8* Bm,
-                                              const bf16x8* Bl, bool lo_pass) {
+__device__ __forceinline__ f32x16 tile_scores(const uint4* As, const float* Cn, int lane, int t,
+                                              const bf16x8* Bm, const bf16x8* Bl, bool lo_pass) {
     using P = Plan<D>;
     bf16x8 a[P::PA];
 #pragma unroll
     for (int p = 0; p < P::PA; ++p)
         a[p] = *reinterpret_cast<const bf16x8*>(&As[(p * kTiles + t) * 64 + lane]);
-    return tile_scores_a<D>(a, Bm, Bl, lo_pass);
+    return tile_scores_a<D>(a, Bm, Bl, lo_pass, tile_norms(Cn, t, lane >> 5));
 }
 
 // centroid row of accumulator register i of tile t for half-wave h (32x32x16 output layout)
@@ -332,7 +352,8 @@ __device__ __forceinline__ int tile_row(int t, int i, int h) {
 template <int D, typename CodeT>
 __global__ void __launch_bounds__(64 * kWavesPerWG, PQH_ASSIGN_OCC)
 pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_total,
-               const bf16x8* __restrict__ afrag, const float* __restrict__ cent,
+               const bf16x8* __restrict__ afrag, const float* __restrict__ cnorm,
+               const float* __restrict__ cent,
                const float* __restrict__ cmax, const float* __restrict__ sqrt_cmax,
                CodeT* __restrict__ codes, uint32_t* __restrict__ counts,
                unsigned long long* __restrict__ rerank, uint32_t* __restrict__ sched, int gx,
@@ -343,6 +364,8 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     // the subspace's A fragments, shared by the workgroup's waves (24 KB at D = 16): keeping
     // them out of VGPRs is what lets several waves share each SIMD
     __shared__ uint4 As[P::PA * kTiles * 64];
+    // ||c_k||^2 (fp32) of the subspace in accumulator order: [tile][half-wave][16 registers]
+    __shared__ __attribute__((aligned(64))) float Cn[kTiles * 2 * 16];
     // each wave's re-rank queue (the LDS budget stays at 32 KB, so a workgroup still fits on
     // a CU beside a code-table build's 112 KB)
     __shared__ uint2 rqs[kWavesPerWG][kRqLds];
@@ -377,6 +400,8 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     {
         const uint4* src = reinterpret_cast<const uint4*>(afrag) + (long long)m * P::PA * kTiles * 64;
         for (int i = threadIdx.x; i < P::PA * kTiles * 64; i += blockDim.x) As[i] = src[i];
+        for (int i = threadIdx.x; i < kTiles * 2 * 16; i += blockDim.x)
+            Cn[i] = cnorm[(long long)m * kTiles * 2 * 16 + i];
         if (counts)
             for (int i = lane; i < K; i += 64) hist[wave][i] = 0;
         __syncthreads();   // the only workgroup barrier
@@ -388,8 +413,8 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
 #endif
     const float cm = cmax[m];
     const float sc = sqrt_cmax[m];
-    const float cmb = fmaf(cm, 0x1p-10f, 1e-30f);   // see screen_bias
     const TauCoef tq = tau_coef(cm, sc);
+    const float ninf = opaque_ninf();
     const float* cl = cent + (long long)m * K * D;   // fp32 centroids (L2-resident, 16 KB)
     const long long nblk = (n + 31) / 32;
     unsigned long long slow_count = 0;
@@ -452,7 +477,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         for (int b = 0; b < kNB; ++b) {
             v[b] = (blk0 + b) * 32 + r;
             valid[b] = v[b] < n;   // rows past n hold row n - 1 (clamped loads), never stored
-            make_b<D, LO>(xs[b], screen_bias(X[b], finite_x[b], cmb), h, Bm[b], Bl[b]);
+            make_b<D, LO>(xs[b], h, Bm[b], Bl[b]);
         }
         // The lane's 128 scores of a block form an 8 x 16 grid: tile t (row) x accumulator
         // register i (column).  Instead of ranking every score with its index attached, two
@@ -480,7 +505,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
             // P: the tile's two group minima, keyed (P-group index 2t + g in the low 4 bits)
             // and folded into the running top two of the P keys
             // (e0, e1: the compiler-generated first reads of the tile's results, see min3d)
-            const unsigned e0 = min(a[6], a[7]), e1 = min(a[14], a[15]);
+            const unsigned e0 = anchor_min(a[6], a[7], ninf), e1 = anchor_min(a[14], a[15], ninf);
             const unsigned k0 =
                 (min3u(min3d(a[0], a[1], a[2], e0), min3d(a[3], a[4], a[5], e0), e0) & ~15u) |
                 (unsigned)(2 * t);
@@ -488,34 +513,39 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
                 (min3u(min3d(a[8], a[9], a[10], e1), min3d(a[11], a[12], a[13], e1), e1) & ~15u) |
                 (unsigned)(2 * t + 1);
             if (t == 0) {
-                pm1[b] = min(k0, k1);
-                pm2[b] = max(k0, k1);
+                pm1[b] = minu(k0, k1);
+                pm2[b] = maxu(k0, k1);
             } else {
                 pm2[b] = med3u(pm1[b], pm2[b], k0);
-                pm1[b] = min(pm1[b], k0);
+                pm1[b] = minu(pm1[b], k0);
                 pm2[b] = med3u(pm1[b], pm2[b], k1);
-                pm1[b] = min(pm1[b], k1);
+                pm1[b] = minu(pm1[b], k1);
             }
             // Q: running minima of the register pairs (j, j + 8)
 #pragma unroll
             for (int j = 0; j < 8; ++j)
-                qg[b][j] = t == 0 ? min(a[j], a[j + 8]) : min3d(qg[b][j], a[j], a[j + 8], e1);
+                qg[b][j] = t == 0 ? min3d(a[j], a[j + 8], a[j + 8], e1)
+                                  : min3d(qg[b][j], a[j], a[j + 8], e1);
         };
         // Software pipeline over the tiles: block b's MFMA chain for tile t + 1 is issued
         // right after its tile-t keys are reduced, so it runs while the other block's keys
         // are (the scheduling barriers keep the compiler from sinking the chain behind them).
         bf16x8 a[P::PA];
         load_a(0, a);
+        f32x16 cn = tile_norms(Cn, 0, h);
         f32x16 acc[kNB];
 #pragma unroll
-        for (int b = 0; b < kNB; ++b) acc[b] = tile_scores_a<D>(a, Bm[b], Bl[b], LO);
+        for (int b = 0; b < kNB; ++b) acc[b] = tile_scores_a<D>(a, Bm[b], Bl[b], LO, cn);
 #pragma unroll
         for (int t = 0; t < kTiles; ++t) {
-            if (t + 1 < kTiles) load_a(t + 1, a);
+            if (t + 1 < kTiles) {
+                load_a(t + 1, a);
+                cn = tile_norms(Cn, t + 1, h);
+            }
 #pragma unroll
             for (int b = 0; b < kNB; ++b) {
                 reduce(acc[b], t, b);
-                if (t + 1 < kTiles) acc[b] = tile_scores_a<D>(a, Bm[b], Bl[b], LO);
+                if (t + 1 < kTiles) acc[b] = tile_scores_a<D>(a, Bm[b], Bl[b], LO, cn);
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
@@ -529,23 +559,24 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
             unsigned q1, q2;
             top2_8(qk, q1, q2);
             const unsigned own1 = p1;
-            const unsigned own2 = min(p2, q2);
+            const unsigned own2 = minu(p2, q2);
             const int wt = (int)((p1 & 15u) >> 1);
             const int wi = (int)(q1 & 7u) + 8 * (int)(p1 & 1u);
             // ... then the two half-waves (lanes l and l^32 hold the same vector): after the
             // swap, s[0] holds the lower half's value and s[1] the upper half's, in every lane
             const auto s1 = __builtin_amdgcn_permlane32_swap(own1, own1, false, false);
             const auto s2 = __builtin_amdgcn_permlane32_swap(own2, own2, false, false);
-            const unsigned b1 = min((unsigned)s1[0], (unsigned)s1[1]);
-            const unsigned b2 = min(min((unsigned)s2[0], (unsigned)s2[1]),
-                                    max((unsigned)s1[0], (unsigned)s1[1]));
+            const unsigned b1 = minu((unsigned)s1[0], (unsigned)s1[1]);
+            const unsigned b2 = minu(minu((unsigned)s2[0], (unsigned)s2[1]),
+                                     maxu((unsigned)s1[0], (unsigned)s1[1]));
             const bool mine = own1 == b1;   // this half holds the winner (both: a tie -> slow)
             int code = tile_row(wt, wi, h);
             const float tau = screen_tau(X[b], any_lo[b], tq);
-            // a key differs from its score by less than 16 ulp (2^-19 relative): 2^-17 K2
-            // covers both keys of the gap
+            // a key differs from its score by less than 16 ulp (2^-19 relative): 2^-17 of the
+            // larger magnitude covers both keys of the gap (and the rounding of K2 - K1)
             const float K1 = __uint_as_float(b1), K2 = __uint_as_float(b2);
-            const bool slow = !(K2 - K1 > fmaf(0x1p-17f, K2, tau)) || !finite_x[b];
+            const float KA = fmaxf(fabsf(K1), fabsf(K2));
+            const bool slow = !(K2 - K1 > fmaf(0x1p-17f, KA, tau)) || !finite_x[b];
 
             unsigned long long need = __ballot(slow && valid[b] && h == 0);
             bool deferred = false;
@@ -553,12 +584,12 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
                 slow_count += __popcll(need);
                 // finite vectors go to the queue with their candidate window: every centroid
                 // that can be the fp32 argmin (or tie with it) screens below
-                // (K1 + tau)(1 + 2^-16) -- see the tail; non-finite ones stay inline
+                // K1 + tau + 2^-16 |K1| -- see the tail; non-finite ones stay inline
                 const unsigned long long fin = need & __ballot(finite_x[b]);
                 const unsigned cnt = (unsigned)__popcll(fin);
                 if (PQH_ASSIGN_DEFER && cnt && qn + cnt <= (unsigned)kRqLds) {
                     if (slow && valid[b] && h == 0 && finite_x[b]) {
-                        const float thr = (K1 + tau) * (1.0f + 0x1p-16f);
+                        const float thr = fmaf(0x1p-16f, fabsf(K1), K1 + tau);
                         rqs[wave][qn + __builtin_amdgcn_mbcnt_hi((unsigned)(fin >> 32),
                                       __builtin_amdgcn_mbcnt_lo((unsigned)fin, 0u))] =
                             make_uint2((uint32_t)v[b], __float_as_uint(thr));
@@ -697,11 +728,11 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
 #endif
         ch = nc;
     }
-    // Tail: this wave's queued vectors, 32 at a time.  thr = (K1 + tau)(1 + 2^-16) bounds the
+    // Tail: this wave's queued vectors, 32 at a time.  thr = K1 + tau + 2^-16 |K1| bounds the
     // screened score of every centroid whose fp32 direct-form distance can equal the minimum
-    // (S_k <= D_k + b + E0 <= D_min + b + E0 <= S_k1 + 2 E0 <= K1 (1 + 2^-19) + 2 E0 < thr):
+    // (S_k <= D_k - X + E0 <= D_min - X + E0 <= S_k1 + 2 E0 <= K1 + 2^-19 |K1| + 2 E0 < thr):
     // the vectors are re-screened with the main loop's own instruction sequence (bitwise the
-    // same scores: same bias, and a lo pass adds exact zeros for bf16-exact x), the centroids
+    // same scores: same norms, and a lo pass adds exact zeros for bf16-exact x), the centroids
     // screening at or below thr are collected per lane, and only those few are evaluated in
     // exact fp32 direct form (first index among equal distances) -- instead of all K.
     // The workgroup's waves share their queues (they finish their chunks within about one
@@ -744,13 +775,13 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         split_x<D>(xs, X, lo, xh, xl);
         bf16x8 Bm[P::PM];
         bf16x8 Bl[P::PL];
-        build_b<D>(xh, xl, screen_bias(X, true, cmb), h, Bm, Bl);
+        build_b<D>(xh, xl, h, Bm, Bl);
         const bool lo_pass = __any(lo);
         float best = INFINITY;
         int bidx = 0x7FFFFFFF;
 #pragma unroll 1
         for (int t = 0; t < kTiles; ++t) {   // (rolled: the tail keeps its registers few)
-            const f32x16 acc = tile_scores<D>(As, lane, t, Bm, Bl, lo_pass);
+            const f32x16 acc = tile_scores<D>(As, Cn, lane, t, Bm, Bl, lo_pass);
             uint32_t bits = 0;
 #pragma unroll
             for (int i = 0; i < 16; ++i) bits |= (acc[i] <= thr ? 1u : 0u) << i;
@@ -887,18 +918,22 @@ struct pqh_pq {
     bool mfma_ok = false;
     float* d_cent = nullptr;
     bf16x8* d_afrag = nullptr;
+    float* d_cn = nullptr;     // ||c||^2 in accumulator order, [m][tile][half][16]
     float* d_cmax = nullptr;
     float* d_sqc = nullptr;
 };
 
 namespace {
 
-// A_aug[row][slot] of one subspace for the pass layouts of Plan<D>
+// A[row][slot] of one subspace for the pass layout of Plan<D> (-2 ch | -2 cl, both exact
+// bf16) and the rows' ||c||^2 in accumulator order (the C operand of each tile's chain)
 template <int D>
-void build_afrag(const float* c, int k, std::vector<uint16_t>& out, int m, float& cmax_out) {
+void build_afrag(const float* c, int k, std::vector<uint16_t>& out, std::vector<float>& cn,
+                 int m, float& cmax_out) {
     using P = Plan<D>;
-    const int slots_main = 16 * P::PM;
-    std::vector<uint16_t> main((size_t)k * slots_main, 0), lo((size_t)k * 16 * P::PL, 0);
+    const int slots = 16 * P::PM;
+    std::vector<uint16_t> main((size_t)k * slots, 0);
+    std::vector<double> norm(k);
     double cmax = 0.0;
     for (int row = 0; row < k; ++row) {
         const float* cr = c + (size_t)row * D;
@@ -907,40 +942,30 @@ void build_afrag(const float* c, int k, std::vector<uint16_t>& out, int m, float
             q += (double)cr[j] * (double)cr[j];
             uint16_t hi = bf16_rne(cr[j]);
             uint16_t lw = bf16_rne(cr[j] - bf16_to_f(hi));
-            uint16_t m2hi = bf16_rne(-2.0f * bf16_to_f(hi));   // exact
-            uint16_t m2lo = bf16_rne(-2.0f * bf16_to_f(lw));   // exact
-            main[(size_t)row * slots_main + j] = m2hi;
-            main[(size_t)row * slots_main + D + j] = m2lo;
-            lo[(size_t)row * 16 * P::PL + j] = m2hi;
+            main[(size_t)row * slots + j] = bf16_rne(-2.0f * bf16_to_f(hi));       // exact
+            main[(size_t)row * slots + D + j] = bf16_rne(-2.0f * bf16_to_f(lw));   // exact
         }
+        norm[row] = q;
         cmax = q > cmax ? q : cmax;
-        uint16_t n1 = bf16_rne((float)q);
-        double r1 = q - bf16_to_f(n1);
-        uint16_t n2 = bf16_rne((float)r1);
-        double r2 = r1 - bf16_to_f(n2);
-        uint16_t n3 = bf16_rne((float)r2);
-        main[(size_t)row * slots_main + 2 * D] = n1;
-        main[(size_t)row * slots_main + 2 * D + 1] = n2;
-        main[(size_t)row * slots_main + 2 * D + 2] = n3;
-        main[(size_t)row * slots_main + 2 * D + 3] = bf16_rne(1.0f);
     }
     cmax_out = (float)(cmax * (1.0 + 1e-6)) + 1e-30f;
     // fragment order [m][PA][tile][lane][8]
     const size_t base = (size_t)m * P::PA * kTiles * 64 * 8;
-    for (int p = 0; p < P::PA; ++p) {
-        const bool is_main = p < P::PM;
-        const std::vector<uint16_t>& src = is_main ? main : lo;
-        const int width = is_main ? slots_main : 16 * P::PL;
-        const int pp = is_main ? p : p - P::PM;
+    for (int p = 0; p < P::PA; ++p)
         for (int t = 0; t < kTiles; ++t)
             for (int lane = 0; lane < 64; ++lane)
                 for (int j = 0; j < 8; ++j) {
                     int row = 32 * t + (lane & 31);
-                    int slot = 16 * pp + 8 * (lane >> 5) + j;
+                    int slot = 16 * p + 8 * (lane >> 5) + j;
                     out[base + (((size_t)p * kTiles + t) * 64 + lane) * 8 + j] =
-                        src[(size_t)row * width + slot];
+                        main[(size_t)row * slots + slot];
                 }
-    }
+    // accumulator register i of half-wave h holds row tile_row(t, i, h)
+    for (int t = 0; t < kTiles; ++t)
+        for (int h = 0; h < 2; ++h)
+            for (int i = 0; i < 16; ++i)
+                cn[(size_t)m * kTiles * 32 + (t * 2 + h) * 16 + i] =
+                    (float)norm[32 * t + (i & 3) + 8 * (i >> 2) + 4 * h];
 }
 
 template <int D>
@@ -987,7 +1012,7 @@ int launch_mfma(pqh_ctx* ctx, pqh_pq* pq, const float* x, long long n, long long
         gx = std::max(1ll, std::min(gx, ((nblk + kNB - 1) / kNB + kWavesPerWG - 1) / kWavesPerWG)); \
         if (gx >= 16) gx &= ~7ll;   /* CU-uniform subspace placement (see the kernel) */   \
         hipLaunchKernelGGL((pq_assign_mfma<DD, CodeT>), dim3((unsigned)(gx * groups)), block, \
-                           0, ctx->stream, x, n, ldx, pq->m, pq->d_afrag, pq->d_cent,       \
+                           0, ctx->stream, x, n, ldx, pq->m, pq->d_afrag, pq->d_cn, pq->d_cent, \
                            pq->d_cmax, pq->d_sqc, codes, counts, rr, sched, (int)gx,         \
                            rr_next, sched ? ctx->d_sched + (1 - ring) * kSchedSet : nullptr); \
         PQH_LAUNCH_CHECK(ctx);                                                              \
@@ -1044,25 +1069,28 @@ int pqh_pq_create(pqh_ctx_t* ctx, const float* centroids, int m, int k, int dsub
     (void)hipMemcpy(pq->d_cent, centroids, nc * sizeof(float), hipMemcpyHostToDevice);
     if (pq->mfma_ok) {
         std::vector<uint16_t> frag((size_t)m * pa * kTiles * 64 * 8);
+        std::vector<float> cn((size_t)m * kTiles * 32);
         std::vector<float> cmax(m), sqc(m);
         for (int i = 0; i < m; ++i) {
             const float* c = centroids + (size_t)i * k * dsub;
             switch (dsub) {
-                case 4: build_afrag<4>(c, k, frag, i, cmax[i]); break;
-                case 6: build_afrag<6>(c, k, frag, i, cmax[i]); break;
-                case 8: build_afrag<8>(c, k, frag, i, cmax[i]); break;
-                case 12: build_afrag<12>(c, k, frag, i, cmax[i]); break;
-                case 16: build_afrag<16>(c, k, frag, i, cmax[i]); break;
+                case 4: build_afrag<4>(c, k, frag, cn, i, cmax[i]); break;
+                case 6: build_afrag<6>(c, k, frag, cn, i, cmax[i]); break;
+                case 8: build_afrag<8>(c, k, frag, cn, i, cmax[i]); break;
+                case 12: build_afrag<12>(c, k, frag, cn, i, cmax[i]); break;
+                case 16: build_afrag<16>(c, k, frag, cn, i, cmax[i]); break;
             }
             sqc[i] = (float)(std::sqrt((double)cmax[i]) * (1.0 + 1e-6)) + 1e-30f;
         }
         if (hipMalloc(&pq->d_afrag, frag.size() * 2) != hipSuccess ||
+            hipMalloc(&pq->d_cn, cn.size() * sizeof(float)) != hipSuccess ||
             hipMalloc(&pq->d_cmax, m * sizeof(float)) != hipSuccess ||
             hipMalloc(&pq->d_sqc, m * sizeof(float)) != hipSuccess) {
             pqh_pq_destroy(pq);
             return pqh_set_error(ctx, PQH_ERR_NOMEM, "hipMalloc fragments");
         }
         (void)hipMemcpy(pq->d_afrag, frag.data(), frag.size() * 2, hipMemcpyHostToDevice);
+        (void)hipMemcpy(pq->d_cn, cn.data(), cn.size() * sizeof(float), hipMemcpyHostToDevice);
         (void)hipMemcpy(pq->d_cmax, cmax.data(), m * sizeof(float), hipMemcpyHostToDevice);
         (void)hipMemcpy(pq->d_sqc, sqc.data(), m * sizeof(float), hipMemcpyHostToDevice);
     }
@@ -1076,6 +1104,7 @@ int pqh_pq_destroy(pqh_pq_t* pq) {
     (void)hipStreamSynchronize(pq->ctx->stream);
     (void)hipFree(pq->d_cent);
     (void)hipFree(pq->d_afrag);
+    (void)hipFree(pq->d_cn);
     (void)hipFree(pq->d_cmax);
     (void)hipFree(pq->d_sqc);
     delete pq;
