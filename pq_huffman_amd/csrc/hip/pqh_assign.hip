@@ -699,6 +699,9 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
                 xr = (xr + 1) & (kXcds - 1);
                 traw = ticket();
             }
+#ifdef PQH_ASSIGN_ENDPRIO   // (experiment) the end phase: waves past their home range first
+            __builtin_amdgcn_s_setprio(PQH_ASSIGN_ENDPRIO);
+#endif
         }
         return -1;
     };
@@ -739,6 +742,9 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     // chunk of each other): batch j of the concatenated queues goes to wave j % waves.
     __shared__ unsigned qlen[kWavesPerWG];
     if (lane == 0) qlen[wave] = qn;
+#ifdef PQH_ASSIGN_TAILPRIO   // (experiment) the re-rank tail ahead of other waves' main loops
+    __builtin_amdgcn_s_setprio(PQH_ASSIGN_TAILPRIO);
+#endif
     __syncthreads();
     unsigned qoff[kWavesPerWG + 1];
     qoff[0] = 0;

@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "pqh_internal.h"
+#include "pqh_heap_asm.h"
 
 namespace {
 
@@ -215,9 +216,305 @@ struct SentinelHeap {
     }
 };
 
-// diagnostics: s_memtime stamps of the first workgroup's phases (pqh_debug_stamps):
-// [0..6] huff_trees tree 0, [8..13] dec_chunks workgroup 0 lane 0
+// ---- one wavefront per tree: the heap in registers ------------------------------------
+// The reference heap (huffman_encode.c:33-76) simulated with its entries spread over the
+// lanes of five VGPRs: slot s lives in register (s + 1) >> 6 at lane (s + 1) & 63, so every
+// heap depth but the seventh has one fixed register (depth 7 has two, picked by bit 6).
+// The tree's control state (slot index, keys being sifted) is wave-uniform and lives in
+// SGPRs; a heap read is one v_readlane with a scalar lane index, a write a lane select --
+// no LDS round trip on the serial chain of sifts, which is what bounds a tree build (one
+// lane per tree through LDS: ~4,000 cycles a merge).  The sifts are unrolled by depth so
+// every access names its register statically.
+// Keys are the SentinelHeap's: weight << 10 | tie << 9 | node, u32 while the tree's total
+// weight is below 2^22, else u64 (two words per slot); slots past the heap hold all ones, so
+// children need no bounds checks.
+template <typename Key>
+__device__ __forceinline__ Key lane_read(const Key& v, int ln) {
+    if constexpr (sizeof(Key) == 4) {
+        return (Key)__builtin_amdgcn_readlane((int)v, ln);
+    } else {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, ln);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), ln);
+        return ((Key)hi << 32) | lo;
+    }
+}
+
+template <typename Key>
+struct WaveHeap {
+    static constexpr Key kTie = (Key)1 << 9, kLow = ((Key)1 << 10) - 1, kMax = ~(Key)0;
+    Key r0, r1, r2, r3, r4;   // slots with s + 1 in 1..63 | 64..127 | 128..191 | 192..255 | 256
+    int size;
+    int me;                    // this lane's id
+    __device__ __forceinline__ void init() {
+        r0 = r1 = r2 = r3 = r4 = kMax;
+        size = 0;
+        me = (int)(threadIdx.x & 63);
+    }
+    // register of slot s (as a value: a uniform select, no branch)
+    __device__ __forceinline__ Key reg(int s) const {
+        const int r = (s + 1) >> 6;
+        return r == 0 ? r0 : r == 1 ? r1 : r == 2 ? r2 : r == 3 ? r3 : r4;
+    }
+    __device__ __forceinline__ Key get(int s) const {
+        return s < 256 ? lane_read(reg(s), (s + 1) & 63) : kMax;   // past 255: never in the heap
+    }
+    __device__ __forceinline__ void set(int s, Key v) {
+        const int r = (s + 1) >> 6;
+        const bool hit = me == ((s + 1) & 63);
+        r0 = hit && r == 0 ? v : r0;
+        r1 = hit && r == 1 ? v : r1;
+        r2 = hit && r == 2 ? v : r2;
+        r3 = hit && r == 3 ? v : r3;
+        r4 = hit && r == 4 ? v : r4;
+    }
+    // sift up while strictly lighter than the parent (huffman_encode.c:33-46)
+    __device__ __forceinline__ void push(Key e) {
+        int i = size++;
+        while (i > 0) {
+            const int p = (i - 1) >> 1;
+            const Key hp = get(p);
+            if (!(e < (hp & ~kLow))) break;
+            set(i, hp);
+            i = p;
+        }
+        set(i, e);
+    }
+    // the last entry sifts down from the root: the left child unless the right one is
+    // strictly lighter (min(left, right | TIE)), moving while it is strictly heavier than
+    // that child (huffman_encode.c:48-76).  Both children share a register.
+    __device__ __forceinline__ Key pop() {
+        const Key top = lane_read(r0, 1);
+        const Key last = get(--size);
+        set(size, kMax);   // the vacated slot becomes a sentinel
+        const Key lw = last & ~kLow;
+        int i = 0;
+        while (i < 128) {
+            const int c = 2 * i + 1;
+            const Key rc = reg(c);
+            const Key kl = lane_read(rc, (c + 1) & 63);
+            const Key kr = c + 1 < 256 ? lane_read(rc, (c + 2) & 63) : kMax;
+            const Key kc = min(kl, kr | kTie);
+            if (!(kc < lw)) break;
+            set(i, kc & ~kTie);
+            i = c + ((kc & kTie) ? 1 : 0);
+        }
+        set(i, last);
+        return top;
+    }
+};
+
+// The u32-key heap (tree totals below 2^22: every bench and test alphabet but the heaviest)
+// with its sifts as generated inline asm (pqh_heap_asm.h): the heap occupies v40..v47, the
+// operands are SGPRs.  Same slot layout and semantics as WaveHeap<uint32_t>.
+typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+struct WaveHeapAsm {
+    u32x8 h;
+    int size;
+    __device__ __forceinline__ void init() {
+        h = u32x8(0xFFFFFFFFu);
+        size = 0;
+    }
+    __device__ __forceinline__ void push(uint32_t e) {
+        uint32_t i = (uint32_t)size++, p, ln, hp, hw, t, d, m0s;
+        asm volatile(PQH_HEAP_PUSH_ASM
+                     : [i] "+&s"(i), [p] "=&s"(p), [ln] "=&s"(ln), [hp] "=&s"(hp), [hw] "=&s"(hw),
+                       [t] "=&s"(t), [d] "=&s"(d), [m0s] "=&s"(m0s), "+{v[40:47]}"(h)
+                     : [e] "s"(e)
+                     : "scc");
+    }
+    __device__ __forceinline__ uint32_t pop() {
+        const uint32_t sz = (uint32_t)(--size);
+        uint32_t top, i, c, ln, kl, kr, kc, lw, last, t, m0s;
+        asm volatile(PQH_HEAP_POP_ASM
+                     : [top] "=&s"(top), [i] "=&s"(i), [c] "=&s"(c), [ln] "=&s"(ln),
+                       [kl] "=&s"(kl), [kr] "=&s"(kr), [kc] "=&s"(kc), [lw] "=&s"(lw),
+                       [last] "=&s"(last), [t] "=&s"(t), [m0s] "=&s"(m0s), "+{v[40:47]}"(h)
+                     : [sz] "s"(sz)
+                     : "scc");
+        return top;
+    }
+};
+
+template <typename Key>
+struct HeapFor { using type = WaveHeap<Key>; };
+template <>
+struct HeapFor<uint32_t> { using type = WaveHeapAsm; };
+
 __device__ unsigned long long g_tree_stamps[16];
+
+template <typename Key>
+__device__ __forceinline__ int wave_merge(uint32_t lc0, uint32_t lc1, uint32_t lc2, uint32_t lc3,
+                                          int nz, uint32_t* kid, int lane, bool stamp_tree) {
+    typename HeapFor<Key>::type hp;
+    hp.init();
+    const bool stamp = stamp_tree;
+    for (int j = 0; j < nz; ++j) {
+        const uint32_t lcr = (j >> 6) == 0 ? lc0 : (j >> 6) == 1 ? lc1 : (j >> 6) == 2 ? lc2 : lc3;
+        hp.push(((Key)(uint32_t)__builtin_amdgcn_readlane((int)lcr, j & 63) << 10) | (Key)j);
+    }
+    if (stamp && lane == 0) g_tree_stamps[2] = __builtin_amdgcn_s_memtime();
+    int next = nz;
+    constexpr Key kNode = 511, kW = ~(Key)1023;
+    if (hp.size == 1) {   // lone symbol: code "0" (huffman_encode.c:168-177)
+        const Key e = hp.pop();
+        if (lane == 0) kid[0] = (uint32_t)(e & kNode) | 0xFFFF0000u;
+        hp.push((e & kW) | (Key)next);
+        ++next;
+    }
+    while (hp.size > 1) {
+        const Key a = hp.pop();
+        const Key b = hp.pop();
+        if (lane == 0) kid[next - nz] = (uint32_t)(a & kNode) | ((uint32_t)(b & kNode) << 16);
+        hp.push(((a & kW) + (b & kW)) | (Key)next);
+        ++next;
+    }
+    return next;
+}
+
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// One wavefront per (part, context) alphabet, K <= 256: counts -> code table entries
+// len << 56 | code for every symbol (0 for symbols that never occur).  Four trees per
+// workgroup; waves are independent (no workgroup barrier).  Codes come from the merge record
+// by pointer jumping over the tree (code(v) = code(anc) << len | bits) -- eight parallel
+// rounds instead of a serial walk from the root.
+constexpr int kTreeWaves = 4;
+__global__ void __launch_bounds__(64 * kTreeWaves)
+huff_trees_wave(const uint32_t* __restrict__ counts, int k, long long trees,
+                unsigned long long* __restrict__ enc, uint32_t* __restrict__ err) {
+    __shared__ uint32_t s_kid[kTreeWaves][256];
+    __shared__ uint32_t s_leaf[kTreeWaves][256];              // count, then the symbol
+    __shared__ uint32_t s_al[kTreeWaves][512];                // anc | len << 16
+    __shared__ unsigned long long s_code[kTreeWaves][512];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const long long tree = (long long)blockIdx.x * kTreeWaves + w;
+    if (tree >= trees) return;   // no workgroup barriers below
+    const uint32_t* cnt = counts + tree * k;
+    unsigned long long* out = enc + tree * k;
+    if (tree == 0 && lane == 0) g_tree_stamps[0] = __builtin_amdgcn_s_memtime();
+    uint32_t* kid = s_kid[w];
+    uint32_t* leaf = s_leaf[w];
+    uint32_t* al = s_al[w];
+    unsigned long long* code = s_code[w];
+    // nonzero counts in symbol order (huffman_encode.c:158), compacted by ballot
+    int nz = 0;
+    unsigned long long total = 0;
+    uint32_t cg[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const int sy = 64 * g + lane;
+        cg[g] = sy < k ? cnt[sy] : 0u;
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const int sy = 64 * g + lane;
+        const unsigned long long mask = __ballot(cg[g] != 0u);
+        const int pos = nz + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+        if (cg[g]) {
+            leaf[pos] = cg[g];
+            kid[pos] = (uint32_t)sy;   // (kid is free until the merges: symbols parked here)
+        } else if (sy < k) {
+            out[sy] = 0ull;            // a symbol that never occurs has no code
+        }
+        nz += __popcll(mask);
+        unsigned long long v = cg[g];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+        total += v;
+    }
+    if (nz == 0) return;
+    wave_sync_lds();
+    const uint32_t lc0 = leaf[lane], lc1 = leaf[64 + lane], lc2 = leaf[128 + lane],
+                   lc3 = leaf[192 + lane];
+    uint32_t sym[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) sym[g] = kid[64 * g + lane];
+    wave_sync_lds();
+    const bool stamp = tree == 0;
+    if (stamp && lane == 0) g_tree_stamps[1] = __builtin_amdgcn_s_memtime();
+    const int next = total < (1ull << 22)
+                         ? wave_merge<uint32_t>(lc0, lc1, lc2, lc3, nz, kid, lane, stamp)
+                         : wave_merge<unsigned long long>(lc0, lc1, lc2, lc3, nz, kid, lane, stamp);
+    if (stamp && lane == 0) g_tree_stamps[3] = __builtin_amdgcn_s_memtime();
+    wave_sync_lds();
+    // the parent links: child 0 gets bit 0, child 1 bit 1 (huffman_encode.c:100-132)
+    const int root = next - 1;
+    for (int q = nz + lane; q < next; q += 64) {
+        const uint32_t kk = kid[q - nz];
+        const uint32_t a = kk & 0xFFFFu, b = kk >> 16;
+        al[a] = (uint32_t)q | (1u << 16);
+        code[a] = 0ull;
+        if (b != 0xFFFFu) {
+            al[b] = (uint32_t)q | (1u << 16);
+            code[b] = 1ull;
+        }
+    }
+    if (lane == 0) {
+        al[root] = 0xFFFFu;   // no ancestor, length 0
+        code[root] = 0ull;
+    }
+    wave_sync_lds();
+    // pointer jumping: after round r every node's link spans 2^r levels (depth <= 255)
+    for (int round = 0; round < 9; ++round) {
+        uint32_t nal[8];
+        unsigned long long ncode[8];
+        bool live = false;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int v = lane + 64 * u;
+            nal[u] = 0xFFFFu;
+            ncode[u] = 0ull;
+            if (v < next) {
+                const uint32_t x = al[v];
+                nal[u] = x;
+                ncode[u] = code[v];
+                const uint32_t anc = x & 0xFFFFu;
+                if (anc != 0xFFFFu) {
+                    const uint32_t y = al[anc];
+                    const uint32_t len = (x >> 16) & 0xFFu, len2 = (y >> 16) & 0xFFu;
+                    const uint32_t nl = min(len + len2, 255u);
+                    ncode[u] = (len < 64 ? code[anc] << len : 0ull) | ncode[u];
+                    nal[u] = (y & 0xFFFFu) | (nl << 16);
+                    live = true;
+                }
+            }
+        }
+        wave_sync_lds();
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int v = lane + 64 * u;
+            if (v < next) {
+                al[v] = nal[u];
+                code[v] = ncode[u];
+            }
+        }
+        wave_sync_lds();
+        if (!__any(live)) break;
+    }
+    bool too_long = false;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const int j = 64 * g + lane;
+        if (j < nz) {
+            const unsigned long long len = (al[j] >> 16) & 0xFFu;
+            if (len > (unsigned long long)kMaxCodeLen) too_long = true;
+            else out[sym[g]] = (len << 56) | (code[j] & kCodeMask);
+        }
+    }
+    if (too_long) atomicOr(err, 1u);
+    if (tree == 0 && lane == 0) {
+        g_tree_stamps[4] = __builtin_amdgcn_s_memtime();
+        g_tree_stamps[5] = (unsigned long long)nz;
+        g_tree_stamps[6] = (unsigned long long)next;
+    }
+}
+
+// diagnostics: s_memtime stamps of the first workgroup's phases (pqh_debug_stamps):
+// [0..6] huff_trees tree 0, [8..13] dec_chunks workgroup 0 lane 0 (g_tree_stamps, above)
 
 // Compact per-tree layout for K <= 256 (3.5 KB, so 32 trees fit one workgroup and the
 // whole build occupies 64 CUs -- it can run beside the next batch's assignment):
@@ -972,8 +1269,25 @@ int pqh_tables_build(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts) 
     if (rc) return rc;
     PQH_HIP(ctx, hipMemsetAsync(t->d_err, 0, 4, ctx->stream));
     if (reinterpret_cast<uintptr_t>(d_counts) & 15u) return PQH_ERR_ARG;
-    PQH_HIP(ctx, hipMemsetAsync(t->d_enc, 0, (size_t)t->m * t->items * 8, ctx->stream));
     const long long trees = t->tables;
+    // Two builds of the same trees:
+    //  * one lane per tree through LDS (huff_trees_small, the default): 128 wavefronts of 16
+    //    trees -- a small footprint beside the next batches' assignment in the pipelined
+    //    bench (0.79 ms a batch there, 0.64 ms alone);
+    //  * one wavefront per tree with the heap in registers (huff_trees_wave,
+    //    PQH_TREE_IMPL=wave): half the latency alone (0.40 vs 0.70 ms with the decode
+    //    tables), but its 2,048 wavefronts take wave slots and issue cycles from the
+    //    concurrent assignment (bench 1,610-1,880 Mvec/s against 2,270).
+    const char* impl = std::getenv("PQH_TREE_IMPL");
+    if (t->k <= 256 && impl && std::strcmp(impl, "wave") == 0) {
+        // writes every entry (0 for symbols that never occur): no memset
+        hipLaunchKernelGGL(huff_trees_wave, dim3((unsigned)((trees + kTreeWaves - 1) / kTreeWaves)),
+                           dim3(64 * kTreeWaves), 0, ctx->stream, d_counts, t->k, trees, t->d_enc,
+                           t->d_err);
+        PQH_LAUNCH_CHECK(ctx);
+        return launch_luts(ctx, t);
+    }
+    PQH_HIP(ctx, hipMemsetAsync(t->d_enc, 0, (size_t)t->m * t->items * 8, ctx->stream));
     if (t->k <= 256) {
         // trees per workgroup: fewer = more, smaller workgroups (3.5 KB of LDS per tree), so
         // the build spreads over more CUs and leaves each CU's LDS to concurrent kernels

@@ -202,8 +202,10 @@ def test_full_size_roundtrip_sift1m(gpu, oracle, ctxm):
 @pytest.mark.parametrize("case", ["enc_test_many", "enc_test_one", "enc_test_zero",
                                   "ties_small_ints", "ties_all_equal", "ties_powers",
                                   "single_symbol", "empty", "geometric"])
-def test_gpu_tree_builder_vs_reference_codebooks(gpu, case):
-    """pqh_tables_build (GPU heap simulation) == the reference's codebook bytes."""
+@pytest.mark.parametrize("impl", ["lane", "wave"])
+def test_gpu_tree_builder_vs_reference_codebooks(gpu, case, impl, monkeypatch):
+    """pqh_tables_build (GPU heap simulation, both builds) == the reference's codebook bytes."""
+    monkeypatch.setenv("PQH_TREE_IMPL", impl)
     torch, codec, ctx = gpu
     g = golden("codebooks.npz")
     k, c = (int(v) for v in g[case + "__alphabet"])
@@ -214,8 +216,10 @@ def test_gpu_tree_builder_vs_reference_codebooks(gpu, case):
 
 
 @pytest.mark.parametrize("ctxm", [True, False])
-def test_gpu_tree_builder_vs_host_builder_ties(gpu, ctxm):
+@pytest.mark.parametrize("impl", ["lane", "wave"])
+def test_gpu_tree_builder_vs_host_builder_ties(gpu, ctxm, impl, monkeypatch):
     """2048 tie-heavy context trees (or 8 plain ones): GPU tables == host codebooks."""
+    monkeypatch.setenv("PQH_TREE_IMPL", impl)
     torch, codec, ctx = gpu
     rng = np.random.default_rng(17)
     items = 256 * 256 if ctxm else 256
@@ -231,6 +235,29 @@ def test_gpu_tree_builder_vs_host_builder_ties(gpu, ctxm):
     host = codec.Codebooks(counts.astype(np.float64), 256, ctxm)
     dev = codec.Tables(ctx, 8, 256, ctxm).build(torch.from_numpy(counts.astype(np.int32)).cuda())
     assert dev.codebooks().file_bytes() == host.file_bytes()
+
+
+@pytest.mark.parametrize("ctxm", [True, False])
+@pytest.mark.parametrize("impl", ["lane", "wave"])
+def test_gpu_tree_builder_heavy_and_rebuilt(gpu, ctxm, impl, monkeypatch):
+    """Trees whose total weight reaches 2^22 (64-bit heap keys) with ties, and a table set
+    rebuilt from a histogram with fewer symbols: every entry is rewritten (the build does not
+    memset), so the second build equals the host codebooks of the second histogram."""
+    monkeypatch.setenv("PQH_TREE_IMPL", impl)
+    torch, codec, ctx = gpu
+    rng = np.random.default_rng(23)
+    items = 256 * 256 if ctxm else 256
+    heavy = rng.integers(0, 3, (8, items)).astype(np.int64) * 3_000_000
+    heavy[:, ::7] += 5                        # ties among light and heavy leaves
+    heavy[3, : items // 2] = 0
+    sparse = np.zeros((8, items), np.int64)
+    sparse[:, ::5] = rng.integers(1, 9, (8, len(range(0, items, 5))))
+    tabs = codec.Tables(ctx, 8, 256, ctxm)
+    for counts in (heavy, sparse):
+        assert counts.max() < 2 ** 31
+        tabs.build(torch.from_numpy(counts.astype(np.int32)).cuda())
+        host = codec.Codebooks(counts.astype(np.float64), 256, ctxm)
+        assert tabs.codebooks().file_bytes() == host.file_bytes()
 
 
 def _run(args, cwd=None):
