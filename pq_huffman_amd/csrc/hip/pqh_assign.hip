@@ -40,7 +40,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
-constexpr int kTiles = 8;        // K = 256 centroids = 8 tiles of 32 rows
+constexpr int kTiles = 8;        // K = 256 centroids = 8 tiles of 32 rows (K = 4096: 128 tiles)
 #ifndef PQH_ASSIGN_WPG
 #define PQH_ASSIGN_WPG 4
 #endif
@@ -162,10 +162,18 @@ __device__ unsigned long long g_assign_stamps[kStampWaves][4];
 
 // ---- screening steps shared by pq_assign_mfma and pq_rerank_window: a deferred vector is
 // re-screened by the same instruction sequence, so its scores are bitwise the same.
+// D = 16, 32 ("HALF"): lane (r, h) holds dims [16p + 8h, 16p + 8h + 8) of vector r for
+// every 16-dim piece p -- exactly the B-fragment slots it feeds -- as xs[8p .. 8p + 8);
+// other D: both half-waves hold all D dims.
 template <int D>
 struct Slice {
-    static constexpr bool HALF = D == 16;   // lane (r, h) holds dims [8h, 8h + 8) of vector r
-    static constexpr int XD = HALF ? 8 : D;
+    static constexpr bool HALF = D % 16 == 0;
+    static constexpr int NP = HALF ? D / 16 : 1;    // 16-dim pieces
+    static constexpr int XD = HALF ? D / 2 : D;     // values per lane
+    // dim of the lane's value j
+    static __device__ __forceinline__ int dim(int j, int h) {
+        return HALF ? 16 * (j >> 3) + 8 * h + (j & 7) : j;
+    }
 };
 
 // the value of lane l ^ 32 (a VALU lane swap, no LDS round trip)
@@ -251,13 +259,18 @@ __device__ __forceinline__ void build_b(const float* xh, const float* xl, int h,
                                         bf16x8* Bm, bf16x8* Bl) {
     using P = Plan<D>;
     if constexpr (Slice<D>::HALF) {
-        // slots 16p + 8h + j: p = 0, 1 -> xh[8h + j]
+        // pass p < NP: slots 16p + 8h + j = dims of piece p (the lane's xs[8p + j]); passes
+        // NP .. 2 NP - 1 repeat them (x . cl); lo pass p: the remainders of piece p
+        constexpr int NP = Slice<D>::NP;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            Bm[0][j] = (__bf16)xh[j];
-            Bl[0][j] = (__bf16)xl[j];
+        for (int p = 0; p < NP; ++p) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                Bm[p][j] = (__bf16)xh[8 * p + j];
+                Bl[p][j] = (__bf16)xl[8 * p + j];
+            }
+            Bm[NP + p] = Bm[p];
         }
-        Bm[1] = Bm[0];
     } else {
 #pragma unroll
         for (int p = 0; p < P::PM; ++p)
@@ -285,16 +298,20 @@ template <int D, bool LO>
 __device__ __forceinline__ void make_b(const float* xs, int h, bf16x8* Bm, bf16x8* Bl) {
     if constexpr (Slice<D>::HALF) {
         typedef float f32x8 __attribute__((ext_vector_type(8)));
-        f32x8 xv;
+        constexpr int NP = Slice<D>::NP;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) xv[j] = xs[j];
-        Bm[0] = __builtin_convertvector(xv, bf16x8);
-        Bm[1] = Bm[0];
-        if constexpr (LO) {
-            f32x8 rem;
+        for (int p = 0; p < NP; ++p) {
+            f32x8 xv;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) rem[j] = xs[j] - (float)Bm[0][j];
-            Bl[0] = __builtin_convertvector(rem, bf16x8);
+            for (int j = 0; j < 8; ++j) xv[j] = xs[8 * p + j];
+            Bm[p] = __builtin_convertvector(xv, bf16x8);
+            Bm[NP + p] = Bm[p];
+            if constexpr (LO) {
+                f32x8 rem;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) rem[j] = xs[8 * p + j] - (float)Bm[p][j];
+                Bl[p] = __builtin_convertvector(rem, bf16x8);
+            }
         }
     } else {
         constexpr int XD = Slice<D>::XD;
@@ -332,15 +349,21 @@ __device__ __forceinline__ f32x16 tile_norms(const float* Cn, int t, int h) {
     return *reinterpret_cast<const f32x16*>(Cn + (t * 2 + h) * 16);
 }
 
-// tile t with its A fragments read from the LDS copy
-template <int D>
-__device__ __forceinline__ f32x16 tile_scores(const uint4* As, const float* Cn, int lane, int t,
+// A fragment p of tile t, [PA][KT][64 lanes] per subspace: from the workgroup's LDS copy
+// (K = 256) or straight from L2 (K = 4096: 256 KB per subspace, streamed)
+template <int KT>
+__device__ __forceinline__ bf16x8 frag_at(const uint4* src, int p, int t, int lane) {
+    return *reinterpret_cast<const bf16x8*>(&src[(p * KT + t) * 64 + lane]);
+}
+
+// tile t with its A fragments read from `src` (LDS copy or global)
+template <int D, int KT>
+__device__ __forceinline__ f32x16 tile_scores(const uint4* src, const float* Cn, int lane, int t,
                                               const bf16x8* Bm, const bf16x8* Bl, bool lo_pass) {
     using P = Plan<D>;
     bf16x8 a[P::PA];
 #pragma unroll
-    for (int p = 0; p < P::PA; ++p)
-        a[p] = *reinterpret_cast<const bf16x8*>(&As[(p * kTiles + t) * 64 + lane]);
+    for (int p = 0; p < P::PA; ++p) a[p] = frag_at<KT>(src, p, t, lane);
     return tile_scores_a<D>(a, Bm, Bl, lo_pass, tile_norms(Cn, t, lane >> 5));
 }
 
@@ -349,8 +372,11 @@ __device__ __forceinline__ int tile_row(int t, int i, int h) {
     return 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
 }
 
-template <int D, typename CodeT>
-__global__ void __launch_bounds__(64 * kWavesPerWG, PQH_ASSIGN_OCC)
+// KT = centroid tiles of 32 (8: K = 256, A fragments in LDS; 128: K = 4096, A fragments
+// streamed from L2 a few tiles ahead, no fused histogram)
+// (dsub 32 and K = 4096 hold more live state per wave: two waves per SIMD, no spills)
+template <int D, int KT, typename CodeT>
+__global__ void __launch_bounds__(64 * kWavesPerWG, (D == 32 || KT > 8) ? 2 : PQH_ASSIGN_OCC)
 pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_total,
                const bf16x8* __restrict__ afrag, const float* __restrict__ cnorm,
                const float* __restrict__ cent,
@@ -359,13 +385,18 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
                unsigned long long* __restrict__ rerank, uint32_t* __restrict__ sched, int gx,
                unsigned long long* __restrict__ rerank_next, uint32_t* __restrict__ sched_next) {
     using P = Plan<D>;
-    constexpr int K = kTiles * 32;
-    __shared__ uint32_t hist[kWavesPerWG][K];
-    // the subspace's A fragments, shared by the workgroup's waves (24 KB at D = 16): keeping
+    constexpr int K = KT * 32;
+    constexpr bool kLdsA = KT <= 8;
+    // P-key index bits (tile and half: 2 KT groups) and the key truncation they cost
+    constexpr int PB = KT <= 8 ? 4 : 8;
+    constexpr unsigned PMASK = (1u << PB) - 1;
+    static_assert(2 * KT <= (1 << PB), "P-group index must fit the key's low bits");
+    __shared__ uint32_t hist[kWavesPerWG][kLdsA ? K : 1];
+    // the subspace's A fragments, shared by the workgroup's waves (16 KB at D = 16): keeping
     // them out of VGPRs is what lets several waves share each SIMD
-    __shared__ uint4 As[P::PA * kTiles * 64];
+    __shared__ uint4 As[kLdsA ? P::PA * KT * 64 : 1];
     // ||c_k||^2 (fp32) of the subspace in accumulator order: [tile][half-wave][16 registers]
-    __shared__ __attribute__((aligned(64))) float Cn[kTiles * 2 * 16];
+    __shared__ __attribute__((aligned(64))) float Cn[KT * 2 * 16];
     // each wave's re-rank queue (the LDS budget stays at 32 KB, so a workgroup still fits on
     // a CU beside a code-table build's 112 KB)
     __shared__ uint2 rqs[kWavesPerWG][kRqLds];
@@ -398,14 +429,18 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
             __hip_atomic_store(rerank_next, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     {
-        const uint4* src = reinterpret_cast<const uint4*>(afrag) + (long long)m * P::PA * kTiles * 64;
-        for (int i = threadIdx.x; i < P::PA * kTiles * 64; i += blockDim.x) As[i] = src[i];
-        for (int i = threadIdx.x; i < kTiles * 2 * 16; i += blockDim.x)
-            Cn[i] = cnorm[(long long)m * kTiles * 2 * 16 + i];
-        if (counts)
+        const uint4* src = reinterpret_cast<const uint4*>(afrag) + (long long)m * P::PA * KT * 64;
+        if constexpr (kLdsA)
+            for (int i = threadIdx.x; i < P::PA * KT * 64; i += blockDim.x) As[i] = src[i];
+        for (int i = threadIdx.x; i < KT * 2 * 16; i += blockDim.x)
+            Cn[i] = cnorm[(long long)m * KT * 2 * 16 + i];
+        if (kLdsA && counts)
             for (int i = lane; i < K; i += 64) hist[wave][i] = 0;
         __syncthreads();   // the only workgroup barrier
     }
+    // where the A fragments come from: the LDS copy, or this subspace's slice in global
+    const uint4* const asrc =
+        kLdsA ? As : reinterpret_cast<const uint4*>(afrag) + (long long)m * P::PA * KT * 64;
 #ifdef PQH_ASSIGN_STAMPS
     const unsigned long long st0 = __builtin_amdgcn_s_memtime();
     const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
@@ -446,7 +481,8 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
             for (int j = 0; j < XD; j += 4) {
                 // (plain loads: the 8 subspaces read the two 64-B halves of each row's lines,
                 // and non-temporal loads re-fetch the line per half -- 1.6x the HBM bytes)
-                const f32x4 q = *reinterpret_cast<const f32x4*>(xp + j);
+                // HALF: piece j / 8 sits 16 dims after the previous one
+                const f32x4 q = *reinterpret_cast<const f32x4*>(xp + (HALF ? 16 * (j >> 3) + (j & 7) : j));
                 dst[j] = q.x; dst[j + 1] = q.y; dst[j + 2] = q.z; dst[j + 3] = q.w;
             }
         } else {
@@ -494,11 +530,15 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         // bits, its Q-group in the low 3).
         unsigned pm1[kNB], pm2[kNB], qg[kNB][8];
         auto load_a = [&](int t, bf16x8* a) {
+#ifdef PQH_ASSIGN_KTNOMEM   // diagnostic: every tile re-reads tile t % 4 (cache hits)
+            if constexpr (!kLdsA) t &= 3;
+#endif
 #pragma unroll
-            for (int p = 0; p < P::PA; ++p)
-                a[p] = *reinterpret_cast<const bf16x8*>(&As[(p * kTiles + t) * 64 + lane]);
+            for (int p = 0; p < P::PA; ++p) a[p] = frag_at<KT>(asrc, p, t, lane);
         };
-        auto reduce = [&](const f32x16& acc, int t, int b) {
+        // first: the tile that starts the running minima (compile-time in the unrolled
+        // K = 256 loop; the streamed K = 4096 loop starts them at +inf instead)
+        auto reduce = [&](const f32x16& acc, int t, int b, bool first) {
             unsigned a[16];
 #pragma unroll
             for (int i = 0; i < 16; ++i) a[i] = __float_as_uint(acc[i]);
@@ -507,12 +547,12 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
             // (e0, e1: the compiler-generated first reads of the tile's results, see min3d)
             const unsigned e0 = anchor_min(a[6], a[7], ninf), e1 = anchor_min(a[14], a[15], ninf);
             const unsigned k0 =
-                (min3u(min3d(a[0], a[1], a[2], e0), min3d(a[3], a[4], a[5], e0), e0) & ~15u) |
+                (min3u(min3d(a[0], a[1], a[2], e0), min3d(a[3], a[4], a[5], e0), e0) & ~PMASK) |
                 (unsigned)(2 * t);
             const unsigned k1 =
-                (min3u(min3d(a[8], a[9], a[10], e1), min3d(a[11], a[12], a[13], e1), e1) & ~15u) |
+                (min3u(min3d(a[8], a[9], a[10], e1), min3d(a[11], a[12], a[13], e1), e1) & ~PMASK) |
                 (unsigned)(2 * t + 1);
-            if (t == 0) {
+            if (first) {
                 pm1[b] = minu(k0, k1);
                 pm2[b] = maxu(k0, k1);
             } else {
@@ -524,29 +564,63 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
             // Q: running minima of the register pairs (j, j + 8)
 #pragma unroll
             for (int j = 0; j < 8; ++j)
-                qg[b][j] = t == 0 ? min3d(a[j], a[j + 8], a[j + 8], e1)
-                                  : min3d(qg[b][j], a[j], a[j + 8], e1);
+                qg[b][j] = first ? min3d(a[j], a[j + 8], a[j + 8], e1)
+                                 : min3d(qg[b][j], a[j], a[j + 8], e1);
         };
         // Software pipeline over the tiles: block b's MFMA chain for tile t + 1 is issued
         // right after its tile-t keys are reduced, so it runs while the other block's keys
         // are (the scheduling barriers keep the compiler from sinking the chain behind them).
-        bf16x8 a[P::PA];
-        load_a(0, a);
-        f32x16 cn = tile_norms(Cn, 0, h);
         f32x16 acc[kNB];
+        if constexpr (kLdsA) {
+            bf16x8 a[P::PA];
+            load_a(0, a);
+            f32x16 cn = tile_norms(Cn, 0, h);
 #pragma unroll
-        for (int b = 0; b < kNB; ++b) acc[b] = tile_scores_a<D>(a, Bm[b], Bl[b], LO, cn);
+            for (int b = 0; b < kNB; ++b) acc[b] = tile_scores_a<D>(a, Bm[b], Bl[b], LO, cn);
 #pragma unroll
-        for (int t = 0; t < kTiles; ++t) {
-            if (t + 1 < kTiles) {
-                load_a(t + 1, a);
-                cn = tile_norms(Cn, t + 1, h);
+            for (int t = 0; t < KT; ++t) {
+                if (t + 1 < KT) {
+                    load_a(t + 1, a);
+                    cn = tile_norms(Cn, t + 1, h);
+                }
+#pragma unroll
+                for (int b = 0; b < kNB; ++b) {
+                    reduce(acc[b], t, b, t == 0);
+                    if (t + 1 < KT) acc[b] = tile_scores_a<D>(a, Bm[b], Bl[b], LO, cn);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
             }
+        } else {
+            // A fragments from L2 into a ring of kRing tile sets, kRing - 1 tiles ahead of use
+            constexpr int kRing = 4;
+            static_assert(KT % kRing == 0, "the ring unrolls the tile loop");
 #pragma unroll
             for (int b = 0; b < kNB; ++b) {
-                reduce(acc[b], t, b);
-                if (t + 1 < kTiles) acc[b] = tile_scores_a<D>(a, Bm[b], Bl[b], LO, cn);
-                __builtin_amdgcn_sched_barrier(0);
+                pm1[b] = pm2[b] = 0x7F800000u;   // +inf: any key is smaller
+#pragma unroll
+                for (int j = 0; j < 8; ++j) qg[b][j] = 0x7F800000u;
+            }
+            bf16x8 ar[kRing][P::PA];
+#pragma unroll
+            for (int u = 0; u < kRing - 1; ++u) load_a(u, ar[u]);
+            f32x16 cn = tile_norms(Cn, 0, h);
+#pragma unroll
+            for (int b = 0; b < kNB; ++b) acc[b] = tile_scores_a<D>(ar[0], Bm[b], Bl[b], LO, cn);
+#pragma unroll 1
+            for (int t0 = 0; t0 < KT; t0 += kRing) {
+#pragma unroll
+                for (int u = 0; u < kRing; ++u) {
+                    const int t = t0 + u;
+                    if (t + kRing - 1 < KT) load_a(t + kRing - 1, ar[(u + kRing - 1) % kRing]);
+                    if (t + 1 < KT) cn = tile_norms(Cn, t + 1, h);
+#pragma unroll
+                    for (int b = 0; b < kNB; ++b) {
+                        reduce(acc[b], t, b, false);
+                        if (t + 1 < KT)
+                            acc[b] = tile_scores_a<D>(ar[(u + 1) % kRing], Bm[b], Bl[b], LO, cn);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                }
             }
         }
 #pragma unroll
@@ -560,7 +634,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
             top2_8(qk, q1, q2);
             const unsigned own1 = p1;
             const unsigned own2 = minu(p2, q2);
-            const int wt = (int)((p1 & 15u) >> 1);
+            const int wt = (int)((p1 & PMASK) >> 1);
             const int wi = (int)(q1 & 7u) + 8 * (int)(p1 & 1u);
             // ... then the two half-waves (lanes l and l^32 hold the same vector): after the
             // swap, s[0] holds the lower half's value and s[1] the upper half's, in every lane
@@ -572,11 +646,13 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
             const bool mine = own1 == b1;   // this half holds the winner (both: a tie -> slow)
             int code = tile_row(wt, wi, h);
             const float tau = screen_tau(X[b], any_lo[b], tq);
-            // a key differs from its score by less than 16 ulp (2^-19 relative): 2^-17 of the
-            // larger magnitude covers both keys of the gap (and the rounding of K2 - K1)
+            // a key differs from its score by less than 2^PB ulp (2^(PB-23) relative):
+            // 2^(PB-21) of the larger magnitude covers both keys of the gap (and the rounding
+            // of K2 - K1)
+            constexpr float kKeySlack = PB == 4 ? 0x1p-17f : 0x1p-13f;
             const float K1 = __uint_as_float(b1), K2 = __uint_as_float(b2);
             const float KA = fmaxf(fabsf(K1), fabsf(K2));
-            const bool slow = !(K2 - K1 > fmaf(0x1p-17f, KA, tau)) || !finite_x[b];
+            const bool slow = !(K2 - K1 > fmaf(kKeySlack, KA, tau)) || !finite_x[b];
 
             unsigned long long need = __ballot(slow && valid[b] && h == 0);
             bool deferred = false;
@@ -589,7 +665,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
                 const unsigned cnt = (unsigned)__popcll(fin);
                 if (PQH_ASSIGN_DEFER && cnt && qn + cnt <= (unsigned)kRqLds) {
                     if (slow && valid[b] && h == 0 && finite_x[b]) {
-                        const float thr = fmaf(0x1p-16f, fabsf(K1), K1 + tau);
+                        const float thr = fmaf(2.0f * kKeySlack, fabsf(K1), K1 + tau);
                         rqs[wave][qn + __builtin_amdgcn_mbcnt_hi((unsigned)(fin >> 32),
                                       __builtin_amdgcn_mbcnt_lo((unsigned)fin, 0u))] =
                             make_uint2((uint32_t)v[b], __float_as_uint(thr));
@@ -627,7 +703,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
             // unless the vector waits in the queue
             if (valid[b] && (slow ? (h == 0 && !deferred) : mine)) {
                 codes[v[b] * m_total + m] = (CodeT)code;
-                if (counts) atomicAdd(&hist[wave][code], 1u);
+                if (kLdsA && counts) atomicAdd(&hist[wave][code], 1u);
             }
         }
     };
@@ -774,7 +850,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         }
         float xs[XD];
 #pragma unroll
-        for (int j = 0; j < XD; ++j) xs[j] = valid ? xv[HALF ? (h ? 8 + j : j) : j] : 0.0f;
+        for (int j = 0; j < XD; ++j) xs[j] = valid ? xv[Slice<D>::dim(j, h)] : 0.0f;
         float X;
         bool lo;
         float xh[XD], xl[XD];
@@ -786,8 +862,8 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         float best = INFINITY;
         int bidx = 0x7FFFFFFF;
 #pragma unroll 1
-        for (int t = 0; t < kTiles; ++t) {   // (rolled: the tail keeps its registers few)
-            const f32x16 acc = tile_scores<D>(As, Cn, lane, t, Bm, Bl, lo_pass);
+        for (int t = 0; t < KT; ++t) {   // (rolled: the tail keeps its registers few)
+            const f32x16 acc = tile_scores<D, KT>(asrc, Cn, lane, t, Bm, Bl, lo_pass);
             uint32_t bits = 0;
 #pragma unroll
             for (int i = 0; i < 16; ++i) bits |= (acc[i] <= thr ? 1u : 0u) << i;
@@ -808,7 +884,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         if (valid && h == 0) {
             const int code = bidx == 0x7FFFFFFF ? 0 : bidx;
             codes[v * m_total + m] = (CodeT)code;
-            if (counts) atomicAdd(&hist[wave][code], 1u);
+            if (kLdsA && counts) atomicAdd(&hist[wave][code], 1u);
         }
     }
 #ifdef PQH_ASSIGN_STAMPS
@@ -822,7 +898,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         }
     }
 #endif
-    if (counts) {
+    if (kLdsA && counts) {
         __builtin_amdgcn_wave_barrier();
         for (int i = lane; i < K; i += 64) {
             uint32_t c = hist[wave][i];
@@ -956,21 +1032,22 @@ void build_afrag(const float* c, int k, std::vector<uint16_t>& out, std::vector<
     }
     cmax_out = (float)(cmax * (1.0 + 1e-6)) + 1e-30f;
     // fragment order [m][PA][tile][lane][8]
-    const size_t base = (size_t)m * P::PA * kTiles * 64 * 8;
+    const int kt = k / 32;
+    const size_t base = (size_t)m * P::PA * kt * 64 * 8;
     for (int p = 0; p < P::PA; ++p)
-        for (int t = 0; t < kTiles; ++t)
+        for (int t = 0; t < kt; ++t)
             for (int lane = 0; lane < 64; ++lane)
                 for (int j = 0; j < 8; ++j) {
                     int row = 32 * t + (lane & 31);
                     int slot = 16 * p + 8 * (lane >> 5) + j;
-                    out[base + (((size_t)p * kTiles + t) * 64 + lane) * 8 + j] =
+                    out[base + (((size_t)p * kt + t) * 64 + lane) * 8 + j] =
                         main[(size_t)row * slots + slot];
                 }
     // accumulator register i of half-wave h holds row tile_row(t, i, h)
-    for (int t = 0; t < kTiles; ++t)
+    for (int t = 0; t < kt; ++t)
         for (int h = 0; h < 2; ++h)
             for (int i = 0; i < 16; ++i)
-                cn[(size_t)m * kTiles * 32 + (t * 2 + h) * 16 + i] =
+                cn[(size_t)m * kt * 32 + (t * 2 + h) * 16 + i] =
                     (float)norm[32 * t + (i & 3) + 8 * (i >> 2) + 4 * h];
 }
 
@@ -984,6 +1061,7 @@ int plan_pa(int dsub) {
         case 8: return pa_of<8>();
         case 12: return pa_of<12>();
         case 16: return pa_of<16>();
+        case 32: return pa_of<32>();
         default: return 0;
     }
 }
@@ -1007,32 +1085,48 @@ int launch_mfma(pqh_ctx* ctx, pqh_pq* pq, const float* x, long long n, long long
 #endif
     // grid = the workgroups that are resident at once (persistent, grid-stride over the
     // 32-vector blocks): more would only queue behind the first wave of workgroups
-#define PQH_CASE(DD)                                                                        \
+#define PQH_CASE(DD) PQH_CASE_KT(DD, 8)
+#define PQH_CASE_KT(DD, KTT)                                                                \
     case DD: {                                                                              \
         int per_cu = 1;                                                                     \
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(                                   \
-                &per_cu, (const void*)(pq_assign_mfma<DD, CodeT>), (int)block.x, 0) !=      \
+                &per_cu, (const void*)(pq_assign_mfma<DD, KTT, CodeT>), (int)block.x, 0) != \
                 hipSuccess || per_cu < 1)                                                   \
             per_cu = 1;                                                                     \
         long long gx = (long long)ctx->num_cus * per_cu / groups;                           \
         gx = std::max(1ll, std::min(gx, ((nblk + kNB - 1) / kNB + kWavesPerWG - 1) / kWavesPerWG)); \
         if (gx >= 16) gx &= ~7ll;   /* CU-uniform subspace placement (see the kernel) */   \
-        hipLaunchKernelGGL((pq_assign_mfma<DD, CodeT>), dim3((unsigned)(gx * groups)), block, \
+        hipLaunchKernelGGL((pq_assign_mfma<DD, KTT, CodeT>), dim3((unsigned)(gx * groups)), block, \
                            0, ctx->stream, x, n, ldx, pq->m, pq->d_afrag, pq->d_cn, pq->d_cent, \
                            pq->d_cmax, pq->d_sqc, codes, counts, rr, sched, (int)gx,         \
                            rr_next, sched ? ctx->d_sched + (1 - ring) * kSchedSet : nullptr); \
         PQH_LAUNCH_CHECK(ctx);                                                              \
         break;                                                                              \
     }
-    switch (pq->dsub) {
-        PQH_CASE(4)
-        PQH_CASE(6)
-        PQH_CASE(8)
-        PQH_CASE(12)
-        PQH_CASE(16)
-        default: return PQH_ERR_UNSUPPORTED;
+    if (pq->k == 4096) {   // A fragments streamed from L2; u16 codes; no fused histogram
+        if constexpr (sizeof(CodeT) == 2) {
+            switch (pq->dsub) {
+                PQH_CASE_KT(16, 128)
+                default: return PQH_ERR_UNSUPPORTED;
+            }
+        } else {
+            return PQH_ERR_UNSUPPORTED;
+        }
+    } else if constexpr (sizeof(CodeT) == 1) {
+        switch (pq->dsub) {
+            PQH_CASE(4)
+            PQH_CASE(6)
+            PQH_CASE(8)
+            PQH_CASE(12)
+            PQH_CASE(16)
+            PQH_CASE(32)
+            default: return PQH_ERR_UNSUPPORTED;
+        }
+    } else {
+        return PQH_ERR_UNSUPPORTED;
     }
 #undef PQH_CASE
+#undef PQH_CASE_KT
     PQH_LAUNCH_CHECK(ctx);
     return PQH_OK;
 }
@@ -1067,15 +1161,16 @@ int pqh_pq_create(pqh_ctx_t* ctx, const float* centroids, int m, int k, int dsub
     bool finite = true;
     for (size_t i = 0; i < nc; ++i) finite &= std::isfinite(centroids[i]);
     const int pa = plan_pa(dsub);
-    pq->mfma_ok = finite && k == 256 && pa > 0;
+    // MFMA screening: K = 256 at dsub 4, 6, 8, 12, 16, 32; K = 4096 at dsub 16
+    pq->mfma_ok = finite && pa > 0 && (k == 256 || (k == 4096 && dsub == 16));
     if (hipMalloc(&pq->d_cent, nc * sizeof(float)) != hipSuccess) {
         delete pq;
         return pqh_set_error(ctx, PQH_ERR_NOMEM, "hipMalloc centroids");
     }
     (void)hipMemcpy(pq->d_cent, centroids, nc * sizeof(float), hipMemcpyHostToDevice);
     if (pq->mfma_ok) {
-        std::vector<uint16_t> frag((size_t)m * pa * kTiles * 64 * 8);
-        std::vector<float> cn((size_t)m * kTiles * 32);
+        std::vector<uint16_t> frag((size_t)m * pa * (k / 32) * 64 * 8);
+        std::vector<float> cn((size_t)m * (k / 32) * 32);
         std::vector<float> cmax(m), sqc(m);
         for (int i = 0; i < m; ++i) {
             const float* c = centroids + (size_t)i * k * dsub;
@@ -1085,6 +1180,7 @@ int pqh_pq_create(pqh_ctx_t* ctx, const float* centroids, int m, int k, int dsub
                 case 8: build_afrag<8>(c, k, frag, cn, i, cmax[i]); break;
                 case 12: build_afrag<12>(c, k, frag, cn, i, cmax[i]); break;
                 case 16: build_afrag<16>(c, k, frag, cn, i, cmax[i]); break;
+                case 32: build_afrag<32>(c, k, frag, cn, i, cmax[i]); break;
             }
             sqc[i] = (float)(std::sqrt((double)cmax[i]) * (1.0 + 1e-6)) + 1e-30f;
         }
@@ -1142,7 +1238,13 @@ int pqh_pq_assign(pqh_ctx_t* ctx, const pqh_pq_t* cpq, const float* d_x, long lo
         return mfma ? launch_mfma(ctx, pq, d_x, n, ld_x, c, d_counts)
                     : launch_exact(ctx, pq, d_x, n, ld_x, c, d_counts);
     }
-    return launch_exact(ctx, pq, d_x, n, ld_x, static_cast<uint16_t*>(d_codes), d_counts);
+    uint16_t* c16 = static_cast<uint16_t*>(d_codes);
+    if (!mfma) return launch_exact(ctx, pq, d_x, n, ld_x, c16, d_counts);
+    // K = 4096: the screening kernel keeps no per-workgroup histogram (16 KB of counters per
+    // wave); the requested counts come from the histogram kernel over the codes just written
+    rc = launch_mfma(ctx, pq, d_x, n, ld_x, c16, nullptr);
+    if (rc || !d_counts) return rc;
+    return pqh_histogram(ctx, d_codes, n, pq->m, pq->k, 0, nullptr, d_counts);
 }
 
 // diagnostics: the per-wave stamps of the last assignment launch (PQH_ASSIGN_STAMPS builds;

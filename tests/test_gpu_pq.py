@@ -36,14 +36,18 @@ def test_assign_golden(gpu, name, mode):
 
 
 @pytest.mark.parametrize("kind,d,m", [("sift", 128, 8), ("deep", 96, 16), ("deep", 96, 8),
-                                      ("sift", 128, 16), ("sift", 128, 32), ("sift", 64, 4)])
+                                      ("sift", 128, 16), ("sift", 128, 32), ("sift", 64, 4),
+                                      ("sift", 128, 4), ("deep", 96, 3)])
 def test_assign_vs_oracle_random(gpu, oracle, kind, d, m):
+    """Every dsub the MFMA kernel serves (4, 6, 8, 12, 16, 32): codes == oracle; the
+    screening ran (near ties were re-ranked: the exact-only kernel reports none)."""
     n = 6001  # not a multiple of 32
     x = datagen.sift_like(n, d, seed=11) if kind == "sift" else datagen.deep_like(n, d, seed=12)
     cent = datagen.lloyd_centroids(x, m, 256, iters=2, sample=4000, seed=3)
     want, _ = oracle.pq_assign(x, cent, threads=0)
     got, rr = _assign(gpu, x, cent, 0)
     assert np.array_equal(got, want), (got != want).sum()
+    assert rr > 0
     got1, _ = _assign(gpu, x, cent, 1)
     assert np.array_equal(got1, want)
 
@@ -99,6 +103,32 @@ def test_assign_small_and_ragged(gpu, oracle):
         want, _ = oracle.pq_assign(x[:n], cent)
         got, _ = _assign(gpu, x[:n], cent)
         assert np.array_equal(got, want), n
+
+
+@pytest.mark.parametrize("kind", ["sift", "deep"])
+def test_assign_k4096_vs_oracle(gpu, oracle, kind):
+    """K = 4,096 (u16 codes, BASELINE configs[4]): the MFMA screening with centroid tiles
+    streamed from L2 == the oracle, with the counts the call asked for, and the exact kernel
+    agrees; first-index ties among duplicated centroids and non-finite rows too."""
+    torch, codec, ctx = gpu
+    n = 3001
+    x = datagen.sift_like(n, 128, seed=51) if kind == "sift" else datagen.deep_like(n, 128, seed=52)
+    rng = np.random.default_rng(53)
+    rows = x[rng.choice(n, 2048, replace=False)].reshape(2048, 8, 16).transpose(1, 0, 2)
+    cent = np.concatenate([rows, rows + rng.normal(0, 0.3, rows.shape)], axis=1)
+    cent = np.ascontiguousarray(cent).astype(np.float32)          # (8, 4096, 16)
+    cent[:, 4000:4096] = cent[:, 100:196]                          # duplicates: ties
+    x[7, 5] = np.nan
+    x[8, 60] = np.inf
+    want, _ = oracle.pq_assign(x, cent, threads=0)
+    counts = torch.zeros((8, 4096), dtype=torch.int32, device="cuda")
+    got, rr = _assign(gpu, x, cent, 0, counts)
+    got = got.view(np.uint16)                      # (torch keeps u16 codes as int16)
+    assert np.array_equal(got, want.astype(np.uint16)), (got != want).sum()
+    assert rr > 0
+    assert np.array_equal(codec.counts_to_host(counts), oracle.histogram(want, 4096, False))
+    got1, rr1 = _assign(gpu, x, cent, 1)
+    assert np.array_equal(got1.view(np.uint16), want.astype(np.uint16)) and rr1 == 0
 
 
 def test_assign_k_not_256_uses_exact_kernel(gpu, oracle):
