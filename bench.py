@@ -66,6 +66,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--vectors", type=int, default=1_000_000, help="vectors per GPU")
     ap.add_argument("--mode", choices=["ctx", "noctx"], default="ctx")
+    ap.add_argument("--config", choices=["sift", "deep", "k4096"], default="sift",
+                    help="sift: BASELINE configs[1]/[2] (128-d, M=8, K=256; the headline); "
+                         "deep: configs[3] (96-d unit-norm, M=16, K=256); k4096: configs[4] "
+                         "(128-d, M=8, K=4096, u16 codes, non-context)")
     ap.add_argument("--chunk", type=int, default=8,
                     help="vectors per decode chunk (chunk-index sidecar granularity)")
     ap.add_argument("--cpu-sample", type=int, default=200_000)
@@ -129,6 +133,25 @@ def make_data(torch, n, d, seed, rank, device):
     return x
 
 
+def make_deep(torch, n, d, seed, rank, device):
+    """Deep1B-style shard: a Gaussian mixture of 1,024 centres with
+    Zipf(1.1) weights, rows normalised to unit length; generated on the device in chunks."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    mu = torch.randn((1024, d), generator=g, device=device)
+    w = 1.0 / torch.arange(1, 1025, dtype=torch.float64, device=device) ** 1.1
+    w = w / w.sum()
+    x = torch.empty((n, d), dtype=torch.float32, device=device)
+    for c, r0 in enumerate(range(0, n, GEN_CHUNK)):
+        r1 = min(n, r0 + GEN_CHUNK)
+        g.manual_seed(seed * 1000003 + rank + c * 7919 * 1000003)
+        lab = torch.multinomial(w, r1 - r0, replacement=True, generator=g)
+        xc = mu[lab] + 0.35 * torch.randn((r1 - r0, d), generator=g, device=device)
+        x[r0:r1] = torch.nn.functional.normalize(xc, dim=1)
+        del lab, xc
+    return x
+
+
 def train_centroids(torch, x, m, k, iters=4, sample=50_000, seed=7):
     """Setup only (not timed): Lloyd iterations on a device sample, float64 accumulation.
     Centroid sums are taken on the host so the setup is deterministic run to run."""
@@ -159,7 +182,7 @@ def cpu_leg(orc, xs, cent, ctxm, threads):
     t0 = time.perf_counter()
     codes, _ = orc.pq_assign(xs, cent, threads=threads)
     t1 = time.perf_counter()
-    cbs = orc.build_codebooks(codes, 256, ctxm)
+    cbs = orc.build_codebooks(codes, cent.shape[1], ctxm)
     stream, bits = orc.encode(codes, cbs)
     t2 = time.perf_counter()
     dec = orc.decode(stream, len(codes), codes.shape[1], cbs)
@@ -190,7 +213,8 @@ def cpu_baseline(x_host, cent, ctxm, sample):
     orc.use_build("O2")
     mode = "context" if ctxm else "non-context"
     return {"value": one["value"], "unit": "Mvec/s", "cores": 1, "kind": "port",
-            "sample": f"{sample} vectors of the rank-0 shard, M=8 K=256 {mode}: oracle assign "
+            "sample": f"{sample} vectors of the rank-0 shard, M={cent.shape[0]} "
+                      f"K={cent.shape[1]} {mode}: oracle assign "
                       f"+ histogram + codebooks + bit-serial encode + trie decode, single "
                       f"thread -O2",
             "stages_s": one["stages_s"],
@@ -248,11 +272,15 @@ def main():
     else:
         torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    ctxm = args.mode == "ctx"
-    n, d, m, k = args.vectors, 128, 8, 256
+    n = args.vectors
+    d, m, k = {"sift": (128, 8, 256), "deep": (96, 16, 256), "k4096": (128, 8, 4096)}[args.config]
+    ctxm = args.mode == "ctx" and k == 256     # context coding needs K = 256
+    gen = make_deep if args.config == "deep" else make_data
+    code_t = torch.uint8 if k <= 256 else torch.int16   # (u16 codes live in int16 tensors)
+    code_bytes = 1 if k <= 256 else 2
 
-    x = make_data(torch, n, d, 0x5EED, rank, dev)
-    cent = train_centroids(torch, make_data(torch, 200_000, d, 0x5EED, 0, dev), m, k)
+    x = gen(torch, n, d, 0x5EED, rank, dev)
+    cent = train_centroids(torch, gen(torch, 200_000, d, 0x5EED, 0, dev), m, k)
     if world > 1:   # one quantizer for the whole job: rank 0's centroids
         ct = torch.from_numpy(cent).to(dev)
         dist.broadcast(ct, 0)
@@ -287,7 +315,7 @@ def main():
     # codes / counts buffers: the assignment runs up to `slots` batches ahead of the oldest
     # batch not yet encoded
     slots = nl + max(1, args.extra_slots)
-    codes = [torch.empty((n, m), dtype=torch.uint8, device=dev) for _ in range(slots)]
+    codes = [torch.empty((n, m), dtype=code_t, device=dev) for _ in range(slots)]
     counts = [torch.zeros((m, items), dtype=torch.int32, device=dev) for _ in range(slots)]
     halo = [None] * slots
     ev_hist = [torch.cuda.Event() for _ in range(slots)]
@@ -303,7 +331,7 @@ def main():
 
     def tab_index(i):
         return (i % nl) * nbuf + (i // nl) % nbuf
-    dec = [torch.empty((n, m), dtype=torch.uint8, device=dev) for _ in elanes]
+    dec = [torch.empty((n, m), dtype=code_t, device=dev) for _ in elanes]
     coff = [torch.empty(chunks, dtype=torch.int64, device=dev) for _ in elanes]
     cprev = [torch.empty((chunks, m), dtype=torch.uint8, device=dev) if ctxm else None
              for _ in elanes]
@@ -493,11 +521,27 @@ def main():
 
     if rank == 0:
         t_assign = acc["assign"] / args.steps
-        achieved = (BYTES_PER_VEC_READ + BYTES_PER_VEC_WRITE) * n / t_assign / 1e9
+        vec_read, vec_write = 4 * d, m * code_bytes
+        achieved = (vec_read + vec_write) * n / t_assign / 1e9
         traffic, traffic_src, prof_avg_us = pmc_traffic("pq_assign_mfma")
         t_enc = (acc["assign"] + acc["hist"] + acc["codebook"] + acc["encode"]) / args.steps
+        tf = 2.0 * k * d * n / t_assign / 1e12   # algorithmic: 2 K D flop per vector
+        workload = {
+            "sift": f"SIFT1M-shaped: {n:,} x 128-d fp32 per GPU, M=8, K=256, ",
+            "deep": f"Deep1B-style (BASELINE configs[3]): {n:,} x 96-d unit-norm fp32 per GPU, "
+                    "M=16, K=256 (dsub 6), ",
+            "k4096": f"large codebook (BASELINE configs[4]): {n:,} x 128-d fp32 per GPU, M=8, "
+                     "K=4096 (12-bit codes stored u16), "}[args.config]
+        data = {
+            "sift": "synthetic SIFT-like (integer-valued fp32 in [0,255], Gaussian mixture, "
+                    "Zipf(1.1) weights), generated on device",
+            "deep": "synthetic Deep-like (Gaussian mixture of 1,024 centres, Zipf(1.1) weights, "
+                    "rows normalised to unit length), generated on device",
+            "k4096": "synthetic SIFT-like (integer-valued fp32 in [0,255], Gaussian mixture, "
+                     "Zipf(1.1) weights), generated on device"}[args.config]
         res = {
-            "metric": METRIC,
+            "metric": METRIC if args.config == "sift" else
+            f"Mvec/s encode+decode round-trip, {d}-d fp32 M={m} K={k}; % HBM-read roofline",
             "value": round(world * n * args.steps / elapsed / 1e6, 2),
             "unit": "Mvec/s",
             "n_gpus": world,
@@ -508,13 +552,12 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic SIFT-like (integer-valued fp32 in [0,255], Gaussian mixture, "
-                    "Zipf(1.1) weights), generated on device; centroids from 4 Lloyd "
-                    "iterations on a 50k sample (setup, untimed)",
-            "config": {"workload": "SIFT1M-shaped: 1,000,000 x 128-d fp32 per GPU, M=8, K=256, "
+            "data": data + "; centroids from 4 Lloyd iterations on a 50k sample (setup, untimed)",
+            "config": {"workload": workload
                                    + ("order-1 context Huffman (reference default coding), "
                                       "no sort" if ctxm else "non-context Huffman, no sort"),
-                       "vectors_per_gpu": n, "m": m, "k": k, "mode": args.mode,
+                       "vectors_per_gpu": n, "d": d, "m": m, "k": k,
+                       "mode": "ctx" if ctxm else "noctx",
                        "chunk_vectors": args.chunk, "parallelism": f"dp{world} row shards",
                        "schedule": ("serial" if serial else
                                     f"lanes: assignment + histogram of every batch on one stream; "
@@ -526,11 +569,14 @@ def main():
                          # what actually limits the kernel (PMC): the
                          # wave64 VALU issue of the top-2 key reduction, ~4 cycles each
                          "limiter": "VALU issue (top-2 key reduction), not HBM",
-                         "mfma_tflops_algorithmic": round(65536 * n / t_assign / 1e12, 1),
+                         "mfma_tflops_algorithmic": round(tf, 1),
+                         # of the dense bf16 peak (~2.5 PF/s); each fp32 product costs two or
+                         # three bf16 MFMA passes (the hi/lo split), so issued MFMA work is 2-3x
+                         "mfma_frac_bf16_dense": round(tf / 2500.0, 4),
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "bytes_per_vector": BYTES_PER_VEC_READ + BYTES_PER_VEC_WRITE,
+                         "bytes_per_vector": vec_read + vec_write,
                          "avg_ms": round(t_assign * 1e3, 4),
                          # rocprofv3 kernel-trace average of this bench command (dispatch
                          # begin -> end); avg_ms above is HIP events around the launch on its
@@ -544,9 +590,9 @@ def main():
             # encode-side HBM-read roofline = 512 B/vec x N / t_encode / 8 TB/s, with
             # t_encode = the summed encode-side stage times of one batch (latency view) and,
             # for the throughput view, the whole round-trip step time
-            "encode_read_roofline_frac": round(BYTES_PER_VEC_READ * n / t_enc / 1e9 / HBM_PEAK_GBS, 4),
+            "encode_read_roofline_frac": round(vec_read * n / t_enc / 1e9 / HBM_PEAK_GBS, 4),
             "roundtrip_read_roofline_frac": round(
-                BYTES_PER_VEC_READ * n * world * args.steps / elapsed / 1e9 / HBM_PEAK_GBS / world, 4),
+                vec_read * n * world * args.steps / elapsed / 1e9 / HBM_PEAK_GBS / world, 4),
             "host_issue_ms_per_step": round(t_issue / args.steps * 1e3, 3),
             "bits_per_vector": round(bits_per_vec, 3),
             "rerank_fraction": round(rerank / (n * m), 6),
@@ -558,8 +604,9 @@ def main():
                                      (bits_per_vec * r1 + 7) // 8)
             res["pcie_ms"]["rows"] = r1
         if not args.no_cpu_baseline and world == 1:
-            xh = x[:args.cpu_sample].cpu().numpy()
-            res["cpu_baseline"] = cpu_baseline(xh, cent, ctxm, args.cpu_sample)
+            sample = max(1000, args.cpu_sample * 256 // k)   # ~the same CPU time at any K
+            xh = x[:sample].cpu().numpy()
+            res["cpu_baseline"] = cpu_baseline(xh, cent, ctxm, sample)
             res["cpu_baseline"]["host_cpu"] = _cpu_name()
             res["cpu_baseline"]["nproc"] = os.cpu_count()
         print(json.dumps(res), flush=True)

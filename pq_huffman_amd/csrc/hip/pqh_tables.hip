@@ -1215,8 +1215,13 @@ int pqh_tables_alloc(pqh_ctx_t* ctx, int m, int k, int context, pqh_tables_t** o
     t->items = (long long)t->roots * k;
     t->tables = (long long)m * t->roots;
     t->l1_bits = context ? 9 : kL1Max;   // 1 KB first level per context alphabet
-    t->l2_bits = 8;
-    t->lut2_cap = std::min<long long>(t->tables * 2048 + 65536, kL2BaseMax - 1);
+    // Second-level width: 8 bits for K <= 256 (codes past W1 + 8 bits are rare); 12 bits
+    // for larger alphabets, whose rarest symbols sit ~log2(N) bits deep -- with 8 bits
+    // (19 covered) a K = 4096 stream spent its decode in the long-code list (133 ms per
+    // 1M vectors).  A larger pool for those few alphabets.
+    t->l2_bits = k > 256 ? 12 : 8;
+    t->lut2_cap = std::min<long long>(k > 256 ? t->tables * (1ll << 20) : t->tables * 2048 + 65536,
+                                      kL2BaseMax - 1);
     if (hipMalloc(&t->d_enc, (size_t)m * t->items * 8) != hipSuccess ||
         hipMalloc(&t->d_enc32, (size_t)m * t->items * 4) != hipSuccess ||
         hipMalloc(&t->d_lut1, (size_t)(t->tables << kL1Max) * 2) != hipSuccess ||
