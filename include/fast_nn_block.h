@@ -1,7 +1,8 @@
 /*
  * fast_nn_block.h -- drop-in for the reference's src/fast_nn_block.h:4-25: a growable
  * batch of vectors with global row ids.  On the GPU path a block_t is the host-side
- * shard descriptor (row range [id, id+size) of the input); see pqh.h pqh_shard_t.
+ * shard descriptor (row range [id, id+size) of the input); see pqh.h pqh_shard_block and
+ * pqh_shard_encode.
  */
 #ifndef _FAST_NN_BLOCK_H_
 #define _FAST_NN_BLOCK_H_

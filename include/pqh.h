@@ -23,6 +23,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "fast_nn_block.h"
 #include "huffman.h"
 
 #ifdef __cplusplus
@@ -200,6 +201,68 @@ int pqh_chunk_index_host(const pqh_tables_t* t, const unsigned char* stream,
 /* Stable sort of the n rows by key(row) = row with every byte after its first 0 zeroed
  * (strncmp order), uint8 codes only.  d_tmp: n*m bytes scratch. */
 int pqh_sort_rows(pqh_ctx_t* ctx, void* d_codes, long long n, int m, void* d_tmp);
+
+/* ---- multi-GPU row shards ------------------------------------------
+ * One process per GPU; rank r owns a contiguous row range, described by a block_t
+ * (src/fast_nn_block.h:4-25: id = first global row, size = rows; data / indices unused on
+ * the device path).  The only exchanges are small: the one-row halo (context mode), the
+ * histogram all-reduce that feeds the shared code tables (huffman_encoder.c:139-205 over
+ * the whole input), and an all-gather of the shards' bit lengths whose exclusive scan places
+ * every shard in the global stream (the bit cursor of bitstream.c:71-101).  The transport is
+ * the caller's communicator, passed as hooks (RCCL, MPI, torch.distributed, gloo ...). */
+
+/* rank `rank`'s rows of n_total over `world` ranks: sizes differ by at most one row.
+ * Fills block->id / size (capacity = size, num_dimensions 0, data / indices NULL). */
+int pqh_shard_block(long long n_total, int world, int rank, block_t* block);
+
+/* Collective hooks over DEVICE buffers, ordered on `stream` (the context's): return 0 on
+ * success.  all_reduce_sum_u32: in-place sum over ranks; all_gather: d_recv[world][bytes]
+ * = every rank's d_send[bytes], in rank order. */
+typedef struct {
+    void* user;
+    int world, rank;
+    int (*all_reduce_sum_u32)(void* user, uint32_t* d_buf, long long count, void* stream);
+    int (*all_gather)(void* user, const void* d_send, void* d_recv, long long bytes,
+                      void* stream);
+} pqh_shard_comm_t;
+
+/* Scratch bytes pqh_shard_encode needs in d_scratch (device, 16-byte aligned). */
+long long pqh_shard_scratch_bytes(int world, int m);
+
+/* One rank's encode of its shard (uint8 codes, K <= 256 -- context mode needs K = 256):
+ *   context mode: all-gather of every rank's (non-empty flag, last row) -> the halo of this
+ *     shard = the last row of the nearest non-empty rank before it, and the raw first row
+ *     (huffman_encoder.c:234) belongs to the first non-empty rank (one host read of the
+ *     flags: a shard may be empty, e.g. a slice of the distributed sort);
+ *   histogram of the shard (+ the halo pair) -> all_reduce_sum_u32 -> GPU code tables
+ *   (identical on every rank: no broadcast) -> the shard's exact bit length -> all_gather
+ *   of the lengths -> exclusive scan on the device -> pqh_encode_write_at.
+ * Outputs: d_counts [m][items] the GLOBAL histogram; tables built from it; d_out holds the
+ * shard's bits at (global offset % 32) with word 0 = the global stream's word offset / 32
+ * (buffers compose by OR-ing boundary words: pqh_shard_stitch); d_offsets[2] (device u64) =
+ * {this shard's global bit offset, the global stream's length in bits}; the chunk index
+ * (optional, chunk_vectors > 0) is relative to d_out bit 0.  *raw_first (may be NULL)
+ * reports whether this shard wrote the raw first row. */
+int pqh_shard_encode(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm, const block_t* shard,
+                     const void* d_codes, int m, int k, int context, pqh_tables_t* tables,
+                     uint32_t* d_counts, unsigned char* d_out, unsigned long long out_bytes,
+                     int chunk_vectors, unsigned long long* d_chunk_offsets, void* d_chunk_prev,
+                     unsigned long long* d_offsets, void* d_scratch, int* raw_first);
+
+/* Host: (this rank's global bit offset, the global length) from every rank's bit length. */
+int pqh_shard_offsets(const unsigned long long* lengths, int world, int rank,
+                      unsigned long long* offset, unsigned long long* total);
+/* Host: the global stream (huffman_indices.bin after its 8-byte header) from the ranks'
+ * shard buffers: buffer r holds its bits at offsets[r] % 32, its byte 0 being global byte
+ * (offsets[r] / 32) * 4; bits outside each range are zero.  out (zeroed here) needs
+ * ceil(sum(bits) / 8) bytes. */
+int pqh_shard_stitch(int world, const unsigned char* const* bufs,
+                     const unsigned long long* offsets, const unsigned long long* bits,
+                     unsigned char* out, unsigned long long out_bytes);
+/* Host: for shards that may be empty (sorted slices): the rank whose last row is this
+ * shard's halo (-1: none) and whether this shard writes the raw first row. */
+int pqh_shard_halo_source(const int* nonempty, int world, int rank, int* prev_rank,
+                          int* raw_first);
 
 /* ---- tree-ordered context coding (huffman_encoder.c --tree: :240-286, :321-375) ---- */
 /* DFS order of a stored forest (mst.tree: tree_load_file, mst.c:273-288 -- num_edges

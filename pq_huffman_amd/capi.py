@@ -53,6 +53,18 @@ class Block(ctypes.Structure):                    # fast_nn_block.h block_t
                 ("data", ctypes.POINTER(ctypes.c_float)), ("size", ctypes.c_longlong)]
 
 
+# pqh.h pqh_shard_comm_t: collective hooks over device buffers
+ALL_REDUCE_U32 = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                  ctypes.c_longlong, ctypes.c_void_p)
+ALL_GATHER = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                              ctypes.c_longlong, ctypes.c_void_p)
+
+
+class ShardComm(ctypes.Structure):
+    _fields_ = [("user", ctypes.c_void_p), ("world", ctypes.c_int), ("rank", ctypes.c_int),
+                ("all_reduce_sum_u32", ALL_REDUCE_U32), ("all_gather", ALL_GATHER)]
+
+
 class EncodeOptions(ctypes.Structure):            # pqh.h pqh_encode_options_t
     _fields_ = [("context", I), ("sort", I), ("chunk_vectors", I), ("only_estimate", I)]
 
@@ -124,6 +136,11 @@ SIGNATURES = [
     ("pqh_decode_status", I, [P]), ("pqh_encode_status", I, [P]),
     ("pqh_chunk_index_host", I, [P, P, ULL, LL, I, I, P, P]),
     ("pqh_sort_rows", I, [P, P, LL, I, P]),
+    ("pqh_shard_block", I, [LL, I, I, P]), ("pqh_shard_scratch_bytes", LL, [I, I]),
+    ("pqh_shard_encode", I, [P, P, P, P, I, I, I, P, P, P, ULL, I, P, P, P, P, P]),
+    ("pqh_shard_offsets", I, [P, I, I, P, P]),
+    ("pqh_shard_stitch", I, [I, P, P, P, P, ULL]),
+    ("pqh_shard_halo_source", I, [P, I, I, P, P]),
     ("pqh_tree_order", I, [LL, LL, P, P, P, P, P]),
     ("pqh_tree_gather", I, [P, P, LL, I, I, P, P, P, P]),
     ("pqh_tree_status", I, [P]),

@@ -1,0 +1,178 @@
+// pqh_shard.hip -- the multi-GPU row-shard protocol of the encode path behind the C ABI
+// (include/pqh.h "multi-GPU row shards").
+//
+// The reference encodes one file on one host (huffman_encoder.c:139-238); sharded over
+// ranks the only data that crosses ranks is small:
+//   * the one-row halo: the pair (last row of the previous shard, first row of this one) is
+//     counted (huffman_encoder.c:166-205) and coded with that row as context (:220-238), and
+//     only the shard holding global row 0 writes it raw (:234);
+//   * the histogram all-reduce feeding the shared code tables (built identically on every
+//     rank, so no broadcast);
+//   * an all-gather of the shards' bit lengths, whose exclusive scan is the bit cursor of
+//     bitstream.c:71-101 at each shard's start.
+// The transport is the caller's (pqh_shard_comm_t hooks over device buffers).
+#include <cstring>
+#include <vector>
+
+#include "pqh_internal.h"
+
+namespace {
+
+// d_offsets = {sum of the lengths of the ranks before `rank`, sum of all lengths}
+__global__ void shard_prefix(const unsigned long long* __restrict__ lengths, int world, int rank,
+                             unsigned long long* __restrict__ offsets) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    unsigned long long before = 0, all = 0;
+    for (int r = 0; r < world; ++r) {
+        before += r < rank ? lengths[r] : 0ull;
+        all += lengths[r];
+    }
+    offsets[0] = before;
+    offsets[1] = all;
+}
+
+constexpr long long kHaloData = 16;   // a halo record: flag byte, pad, the row at byte 16
+
+long long halo_record_bytes(int m) { return ((kHaloData + m + 15) / 16) * 16; }
+
+}  // namespace
+
+extern "C" {
+
+int pqh_shard_block(long long n_total, int world, int rank, block_t* block) {
+    if (!block || n_total < 0 || world <= 0 || rank < 0 || rank >= world) return PQH_ERR_ARG;
+    const long long base = n_total / world, extra = n_total % world;
+    block->id = (long long)rank * base + (rank < extra ? rank : extra);
+    block->size = base + (rank < extra ? 1 : 0);
+    block->capacity = block->size;
+    block->num_dimensions = 0;
+    block->data = nullptr;
+    block->indices = nullptr;
+    return PQH_OK;
+}
+
+long long pqh_shard_scratch_bytes(int world, int m) {
+    if (world <= 0 || m <= 0) return PQH_ERR_ARG;
+    return halo_record_bytes(m) * (world + 1) + 8ll * (world + 1) + 64;
+}
+
+int pqh_shard_offsets(const unsigned long long* lengths, int world, int rank,
+                      unsigned long long* offset, unsigned long long* total) {
+    if (!lengths || world <= 0 || rank < 0 || rank >= world || !offset || !total)
+        return PQH_ERR_ARG;
+    unsigned long long before = 0, all = 0;
+    for (int r = 0; r < world; ++r) {
+        if (r < rank) before += lengths[r];
+        all += lengths[r];
+    }
+    *offset = before;
+    *total = all;
+    return PQH_OK;
+}
+
+int pqh_shard_stitch(int world, const unsigned char* const* bufs,
+                     const unsigned long long* offsets, const unsigned long long* bits,
+                     unsigned char* out, unsigned long long out_bytes) {
+    if (world <= 0 || !bufs || !offsets || !bits || (!out && out_bytes)) return PQH_ERR_ARG;
+    unsigned long long total = 0;
+    for (int r = 0; r < world; ++r) total += bits[r];
+    if (out_bytes < (total + 7) / 8) return PQH_ERR_CAPACITY;
+    memset(out, 0, (size_t)((total + 7) / 8));
+    for (int r = 0; r < world; ++r) {
+        if (!bits[r]) continue;
+        if (!bufs[r] || offsets[r] + bits[r] > total) return PQH_ERR_ARG;
+        const unsigned long long start = (offsets[r] / 32) * 4;          // buffer byte 0
+        const unsigned long long end = (offsets[r] + bits[r] + 7) / 8;   // past the last byte
+        for (unsigned long long j = start; j < end; ++j) out[j] |= bufs[r][j - start];
+    }
+    return PQH_OK;
+}
+
+int pqh_shard_halo_source(const int* nonempty, int world, int rank, int* prev_rank,
+                          int* raw_first) {
+    if (!nonempty || world <= 0 || rank < 0 || rank >= world || !prev_rank || !raw_first)
+        return PQH_ERR_ARG;
+    int prev = -1, first = -1;
+    for (int r = 0; r < world; ++r) {
+        if (!nonempty[r]) continue;
+        if (first < 0) first = r;
+        if (r < rank) prev = r;
+    }
+    *prev_rank = prev;
+    *raw_first = first == rank ? 1 : 0;
+    return PQH_OK;
+}
+
+int pqh_shard_encode(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm, const block_t* shard,
+                     const void* d_codes, int m, int k, int context, pqh_tables_t* tables,
+                     uint32_t* d_counts, unsigned char* d_out, unsigned long long out_bytes,
+                     int chunk_vectors, unsigned long long* d_chunk_offsets, void* d_chunk_prev,
+                     unsigned long long* d_offsets, void* d_scratch, int* raw_first_out) {
+    if (!ctx || !comm || !shard || !tables || !d_counts || !d_out || out_bytes < 4 ||
+        !d_offsets || !d_scratch || m <= 0 || k <= 0 || k > 256 || (context && k != 256) ||
+        shard->size < 0 || (shard->size > 0 && !d_codes) || comm->world <= 0 ||
+        comm->rank < 0 || comm->rank >= comm->world || !comm->all_gather ||
+        !comm->all_reduce_sum_u32 || (reinterpret_cast<uintptr_t>(d_scratch) & 15u))
+        return PQH_ERR_ARG;
+    int rc = pqh_use_device(ctx);
+    if (rc) return rc;
+    const long long n = shard->size;
+    const int world = comm->world, rank = comm->rank;
+    unsigned char* scratch = static_cast<unsigned char*>(d_scratch);
+    const long long recb = halo_record_bytes(m);
+    unsigned char* halo_send = scratch;
+    unsigned char* halo_recv = scratch + recb;
+    unsigned long long* len_send =
+        reinterpret_cast<unsigned long long*>(scratch + recb * (world + 1));
+    unsigned long long* len_recv = len_send + 1;
+    void* const st = ctx->stream;
+    // 1. the halo (context mode): every rank's (non-empty flag, last row)
+    int raw_first = rank == 0 ? 1 : 0;
+    const void* d_prev = nullptr;
+    if (context) {
+        PQH_HIP(ctx, hipMemsetAsync(halo_send, 0, recb, ctx->stream));
+        if (n > 0) {
+            PQH_HIP(ctx, hipMemsetAsync(halo_send, 1, 1, ctx->stream));
+            PQH_HIP(ctx, hipMemcpyAsync(halo_send + kHaloData,
+                                        static_cast<const unsigned char*>(d_codes) + (n - 1) * m,
+                                        m, hipMemcpyDeviceToDevice, ctx->stream));
+        }
+        if (comm->all_gather(comm->user, halo_send, halo_recv, recb, st))
+            return pqh_set_error(ctx, PQH_ERR_ARG, "shard halo all-gather failed");
+        // which rank's row is the halo, and who writes the raw first row: the flags of
+        // every rank (one small host read; a shard may be empty)
+        std::vector<unsigned char> recs((size_t)(recb * world));
+        PQH_HIP(ctx, hipMemcpyAsync(recs.data(), halo_recv, recs.size(), hipMemcpyDeviceToHost,
+                                    ctx->stream));
+        PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        std::vector<int> nonempty(world);
+        for (int r = 0; r < world; ++r) nonempty[r] = recs[(size_t)(r * recb)] ? 1 : 0;
+        int prev = -1;
+        pqh_shard_halo_source(nonempty.data(), world, rank, &prev, &raw_first);
+        if (prev >= 0) d_prev = halo_recv + prev * recb + kHaloData;
+    }
+    // 2. the shard's histogram (+ the halo pair), summed over ranks -> identical tables
+    if ((rc = pqh_histogram_set(ctx, d_codes, n, m, k, context, d_prev, d_counts))) return rc;
+    const long long items = context ? (long long)k * k : k;
+    if (comm->all_reduce_sum_u32(comm->user, d_counts, (long long)m * items, st))
+        return pqh_set_error(ctx, PQH_ERR_ARG, "shard histogram all-reduce failed");
+    if ((rc = pqh_tables_build(ctx, tables, d_counts))) return rc;
+    // 3. place the shard: its exact length, everyone's, the exclusive scan on the device
+    if ((rc = pqh_encode_size(ctx, tables, d_codes, n, raw_first, d_prev, len_send))) return rc;
+    if (comm->all_gather(comm->user, len_send, len_recv, 8, st))
+        return pqh_set_error(ctx, PQH_ERR_ARG, "shard length all-gather failed");
+    hipLaunchKernelGGL(shard_prefix, dim3(1), dim3(64), 0, ctx->stream, len_recv, world, rank,
+                       d_offsets);
+    PQH_LAUNCH_CHECK(ctx);
+    // 4. write it (word 0 of d_out = the global word offset / 32; the bits before the shard's
+    // offset in that word belong to the previous shard and stay zero here)
+    PQH_HIP(ctx, hipMemsetAsync(d_out, 0, 4, ctx->stream));
+    if ((rc = pqh_encode_write_at(ctx, tables, d_codes, n, raw_first, d_prev, d_offsets, d_out,
+                                  out_bytes, chunk_vectors, d_chunk_offsets, d_chunk_prev,
+                                  nullptr)))
+        return rc;
+    if (raw_first_out) *raw_first_out = raw_first;
+    return PQH_OK;
+}
+
+}  // extern "C"

@@ -15,19 +15,32 @@ writes its shard at bit `offset % 32` of its own word-aligned buffer; `stitch` O
 buffers into the single reference stream.  Context mode's raw first row belongs to global
 row 0 only (huffman_encoder.c:234).
 
-The functions take a torch.distributed process group (RCCL on the GPU, gloo in the CPU
-tests) and torch tensors on the group's device.
+The protocol itself is the library's (include/pqh.h "multi-GPU row shards"):
+pqh_shard_encode runs a rank's whole encode with the caller's collectives as hooks (TorchComm
+adapts a torch.distributed process group: RCCL on the GPU, gloo in the rehearsals), and the
+host pieces -- row ranges (pqh_shard_block), offsets (pqh_shard_offsets), the stitch
+(pqh_shard_stitch), the ragged halo's source (pqh_shard_halo_source) -- are C functions this
+module calls.  The remaining helpers issue torch.distributed collectives for the bench's
+overlapped schedule (bench.py), which interleaves the same steps across batches and streams.
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Iterable, Sequence, Tuple
 
 
+def _lib():
+    from .capi import lib
+    return lib()
+
+
 def row_range(n_total: int, world: int, rank: int) -> Tuple[int, int]:
-    """Contiguous shard [begin, end) of rank `rank`: sizes differ by at most one row."""
-    base, extra = divmod(n_total, world)
-    begin = rank * base + min(rank, extra)
-    return begin, begin + base + (1 if rank < extra else 0)
+    """Contiguous shard [begin, end) of rank `rank`: sizes differ by at most one row
+    (pqh_shard_block, a block_t descriptor)."""
+    from .capi import Block, check
+    b = Block()
+    check(_lib().pqh_shard_block(n_total, world, rank, ctypes.byref(b)), "pqh_shard_block")
+    return b.id, b.id + b.size
 
 
 def exchange_halo(last_row, world: int, rank: int, group=None):
@@ -51,6 +64,18 @@ def reduce_counts(counts, world: int, group=None):
     return counts
 
 
+def offsets_of(lengths: Sequence[int], rank: int) -> Tuple[int, int]:
+    """(this rank's global bit offset, the global length) from every rank's bit length
+    (pqh_shard_offsets)."""
+    from .capi import check
+    w = len(lengths)
+    arr = (ctypes.c_ulonglong * w)(*[int(v) for v in lengths])
+    off, tot = ctypes.c_ulonglong(), ctypes.c_ulonglong()
+    check(_lib().pqh_shard_offsets(arr, w, rank, ctypes.byref(off), ctypes.byref(tot)),
+          "pqh_shard_offsets")
+    return off.value, tot.value
+
+
 def bit_offsets(total_bits, world: int, rank: int, group=None) -> Tuple[int, int]:
     """(global bit offset of this shard, global stream length in bits) from every shard's
     exact bit length.  `total_bits` is a (1,) int64 tensor."""
@@ -61,8 +86,7 @@ def bit_offsets(total_bits, world: int, rank: int, group=None) -> Tuple[int, int
         return 0, t
     everyone = torch.empty(world, dtype=torch.int64, device=total_bits.device)
     dist.all_gather_into_tensor(everyone, total_bits.reshape(1).to(torch.int64), group=group)
-    host = [int(v) for v in everyone.cpu().tolist()]
-    return sum(host[:rank]), sum(host)
+    return offsets_of(everyone.cpu().tolist(), rank)
 
 
 def bit_offsets_device(total_bits, world: int, rank: int, group=None):
@@ -91,24 +115,29 @@ def buffer_byte_start(global_offset: int) -> int:
 
 
 def stitch(shards: Iterable[Tuple[bytes, int, int]], total_bits: int) -> bytes:
-    """Concatenate shard buffers into the global stream (huffman_indices.bin payload).
+    """Concatenate shard buffers into the global stream (huffman_indices.bin payload) with
+    pqh_shard_stitch.
 
     shards: (buffer, global_bit_offset, bits) per shard, where buffer holds the shard's
     stream starting at bit `global_bit_offset % 32` and is zero elsewhere.  Bit ranges are
     disjoint, so OR-ing the buffers at their word positions yields the reference stream
     (zero padded to a byte, bitstream.c:104-110)."""
-    out = bytearray((total_bits + 7) // 8)
+    from .capi import check
+    shards = list(shards)
+    w = len(shards)
     for buf, goff, bits in shards:
-        if bits == 0:
-            continue
-        start = buffer_byte_start(goff)
-        end_byte = (goff + bits + 7) // 8            # last global byte holding shard bits
-        need = end_byte - start
-        if need > len(buf):
+        if bits and (goff + bits + 7) // 8 - buffer_byte_start(goff) > len(buf):
             raise ValueError("shard buffer shorter than its bit range")
-        for j in range(need):
-            out[start + j] |= buf[j]
-    return bytes(out)
+    keep = [ctypes.create_string_buffer(bytes(b), max(1, len(b))) for b, _, _ in shards]
+    bufs = (ctypes.c_void_p * w)(*[ctypes.addressof(k) for k in keep])
+    offs = (ctypes.c_ulonglong * w)(*[int(g) for _, g, _ in shards])
+    bits = (ctypes.c_ulonglong * w)(*[int(n) for _, _, n in shards])
+    nb = (sum(int(n) for _, _, n in shards) + 7) // 8
+    if sum(int(n) for _, _, n in shards) != total_bits:
+        raise ValueError("shard lengths do not add up to total_bits")
+    out = ctypes.create_string_buffer(max(1, nb))
+    check(_lib().pqh_shard_stitch(w, bufs, offs, bits, out, nb), "pqh_shard_stitch")
+    return out.raw[:nb]
 
 
 def stitch_np(shards: Sequence[Tuple["object", int, int]], total_bits: int):
@@ -267,8 +296,105 @@ def halo_ragged(last_row, world: int, rank: int, group=None, device=None, dtype=
         row[:last_row.numel()] = last_row.reshape(-1).to(torch.int64)
     rows = torch.empty(world * mm, dtype=torch.int64, device=dev)
     dist.all_gather_into_tensor(rows, row, group=group)
-    has = [r[0] for r in allinfo]
-    prev = next((r for r in range(rank - 1, -1, -1) if has[r]), None)
-    first = next((r for r in range(world) if has[r]), None)
-    halo = rows.view(world, mm)[prev].to(dt).contiguous() if prev is not None else None
-    return halo, 1 if first == rank else 0
+    from .capi import check
+    has = (ctypes.c_int * world)(*[int(r[0]) for r in allinfo])
+    prev, raw = ctypes.c_int(), ctypes.c_int()
+    check(_lib().pqh_shard_halo_source(has, world, rank, ctypes.byref(prev), ctypes.byref(raw)),
+          "pqh_shard_halo_source")
+    halo = rows.view(world, mm)[prev.value].to(dt).contiguous() if prev.value >= 0 else None
+    return halo, raw.value
+
+
+# ---- the library's whole-shard encode (pqh_shard_encode) with torch.distributed hooks ----
+
+class TorchComm:
+    """pqh_shard_comm_t over a torch.distributed process group.  The library hands the hooks
+    raw device pointers; they must lie inside tensors registered here (the counts and the
+    scratch the encode uses), which the hooks slice and pass to all_reduce /
+    all_gather_into_tensor, ordered on the library context's stream."""
+
+    def __init__(self, world: int, rank: int, group=None):
+        from .capi import ALL_GATHER, ALL_REDUCE_U32, ShardComm
+        self.world, self.rank, self.group = world, rank, group
+        self._tensors = []
+        self._reduce = ALL_REDUCE_U32(self._all_reduce)
+        self._gather = ALL_GATHER(self._all_gather)
+        self.struct = ShardComm(None, world, rank, self._reduce, self._gather)
+        self.error = None
+
+    def register(self, *tensors):
+        for t in tensors:
+            if t is not None:
+                self._tensors.append(t)
+        return self
+
+    def _view(self, ptr, nbytes, dtype):
+        import torch
+        for t in self._tensors:
+            base = t.data_ptr()
+            size = t.numel() * t.element_size()
+            if base <= ptr and ptr + nbytes <= base + size:
+                flat = t.view(-1).view(torch.uint8)
+                return flat[ptr - base:ptr - base + nbytes].view(dtype)
+        raise ValueError(f"device pointer {ptr:#x} is in no registered tensor")
+
+    def _on_stream(self, stream, fn):
+        import torch
+        try:
+            with torch.cuda.stream(torch.cuda.ExternalStream(stream)) if stream else _null():
+                fn()
+            return 0
+        except Exception as e:  # the C caller gets a status; keep the reason
+            self.error = e
+            return 1
+
+    def _all_reduce(self, user, ptr, count, stream):
+        import torch
+        import torch.distributed as dist
+        return self._on_stream(stream, lambda: dist.all_reduce(
+            self._view(ptr, count * 4, torch.int32), group=self.group))
+
+    def _all_gather(self, user, send, recv, nbytes, stream):
+        import torch
+        import torch.distributed as dist
+        return self._on_stream(stream, lambda: dist.all_gather_into_tensor(
+            self._view(recv, nbytes * self.world, torch.uint8),
+            self._view(send, nbytes, torch.uint8), group=self.group))
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def shard_encode(ctx, comm: TorchComm, codes, tables, counts, out, chunk_vectors=0,
+                 chunk_offsets=None, chunk_prev=None, first_row=0):
+    """This rank's encode through pqh_shard_encode (halo, histogram all-reduce, GPU code
+    tables, lengths all-gather, device offsets, write).  codes: (n, m) uint8 cuda tensor
+    (n may be 0); counts: (m, items) int32; out: uint8 buffer.  Returns (offsets, raw_first):
+    offsets a (2,) int64 device tensor {global bit offset, global length}."""
+    import torch
+    from .capi import Block, check
+    n, m = codes.shape
+    dev = codes.device
+    scratch = torch.empty(int(_lib().pqh_shard_scratch_bytes(comm.world, m)), dtype=torch.uint8,
+                          device=dev)
+    offsets = torch.zeros(2, dtype=torch.int64, device=dev)
+    comm.register(counts, scratch)
+    b = Block()
+    b.id, b.size, b.capacity = first_row, n, n
+    raw = ctypes.c_int()
+    ptr = (lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None)
+    comm.error = None
+    rc = _lib().pqh_shard_encode(ctx.ptr, ctypes.byref(comm.struct), ctypes.byref(b),
+                                 ptr(codes) if n else None, m, tables.k, int(tables.context),
+                                 tables.ptr, ptr(counts), ptr(out), out.numel(), chunk_vectors,
+                                 ptr(chunk_offsets), ptr(chunk_prev), ptr(offsets), ptr(scratch),
+                                 ctypes.byref(raw))
+    if comm.error is not None:
+        raise comm.error
+    check(rc, "pqh_shard_encode")
+    return offsets, raw.value

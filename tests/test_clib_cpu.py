@@ -248,3 +248,51 @@ def test_block_matches_reference_behaviour():
     lib().block_init(ctypes.byref(b), 0, 2, 0, 0x01)
     assert not b.indices and b.data
     lib().block_destroy(ctypes.byref(b))
+
+
+def test_shard_host_protocol():
+    """pqh_shard_block / _offsets / _halo_source / _stitch (the host half of the multi-GPU
+    protocol): row ranges partition the rows, offsets are the exclusive scan,
+    the ragged halo comes from the nearest non-empty rank before, and stitching word-aligned
+    shard buffers reproduces one stream."""
+    from pq_huffman_amd.capi import Block
+    L = lib()
+    for n_total in (0, 1, 7, 1000, 10 ** 9 + 7):
+        for world in (1, 3, 8):
+            spans = []
+            for r in range(world):
+                b = Block()
+                assert L.pqh_shard_block(n_total, world, r, ctypes.byref(b)) == 0
+                spans.append((b.id, b.size))
+            assert spans[0][0] == 0 and sum(s for _, s in spans) == n_total
+            assert all(spans[i][0] + spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+            assert max(s for _, s in spans) - min(s for _, s in spans) <= 1
+    b = Block()
+    assert L.pqh_shard_block(10, 2, 2, ctypes.byref(b)) != 0           # rank out of range
+    lens = (ctypes.c_ulonglong * 4)(13, 0, 40, 7)
+    off, tot = ctypes.c_ulonglong(), ctypes.c_ulonglong()
+    assert L.pqh_shard_offsets(lens, 4, 2, ctypes.byref(off), ctypes.byref(tot)) == 0
+    assert (off.value, tot.value) == (13, 60)
+    prev, raw = ctypes.c_int(), ctypes.c_int()
+    has = (ctypes.c_int * 5)(0, 1, 0, 0, 1)
+    for rank, want in ((0, (-1, 0)), (1, (-1, 1)), (3, (1, 0)), (4, (1, 0))):
+        assert L.pqh_shard_halo_source(has, 5, rank, ctypes.byref(prev), ctypes.byref(raw)) == 0
+        assert (prev.value, raw.value) == want
+    # three shards of a 90-bit stream: 13 bits, 0 bits, 77 bits at global bit 13
+    rng = np.random.default_rng(4)
+    bits = rng.integers(0, 2, 90).astype(np.uint8)
+    def buf(goff, nb):
+        out = np.zeros(((goff % 32) + nb + 31) // 32 * 4 + 4, np.uint8)
+        for j in range(nb):
+            if bits[goff + j]:
+                p = goff % 32 + j
+                out[p // 8] |= 1 << (7 - p % 8)
+        return out
+    parts = [(buf(0, 13), 0, 13), (np.zeros(4, np.uint8), 13, 0), (buf(13, 77), 13, 77)]
+    ptrs = (ctypes.c_void_p * 3)(*[p[0].ctypes.data for p in parts])
+    offs = (ctypes.c_ulonglong * 3)(*[p[1] for p in parts])
+    nbs = (ctypes.c_ulonglong * 3)(*[p[2] for p in parts])
+    out = np.full(12, 0xAA, np.uint8)
+    assert L.pqh_shard_stitch(3, ptrs, offs, nbs, out.ctypes.data, 12) == 0
+    assert np.array_equal(out, np.packbits(bits))
+    assert L.pqh_shard_stitch(3, ptrs, offs, nbs, out.ctypes.data, 11) != 0   # too small

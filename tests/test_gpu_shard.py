@@ -1,0 +1,48 @@
+"""The library's multi-GPU encode (pqh_shard_encode via shard.shard_encode) with two ranks
+on one GPU (gloo hooks, fresh child processes): the stitched stream (pqh_shard_stitch) and
+the global histogram must equal the oracle's one-shot results over all ranks' rows
+(huffman_encoder.c:139-238), for even shards, a shard with no rows, and the slices of the
+distributed sort (whose ragged halo also goes through shard.halo_ragged)."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("case,mode", [("even", "ctx"), ("even", "noctx"), ("ragged", "ctx"),
+                                       ("sort", "ctx")])
+def test_two_rank_library_shard_encode(oracle, tmp_path, case, mode):
+    dump = tmp_path / "shard.npz"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(ROOT, "tests", "shard_worker.py"), "--case", case, "--mode", mode,
+           "--out", str(dump)]
+    r = subprocess.run(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1"), capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    d = np.load(dump, allow_pickle=False)
+    rows = d["rows"]
+    ctxm = mode == "ctx"
+    if case == "sort":   # the slices in rank order are the stable strncmp-key sort of all rows
+        import datagen
+        allc = datagen.skewed_codes(20011, 8, 256, seed=77)
+        allc[np.random.default_rng(3).random(allc.shape) < 0.2] = 0
+        np.testing.assert_array_equal(rows, oracle.sort_rows(allc))
+    np.testing.assert_array_equal(d["counts"].astype(np.int64),
+                                  oracle.histogram(rows, 256, ctxm))
+    want, bits = oracle.encode(rows, oracle.build_codebooks(rows, 256, ctxm))
+    assert int(d["total"]) == bits
+    assert d["stream"].tobytes() == want

@@ -1,10 +1,12 @@
 """Multi-rank protocol of the encode path (pq_huffman_amd/shard.py) on CPU:
-world_size 2 and 3 over gloo.  Each rank takes its row shard, exchanges the one-vector
-halo, all-reduces its histogram, builds the (oracle) code tables from the global counts,
-encodes its shard at the all-gathered bit offset, and rank 0 stitches the shard buffers.
-The stitched stream and the reduced histogram must equal the oracle's single-process
-results bit for bit.  The per-shard bit packer here is test code standing in for the GPU
-encoder (which has its own sharded-composition test in test_gpu_huffman.py)."""
+world_size 2 and 3 over gloo.  Each rank takes its row shard (pqh_shard_block), exchanges
+the one-vector halo (the ragged halo's source: pqh_shard_halo_source), all-reduces its
+histogram, builds the (oracle) code tables from the global counts, encodes its shard at the
+all-gathered bit offset (pqh_shard_offsets), and rank 0 stitches the shard buffers
+(pqh_shard_stitch).  The stitched stream and the reduced histogram must equal the oracle's
+single-process results bit for bit.  The library's host half of the protocol runs here;
+the per-shard bit packer is test code standing in for the GPU encoder, which needs a GPU
+(its two-rank run of the whole library protocol, pqh_shard_encode, is test_gpu_shard.py)."""
 import os
 import socket
 
