@@ -70,6 +70,10 @@ def parse():
                     help="sift: BASELINE configs[1]/[2] (128-d, M=8, K=256; the headline); "
                          "deep: configs[3] (96-d unit-norm, M=16, K=256); k4096: configs[4] "
                          "(128-d, M=8, K=4096, u16 codes, non-context)")
+    ap.add_argument("--sort", action="store_true",
+                    help="the reference's default mode: rows sorted by the strncmp key before "
+                         "the context histogram and encode (huffman_encoder.c:301-318); the "
+                         "round trip then returns the sorted rows")
     ap.add_argument("--chunk", type=int, default=8,
                     help="vectors per decode chunk (chunk-index sidecar granularity)")
     ap.add_argument("--cpu-sample", type=int, default=200_000)
@@ -176,11 +180,14 @@ def train_centroids(torch, x, m, k, iters=4, sample=50_000, seed=7):
     return out.numpy()
 
 
-def cpu_leg(orc, xs, cent, ctxm, threads):
-    """One timed pass of the CPU path on xs: assign (threads) + histogram + codebooks +
-    bit-serial encode + trie decode (single thread, as the reference's Huffman half)."""
+def cpu_leg(orc, xs, cent, ctxm, threads, sort=False):
+    """One timed pass of the CPU path on xs: assign (threads) + [stable strncmp-key sort] +
+    histogram + codebooks + bit-serial encode + trie decode (single thread, as the
+    reference's Huffman half)."""
     t0 = time.perf_counter()
     codes, _ = orc.pq_assign(xs, cent, threads=threads)
+    if sort:
+        codes = orc.sort_rows(codes)
     t1 = time.perf_counter()
     cbs = orc.build_codebooks(codes, cent.shape[1], ctxm)
     stream, bits = orc.encode(codes, cbs)
@@ -193,7 +200,7 @@ def cpu_leg(orc, xs, cent, ctxm, threads):
                          "decode": round(t3 - t2, 3)}}
 
 
-def cpu_baseline(x_host, cent, ctxm, sample):
+def cpu_baseline(x_host, cent, ctxm, sample, sort=False):
     """The reference CPU path (the oracle: a byte-exact restatement of the reference) on
     bounded samples of the shard, on this host:
       1 thread -O2 (the headline `value`), all granted threads -O2 (OpenMP over rows for the
@@ -205,18 +212,19 @@ def cpu_baseline(x_host, cent, ctxm, sample):
     # sets OMP_NUM_THREADS to it)
     threads = int(os.environ.get("OMP_NUM_THREADS") or len(os.sched_getaffinity(0)))
     orc.use_build("O2")
-    one = cpu_leg(orc, xs, cent, ctxm, 1)
-    allc = cpu_leg(orc, xs, cent, ctxm, threads)
+    one = cpu_leg(orc, xs, cent, ctxm, 1, sort)
+    allc = cpu_leg(orc, xs, cent, ctxm, threads, sort)
     q = max(1, sample // 4)
     orc.use_build("O0")
-    o0 = cpu_leg(orc, np.ascontiguousarray(xs[:q]), cent, ctxm, 1)
+    o0 = cpu_leg(orc, np.ascontiguousarray(xs[:q]), cent, ctxm, 1, sort)
     orc.use_build("O2")
     mode = "context" if ctxm else "non-context"
     return {"value": one["value"], "unit": "Mvec/s", "cores": 1, "kind": "port",
             "sample": f"{sample} vectors of the rank-0 shard, M={cent.shape[0]} "
                       f"K={cent.shape[1]} {mode}: oracle assign "
-                      f"+ histogram + codebooks + bit-serial encode + trie decode, single "
-                      f"thread -O2",
+                      + ("+ stable strncmp-key sort " if sort else "") +
+                      "+ histogram + codebooks + bit-serial encode + trie decode, single "
+                      "thread -O2",
             "stages_s": one["stages_s"],
             "legs": [
                 dict(one, cores=1, build="-O2", sample=sample),
@@ -339,7 +347,10 @@ def main():
            for _ in elanes]
     tot_dev = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in elanes]
     raw_first = shard.raw_first(rank)
-    stages = ("assign", "hist", "codebook", "encode", "decode")
+    stages = ("assign", "sort", "hist", "codebook", "encode", "decode")
+    if args.sort and (k > 256 or world > 1):
+        raise SystemExit("--sort: one rank, K <= 256 (the distributed sort is shard.py's)")
+    sort_tmp = torch.empty((n, m), dtype=torch.uint8, device=dev) if args.sort else None
     events = []          # (stage, start, end) of timed steps, read after the timed region
     acc = {s: 0.0 for s in list(stages) + ["collectives"]}
     state = {"timed": False}
@@ -389,6 +400,10 @@ def main():
             e = rec("assign", sF)
             pq.assign(x, codes[s], ctx=cF)
             done(e, sF)
+            if args.sort:            # stable strncmp-key sort of the batch's rows (in place)
+                e = rec("sort", sF)
+                codec.sort_rows(cF, codes[s], sort_tmp)
+                done(e, sF)
             halo[s] = None
             if not hist_on_lane:     # (the shard-boundary pair is added on the lane)
                 hist(s, cF, sF)
@@ -555,7 +570,10 @@ def main():
             "data": data + "; centroids from 4 Lloyd iterations on a 50k sample (setup, untimed)",
             "config": {"workload": workload
                                    + ("order-1 context Huffman (reference default coding), "
-                                      "no sort" if ctxm else "non-context Huffman, no sort"),
+                                      if ctxm else "non-context Huffman, ")
+                                   + ("rows sorted by the strncmp key (the reference's default "
+                                      "mode)" if args.sort else "no sort"),
+                       "sort": bool(args.sort),
                        "vectors_per_gpu": n, "d": d, "m": m, "k": k,
                        "mode": "ctx" if ctxm else "noctx",
                        "chunk_vectors": args.chunk, "parallelism": f"dp{world} row shards",
@@ -583,7 +601,8 @@ def main():
                          # stream, which also count the wait for CUs held by the lanes
                          "profile_avg_ms": (round(prof_avg_us / 1e3, 4)
                                             if prof_avg_us is not None else None)},
-            "stages_ms": {s: round(v / args.steps * 1e3, 4) for s, v in acc.items()},
+            "stages_ms": {s: round(v / args.steps * 1e3, 4) for s, v in acc.items()
+                          if s != "sort" or args.sort},
             "stages_note": ("per-stage HIP-event times on their own streams" +
                             ("" if serial else "; the stages of consecutive batches run "
                              "concurrently, so they sum to more than ms_per_step")),
@@ -606,7 +625,7 @@ def main():
         if not args.no_cpu_baseline and world == 1:
             sample = max(1000, args.cpu_sample * 256 // k)   # ~the same CPU time at any K
             xh = x[:sample].cpu().numpy()
-            res["cpu_baseline"] = cpu_baseline(xh, cent, ctxm, sample)
+            res["cpu_baseline"] = cpu_baseline(xh, cent, ctxm, sample, args.sort)
             res["cpu_baseline"]["host_cpu"] = _cpu_name()
             res["cpu_baseline"]["nproc"] = os.cpu_count()
         print(json.dumps(res), flush=True)

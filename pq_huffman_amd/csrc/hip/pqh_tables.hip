@@ -106,8 +106,10 @@ struct LdsHeap {
 };
 
 // Count scan: calls f(symbol, count) for every nonzero count in symbol order.
-template <typename F>
-__device__ __forceinline__ void scan_counts(const uint32_t* __restrict__ cnt, int k, F&& f) {
+// zero(symbol) is called for the symbols that never occur (their code table entry).
+template <typename F, typename Z>
+__device__ __forceinline__ void scan_counts(const uint32_t* __restrict__ cnt, int k, F&& f,
+                                            Z&& zero) {
     const int kv = (k & 31) ? 0 : k;           // vector part (count rows are 16-B aligned)
     const uint4* cnt4 = reinterpret_cast<const uint4*>(cnt);
     for (int s0 = 0; s0 < kv; s0 += 32) {      // 128 B of counts in flight per lane
@@ -119,11 +121,13 @@ __device__ __forceinline__ void scan_counts(const uint32_t* __restrict__ cnt, in
             const uint32_t c = u % 4 == 0 ? q[u / 4].x : u % 4 == 1 ? q[u / 4].y
                              : u % 4 == 2 ? q[u / 4].z : q[u / 4].w;
             if (c) f(s0 + u, c);
+            else zero(s0 + u);
         }
     }
     for (int s = kv; s < k; ++s) {             // small / odd alphabets
         const uint32_t c = cnt[s];
         if (c) f(s, c);
+        else zero(s);
     }
 }
 
@@ -556,7 +560,7 @@ huff_trees_small(const uint32_t* __restrict__ counts, int k, long long trees,
         lcnt[nz * TPW] = c;
         total += c;
         ++nz;
-    });
+    }, [&](int s) { out[s] = 0ull; });   // no code (the table set is not memset)
     if (nz == 0) return;
     if (stamp) g_tree_stamps[1] = __builtin_amdgcn_s_memtime();
     int next;
@@ -656,7 +660,7 @@ huff_trees(const uint32_t* __restrict__ counts, int k, long long trees,
         lcnt[nz * TPW] = c;
         total += c;
         ++nz;
-    });
+    }, [&](int s) { out[s] = 0ull; });   // no code (the table set is not memset)
     if (nz == 0) return;
     if (stamp) g_tree_stamps[1] = __builtin_amdgcn_s_memtime();
     int next;
@@ -1292,7 +1296,7 @@ int pqh_tables_build(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts) 
         PQH_LAUNCH_CHECK(ctx);
         return launch_luts(ctx, t);
     }
-    PQH_HIP(ctx, hipMemsetAsync(t->d_enc, 0, (size_t)t->m * t->items * 8, ctx->stream));
+    // (every build writes every entry, 0 for symbols that never occur: no memset)
     if (t->k <= 256) {
         // trees per workgroup: fewer = more, smaller workgroups (3.5 KB of LDS per tree), so
         // the build spreads over more CUs and leaves each CU's LDS to concurrent kernels
