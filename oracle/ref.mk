@@ -20,6 +20,7 @@ LIBSRC := $(REF)/huffman_encode.c $(REF)/huffman_decode.c $(REF)/huffman_codeboo
 TREESRC := $(REF)/mst.c $(REF)/dsu.c
 
 BINS := $(OUT)/huffman_encoder $(OUT)/huffman_decoder \
+        $(OUT)/relink/huffman_encoder $(OUT)/relink/huffman_decoder \
         $(OUT)/huffman_encoder_O0 $(OUT)/huffman_decoder_O0 \
         $(OUT)/bitstream_test $(OUT)/huffman_encode_test $(OUT)/huffman_decode_test \
         $(OUT)/huffman_codebook_test $(OUT)/libref.so
@@ -38,6 +39,19 @@ $(OUT)/huffman_encoder_O0: $(REF)/huffman_encoder.c $(LIBSRC) $(TREESRC) | $(OUT
 	$(CC) $(CFLAGS_O0) -o $@ $^ -lm
 $(OUT)/huffman_decoder_O0: $(REF)/huffman_decoder.c $(LIBSRC) $(TREESRC) | $(OUT)
 	$(CC) $(CFLAGS_O0) -o $@ $^ -lm
+
+# the reference CLIs relinked against libpqh -- its own
+# huffman_encoder.c / huffman_decoder.c (+ mst.c, dsu.c: the forest loader libpqh does not
+# replace) compiled against include/*.h (`-I-`: quote includes skip the source's own
+# directory, so huffman.h, bitstream.h, stats.h, misc.h, vecs_io.h come from include/),
+# linked with -lpqh instead of the reference's library objects.
+PQH_LIB := pq_huffman_amd/lib
+CFLAGS_RELINK := -std=c99 -O2 -w -Iinclude -I- -I$(REF)
+$(OUT)/relink:
+	mkdir -p $(OUT)/relink
+$(OUT)/relink/%: $(REF)/%.c $(TREESRC) $(PQH_LIB)/libpqh.so | $(OUT)/relink
+	$(CC) $(CFLAGS_RELINK) -o $@ $< $(TREESRC) -L$(PQH_LIB) -lpqh \
+	    -Wl,-rpath,$(abspath $(PQH_LIB)) -lm
 
 # embedded `#ifdef _X_TEST` mains (src/bitstream.c:196, huffman_encode.c:280,
 # huffman_decode.c:193, huffman_codebook.c:145); not built by the reference Makefile
