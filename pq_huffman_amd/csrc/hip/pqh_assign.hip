@@ -122,6 +122,19 @@ __device__ __forceinline__ float opaque_ninf() {
     return r;
 }
 
+// max(|a|, |b|) in one instruction (fmaxf(fabsf, fabsf) adds two canonicalising maxes)
+__device__ __forceinline__ float max_abs(float a, float b) {
+    float r;
+    asm("v_max_f32_e64 %0, |%1|, |%2|" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+// The index bits of Q-group j's key: register j of the tile's lower half is accumulator row
+// (j & 3) + 8 (j >> 2) (tile_row), so the winner's row is an OR of its two keys' low bits.
+__device__ __forceinline__ unsigned q_code_bits(int j) {
+    return (unsigned)((j & 3) | ((j & 4) << 1));
+}
+
 // Smallest and second smallest of 8 distinct keys (10 VALU): two triples and a pair give
 // their (min, second); every key but the overall minimum is >= one of the three seconds or
 // is the second smallest of the three minima, and each of those is a key other than the
@@ -402,7 +415,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     __shared__ uint2 rqs[kWavesPerWG][kRqLds];
 
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // (uniform: SGPR math)
     // One subspace per workgroup, gx workgroups per subspace, 1-D grid.  Workgroup L is
     // placed on XCD L % 8 and, within it, round robin over the CUs, so L, L + 256, L + 512 ...
     // tend to share a CU.  The waves of a SIMD run at very different speeds (VALU issue goes
@@ -444,7 +457,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
 #ifdef PQH_ASSIGN_STAMPS
     const unsigned long long st0 = __builtin_amdgcn_s_memtime();
     const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
-    unsigned long long nbdone = 0;
+    unsigned long long nbdone = 0, rr_ticks = 0, rr_batches = 0;
 #endif
     const float cm = cmax[m];
     const float sc = sqrt_cmax[m];
@@ -463,19 +476,27 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     // the slice is used), so the prefetch stays in flight across a whole block.
     // The lane's slice of row r of block 0; a block's rows are a uniform offset away.  Only
     // the last, partial block clamps its rows (to n - 1), on a wave-uniform branch.
-    const float* const xlane = x + (long long)r * ldx + (long long)m * D + (HALF ? 8 * h : 0);
+    // Addresses are a wave-uniform 64-bit base (SGPRs) plus the lane's 32-bit byte offset
+    // within the block (global loads / stores with an SGPR base): no per-lane 64-bit math.
+    // (ld_x < 2^22 on the host, so the offsets fit 24 bits.)
+    const unsigned ldx4 = (unsigned)ldx * 4u;
+    const unsigned xh_off = HALF ? 32u * (unsigned)h : 0u;
+    const unsigned xlane_off = __umul24((unsigned)r, ldx4) + xh_off;
+    const char* const xm = reinterpret_cast<const char*>(x + (long long)m * D);
+    const unsigned code_lane_off = (unsigned)r * (unsigned)m_total * (unsigned)sizeof(CodeT);
     auto load_x = [&](long long b, float* dst) {
 #ifdef PQH_ASSIGN_NOMEM   // diagnostic: every chunk re-reads the first 64 blocks (cache hits)
         b &= 63;
 #endif
-        const float* xp;
-        if (b * 32 + 32 <= n) {
-            xp = xlane + b * 32 * ldx;
-        } else {
-            long long vv = b * 32 + r;
-            vv = vv < n ? vv : n - 1;
-            xp = x + vv * ldx + (long long)m * D + (HALF ? 8 * h : 0);
+        long long row0 = b * 32;
+        unsigned off = xlane_off;
+        if (row0 + 32 > n) {   // (uniform) the last, partial block: rows past n read row n - 1
+            row0 = row0 < n - 1 ? row0 : n - 1;
+            const long long left = n - 1 - row0;
+            const unsigned last = (unsigned)(left < 31 ? left : 31);
+            off = __umul24(min((unsigned)r, last), ldx4) + xh_off;
         }
+        const float* xp = reinterpret_cast<const float*>(xm + row0 * (long long)ldx4 + off);
         if constexpr (XD % 4 == 0) {
 #pragma unroll
             for (int j = 0; j < XD; j += 4) {
@@ -506,13 +527,14 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     auto body = [&](auto lo_c, long long blk0, float (*xs)[XD], const float* X,
                     const bool* any_lo, const bool* finite_x) {
         constexpr bool LO = decltype(lo_c)::value;
-        long long v[kNB];
+        long long row0[kNB];   // (uniform) the block's first row
         bool valid[kNB];
         bf16x8 Bm[kNB][P::PM], Bl[kNB][P::PL];
 #pragma unroll
         for (int b = 0; b < kNB; ++b) {
-            v[b] = (blk0 + b) * 32 + r;
-            valid[b] = v[b] < n;   // rows past n hold row n - 1 (clamped loads), never stored
+            row0[b] = (blk0 + b) * 32;
+            // rows past n hold row n - 1 (clamped loads), never stored
+            valid[b] = row0[b] + 32 <= n || (long long)r < n - row0[b];
             make_b<D, LO>(xs[b], h, Bm[b], Bl[b]);
         }
         // The lane's 128 scores of a block form an 8 x 16 grid: tile t (row) x accumulator
@@ -527,7 +549,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         // versa), and the winner's cell is (argmin P, argmin Q).  A score is touched by one
         // min3 of each partition -- 1 VALU per score instead of 2.25 for keys + tournament --
         // and only the 24 group minima get index bits (the winner's P-group in the low 4
-        // bits, its Q-group in the low 3).
+        // bits, its Q-group as row bits in the low 4).
         unsigned pm1[kNB], pm2[kNB], qg[kNB][8];
         auto load_a = [&](int t, bf16x8* a) {
 #ifdef PQH_ASSIGN_KTNOMEM   // diagnostic: every tile re-reads tile t % 4 (cache hits)
@@ -628,14 +650,12 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
             // the lane's 128 centroids: keyed group minima, top two of each partition ...
             unsigned qk[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) qk[j] = (qg[b][j] & ~7u) | (unsigned)j;
+            for (int j = 0; j < 8; ++j) qk[j] = (qg[b][j] & ~15u) | q_code_bits(j);
             const unsigned p1 = pm1[b], p2 = pm2[b];
             unsigned q1, q2;
             top2_8(qk, q1, q2);
             const unsigned own1 = p1;
             const unsigned own2 = minu(p2, q2);
-            const int wt = (int)((p1 & PMASK) >> 1);
-            const int wi = (int)(q1 & 7u) + 8 * (int)(p1 & 1u);
             // ... then the two half-waves (lanes l and l^32 hold the same vector): after the
             // swap, s[0] holds the lower half's value and s[1] the upper half's, in every lane
             const auto s1 = __builtin_amdgcn_permlane32_swap(own1, own1, false, false);
@@ -644,14 +664,15 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
             const unsigned b2 = minu(minu((unsigned)s2[0], (unsigned)s2[1]),
                                      maxu((unsigned)s1[0], (unsigned)s1[1]));
             const bool mine = own1 == b1;   // this half holds the winner (both: a tie -> slow)
-            int code = tile_row(wt, wi, h);
+            // the winner's row (tile_row): 16 (2t + g) from its P key, the rest from its Q key
+            int code = (int)(((p1 & PMASK) << 4) | (q1 & 15u)) | (h << 2);
             const float tau = screen_tau(X[b], any_lo[b], tq);
             // a key differs from its score by less than 2^PB ulp (2^(PB-23) relative):
             // 2^(PB-21) of the larger magnitude covers both keys of the gap (and the rounding
             // of K2 - K1)
             constexpr float kKeySlack = PB == 4 ? 0x1p-17f : 0x1p-13f;
             const float K1 = __uint_as_float(b1), K2 = __uint_as_float(b2);
-            const float KA = fmaxf(fabsf(K1), fabsf(K2));
+            const float KA = max_abs(K1, K2);
             const bool slow = !(K2 - K1 > fmaf(kKeySlack, KA, tau)) || !finite_x[b];
 
             unsigned long long need = __ballot(slow && valid[b] && h == 0);
@@ -668,7 +689,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
                         const float thr = fmaf(2.0f * kKeySlack, fabsf(K1), K1 + tau);
                         rqs[wave][qn + __builtin_amdgcn_mbcnt_hi((unsigned)(fin >> 32),
                                       __builtin_amdgcn_mbcnt_lo((unsigned)fin, 0u))] =
-                            make_uint2((uint32_t)v[b], __float_as_uint(thr));
+                            make_uint2((uint32_t)row0[b] + (uint32_t)r, __float_as_uint(thr));
                     }
                     qn += cnt;
                     deferred = finite_x[b];
@@ -702,7 +723,8 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
             // fast path: the winner's half stores; slow path: the lower half (inline code),
             // unless the vector waits in the queue
             if (valid[b] && (slow ? (h == 0 && !deferred) : mine)) {
-                codes[v[b] * m_total + m] = (CodeT)code;
+                *reinterpret_cast<CodeT*>(reinterpret_cast<char*>(codes + (row0[b] * m_total + m)) +
+                                          code_lane_off) = (CodeT)code;
                 if (kLdsA && counts) atomicAdd(&hist[wave][code], 1u);
             }
         }
@@ -781,59 +803,12 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         }
         return -1;
     };
-    long long ch = wave_id;
-    float xn[kNB][XD];
-#pragma unroll
-    for (int b = 0; b < kNB; ++b) load_x(ch * kNB + b, xn[b]);
-    while (ch < nchunk) {
-        float xa[kNB][XD];
-#pragma unroll
-        for (int b = 0; b < kNB; ++b)
-#pragma unroll
-            for (int j = 0; j < XD; ++j) xa[b][j] = xn[b][j];
-        long long nc;
-        if (!head) {
-            nc = ch + waves_m;
-        } else {
-            const long long c = next_dyn();
-            nc = c < 0 ? nchunk : c;
-        }
-        const long long pre = nc < nchunk ? nc : ch;   // branch-free: re-load at the end
-#pragma unroll
-        for (int b = 0; b < kNB; ++b) load_x(pre * kNB + b, xn[b]);
-        step(ch * kNB, xa);
+    // One batch of queued vectors (lane r: entry r; invalid lanes idle): re-screen, collect
+    // the candidates at or below the entry's threshold, evaluate them exactly (see the tail).
+    auto rerank32 = [&](const uint2 ent, const bool valid) {
 #ifdef PQH_ASSIGN_STAMPS
-        nbdone += kNB;
+        const unsigned long long rr0 = __builtin_amdgcn_s_memrealtime();
 #endif
-        ch = nc;
-    }
-    // Tail: this wave's queued vectors, 32 at a time.  thr = K1 + tau + 2^-16 |K1| bounds the
-    // screened score of every centroid whose fp32 direct-form distance can equal the minimum
-    // (S_k <= D_k - X + E0 <= D_min - X + E0 <= S_k1 + 2 E0 <= K1 + 2^-19 |K1| + 2 E0 < thr):
-    // the vectors are re-screened with the main loop's own instruction sequence (bitwise the
-    // same scores: same norms, and a lo pass adds exact zeros for bf16-exact x), the centroids
-    // screening at or below thr are collected per lane, and only those few are evaluated in
-    // exact fp32 direct form (first index among equal distances) -- instead of all K.
-    // The workgroup's waves share their queues (they finish their chunks within about one
-    // chunk of each other): batch j of the concatenated queues goes to wave j % waves.
-    __shared__ unsigned qlen[kWavesPerWG];
-    if (lane == 0) qlen[wave] = qn;
-#ifdef PQH_ASSIGN_TAILPRIO   // (experiment) the re-rank tail ahead of other waves' main loops
-    __builtin_amdgcn_s_setprio(PQH_ASSIGN_TAILPRIO);
-#endif
-    __syncthreads();
-    unsigned qoff[kWavesPerWG + 1];
-    qoff[0] = 0;
-#pragma unroll
-    for (int w = 0; w < kWavesPerWG; ++w) qoff[w + 1] = qoff[w] + qlen[w];
-    const unsigned qtot = qoff[kWavesPerWG];
-    for (unsigned e0 = 32u * wave; e0 < qtot; e0 += 32u * kWavesPerWG) {
-        const unsigned e = e0 + (unsigned)r;
-        const bool valid = e < qtot;
-        int qw = 0;
-#pragma unroll
-        for (int w = 1; w < kWavesPerWG; ++w) qw += e >= qoff[w] ? 1 : 0;
-        const uint2 ent = valid ? rqs[qw][e - qoff[qw]] : make_uint2(0u, 0u);
         const long long v = (long long)ent.x;
         const float thr = __uint_as_float(ent.y);
         float xv[D];
@@ -861,20 +836,65 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         const bool lo_pass = __any(lo);
         float best = INFINITY;
         int bidx = 0x7FFFFFFF;
+        // Eight tiles at a time: screen them all (a candidate bit mask per tile pair), then
+        // evaluate the candidates kCand per lane per round, their centroid rows loaded
+        // together -- the tail's time is L2 round trips, so they are few (one or two rounds
+        // per vector instead of one per tile holding a candidate).
+        constexpr int kGT = KT < 8 ? KT : 8;
+        constexpr int kCand = D <= 16 ? 4 : 2;
 #pragma unroll 1
-        for (int t = 0; t < KT; ++t) {   // (rolled: the tail keeps its registers few)
-            const f32x16 acc = tile_scores<D, KT>(asrc, Cn, lane, t, Bm, Bl, lo_pass);
-            uint32_t bits = 0;
+        for (int t0 = 0; t0 < KT; t0 += kGT) {
+            uint32_t cw[(kGT + 1) / 2];   // tiles t0 + 2w (bits 0-15) and t0 + 2w + 1 (16-31)
 #pragma unroll
-            for (int i = 0; i < 16; ++i) bits |= (acc[i] <= thr ? 1u : 0u) << i;
-            bits = valid ? bits : 0u;
-            while (__any(bits != 0)) {
-                if (bits) {
-                    const int i = __builtin_ctz(bits);
-                    bits &= bits - 1;
-                    const int k = tile_row(t, i, h);
-                    const float dd = exact_dist<D>(xv, cl + k * D);
-                    if (dd < best || (dd == best && k < bidx)) { best = dd; bidx = k; }
+            for (int w = 0; w < (kGT + 1) / 2; ++w) cw[w] = 0u;
+#pragma unroll 1
+            for (int u = 0; u < kGT; ++u) {   // (rolled: the tail keeps its registers few)
+                const f32x16 acc = tile_scores<D, KT>(asrc, Cn, lane, t0 + u, Bm, Bl, lo_pass);
+                uint32_t bits = 0;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) bits |= (acc[i] <= thr ? 1u : 0u) << i;
+                bits = (valid ? bits : 0u) << (16 * (u & 1));
+#pragma unroll
+                for (int w = 0; w < (kGT + 1) / 2; ++w) cw[w] |= w == (u >> 1) ? bits : 0u;
+            }
+            for (;;) {
+                int kc[kCand];
+                bool hc[kCand];
+#pragma unroll
+                for (int c = 0; c < kCand; ++c) {   // the lane's next candidate, if any
+                    hc[c] = false;
+                    kc[c] = 0;
+#pragma unroll
+                    for (int w = 0; w < (kGT + 1) / 2; ++w) {
+                        if (!hc[c] && cw[w]) {
+                            const int i = __builtin_ctz(cw[w]);
+                            cw[w] &= cw[w] - 1;
+                            hc[c] = true;
+                            kc[c] = tile_row(t0 + 2 * w + (i >> 4), i & 15, h);
+                        }
+                    }
+                }
+                if (!__any(hc[0])) break;
+                float cr[kCand][D];   // (lanes without a candidate read row 0)
+#pragma unroll
+                for (int c = 0; c < kCand; ++c) {
+                    const float* cp = cl + kc[c] * D;
+                    if constexpr (D % 4 == 0) {
+#pragma unroll
+                        for (int j = 0; j < D; j += 4) {
+                            const float4 q = *reinterpret_cast<const float4*>(cp + j);
+                            cr[c][j] = q.x; cr[c][j + 1] = q.y; cr[c][j + 2] = q.z; cr[c][j + 3] = q.w;
+                        }
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < D; ++j) cr[c][j] = cp[j];
+                    }
+                }
+#pragma unroll
+                for (int c = 0; c < kCand; ++c) {
+                    const float dd = exact_dist<D>(xv, cr[c]);
+                    const int k = kc[c];
+                    if (hc[c] && (dd < best || (dd == best && k < bidx))) { best = dd; bidx = k; }
                 }
             }
         }
@@ -886,6 +906,59 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
             codes[v * m_total + m] = (CodeT)code;
             if (kLdsA && counts) atomicAdd(&hist[wave][code], 1u);
         }
+#ifdef PQH_ASSIGN_STAMPS
+        rr_ticks += __builtin_amdgcn_s_memrealtime() - rr0;
+        ++rr_batches;
+#endif
+    };
+    long long ch = wave_id;
+    float xn[kNB][XD];
+#pragma unroll
+    for (int b = 0; b < kNB; ++b) load_x(ch * kNB + b, xn[b]);
+    while (ch < nchunk) {
+        float xa[kNB][XD];
+#pragma unroll
+        for (int b = 0; b < kNB; ++b)
+#pragma unroll
+            for (int j = 0; j < XD; ++j) xa[b][j] = xn[b][j];
+        long long nc;
+        if (!head) {
+            nc = ch + waves_m;
+        } else {
+            const long long c = next_dyn();
+            nc = c < 0 ? nchunk : c;
+        }
+        const long long pre = nc < nchunk ? nc : ch;   // branch-free: re-load at the end
+#pragma unroll
+        for (int b = 0; b < kNB; ++b) load_x(pre * kNB + b, xn[b]);
+        step(ch * kNB, xa);
+        while (qn >= 32u) {   // full batches of deferred vectors: done while the SIMD is busy
+            rerank32(rqs[wave][qn - 32u + (unsigned)r], true);
+            qn -= 32u;
+        }
+#ifdef PQH_ASSIGN_STAMPS
+        nbdone += kNB;
+#endif
+        ch = nc;
+    }
+#ifdef PQH_ASSIGN_STAMPS
+    const unsigned long long rt_loop = __builtin_amdgcn_s_memrealtime();
+#endif
+    // Tail: this wave's queued vectors, 32 at a time.  thr = K1 + tau + 2^-16 |K1| bounds the
+    // screened score of every centroid whose fp32 direct-form distance can equal the minimum
+    // (S_k <= D_k - X + E0 <= D_min - X + E0 <= S_k1 + 2 E0 <= K1 + 2^-19 |K1| + 2 E0 < thr):
+    // the vectors are re-screened with the main loop's own instruction sequence (bitwise the
+    // same scores: same norms, and a lo pass adds exact zeros for bf16-exact x), the centroids
+    // screening at or below thr are collected per lane, and only those few are evaluated in
+    // exact fp32 direct form (first index among equal distances) -- instead of all K.
+    // Full batches were finished in the chunk loop (while the SIMD had other waves to run);
+    // the wave's last, partial batch runs here, without waiting for the workgroup's other waves.
+#ifdef PQH_ASSIGN_TAILPRIO   // (experiment) the re-rank tail ahead of other waves' main loops
+    __builtin_amdgcn_s_setprio(PQH_ASSIGN_TAILPRIO);
+#endif
+    if (qn) {   // (qn < 32 here)
+        const bool valid = (unsigned)r < qn;
+        rerank32(valid ? rqs[wave][r] : make_uint2(0u, 0u), valid);
     }
 #ifdef PQH_ASSIGN_STAMPS
     {
@@ -894,7 +967,9 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
             g_assign_stamps[gw][0] = rt0;   // 100 MHz, chip-wide
             g_assign_stamps[gw][1] = __builtin_amdgcn_s_memrealtime();
             g_assign_stamps[gw][2] = nbdone | ((__builtin_amdgcn_s_memtime() - st0) << 16);
-            g_assign_stamps[gw][3] = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 15;
+            g_assign_stamps[gw][3] = (__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15) |
+                                     ((rt_loop - rt0) << 8) |   // chunk loop done
+                                     (rr_ticks << 32) | (rr_batches << 56);   // re-rank batches
         }
     }
 #endif
@@ -1227,6 +1302,7 @@ int pqh_pq_assign(pqh_ctx_t* ctx, const pqh_pq_t* cpq, const float* d_x, long lo
     if (mfma && pq->dsub % 4 == 0 &&
         ((ld_x % 4) != 0 || (reinterpret_cast<uintptr_t>(d_x) & 15u) != 0))
         mfma = false;  // vector loads need 16-byte aligned subspace slices
+    if (ld_x >= (1ll << 22)) mfma = false;   // its lane offsets within a block are 24-bit
     // the other paths re-rank nothing: their count is d_diag[6] = 0
     if (!mfma) {
         ctx->rerank_slot = 6;

@@ -29,11 +29,16 @@ def main():
     a = np.frombuffer(buf, dtype=np.uint64).reshape(W, 4).astype(np.int64)
     a = a[a[:, 1] > 0]
     t0 = a[:, 0].min()
-    st, en, nb, xcc = a[:, 0] - t0, a[:, 1] - t0, a[:, 2] & 0xFFFF, a[:, 3]
+    st, en, nb, xcc = a[:, 0] - t0, a[:, 1] - t0, a[:, 2] & 0xFFFF, a[:, 3] & 15
+    loop_end = st + ((a[:, 3] >> 8) & 0xFFFFFF)   # the chunk loop's end (the tail after it)
+    rr_t, rr_n = (a[:, 3] >> 32) & 0xFFFFFF, (a[:, 3] >> 56) & 0xFF   # re-rank batches
+    tail = en - loop_end
     cyc = a[:, 2] >> 16          # s_memtime lifetime (shader clock)
     life = en - st               # s_memrealtime: 100 MHz ticks, comparable across CUs
     print(f"waves {len(a)}  span {en.max()} ticks of 10 ns")
-    for name, v in (("start", st), ("end", en), ("life", life), ("blocks", nb), ("cycles", cyc)):
+    for name, v in (("start", st), ("end", en), ("loopend", loop_end), ("tail", tail), ("rr_ticks", rr_t), ("rr_batch", rr_n),
+                    ("rr_per_batch", rr_t // np.maximum(rr_n, 1)),
+                    ("life", life), ("blocks", nb), ("cycles", cyc)):
         q = np.percentile(v, [0, 5, 25, 50, 75, 95, 100]).astype(int)
         print(f"{name:7s} p0/5/25/50/75/95/100: {list(q)}")
     for c in range(8):
