@@ -825,7 +825,8 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         }
         float xs[XD];
 #pragma unroll
-        for (int j = 0; j < XD; ++j) xs[j] = valid ? xv[Slice<D>::dim(j, h)] : 0.0f;
+        for (int j = 0; j < XD; ++j)   // (static indices: a dynamic one puts xv in scratch)
+            xs[j] = valid ? (h ? xv[Slice<D>::dim(j, 1)] : xv[Slice<D>::dim(j, 0)]) : 0.0f;
         float X;
         bool lo;
         float xh[XD], xl[XD];
