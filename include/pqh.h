@@ -264,6 +264,38 @@ int pqh_shard_stitch(int world, const unsigned char* const* bufs,
 int pqh_shard_halo_source(const int* nonempty, int world, int rank, int* prev_rank,
                           int* raw_first);
 
+/* ---- forest builder of tree mode (compute_nn_fast.c + mst_builder.c) ---- */
+/* compute_nn_fast's block geometry (blocks_info_init / dimension_info_build,
+ * fast_nn_blocks_info.c:52-112) over n device rows of d floats (row stride ld_x): split i
+ * is coordinate num_split-1-i; h_starts / h_ends [num_split][blocks_per_dim] receive the
+ * block ranges the reference stores in dimension_infos[i].block_starts / block_ends.
+ * blocks_per_dim <= 32, num_split <= 8. */
+int pqh_knn_blocks_info(pqh_ctx_t* ctx, const float* d_x, long long n, long long ld_x, int d,
+                        int num_split, int blocks_per_dim, double overlap, float* h_starts,
+                        float* h_ends);
+/* compute_nn_fast with one block per pass (run, compute_nn_fast.c:510-620; the CLI's
+ * --num-dimensions-at-pass 0): every block's exact kNN among its rows, merged per row in
+ * block order into a num_nn max-heap (fast_nn_heap_push) and sorted -- d_indices / d_dists
+ * [n][num_nn] as nn_indices.ivecsl / nn_dist.fvecsl hold them (never-filled slots:
+ * 0xFFFFFFFF / +inf).  The in-block neighbours are the smallest direct-form fp32 squared
+ * distances (get_real_dist, :304-311), lower block position first on ties (the reference
+ * calls yael's knn_full_thread here: parity unpinned at that call).  d <= 128,
+ * num_nn <= 63.  h_block_sizes (may be NULL): [blocks_per_dim^num_split] rows per block. */
+int pqh_knn_fast(pqh_ctx_t* ctx, const float* d_x, long long n, long long ld_x, int d,
+                 int num_nn, int num_split, int blocks_per_dim, const float* h_starts,
+                 const float* h_ends, uint32_t* d_indices, float* d_dists,
+                 long long* h_block_sizes);
+/* mst_builder's forest (load_mst_edges_from_nn_files + minimum_spanning_tree,
+ * mst.c:80-236): the first `take` neighbours of each of the n rows of the kNN lists
+ * (num_nn per row, device), re-scored first when penalty > 0 (Hamming distance of the
+ * device PQ codes d_pq [n][pq_m] times penalty, or the Hamming distance alone when
+ * infinite), Kruskal in distance order.  Outputs tree_save_file's arrays (mst.c:253-265):
+ * h_targets [*num_edges <= 2 (n - 1)] grouped by source, h_counts [n].  Synchronises.
+ * PQH_ERR_ARG for a neighbour id outside the rows. */
+int pqh_mst_build(pqh_ctx_t* ctx, const uint32_t* d_indices, const float* d_dists, long long n,
+                  int num_nn, int take, const uint8_t* d_pq, int pq_m, float penalty,
+                  uint32_t* h_targets, int* h_counts, long long* num_edges);
+
 /* ---- tree-ordered context coding (huffman_encoder.c --tree: :240-286, :321-375) ---- */
 /* DFS order of a stored forest (mst.tree: tree_load_file, mst.c:273-288 -- num_edges
  * u32 targets grouped by source, children_counts[v] of them per vertex) exactly as

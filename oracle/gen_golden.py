@@ -262,8 +262,74 @@ def pq_fixtures():
                                 np.uint8))
 
 
+def forest_fixtures(tmp):
+    """The forest builder: the REFERENCE's block geometry (blocks_info_init over an .fvecs,
+    oracle/_ref/libref_knn.so), its block membership (is_vector_in_block), its heap merge
+    (fast_nn_heap_push/_sort) of the in-block neighbour lists, and mst_builder's mst.tree
+    (oracle/_ref/mst_builder) for three take / penalty settings.  The in-block neighbour
+    lists themselves (yael's knn_full_thread in the reference) are SELF-GENERATED by the
+    oracle's definition -- parity unpinned at that call -- and stored as the push log."""
+    sys.path.insert(0, ROOT)
+    from oracle import oracle_ctypes as oc
+    R = ctypes.CDLL(os.path.join(ROOT, "oracle", "_ref", "libref_knn.so"))
+    P = ctypes.c_void_p
+    R.refk_blocks_info.argtypes = [ctypes.c_char_p, ctypes.c_longlong, ctypes.c_int,
+                                   ctypes.c_int, ctypes.c_int, ctypes.c_double, P, P]
+    R.refk_in_block.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P,
+                                ctypes.c_longlong]
+    R.refk_merge.argtypes = [ctypes.c_longlong, ctypes.c_int, ctypes.c_longlong, P, P, P, P, P]
+    cases = (("sift_n1200_d16", datagen.sift_like(1200, 16, seed=31), 3, 4, 0.1, 10),
+             ("deep_n800_d12", datagen.deep_like(800, 12, seed=32), 2, 5, 0.3, 8))
+    for name, x, ns, nb, ov, nn in cases:
+        x = np.ascontiguousarray(x, np.float32)
+        n, d = x.shape
+        fv = os.path.join(tmp, f"{name}.fvecs")
+        datagen.write_fvecs(fv, x)
+        st = np.zeros((ns, nb), np.float32)
+        en = np.zeros_like(st)
+        R.refk_blocks_info(fv.encode(), n, d, ns, nb, ov, ptr(st), ptr(en))
+        member = np.zeros((nb ** ns, n), np.uint8)
+        for b in range(nb ** ns):
+            for v in range(n):
+                member[b, v] = R.refk_in_block(ptr(x[v]), d, ns, nb, ptr(st), ptr(en), b)
+        _, _, sizes, (lr, li, ld) = oc.knn_fast(x, nn, st, en, log=True)
+        ri = np.zeros((n, nn), np.uint32)
+        rd = np.zeros((n, nn), np.float32)
+        R.refk_merge(n, nn, len(lr), ptr(lr), ptr(li), ptr(ld), ptr(ri), ptr(rd))
+        nd = os.path.join(tmp, name + "_nn") + "/"
+        os.makedirs(nd, exist_ok=True)
+        for fn, a in (("nn_indices.ivecsl", ri), ("nn_dist.fvecsl", rd)):
+            with open(nd + fn, "wb") as f:
+                f.write(np.array([n, nn], np.uint32).tobytes() + a.tobytes())
+        codes = datagen.skewed_codes(n, 8, seed=33)
+        pqd = os.path.join(tmp, name + "_pq") + "/"
+        os.makedirs(pqd, exist_ok=True)
+        datagen.write_vecsl(pqd + "pq_indices.bvecsl", codes)
+        arrays = dict(x=x, num_split=ns, blocks_per_dim=nb, overlap=ov, num_nn=nn, starts=st,
+                      ends=en, member=member, push_row=lr, push_idx=li, push_dist=ld,
+                      nn_idx=ri, nn_dist=rd, pq=codes)
+        for tag, take, pen in (("t5_p0", 5, "0"), ("t3_p2.5", 3, "2.5"), ("tall_pinf", nn, "inf")):
+            od = os.path.join(tmp, f"{name}_{tag}") + "/"
+            os.makedirs(od, exist_ok=True)
+            subprocess.run([os.path.join(ROOT, "oracle", "_ref", "mst_builder"), nd, od, str(take),
+                            "--pq-template", pqd, "--pq-penalty", pen], check=True,
+                           capture_output=True)
+            arrays[f"tree_{tag}"] = np.frombuffer(read(od + "mst.tree"), np.uint8)
+            arrays[f"stats_{tag}"] = np.frombuffer(read(od + "stats.json"), np.uint8)
+            arrays[f"stats_children_{tag}"] = np.frombuffer(read(od + "stats_num_children.json"),
+                                                            np.uint8)
+        np.savez_compressed(os.path.join(GOLD, f"forest_{name}.npz"), **arrays)
+
+
 def main():
     build()
+    if sys.argv[1:] == ["forest"]:   # only the forest-builder fixtures
+        tmp = tempfile.mkdtemp(prefix="pqh_golden_")
+        try:
+            forest_fixtures(tmp)
+        finally:
+            shutil.rmtree(tmp, ignore_errors=True)
+        return
     if sys.argv[1:] == ["tree"]:   # only the tree-mode fixtures
         tmp = tempfile.mkdtemp(prefix="pqh_golden_")
         try:
@@ -291,6 +357,7 @@ def main():
             json.dump(summaries, f, indent=1)
         k4096_fixture(lib, tmp)
         pq_fixtures()
+        forest_fixtures(tmp)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
     print("golden fixtures written to", GOLD)

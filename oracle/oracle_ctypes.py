@@ -73,6 +73,12 @@ def _load(path):
         L.orc_tree_encode.argtypes = [P, LL, I, I, P, P, P, P, I, P, LL]
         L.orc_tree_encode.restype = LL
         L.orc_bitstream_write.restype = LL
+        L.orc_knn_blocks_info.argtypes = [P, LL, I, I, I, ctypes.c_double, P, P]
+        L.orc_in_block.argtypes = [P, I, I, P, P, LL]
+        L.orc_in_block.restype = I
+        L.orc_knn_fast.argtypes = [P, LL, I, I, I, I, P, P, P, P, P, P, P, P, P]
+        L.orc_mst.argtypes = [LL, I, I, P, P, I, ctypes.c_float, P, P, P]
+        L.orc_mst.restype = LL
         _libs[path] = L
         return L
 
@@ -302,3 +308,73 @@ def children_codebook(num_children) -> tuple[np.ndarray, Codebooks]:
     counts = np.bincount(nch, minlength=alphabet).astype(np.float64)
     lens, cds = codebook(alphabet, counts, False)
     return counts, Codebooks(alphabet, False, lens[None], cds[None], cds.shape[1])
+
+
+# ---- forest builder (compute_nn_fast.c, mst.c) ------------------------------------------
+def knn_blocks_info(x: np.ndarray, num_split: int, blocks_per_dim: int, overlap: float):
+    """(starts, ends) float32 [num_split][blocks_per_dim] -- blocks_info_init."""
+    x = np.ascontiguousarray(x, np.float32)
+    n, d = x.shape
+    st = np.zeros((num_split, blocks_per_dim), np.float32)
+    en = np.zeros_like(st)
+    lib().orc_knn_blocks_info(_p(x), n, d, num_split, blocks_per_dim, overlap, _p(st), _p(en))
+    return st, en
+
+
+def knn_members(x: np.ndarray, starts, ends) -> list:
+    """Rows of every block in block-id order (is_vector_in_block)."""
+    x = np.ascontiguousarray(x, np.float32)
+    st = np.ascontiguousarray(starts, np.float32)
+    en = np.ascontiguousarray(ends, np.float32)
+    ns, nb = st.shape
+    L = lib()
+    out = []
+    for b in range(nb ** ns):
+        out.append(np.array([v for v in range(x.shape[0])
+                             if L.orc_in_block(_p(x[v]), ns, nb, _p(st), _p(en), b)], np.int64))
+    return out
+
+
+def knn_fast(x: np.ndarray, num_nn: int, starts, ends, log: bool = False):
+    """(indices u32 [n][num_nn], dists f32, block_sizes[, (rows, idx, dist) push log])."""
+    x = np.ascontiguousarray(x, np.float32)
+    n, d = x.shape
+    st = np.ascontiguousarray(starts, np.float32)
+    en = np.ascontiguousarray(ends, np.float32)
+    ns, nb = st.shape
+    idx = np.zeros((max(n, 1), num_nn), np.uint32)
+    dist = np.zeros((max(n, 1), num_nn), np.float32)
+    sizes = np.zeros(nb ** ns, np.int64)
+    if log:
+        cap = n * num_nn * (nb ** ns) + 1
+        lr, li, ld = np.zeros(cap, np.int64), np.zeros(cap, np.uint32), np.zeros(cap, np.float32)
+        cnt = np.zeros(1, np.int64)
+        lib().orc_knn_fast(_p(x), n, d, num_nn, ns, nb, _p(st), _p(en), _p(idx), _p(dist),
+                           _p(sizes), _p(lr), _p(li), _p(ld), _p(cnt))
+        c = int(cnt[0])
+        return idx[:n], dist[:n], sizes, (lr[:c], li[:c], ld[:c])
+    lib().orc_knn_fast(_p(x), n, d, num_nn, ns, nb, _p(st), _p(en), _p(idx), _p(dist),
+                       _p(sizes), None, None, None, None)
+    return idx[:n], dist[:n], sizes
+
+
+def mst(indices: np.ndarray, dists: np.ndarray, take: int, pq=None, penalty: float = 0.0):
+    """(targets u32 [num_edges], counts i32 [n]) -- the arrays of mst.tree."""
+    idx = np.ascontiguousarray(indices, np.uint32)
+    dist = np.ascontiguousarray(dists, np.float32)
+    n, num_nn = idx.shape
+    pqa = None if pq is None else np.ascontiguousarray(pq, np.uint8)
+    pq_m = 0 if pqa is None else pqa.shape[1]
+    targets = np.zeros(max(2 * n, 1), np.uint32)
+    counts = np.zeros(max(n, 1), np.int32)
+    ne = lib().orc_mst(n, num_nn, take, _p(idx), _p(dist), pq_m, penalty,
+                       None if pqa is None else _p(pqa), _p(targets), _p(counts))
+    assert ne >= 0, "neighbour id outside the rows"
+    return targets[:ne], counts[:n]
+
+
+def tree_file(n: int, targets: np.ndarray, counts: np.ndarray) -> bytes:
+    """tree_save_file (mst.c:253-265): i64 N, i64 E, u32 targets[E], i32 counts[N]."""
+    return (np.array([n, len(targets)], np.int64).tobytes() +
+            np.ascontiguousarray(targets, np.uint32).tobytes() +
+            np.ascontiguousarray(counts, np.int32).tobytes())

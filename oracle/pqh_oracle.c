@@ -653,3 +653,233 @@ long long orc_tree_encode(const unsigned char* codes, long long n, int m, int k,
     }
     return w.overflow ? -1 : w.bits;
 }
+
+/* ------------------------------------------------------------------------------------
+ * Forest builder (tree mode's kNN graph and minimum spanning forest).
+ *
+ * orc_knn_blocks_info: blocks_info_init + dimension_info_build (fast_nn_blocks_info.c:52-112):
+ * split i (0 <= i < ns) is coordinate ns-1-i; its sorted values (qsort with float_cmp,
+ * :41-50 -- the same glibc qsort, so near-equal values land where the reference puts them)
+ * give block b the range [v[N b/nb - ov], v[min(N (b+1)/nb + ov, N-1)]], ov = (long long)
+ * (N overlap / 2), with the outer ends pushed out by 1.0.  starts/ends: [ns][nb] floats.
+ * ---------------------------------------------------------------------------------- */
+static int orc_float_cmp(const void* a, const void* b) {
+    float v = *(const float*)a - *(const float*)b;
+    if (fabs(v) < 1e-9) return 0;
+    return v < 0 ? -1 : 1;
+}
+
+void orc_knn_blocks_info(const float* x, long long n, int d, int ns, int nb, double overlap,
+                         float* starts, float* ends) {
+    float* vals = malloc(sizeof(float) * (n ? n : 1));
+    for (int i = 0; i < ns; ++i) {
+        const int coord = ns - 1 - i;
+        for (long long v = 0; v < n; ++v) vals[v] = x[v * d + coord];
+        qsort(vals, n, sizeof(float), orc_float_cmp);
+        const long long ov = (long long)(n * overlap / 2);
+        for (int b = 0; b < nb; ++b) {
+            long long s = n * b / nb - ov;
+            s = s < 0 ? 0 : (s > n ? n : s);
+            starts[i * nb + b] = vals[s];
+            long long e = n * (b + 1) / nb + ov;
+            e = e < 0 ? 0 : (e > n ? n : e);
+            ends[i * nb + b] = vals[e < n - 1 ? e : n - 1];
+        }
+        starts[i * nb] = vals[0] - 1.0;
+        ends[i * nb + nb - 1] = vals[n - 1] + 1.0;
+    }
+    free(vals);
+}
+
+/* is_vector_in_block (fast_nn_blocks_info.c:187-239): block id digit of split i is
+ * (B / nb^(ns-1-i)) % nb; inside means start <= x <= end on every split. */
+int orc_in_block(const float* vec, int ns, int nb, const float* starts, const float* ends,
+                 long long block) {
+    for (int i = 0; i < ns; ++i) {
+        const int coord = ns - 1 - i;
+        long long mask = 1;
+        for (int q = 0; q < coord; ++q) mask *= nb;
+        const long long b = block / mask % nb;
+        const float val = vec[coord];
+        if (val < starts[i * nb + b] || val > ends[i * nb + b]) return 0;
+    }
+    return 1;
+}
+
+typedef struct { unsigned index; float dist; } orc_nn_t;
+
+/* fast_nn_heap_push_impl / _push / _sort (fast_nn_temp_file.c:11-63): a max-heap of num_nn
+ * (index, dist) items, initialised to (UINT_MAX, +inf) (:93-108); a candidate enters when
+ * it is strictly closer than the root and its index is not in the heap. */
+static void orc_nn_sift(orc_nn_t* heap, orc_nn_t item, int k) {
+    int i = 0;
+    for (;;) {
+        const int l = 2 * i + 1, r = 2 * i + 2;
+        int sw;
+        if (r < k && heap[r].dist > heap[l].dist && heap[r].dist > item.dist) sw = r;
+        else if (l < k && heap[l].dist > item.dist) sw = l;
+        else break;
+        heap[i] = heap[sw];
+        i = sw;
+    }
+    heap[i] = item;
+}
+
+static void orc_nn_push(orc_nn_t* heap, orc_nn_t item, int k) {
+    if (item.dist >= heap[0].dist) return;
+    for (int q = 0; q < k; ++q)
+        if (heap[q].index == item.index) return;
+    orc_nn_sift(heap, item, k);
+}
+
+static void orc_nn_sort(orc_nn_t* heap, int k, unsigned* idx, float* dist) {
+    while (--k >= 0) {
+        idx[k] = heap[0].index;
+        dist[k] = heap[0].dist;
+        orc_nn_sift(heap, heap[k], k);
+    }
+}
+
+static float orc_l2(const float* a, const float* b, int d) {
+    float acc = 0.0f;   /* get_real_dist (compute_nn_fast.c:304-311), separate roundings */
+    for (int j = 0; j < d; ++j) {
+        const float t = a[j] - b[j];
+        acc = acc + t * t;
+    }
+    return acc;
+}
+
+/* compute_nn_fast run/run_block/run_merge_block (compute_nn_fast.c:469-620) with one block
+ * per pass (--num-dimensions-at-pass 0): blocks in id order, each block's members in row
+ * order; the block kNN (yael knn_full_thread, :479-481 -- parity unpinned: yael is absent)
+ * is defined as the num_nn_real + 1 smallest direct-form fp32 distances with the lower
+ * block position first among equal distances; entries 1.. are pushed into the row's heap
+ * (:490-507); temp_file_to_result sorts the heaps (fast_nn_temp_file.c:253-301).
+ * Also reports (optional, may be NULL) every block's size. */
+void orc_knn_fast(const float* x, long long n, int d, int num_nn, int ns, int nb,
+                  const float* starts, const float* ends, unsigned* out_idx, float* out_dist,
+                  long long* block_sizes, long long* log_row, unsigned* log_idx,
+                  float* log_dist, long long* log_n) {
+    /* log_*: when given, the heap pushes in the reference's order (single-threaded) */
+    orc_nn_t* heaps = malloc(sizeof(orc_nn_t) * (size_t)(n ? n : 1) * num_nn);
+    for (long long q = 0; q < n * num_nn; ++q) { heaps[q].index = 0xFFFFFFFFu; heaps[q].dist = INFINITY; }
+    long long* mem = malloc(sizeof(long long) * (n ? n : 1));
+    long long nblocks = 1;
+    for (int i = 0; i < ns; ++i) nblocks *= nb;
+    for (long long B = 0; B < nblocks; ++B) {
+        long long S = 0;
+        for (long long v = 0; v < n; ++v)
+            if (orc_in_block(x + v * d, ns, nb, starts, ends, B)) mem[S++] = v;
+        if (block_sizes) block_sizes[B] = S;
+        if (S == 0) continue;
+        const int nreal = (int)(num_nn < S - 1 ? num_nn : S - 1);
+        const int kk = nreal + 1;
+        #pragma omp parallel for schedule(dynamic, 16) if (!log_n)
+        for (long long q = 0; q < S; ++q) {
+            long long li[kk];   /* sorted by (dist, position) */
+            float ld[kk];
+            int cnt = 0;
+            const float* xq = x + mem[q] * d;
+            for (long long c = 0; c < S; ++c) {
+                const float dd = orc_l2(xq, x + mem[c] * d, d);
+                if (cnt == kk && !(dd < ld[kk - 1])) continue;
+                int p = cnt < kk ? cnt++ : kk - 1;
+                while (p > 0 && ld[p - 1] > dd) { ld[p] = ld[p - 1]; li[p] = li[p - 1]; --p; }
+                ld[p] = dd;
+                li[p] = c;
+            }
+            orc_nn_t* heap = heaps + mem[q] * num_nn;
+            for (int j = 1; j < cnt; ++j) {
+                orc_nn_t it = {(unsigned)mem[li[j]], ld[j]};
+                if (log_n) {
+                    log_row[*log_n] = mem[q];
+                    log_idx[*log_n] = it.index;
+                    log_dist[*log_n] = it.dist;
+                    ++*log_n;
+                }
+                orc_nn_push(heap, it, num_nn);
+            }
+        }
+    }
+    for (long long v = 0; v < n; ++v)
+        orc_nn_sort(heaps + v * num_nn, num_nn, out_idx + v * num_nn, out_dist + v * num_nn);
+    free(mem);
+    free(heaps);
+}
+
+/* mst_builder (mst_builder.c:98-131): load_mst_edges_from_nn_files (mst.c:80-171) keeps the
+ * first `take` of each row's num_nn neighbours -- with a PQ penalty the row is first re-scored
+ * (dist += Hamming(codes) * penalty, or = Hamming for an infinite penalty) and sorted;
+ * minimum_spanning_tree (mst.c:173-236): qsort by distance (mst_dist_comparator, :15-26),
+ * Kruskal over a DSU, then both directions of every kept edge sorted by source
+ * (mst_source_comparator, :28-32).  glibc qsort as the reference calls it.  Outputs the
+ * tree_save_file arrays (mst.c:253-265): edge targets (2 (kept) of them) and per-vertex
+ * edge counts.  Returns the edge count, -1 for a neighbour id outside the rows. */
+typedef struct { unsigned source, target; float dist; } orc_edge_t;
+
+static int orc_edge_dist_cmp(const void* a, const void* b) {
+    const float diff = ((const orc_edge_t*)a)->dist - ((const orc_edge_t*)b)->dist;
+    if (fabs(diff) < 1e-9) return 0;
+    return diff < 0 ? -1 : 1;
+}
+
+static int orc_edge_src_cmp(const void* a, const void* b) {
+    const long long x = ((const orc_edge_t*)a)->source, y = ((const orc_edge_t*)b)->source;
+    return (int)(x - y);
+}
+
+static unsigned orc_dsu_find(unsigned* parent, unsigned v) {
+    unsigned r = v;
+    while (parent[r] != r) r = parent[r];
+    while (parent[v] != r) { const unsigned nx = parent[v]; parent[v] = r; v = nx; }
+    return r;
+}
+
+long long orc_mst(long long n, int num_nn, int take, const unsigned* idx, const float* dist,
+                  int pq_m, float penalty, const unsigned char* pq, unsigned* targets,
+                  int* counts) {
+    orc_edge_t* e = malloc(sizeof(orc_edge_t) * (size_t)(n * take > 0 ? n * take : 1));
+    orc_edge_t* row = malloc(sizeof(orc_edge_t) * (size_t)(num_nn ? num_nn : 1));
+    for (long long v = 0; v < n; ++v) {
+        for (int j = 0; j < num_nn; ++j) {
+            row[j].source = (unsigned)v;
+            row[j].target = idx[v * num_nn + j];
+            row[j].dist = dist[v * num_nn + j];
+            if (row[j].target >= n) { free(e); free(row); return -1; }
+            if (penalty > 0.0f) {
+                int ham = 0;
+                for (int i = 0; i < pq_m; ++i)
+                    ham += pq[v * pq_m + i] != pq[(long long)row[j].target * pq_m + i];
+                if (isinf(penalty)) row[j].dist = ham;
+                else row[j].dist += ham * penalty;
+            }
+        }
+        if (penalty > 0.0f) qsort(row, num_nn, sizeof(orc_edge_t), orc_edge_dist_cmp);
+        memcpy(e + v * take, row, sizeof(orc_edge_t) * take);
+    }
+    free(row);
+    const long long ne = n * take;
+    qsort(e, ne, sizeof(orc_edge_t), orc_edge_dist_cmp);
+    unsigned* parent = malloc(sizeof(unsigned) * (n ? n : 1));
+    for (long long v = 0; v < n; ++v) { parent[v] = (unsigned)v; counts[v] = 0; }
+    long long good = 0;
+    for (long long q = 0; good + 1 < n && q < ne; ++q) {
+        const unsigned a = orc_dsu_find(parent, e[q].source), b = orc_dsu_find(parent, e[q].target);
+        if (a == b) continue;
+        ++counts[e[q].source];
+        parent[b] = a;
+        const orc_edge_t t = e[q]; e[q] = e[good]; e[good] = t;
+        ++good;
+    }
+    for (long long q = 0; q < good; ++q) {
+        e[good + q].source = e[q].target;
+        e[good + q].target = e[q].source;
+        e[good + q].dist = e[q].dist;
+        ++counts[e[q].target];
+    }
+    qsort(e, 2 * good, sizeof(orc_edge_t), orc_edge_src_cmp);
+    for (long long q = 0; q < 2 * good; ++q) targets[q] = e[q].target;
+    free(parent);
+    free(e);
+    return 2 * good;
+}

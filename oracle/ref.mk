@@ -23,7 +23,8 @@ BINS := $(OUT)/huffman_encoder $(OUT)/huffman_decoder \
         $(OUT)/relink/huffman_encoder $(OUT)/relink/huffman_decoder \
         $(OUT)/huffman_encoder_O0 $(OUT)/huffman_decoder_O0 \
         $(OUT)/bitstream_test $(OUT)/huffman_encode_test $(OUT)/huffman_decode_test \
-        $(OUT)/huffman_codebook_test $(OUT)/libref.so
+        $(OUT)/huffman_codebook_test $(OUT)/libref.so \
+        $(OUT)/mst_builder $(OUT)/libref_knn.so
 
 .PHONY: all clean
 all: $(BINS)
@@ -66,6 +67,16 @@ $(OUT)/huffman_codebook_test: $(LIBSRC) | $(OUT)
 
 $(OUT)/libref.so: oracle/ref_harness.c $(LIBSRC) | $(OUT)
 	$(CC) $(CFLAGS_O2) -fPIC -shared -o $@ $^ -lm
+
+# the forest builder's yael-free parts: mst_builder as shipped (mst_builder.c + mst.c + dsu.c
+# + the library), and the kNN block geometry / heap merge of compute_nn_fast behind
+# oracle/ref_knn_harness.c (compute_nn_fast.c itself includes yael/nn.h: not buildable)
+$(OUT)/mst_builder: $(REF)/mst_builder.c $(LIBSRC) $(TREESRC) | $(OUT)
+	$(CC) $(CFLAGS_O2) -o $@ $^ -lm
+KNNSRC := $(REF)/fast_nn_blocks_info.c $(REF)/fast_nn_temp_file.c $(REF)/fast_nn_block.c \
+          $(REF)/misc.c $(REF)/vecs_io.c
+$(OUT)/libref_knn.so: oracle/ref_knn_harness.c $(KNNSRC) | $(OUT)
+	$(CC) -std=gnu99 -O2 -w -I$(REF) -fPIC -shared -o $@ $^ -lm -lpthread
 
 clean:
 	rm -rf $(OUT)

@@ -152,6 +152,9 @@ SIGNATURES = [
     ("pqh_decode_tree_files", I, [S, P, P, P]),
     ("pqh_encode_files", I, [P, LL, I, P, S]),
     ("pqh_decode_files", I, [S, P, P, P]),
+    ("pqh_knn_blocks_info", I, [P, P, LL, LL, I, I, I, D, P, P]),
+    ("pqh_knn_fast", I, [P, P, LL, LL, I, I, I, I, P, P, P, P, P]),
+    ("pqh_mst_build", I, [P, P, P, LL, I, I, P, I, ctypes.c_float, P, P, P]),
 ]
 
 _lib = None

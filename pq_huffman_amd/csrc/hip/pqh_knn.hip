@@ -1,0 +1,729 @@
+// pqh_knn.hip -- the forest builder of tree mode on gfx950: compute_nn_fast's blocked kNN
+// graph and mst_builder's minimum spanning forest.
+//
+//  knn geometry   blocks_info_init / dimension_info_build (fast_nn_blocks_info.c:52-112):
+//                 split i is coordinate ns-1-i; block b of a split covers the sorted values
+//                 [N b/nb - ov, N (b+1)/nb + ov] (ov = N overlap / 2), outer ends pushed out
+//                 by 1.  The column is sorted on the device (rocPRIM radix sort); see
+//                 "near-equal values" below for the one case that needs the host qsort.
+//  block members  is_vector_in_block (:187-239) for every (row, block) at once: per row and
+//                 split a bit mask of the blocks whose range holds the coordinate, the rows'
+//                 (block, row) pairs emitted in ascending block id, stably sorted by block
+//                 -> every block's rows in row order (block_loader2_thread, :84-150 of
+//                 fast_nn_block_loader2.c).
+//  block kNN      knn_full_thread (compute_nn_fast.c:479-481, yael -- absent here, so the
+//                 in-block neighbours are defined by the oracle: the num_nn_real + 1 smallest
+//                 direct-form fp32 distances (get_real_dist, :304-311), the lower block
+//                 position first among equal distances).  One wave per 64 queries of a
+//                 block: queries in VGPRs, 64-row candidate tiles in LDS read as broadcasts,
+//                 a per-lane sorted top-KMAX list kept by a compare-exchange network.
+//  merge          run_merge_block (:485-508) + fast_nn_heap_push/_sort
+//                 (fast_nn_temp_file.c:11-63): one lane per row replays its blocks' lists
+//                 in block order into its max-heap (LDS), then heap-sorts it.
+//  mst            load_mst_edges_from_nn_files + minimum_spanning_tree (mst.c:80-236): PQ
+//                 penalty re-scoring and the per-row sort on the device, the global edge
+//                 sort by distance as a stable radix sort, Kruskal's union-find on the host
+//                 (a sequential scan), adjacency by a stable counting sort by source.
+//
+// Near-equal values: the reference sorts with comparators that call two floats equal when
+// they differ by less than 1e-9 (fast_nn_blocks_info.c:41-50, mst.c:15-26).  For any array
+// without two DISTINCT values that close, glibc's merge sort with that comparator gives
+// exactly the stable sort by value that the device computes; the device checks every
+// adjacent pair of the sorted values, and if such a pair exists the affected sort is redone
+// by glibc qsort on the host with the reference comparator (so the result stays the
+// reference's), never silently approximated.
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "pqh_internal.h"
+
+namespace {
+
+constexpr int kQ = 64;   // queries (lanes) per kNN workgroup = candidate rows per LDS tile
+
+struct DevBuf {   // device allocations of one call, released on every exit path
+    std::vector<void*> ptrs;
+    ~DevBuf() {
+        for (void* p : ptrs) (void)hipFree(p);
+    }
+    template <typename T>
+    T* get(size_t count) {
+        void* p = nullptr;
+        if (hipMalloc(&p, count ? count * sizeof(T) : 16) != hipSuccess) return nullptr;
+        ptrs.push_back(p);
+        return static_cast<T*>(p);
+    }
+};
+
+// ------------------------------------------------------------------ geometry
+__global__ void __launch_bounds__(256)
+knn_column(const float* __restrict__ x, long long n, long long ld, int coord,
+           uint32_t* __restrict__ keys) {
+    const long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= n) return;
+    float f = x[v * ld + coord];
+    if (f == 0.0f) f = 0.0f;   // -0 sorts with +0 (the comparator calls them equal)
+    const uint32_t b = __float_as_uint(f);
+    keys[v] = (b & 0x80000000u) ? ~b : (b | 0x80000000u);   // order-preserving bits
+}
+
+__device__ __forceinline__ float key_float(uint32_t k) {
+    return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+}
+
+// flag[0] |= 1 when two adjacent sorted values are distinct but closer than 1e-9 (the
+// comparator's "equal" band; float difference, as the reference computes it)
+__global__ void __launch_bounds__(256)
+near_equal_check(const uint32_t* __restrict__ keys, long long n, int* __restrict__ flag) {
+    const long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v + 1 >= n) return;
+    if (keys[v] == keys[v + 1]) return;
+    const float a = key_float(keys[v]), b = key_float(keys[v + 1]);
+    if (fabs((double)(b - a)) < 1e-9) atomicOr(flag, 1);
+}
+
+// the block bounds of one split from its sorted values (dimension_info_build, :70-81)
+__global__ void knn_bounds(const uint32_t* __restrict__ sorted, long long n, int nb, long long ov,
+                           float* __restrict__ starts, float* __restrict__ ends) {
+    const int b = threadIdx.x;
+    if (b >= nb) return;
+    long long s = n * b / nb - ov;
+    s = s < 0 ? 0 : (s > n ? n : s);
+    long long e = n * (b + 1) / nb + ov;
+    e = e < 0 ? 0 : (e > n ? n : e);
+    e = e < n - 1 ? e : n - 1;
+    float sv = key_float(sorted[s < n ? s : n - 1]);
+    float ev = key_float(sorted[e]);
+    if (b == 0) sv = (float)((double)key_float(sorted[0]) - 1.0);
+    if (b == nb - 1) ev = (float)((double)key_float(sorted[n - 1]) + 1.0);
+    starts[b] = sv;
+    ends[b] = ev;
+}
+
+// ------------------------------------------------------------------ block members
+struct Geo {
+    int ns, nb;
+    const float* starts;   // [ns][nb]
+    const float* ends;
+};
+
+// per row and split, the mask of blocks holding the coordinate; count = product of popcounts
+__global__ void __launch_bounds__(256)
+knn_masks(const float* __restrict__ x, long long n, long long ld, Geo g,
+          uint32_t* __restrict__ masks, uint32_t* __restrict__ count) {
+    const long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= n) return;
+    unsigned long long c = 1;
+    for (int i = 0; i < g.ns; ++i) {
+        const float val = x[v * ld + (g.ns - 1 - i)];
+        uint32_t mk = 0;
+        for (int b = 0; b < g.nb; ++b)
+            if (!(val < g.starts[i * g.nb + b] || val > g.ends[i * g.nb + b])) mk |= 1u << b;
+        masks[v * g.ns + i] = mk;
+        c *= (unsigned long long)__popc(mk);
+    }
+    count[v] = (uint32_t)c;
+}
+
+// the row's (block, emission index) pairs in ascending block id: split 0 is the most
+// significant digit (weight nb^(ns-1)), so an odometer over the masks' set bits with split
+// ns-1 fastest enumerates them in order
+__global__ void __launch_bounds__(256)
+knn_emit(const uint32_t* __restrict__ masks, long long n, Geo g,
+         const unsigned long long* __restrict__ off, uint32_t* __restrict__ keys,
+         uint32_t* __restrict__ vals, uint32_t* __restrict__ erow) {
+    const long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= n) return;
+    unsigned long long e = off[v];
+    if (off[v + 1] == e) return;
+    uint32_t mk[8], cur[8];
+    for (int i = 0; i < g.ns; ++i) {
+        mk[i] = masks[v * g.ns + i];
+        cur[i] = mk[i] & (0u - mk[i]);   // lowest set bit
+    }
+    for (;;) {
+        uint32_t B = 0;
+        for (int i = 0; i < g.ns; ++i) B = B * (uint32_t)g.nb + (uint32_t)(__ffs(cur[i]) - 1);
+        keys[e] = B;
+        vals[e] = (uint32_t)e;
+        erow[e] = (uint32_t)v;
+        ++e;
+        int i = g.ns - 1;   // advance: next set bit of the fastest digit, carry to slower ones
+        for (; i >= 0; --i) {
+            const uint32_t rest = mk[i] & ~((cur[i] << 1) - 1u);
+            if (rest) {
+                cur[i] = rest & (0u - rest);
+                break;
+            }
+            cur[i] = mk[i] & (0u - mk[i]);
+        }
+        if (i < 0) break;
+    }
+}
+
+// sorted pair p: its row, and the emission index's position p
+__global__ void __launch_bounds__(256)
+knn_place(const uint32_t* __restrict__ sorted_vals, long long np, const uint32_t* __restrict__ erow,
+          uint32_t* __restrict__ rows, uint32_t* __restrict__ inv) {
+    const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= np) return;
+    const uint32_t e = sorted_vals[p];
+    rows[p] = erow[e];
+    inv[e] = (uint32_t)p;
+}
+
+// boff[b] = first sorted pair of block b (lower bound in the sorted keys)
+__global__ void __launch_bounds__(256)
+knn_block_offsets(const uint32_t* __restrict__ keys, long long np, long long nblocks,
+                  long long* __restrict__ boff) {
+    const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b > nblocks) return;
+    long long lo = 0, hi = np;
+    while (lo < hi) {
+        const long long mid = (lo + hi) >> 1;
+        if ((long long)keys[mid] < b) lo = mid + 1;
+        else hi = mid;
+    }
+    boff[b] = lo;
+}
+
+// ------------------------------------------------------------------ block kNN
+// One wave = up to 64 queries of one block (tile list built on the host).  Every lane keeps
+// its top-KMAX (distance, block position) list sorted ascending -- equal distances in
+// position order, because candidates arrive in position order and a new entry goes after
+// equal ones -- updated by a compare-exchange network with static register indices.  The
+// first kk = min(num_nn, S - 1) + 1 entries are the block kNN (kk <= KMAX).
+template <int DMAX, int KMAX>
+__global__ void __launch_bounds__(kQ)
+knn_block_topk(const float* __restrict__ x, long long ld, int d, int num_nn,
+               const uint32_t* __restrict__ rows, const long long* __restrict__ boff,
+               const long long* __restrict__ tile_block, const long long* __restrict__ tile_q0,
+               int stride, float* __restrict__ out_dist, uint32_t* __restrict__ out_row) {
+    __shared__ float cand[kQ * DMAX];
+    const int lane = threadIdx.x;
+    const long long b = tile_block[blockIdx.x];
+    const long long base = boff[b];
+    const long long S = boff[b + 1] - base;
+    const long long q = tile_q0[blockIdx.x] + lane;
+    const bool valid = q < S;
+    const int kk = (int)((num_nn < S - 1 ? num_nn : S - 1) + 1);
+    float qv[DMAX];
+    {
+        const float* xq = x + (long long)rows[base + (valid ? q : 0)] * ld;
+#pragma unroll
+        for (int j = 0; j < DMAX; ++j) qv[j] = j < d ? xq[j] : 0.0f;
+    }
+    float ld_[KMAX];
+    uint32_t lp_[KMAX];
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) {
+        ld_[j] = INFINITY;
+        lp_[j] = 0xFFFFFFFFu;
+    }
+    float thr = INFINITY;
+    for (long long c0 = 0; c0 < S; c0 += kQ) {
+        const int nc = (int)(S - c0 < kQ ? S - c0 : kQ);
+        __syncthreads();
+        for (int f = lane; f < nc * d; f += kQ) {   // stage the tile (rows in block order)
+            const int r = f / d, j = f - r * d;
+            cand[r * DMAX + j] = x[(long long)rows[base + c0 + r] * ld + j];
+        }
+        __syncthreads();
+        for (int c = 0; c < nc; ++c) {
+            const float* cr = cand + c * DMAX;
+            float acc = 0.0f;   // get_real_dist: (x - y)^2 summed in dimension order
+#pragma unroll
+            for (int j = 0; j < DMAX; ++j) {
+                if (j < d) {
+                    const float t = __fsub_rn(qv[j], cr[j]);
+                    acc = __fadd_rn(acc, __fmul_rn(t, t));
+                }
+            }
+            const bool ins = valid && acc < thr;
+            if (__any(ins)) {
+                const uint32_t pos = (uint32_t)(c0 + c);
+#pragma unroll
+                for (int j = KMAX - 1; j >= 1; --j) {
+                    const bool shift = ld_[j - 1] > acc, put = ld_[j] > acc;
+                    const float nd = shift ? ld_[j - 1] : (put ? acc : ld_[j]);
+                    const uint32_t np = shift ? lp_[j - 1] : (put ? pos : lp_[j]);
+                    ld_[j] = ins ? nd : ld_[j];
+                    lp_[j] = ins ? np : lp_[j];
+                }
+                const bool put0 = ld_[0] > acc;
+                ld_[0] = ins && put0 ? acc : ld_[0];
+                lp_[0] = ins && put0 ? pos : lp_[0];
+                thr = ld_[KMAX - 1];
+            }
+        }
+    }
+    if (!valid) return;
+    const long long pair = base + q;
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) {
+        if (j < kk) {
+            out_dist[pair * stride + j] = ld_[j];
+            out_row[pair * stride + j] = rows[base + lp_[j]];
+        }
+    }
+}
+
+// ------------------------------------------------------------------ merge
+struct NnItem {
+    uint32_t index;
+    float dist;
+};
+
+// fast_nn_heap_push_impl (fast_nn_temp_file.c:23-46): the item replaces the root and sinks
+// while a child is strictly heavier (the right one when it is the heavier of the two)
+__device__ __forceinline__ void nn_sift(NnItem* h, NnItem it, int k) {
+    int i = 0;
+    for (;;) {
+        const int l = 2 * i + 1, r = 2 * i + 2;
+        int sw;
+        if (r < k && h[r].dist > h[l].dist && h[r].dist > it.dist) sw = r;
+        else if (l < k && h[l].dist > it.dist) sw = l;
+        else break;
+        h[i] = h[sw];
+        i = sw;
+    }
+    h[i] = it;
+}
+
+// one lane per row: its blocks' lists (entries 1 .. kk-1) in block order into the heap, then
+// fast_nn_heap_sort into the output row
+__global__ void __launch_bounds__(kQ)
+knn_merge(long long n, int num_nn, const unsigned long long* __restrict__ off,
+          const uint32_t* __restrict__ inv, const uint32_t* __restrict__ keys_sorted,
+          const long long* __restrict__ boff, int stride, const float* __restrict__ ldist,
+          const uint32_t* __restrict__ lrow, uint32_t* __restrict__ out_idx,
+          float* __restrict__ out_dist) {
+    extern __shared__ NnItem heaps[];
+    const long long v = (long long)blockIdx.x * kQ + threadIdx.x;
+    if (v >= n) return;
+    NnItem* h = heaps + threadIdx.x * num_nn;
+    for (int j = 0; j < num_nn; ++j) h[j] = NnItem{0xFFFFFFFFu, INFINITY};
+    for (unsigned long long e = off[v]; e < off[v + 1]; ++e) {
+        const long long p = inv[e];
+        const long long b = keys_sorted[p];
+        const long long S = boff[b + 1] - boff[b];
+        const int kk = (int)((num_nn < S - 1 ? num_nn : S - 1) + 1);
+        for (int j = 1; j < kk; ++j) {
+            const NnItem it{lrow[p * stride + j], ldist[p * stride + j]};
+            if (!(it.dist < h[0].dist)) continue;
+            bool dup = false;
+            for (int q = 0; q < num_nn; ++q) dup |= h[q].index == it.index;
+            if (!dup) nn_sift(h, it, num_nn);
+        }
+    }
+    for (int k = num_nn - 1; k >= 0; --k) {
+        out_idx[v * num_nn + k] = h[0].index;
+        out_dist[v * num_nn + k] = h[0].dist;
+        nn_sift(h, h[k], k);
+    }
+}
+
+// ------------------------------------------------------------------ mst edges
+// Row v's first `take` neighbours as edges; with a PQ penalty every neighbour is re-scored
+// (dist += Hamming * penalty, = Hamming when infinite: mst.c:117-130) and the row stably
+// sorted by the new distance first (qsort at :133-135).  flag bit 1: a neighbour id outside
+// the rows; bit 2: a row holds two distinct re-scored distances closer than 1e-9.
+__global__ void __launch_bounds__(kQ)
+mst_row_edges(const uint32_t* __restrict__ idx, const float* __restrict__ dist, long long n,
+              int num_nn, int take, const uint8_t* __restrict__ pq, int pq_m, float penalty,
+              uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, uint32_t* __restrict__ src,
+              uint32_t* __restrict__ dst, float* __restrict__ edist, int* __restrict__ flag) {
+    extern __shared__ NnItem rowbuf[];
+    const long long v = (long long)blockIdx.x * kQ + threadIdx.x;
+    if (v >= n) return;
+    NnItem* r = rowbuf + threadIdx.x * num_nn;
+    int bad = 0;
+    for (int j = 0; j < num_nn; ++j) {
+        NnItem it{idx[v * num_nn + j], dist[v * num_nn + j]};
+        if (it.index >= n) {
+            bad |= 1;
+            it.index = 0;
+        }
+        if (penalty > 0.0f) {
+            int ham = 0;
+            for (int i = 0; i < pq_m; ++i)
+                ham += pq[v * pq_m + i] != pq[(long long)it.index * pq_m + i];
+            if (isinf(penalty)) it.dist = (float)ham;
+            else it.dist = __fadd_rn(it.dist, __fmul_rn((float)ham, penalty));
+            int p = j;   // stable insertion: after equal distances
+            while (p > 0 && r[p - 1].dist > it.dist) {
+                r[p] = r[p - 1];
+                --p;
+            }
+            r[p] = it;
+        } else {
+            r[j] = it;
+        }
+    }
+    if (penalty > 0.0f)
+        for (int j = 0; j + 1 < num_nn; ++j) {
+            const float df = r[j + 1].dist - r[j].dist;
+            if (df != 0.0f && fabs((double)df) < 1e-9) bad |= 2;
+        }
+    for (int j = 0; j < take; ++j) {
+        const long long e = v * take + j;
+        float f = r[j].dist;
+        if (f == 0.0f) f = 0.0f;
+        const uint32_t bits = __float_as_uint(f);
+        keys[e] = (bits & 0x80000000u) ? ~bits : (bits | 0x80000000u);
+        vals[e] = (uint32_t)e;
+        src[e] = (uint32_t)v;
+        dst[e] = r[j].index;
+        edist[e] = r[j].dist;
+    }
+    if (bad) atomicOr(flag, bad);
+}
+
+__global__ void __launch_bounds__(256)
+gather_pairs(const uint32_t* __restrict__ order, long long ne, const uint32_t* __restrict__ src,
+             const uint32_t* __restrict__ dst, uint2* __restrict__ out) {
+    const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= ne) return;
+    const uint32_t q = order[e];
+    out[e] = make_uint2(src[q], dst[q]);
+}
+
+// ------------------------------------------------------------------ host helpers
+int radix_sort_u32(pqh_ctx* ctx, DevBuf& buf, uint32_t* k_in, uint32_t* k_out, uint32_t* v_in,
+                   uint32_t* v_out, long long n) {
+    size_t temp = 0;
+    PQH_HIP(ctx, rocprim::radix_sort_pairs(nullptr, temp, k_in, k_out, v_in, v_out, (size_t)n,
+                                           0u, 32u, ctx->stream));
+    void* t = buf.get<char>(temp);
+    if (!t) return pqh_set_error(ctx, PQH_ERR_NOMEM, "knn: sort temp (%zu B)", temp);
+    PQH_HIP(ctx, rocprim::radix_sort_pairs(t, temp, k_in, k_out, v_in, v_out, (size_t)n, 0u, 32u,
+                                           ctx->stream));
+    return PQH_OK;
+}
+
+int float_cmp_ref(const void* a, const void* b) {   // fast_nn_blocks_info.c:41-50
+    const float v = *(const float*)a - *(const float*)b;
+    if (fabs(v) < 1e-9) return 0;
+    return v < 0 ? -1 : 1;
+}
+
+struct HostEdge {   // mst_edge_t (mst.h)
+    uint32_t source, target;
+    float dist;
+};
+
+int edge_dist_cmp_ref(const void* a, const void* b) {   // mst.c:15-26
+    const float diff = ((const HostEdge*)a)->dist - ((const HostEdge*)b)->dist;
+    if (fabs(diff) < 1e-9) return 0;
+    return diff < 0 ? -1 : 1;
+}
+
+uint32_t dsu_find(std::vector<uint32_t>& parent, uint32_t v) {
+    uint32_t r = v;
+    while (parent[r] != r) r = parent[r];
+    while (parent[v] != r) {
+        const uint32_t nx = parent[v];
+        parent[v] = r;
+        v = nx;
+    }
+    return r;
+}
+
+template <int DMAX, int KMAX>
+void launch_topk(pqh_ctx* ctx, long long tiles, const float* x, long long ld, int d, int num_nn,
+                 const uint32_t* rows, const long long* boff, const long long* tb,
+                 const long long* tq, int stride, float* od, uint32_t* orow) {
+    hipLaunchKernelGGL((knn_block_topk<DMAX, KMAX>), dim3((unsigned)tiles), dim3(kQ), 0,
+                       ctx->stream, x, ld, d, num_nn, rows, boff, tb, tq, stride, od, orow);
+}
+
+template <int DMAX>
+void launch_topk_k(pqh_ctx* ctx, int kmax, long long tiles, const float* x, long long ld, int d,
+                   int num_nn, const uint32_t* rows, const long long* boff, const long long* tb,
+                   const long long* tq, int stride, float* od, uint32_t* orow) {
+    if (kmax <= 8) launch_topk<DMAX, 8>(ctx, tiles, x, ld, d, num_nn, rows, boff, tb, tq, stride, od, orow);
+    else if (kmax <= 16) launch_topk<DMAX, 16>(ctx, tiles, x, ld, d, num_nn, rows, boff, tb, tq, stride, od, orow);
+    else if (kmax <= 32) launch_topk<DMAX, 32>(ctx, tiles, x, ld, d, num_nn, rows, boff, tb, tq, stride, od, orow);
+    else launch_topk<DMAX, 64>(ctx, tiles, x, ld, d, num_nn, rows, boff, tb, tq, stride, od, orow);
+}
+
+}  // namespace
+
+extern "C" {
+
+int pqh_knn_blocks_info(pqh_ctx_t* ctx, const float* d_x, long long n, long long ld_x, int d,
+                        int num_split, int blocks_per_dim, double overlap, float* h_starts,
+                        float* h_ends) {
+    if (!ctx || !d_x || n <= 0 || d <= 0 || ld_x < d || num_split <= 0 || num_split > d ||
+        num_split > 8 || blocks_per_dim <= 0 || blocks_per_dim > 32 || !h_starts || !h_ends ||
+        n >= (1ll << 32))
+        return PQH_ERR_ARG;
+    int rc = pqh_use_device(ctx);
+    if (rc) return rc;
+    DevBuf buf;
+    uint32_t* k0 = buf.get<uint32_t>(n);
+    uint32_t* k1 = buf.get<uint32_t>(n);
+    uint32_t* i0 = buf.get<uint32_t>(n);
+    uint32_t* i1 = buf.get<uint32_t>(n);
+    float* dse = buf.get<float>(2 * blocks_per_dim);
+    int* flag = buf.get<int>(1);
+    if (!k0 || !k1 || !i0 || !i1 || !dse || !flag)
+        return pqh_set_error(ctx, PQH_ERR_NOMEM, "knn_blocks_info: %lld rows", n);
+    const unsigned g = (unsigned)((n + 255) / 256);
+    const long long ov = (long long)(n * overlap / 2);
+    for (int i = 0; i < num_split; ++i) {
+        const int coord = num_split - 1 - i;
+        hipLaunchKernelGGL(knn_column, dim3(g), dim3(256), 0, ctx->stream, d_x, n, ld_x, coord, k0);
+        PQH_LAUNCH_CHECK(ctx);
+        if ((rc = radix_sort_u32(ctx, buf, k0, k1, i0, i1, n))) return rc;   // (values unused)
+        PQH_HIP(ctx, hipMemsetAsync(flag, 0, sizeof(int), ctx->stream));
+        hipLaunchKernelGGL(near_equal_check, dim3(g), dim3(256), 0, ctx->stream, k1, n, flag);
+        PQH_LAUNCH_CHECK(ctx);
+        hipLaunchKernelGGL(knn_bounds, dim3(1), dim3(64), 0, ctx->stream, k1, n, blocks_per_dim,
+                           ov, dse, dse + blocks_per_dim);
+        PQH_LAUNCH_CHECK(ctx);
+        int hflag = 0;
+        PQH_HIP(ctx, hipMemcpyAsync(&hflag, flag, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+        PQH_HIP(ctx, hipMemcpyAsync(h_starts + i * blocks_per_dim, dse, sizeof(float) * blocks_per_dim,
+                                    hipMemcpyDeviceToHost, ctx->stream));
+        PQH_HIP(ctx, hipMemcpyAsync(h_ends + i * blocks_per_dim, dse + blocks_per_dim,
+                                    sizeof(float) * blocks_per_dim, hipMemcpyDeviceToHost, ctx->stream));
+        PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        if (hflag) {   // near-equal distinct values: the reference's own qsort decides
+            std::vector<float> col((size_t)n);
+            PQH_HIP(ctx, hipMemcpy2DAsync(col.data(), sizeof(float), d_x + coord, ld_x * sizeof(float),
+                                          sizeof(float), (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
+            PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            qsort(col.data(), (size_t)n, sizeof(float), float_cmp_ref);
+            for (int b = 0; b < blocks_per_dim; ++b) {
+                long long s = n * b / blocks_per_dim - ov;
+                s = s < 0 ? 0 : (s > n ? n : s);
+                long long e = n * (b + 1) / blocks_per_dim + ov;
+                e = e < 0 ? 0 : (e > n ? n : e);
+                h_starts[i * blocks_per_dim + b] = col[(size_t)(s < n ? s : n - 1)];
+                h_ends[i * blocks_per_dim + b] = col[(size_t)(e < n - 1 ? e : n - 1)];
+            }
+            h_starts[i * blocks_per_dim] = (float)((double)col[0] - 1.0);
+            h_ends[i * blocks_per_dim + blocks_per_dim - 1] = (float)((double)col[(size_t)n - 1] + 1.0);
+        }
+    }
+    return PQH_OK;
+}
+
+int pqh_knn_fast(pqh_ctx_t* ctx, const float* d_x, long long n, long long ld_x, int d,
+                 int num_nn, int num_split, int blocks_per_dim, const float* h_starts,
+                 const float* h_ends, uint32_t* d_indices, float* d_dists,
+                 long long* h_block_sizes) {
+    if (!ctx || !d_x || n <= 0 || d <= 0 || ld_x < d || num_nn <= 0 || num_nn > 63 ||
+        num_split <= 0 || num_split > d || num_split > 8 || blocks_per_dim <= 0 ||
+        blocks_per_dim > 32 || !h_starts || !h_ends || !d_indices || !d_dists || n >= (1ll << 32))
+        return PQH_ERR_ARG;
+    if (d > 128) return pqh_set_error(ctx, PQH_ERR_UNSUPPORTED, "knn_fast: d = %d > 128", d);
+    long long nblocks = 1;
+    for (int i = 0; i < num_split; ++i) {
+        nblocks *= blocks_per_dim;
+        if (nblocks >= (1ll << 31)) return PQH_ERR_ARG;
+    }
+    int rc = pqh_use_device(ctx);
+    if (rc) return rc;
+    DevBuf buf;
+    const size_t gb = sizeof(float) * num_split * blocks_per_dim;
+    float* dg = buf.get<float>(2 * (size_t)num_split * blocks_per_dim);
+    uint32_t* masks = buf.get<uint32_t>((size_t)n * num_split);
+    uint32_t* cnt = buf.get<uint32_t>(n + 1);
+    unsigned long long* off = buf.get<unsigned long long>(n + 1);
+    if (!dg || !masks || !cnt || !off) return pqh_set_error(ctx, PQH_ERR_NOMEM, "knn_fast: %lld rows", n);
+    PQH_HIP(ctx, hipMemcpyAsync(dg, h_starts, gb, hipMemcpyHostToDevice, ctx->stream));
+    PQH_HIP(ctx, hipMemcpyAsync(dg + num_split * blocks_per_dim, h_ends, gb, hipMemcpyHostToDevice,
+                                ctx->stream));
+    const Geo geo{num_split, blocks_per_dim, dg, dg + num_split * blocks_per_dim};
+    const unsigned g = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(knn_masks, dim3(g), dim3(256), 0, ctx->stream, d_x, n, ld_x, geo, masks, cnt);
+    PQH_LAUNCH_CHECK(ctx);
+    PQH_HIP(ctx, hipMemsetAsync(cnt + n, 0, sizeof(uint32_t), ctx->stream));
+    {   // off[v] = pairs of the rows before v (off[n] = all)
+        size_t temp = 0;
+        PQH_HIP(ctx, rocprim::exclusive_scan(nullptr, temp, cnt, off, 0ull, (size_t)n + 1,
+                                             rocprim::plus<unsigned long long>(), ctx->stream));
+        void* t = buf.get<char>(temp);
+        if (!t) return pqh_set_error(ctx, PQH_ERR_NOMEM, "knn_fast: scan temp");
+        PQH_HIP(ctx, rocprim::exclusive_scan(t, temp, cnt, off, 0ull, (size_t)n + 1,
+                                             rocprim::plus<unsigned long long>(), ctx->stream));
+    }
+    unsigned long long npairs = 0;
+    PQH_HIP(ctx, hipMemcpyAsync(&npairs, off + n, 8, hipMemcpyDeviceToHost, ctx->stream));
+    PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (npairs >= (1ull << 32))
+        return pqh_set_error(ctx, PQH_ERR_UNSUPPORTED, "knn_fast: %llu (block, row) pairs", npairs);
+    const long long np = (long long)npairs;
+    uint32_t* keys = buf.get<uint32_t>(np);
+    uint32_t* keys_s = buf.get<uint32_t>(np);
+    uint32_t* vals = buf.get<uint32_t>(np);
+    uint32_t* vals_s = buf.get<uint32_t>(np);
+    uint32_t* erow = buf.get<uint32_t>(np);
+    uint32_t* rows = buf.get<uint32_t>(np);
+    uint32_t* inv = buf.get<uint32_t>(np);
+    long long* boff = buf.get<long long>(nblocks + 1);
+    const int stride = num_nn + 1;
+    float* ldist = buf.get<float>((size_t)np * stride);
+    uint32_t* lrow = buf.get<uint32_t>((size_t)np * stride);
+    if (!keys || !keys_s || !vals || !vals_s || !erow || !rows || !inv || !boff || !ldist || !lrow)
+        return pqh_set_error(ctx, PQH_ERR_NOMEM, "knn_fast: %lld pairs", np);
+    const unsigned gp = (unsigned)((np + 255) / 256);
+    if (np > 0) {
+        hipLaunchKernelGGL(knn_emit, dim3(g), dim3(256), 0, ctx->stream, masks, n, geo, off, keys,
+                           vals, erow);
+        PQH_LAUNCH_CHECK(ctx);
+        if ((rc = radix_sort_u32(ctx, buf, keys, keys_s, vals, vals_s, np))) return rc;
+        hipLaunchKernelGGL(knn_place, dim3(gp), dim3(256), 0, ctx->stream, vals_s, np, erow, rows, inv);
+        PQH_LAUNCH_CHECK(ctx);
+    }
+    hipLaunchKernelGGL(knn_block_offsets, dim3((unsigned)((nblocks + 256) / 256)), dim3(256), 0,
+                       ctx->stream, keys_s, np, nblocks, boff);
+    PQH_LAUNCH_CHECK(ctx);
+    // the tile list: (block, first query) of every 64 queries of every block
+    std::vector<long long> hb((size_t)nblocks + 1);
+    PQH_HIP(ctx, hipMemcpyAsync(hb.data(), boff, sizeof(long long) * (nblocks + 1),
+                                hipMemcpyDeviceToHost, ctx->stream));
+    PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    std::vector<long long> tb, tq;
+    long long max_s = 0;
+    for (long long b = 0; b < nblocks; ++b) {
+        const long long S = hb[b + 1] - hb[b];
+        if (h_block_sizes) h_block_sizes[b] = S;
+        max_s = S > max_s ? S : max_s;
+        for (long long q0 = 0; q0 < S; q0 += kQ) {
+            tb.push_back(b);
+            tq.push_back(q0);
+        }
+    }
+    const long long tiles = (long long)tb.size();
+    if (tiles > 0) {
+        long long* dtb = buf.get<long long>(tiles);
+        long long* dtq = buf.get<long long>(tiles);
+        if (!dtb || !dtq) return pqh_set_error(ctx, PQH_ERR_NOMEM, "knn_fast: tiles");
+        PQH_HIP(ctx, hipMemcpyAsync(dtb, tb.data(), sizeof(long long) * tiles, hipMemcpyHostToDevice,
+                                    ctx->stream));
+        PQH_HIP(ctx, hipMemcpyAsync(dtq, tq.data(), sizeof(long long) * tiles, hipMemcpyHostToDevice,
+                                    ctx->stream));
+        const int kmax = (int)((num_nn < max_s - 1 ? num_nn : max_s - 1) + 1);
+        if (d <= 16)
+            launch_topk_k<16>(ctx, kmax, tiles, d_x, ld_x, d, num_nn, rows, boff, dtb, dtq, stride, ldist, lrow);
+        else if (d <= 32)
+            launch_topk_k<32>(ctx, kmax, tiles, d_x, ld_x, d, num_nn, rows, boff, dtb, dtq, stride, ldist, lrow);
+        else if (d <= 64)
+            launch_topk_k<64>(ctx, kmax, tiles, d_x, ld_x, d, num_nn, rows, boff, dtb, dtq, stride, ldist, lrow);
+        else
+            launch_topk_k<128>(ctx, kmax, tiles, d_x, ld_x, d, num_nn, rows, boff, dtb, dtq, stride, ldist, lrow);
+        PQH_LAUNCH_CHECK(ctx);
+    }
+    hipLaunchKernelGGL(knn_merge, dim3((unsigned)((n + kQ - 1) / kQ)), dim3(kQ),
+                       sizeof(NnItem) * kQ * num_nn, ctx->stream, n, num_nn, off, inv, keys_s, boff,
+                       stride, ldist, lrow, d_indices, d_dists);
+    PQH_LAUNCH_CHECK(ctx);
+    PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));   // the call's buffers are freed on return
+    return PQH_OK;
+}
+
+int pqh_mst_build(pqh_ctx_t* ctx, const uint32_t* d_indices, const float* d_dists, long long n,
+                  int num_nn, int take, const uint8_t* d_pq, int pq_m, float penalty,
+                  uint32_t* h_targets, int* h_counts, long long* num_edges) {
+    if (!ctx || !d_indices || !d_dists || n <= 0 || num_nn <= 0 || num_nn > 63 || take <= 0 ||
+        take > num_nn || !h_targets || !h_counts || !num_edges || n >= (1ll << 32) ||
+        (penalty > 0.0f && (!d_pq || pq_m <= 0)))
+        return PQH_ERR_ARG;
+    int rc = pqh_use_device(ctx);
+    if (rc) return rc;
+    const long long ne = n * take;
+    if (ne >= (1ll << 32)) return pqh_set_error(ctx, PQH_ERR_UNSUPPORTED, "mst: %lld edges", ne);
+    DevBuf buf;
+    uint32_t* keys = buf.get<uint32_t>(ne);
+    uint32_t* keys_s = buf.get<uint32_t>(ne);
+    uint32_t* vals = buf.get<uint32_t>(ne);
+    uint32_t* vals_s = buf.get<uint32_t>(ne);
+    uint32_t* src = buf.get<uint32_t>(ne);
+    uint32_t* dst = buf.get<uint32_t>(ne);
+    float* edist = buf.get<float>(ne);
+    uint2* pairs = buf.get<uint2>(ne);
+    int* flag = buf.get<int>(2);
+    if (!keys || !keys_s || !vals || !vals_s || !src || !dst || !edist || !pairs || !flag)
+        return pqh_set_error(ctx, PQH_ERR_NOMEM, "mst: %lld edges", ne);
+    PQH_HIP(ctx, hipMemsetAsync(flag, 0, 2 * sizeof(int), ctx->stream));
+    hipLaunchKernelGGL(mst_row_edges, dim3((unsigned)((n + kQ - 1) / kQ)), dim3(kQ),
+                       sizeof(NnItem) * kQ * num_nn, ctx->stream, d_indices, d_dists, n, num_nn,
+                       take, d_pq, pq_m, penalty, keys, vals, src, dst, edist, flag);
+    PQH_LAUNCH_CHECK(ctx);
+    if ((rc = radix_sort_u32(ctx, buf, keys, keys_s, vals, vals_s, ne))) return rc;
+    const unsigned ge = (unsigned)((ne + 255) / 256);
+    hipLaunchKernelGGL(near_equal_check, dim3(ge), dim3(256), 0, ctx->stream, keys_s, ne, flag + 1);
+    PQH_LAUNCH_CHECK(ctx);
+    hipLaunchKernelGGL(gather_pairs, dim3(ge), dim3(256), 0, ctx->stream, vals_s, ne, src, dst, pairs);
+    PQH_LAUNCH_CHECK(ctx);
+    int hflag[2] = {0, 0};
+    std::vector<uint2> ed((size_t)ne);
+    PQH_HIP(ctx, hipMemcpyAsync(hflag, flag, sizeof(hflag), hipMemcpyDeviceToHost, ctx->stream));
+    PQH_HIP(ctx, hipMemcpyAsync(ed.data(), pairs, sizeof(uint2) * ne, hipMemcpyDeviceToHost, ctx->stream));
+    PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (hflag[0] & 1) return pqh_set_error(ctx, PQH_ERR_ARG, "mst: a neighbour id outside the rows");
+    if ((hflag[0] & 2) || hflag[1]) {
+        // distinct distances inside the comparator's 1e-9 band: the reference's qsorts decide
+        std::vector<uint32_t> hi((size_t)n * num_nn);
+        std::vector<float> hd((size_t)n * num_nn);
+        std::vector<uint8_t> hp(penalty > 0.0f ? (size_t)n * pq_m : 0);
+        PQH_HIP(ctx, hipMemcpyAsync(hi.data(), d_indices, hi.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
+        PQH_HIP(ctx, hipMemcpyAsync(hd.data(), d_dists, hd.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
+        if (!hp.empty())
+            PQH_HIP(ctx, hipMemcpyAsync(hp.data(), d_pq, hp.size(), hipMemcpyDeviceToHost, ctx->stream));
+        PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        std::vector<HostEdge> all((size_t)ne), row((size_t)num_nn);
+        for (long long v = 0; v < n; ++v) {
+            for (int j = 0; j < num_nn; ++j) {
+                HostEdge& e = row[j];
+                e.source = (uint32_t)v;
+                e.target = hi[(size_t)v * num_nn + j];
+                e.dist = hd[(size_t)v * num_nn + j];
+                if (penalty > 0.0f) {
+                    int ham = 0;
+                    for (int i = 0; i < pq_m; ++i)
+                        ham += hp[(size_t)v * pq_m + i] != hp[(size_t)e.target * pq_m + i];
+                    if (std::isinf(penalty)) e.dist = (float)ham;
+                    else e.dist += ham * penalty;
+                }
+            }
+            if (penalty > 0.0f) qsort(row.data(), (size_t)num_nn, sizeof(HostEdge), edge_dist_cmp_ref);
+            for (int j = 0; j < take; ++j) all[(size_t)v * take + j] = row[j];
+        }
+        qsort(all.data(), (size_t)ne, sizeof(HostEdge), edge_dist_cmp_ref);
+        for (long long e = 0; e < ne; ++e) ed[e] = make_uint2(all[e].source, all[e].target);
+    }
+    // Kruskal (mst.c:185-201): kept edges in sorted order; then both directions, stably by
+    // source (:204-214) -- a counting sort
+    std::vector<uint32_t> parent((size_t)n);
+    for (long long v = 0; v < n; ++v) {
+        parent[v] = (uint32_t)v;
+        h_counts[v] = 0;
+    }
+    std::vector<uint2> kept;
+    kept.reserve((size_t)(n > 1 ? n - 1 : 0));
+    for (long long e = 0; (long long)kept.size() + 1 < n && e < ne; ++e) {
+        const uint32_t a = dsu_find(parent, ed[e].x), b = dsu_find(parent, ed[e].y);
+        if (a == b) continue;
+        parent[b] = a;
+        ++h_counts[ed[e].x];
+        kept.push_back(ed[e]);
+    }
+    for (const uint2& e : kept) ++h_counts[e.y];
+    std::vector<long long> first((size_t)n + 1, 0);
+    for (long long v = 0; v < n; ++v) first[v + 1] = first[v] + h_counts[v];
+    for (const uint2& e : kept) h_targets[first[e.x]++] = e.y;   // forward copies first ...
+    for (const uint2& e : kept) h_targets[first[e.y]++] = e.x;   // ... then the reversed ones
+    *num_edges = 2 * (long long)kept.size();
+    return PQH_OK;
+}
+
+}  // extern "C"
