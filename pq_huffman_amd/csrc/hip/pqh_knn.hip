@@ -196,25 +196,33 @@ knn_block_offsets(const uint32_t* __restrict__ keys, long long np, long long nbl
 // One wave = up to 64 queries of one block (tile list built on the host).  Every lane keeps
 // its top-KMAX (distance, block position) list sorted ascending -- equal distances in
 // position order, because candidates arrive in position order and a new entry goes after
-// equal ones -- updated by a compare-exchange network with static register indices.  The
-// first kk = min(num_nn, S - 1) + 1 entries are the block kNN (kk <= KMAX).
+// equal ones -- in registers, updated by a compare-exchange network with static indices.
+// The first kk = min(num_nn, S - 1) + 1 entries are the block kNN (kk <= KMAX).
+// Per 64-candidate tile: the rows are staged in LDS zero-padded to DMAX dimensions (a zero
+// term adds +0 to a non-negative sum: exact), every lane computes its 64 distances from
+// broadcast b128 reads, and appends the ones below its current kk-th distance to an LDS
+// buffer; the network then runs once per buffered entry of the busiest lane -- after the
+// first tiles a handful per tile instead of one per candidate.
 template <int DMAX, int KMAX>
 __global__ void __launch_bounds__(kQ)
 knn_block_topk(const float* __restrict__ x, long long ld, int d, int num_nn,
                const uint32_t* __restrict__ rows, const long long* __restrict__ boff,
                const long long* __restrict__ tile_block, const long long* __restrict__ tile_q0,
                int stride, float* __restrict__ out_dist, uint32_t* __restrict__ out_row) {
-    __shared__ float cand[kQ * DMAX];
+    static_assert(DMAX % 4 == 0, "b128 reads");
+    __shared__ __attribute__((aligned(16))) float cand[kQ * DMAX];
+    __shared__ float2 buf[kQ * kQ];   // per lane: (distance, position bits) of this tile
     const int lane = threadIdx.x;
     const long long b = tile_block[blockIdx.x];
     const long long base = boff[b];
-    const long long S = boff[b + 1] - base;
-    const long long q = tile_q0[blockIdx.x] + lane;
+    const int S = (int)(boff[b + 1] - base);
+    const int q = (int)tile_q0[blockIdx.x] + lane;
     const bool valid = q < S;
-    const int kk = (int)((num_nn < S - 1 ? num_nn : S - 1) + 1);
+    const int kk = (num_nn < S - 1 ? num_nn : S - 1) + 1;
+    const uint32_t* brows = rows + base;
     float qv[DMAX];
     {
-        const float* xq = x + (long long)rows[base + (valid ? q : 0)] * ld;
+        const float* xq = x + (long long)brows[valid ? q : 0] * ld;
 #pragma unroll
         for (int j = 0; j < DMAX; ++j) qv[j] = j < d ? xq[j] : 0.0f;
     }
@@ -225,42 +233,60 @@ knn_block_topk(const float* __restrict__ x, long long ld, int d, int num_nn,
         ld_[j] = INFINITY;
         lp_[j] = 0xFFFFFFFFu;
     }
-    float thr = INFINITY;
-    for (long long c0 = 0; c0 < S; c0 += kQ) {
-        const int nc = (int)(S - c0 < kQ ? S - c0 : kQ);
+    float thr = INFINITY;   // the current kk-th distance
+    for (int c0 = 0; c0 < S; c0 += kQ) {
+        const int nc = S - c0 < kQ ? S - c0 : kQ;
         __syncthreads();
-        for (int f = lane; f < nc * d; f += kQ) {   // stage the tile (rows in block order)
-            const int r = f / d, j = f - r * d;
-            cand[r * DMAX + j] = x[(long long)rows[base + c0 + r] * ld + j];
+        for (int f = lane; f < nc * DMAX; f += kQ) {   // stage the tile (rows in block order)
+            const int r = f / DMAX, j = f - r * DMAX;
+            cand[f] = j < d ? x[(long long)brows[c0 + r] * ld + j] : 0.0f;
         }
         __syncthreads();
+        int cnt = 0;
         for (int c = 0; c < nc; ++c) {
-            const float* cr = cand + c * DMAX;
+            const float4* cr = reinterpret_cast<const float4*>(cand + c * DMAX);
             float acc = 0.0f;   // get_real_dist: (x - y)^2 summed in dimension order
 #pragma unroll
-            for (int j = 0; j < DMAX; ++j) {
-                if (j < d) {
-                    const float t = __fsub_rn(qv[j], cr[j]);
-                    acc = __fadd_rn(acc, __fmul_rn(t, t));
-                }
+            for (int j4 = 0; j4 < DMAX / 4; ++j4) {
+                const float4 y = cr[j4];
+                float t = __fsub_rn(qv[4 * j4], y.x);
+                acc = __fadd_rn(acc, __fmul_rn(t, t));
+                t = __fsub_rn(qv[4 * j4 + 1], y.y);
+                acc = __fadd_rn(acc, __fmul_rn(t, t));
+                t = __fsub_rn(qv[4 * j4 + 2], y.z);
+                acc = __fadd_rn(acc, __fmul_rn(t, t));
+                t = __fsub_rn(qv[4 * j4 + 3], y.w);
+                acc = __fadd_rn(acc, __fmul_rn(t, t));
+                // (a group of 8 reads at a time: hoisting all of them costs DMAX registers)
+                if ((j4 & 7) == 7) __builtin_amdgcn_sched_barrier(0);
             }
-            const bool ins = valid && acc < thr;
-            if (__any(ins)) {
-                const uint32_t pos = (uint32_t)(c0 + c);
-#pragma unroll
-                for (int j = KMAX - 1; j >= 1; --j) {
-                    const bool shift = ld_[j - 1] > acc, put = ld_[j] > acc;
-                    const float nd = shift ? ld_[j - 1] : (put ? acc : ld_[j]);
-                    const uint32_t np = shift ? lp_[j - 1] : (put ? pos : lp_[j]);
-                    ld_[j] = ins ? nd : ld_[j];
-                    lp_[j] = ins ? np : lp_[j];
-                }
-                const bool put0 = ld_[0] > acc;
-                ld_[0] = ins && put0 ? acc : ld_[0];
-                lp_[0] = ins && put0 ? pos : lp_[0];
-                thr = ld_[KMAX - 1];
+            if (valid && acc < thr) {
+                buf[lane * kQ + cnt] = make_float2(acc, __uint_as_float((uint32_t)(c0 + c)));
+                ++cnt;
             }
         }
+        for (int i = 0; __any(i < cnt); ++i) {
+            {   // (a lane with no entry left carries +inf: nothing moves)
+                const float2 e = i < cnt ? buf[lane * kQ + i] : make_float2(INFINITY, 0.0f);
+                float cd = e.x;   // the entry goes before the first strictly larger one, and
+                uint32_t cp = __float_as_uint(e.y);   // every later slot shifts by one: the
+                bool mv = false;                      // displaced entry is carried (in place)
+#pragma unroll
+                for (int j = 0; j < KMAX; ++j) {
+                    const bool sw = mv || ld_[j] > cd;   // (selects: fminf/fmaxf canonicalise)
+                    mv = sw;
+                    const float dj = ld_[j];
+                    const uint32_t pj = lp_[j];
+                    ld_[j] = sw ? cd : dj;
+                    lp_[j] = sw ? cp : pj;
+                    cd = sw ? dj : cd;
+                    cp = sw ? pj : cp;
+                }
+            }
+        }
+        // the kk-th entry (kk is uniform: a static select chain)
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) thr = j == kk - 1 ? ld_[j] : thr;
     }
     if (!valid) return;
     const long long pair = base + q;
@@ -268,7 +294,7 @@ knn_block_topk(const float* __restrict__ x, long long ld, int d, int num_nn,
     for (int j = 0; j < KMAX; ++j) {
         if (j < kk) {
             out_dist[pair * stride + j] = ld_[j];
-            out_row[pair * stride + j] = rows[base + lp_[j]];
+            out_row[pair * stride + j] = brows[lp_[j]];
         }
     }
 }
@@ -449,6 +475,7 @@ void launch_topk_k(pqh_ctx* ctx, int kmax, long long tiles, const float* x, long
     if (kmax <= 8) launch_topk<DMAX, 8>(ctx, tiles, x, ld, d, num_nn, rows, boff, tb, tq, stride, od, orow);
     else if (kmax <= 16) launch_topk<DMAX, 16>(ctx, tiles, x, ld, d, num_nn, rows, boff, tb, tq, stride, od, orow);
     else if (kmax <= 32) launch_topk<DMAX, 32>(ctx, tiles, x, ld, d, num_nn, rows, boff, tb, tq, stride, od, orow);
+    else if (kmax <= 52) launch_topk<DMAX, 52>(ctx, tiles, x, ld, d, num_nn, rows, boff, tb, tq, stride, od, orow);
     else launch_topk<DMAX, 64>(ctx, tiles, x, ld, d, num_nn, rows, boff, tb, tq, stride, od, orow);
 }
 
@@ -612,12 +639,16 @@ int pqh_knn_fast(pqh_ctx_t* ctx, const float* d_x, long long n, long long ld_x, 
         PQH_HIP(ctx, hipMemcpyAsync(dtq, tq.data(), sizeof(long long) * tiles, hipMemcpyHostToDevice,
                                     ctx->stream));
         const int kmax = (int)((num_nn < max_s - 1 ? num_nn : max_s - 1) + 1);
-        if (d <= 16)
+        if (d <= 8)
+            launch_topk_k<8>(ctx, kmax, tiles, d_x, ld_x, d, num_nn, rows, boff, dtb, dtq, stride, ldist, lrow);
+        else if (d <= 16)
             launch_topk_k<16>(ctx, kmax, tiles, d_x, ld_x, d, num_nn, rows, boff, dtb, dtq, stride, ldist, lrow);
         else if (d <= 32)
             launch_topk_k<32>(ctx, kmax, tiles, d_x, ld_x, d, num_nn, rows, boff, dtb, dtq, stride, ldist, lrow);
         else if (d <= 64)
             launch_topk_k<64>(ctx, kmax, tiles, d_x, ld_x, d, num_nn, rows, boff, dtb, dtq, stride, ldist, lrow);
+        else if (d <= 96)
+            launch_topk_k<96>(ctx, kmax, tiles, d_x, ld_x, d, num_nn, rows, boff, dtb, dtq, stride, ldist, lrow);
         else
             launch_topk_k<128>(ctx, kmax, tiles, d_x, ld_x, d, num_nn, rows, boff, dtb, dtq, stride, ldist, lrow);
         PQH_LAUNCH_CHECK(ctx);
