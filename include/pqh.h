@@ -296,6 +296,27 @@ int pqh_mst_build(pqh_ctx_t* ctx, const uint32_t* d_indices, const float* d_dist
                   int num_nn, int take, const uint8_t* d_pq, int pq_m, float penalty,
                   uint32_t* h_targets, int* h_counts, long long* num_edges);
 
+/* compute_nn_fast as a whole (the CLI, csrc/tools/compute_nn_fast.c): .fvecs rows in,
+ * <out_template>nn_indices.ivecsl / nn_dist.fvecsl out.  options may be NULL (the reference
+ * CLI's defaults, compute_nn_fast.c:164-175: 5 splits, 3 blocks, overlap 0.3).  A
+ * blocks_info_cache that loads supplies the geometry; otherwise it is written
+ * (fast_nn_blocks_info.c:124-172 layout).  with_blocks_stat writes blocks_stat.txt. */
+typedef struct {
+    int num_split;               /* --num-dims */
+    int blocks_per_dim;          /* --num-blocks-per-dim */
+    double overlap;              /* --block-overlap-fraction */
+    const char* blocks_info_cache;
+    int with_blocks_stat;
+} pqh_knn_options_t;
+int pqh_knn_fast_files(const char* input_fvecs, const char* out_template, int num_nn,
+                       const pqh_knn_options_t* options);
+/* mst_builder as a whole (mst_builder.c:98-131): <nn_template>nn_indices.ivecsl +
+ * nn_dist.fvecsl (+ <pq_template>pq_indices.bvecsl, may be NULL) in; <out_template>mst.tree,
+ * and with PQ codes stats.json / stats_num_children.json (appended) plus the indices stats
+ * line on stdout. */
+int pqh_mst_files(const char* nn_template, const char* out_template, int take,
+                  const char* pq_template, float penalty);
+
 /* ---- tree-ordered context coding (huffman_encoder.c --tree: :240-286, :321-375) ---- */
 /* DFS order of a stored forest (mst.tree: tree_load_file, mst.c:273-288 -- num_edges
  * u32 targets grouped by source, children_counts[v] of them per vertex) exactly as

@@ -40,7 +40,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
-constexpr int kTiles = 8;        // K = 256 centroids = 8 tiles of 32 rows (K = 4096: 128 tiles)
 #ifndef PQH_ASSIGN_WPG
 #define PQH_ASSIGN_WPG 4
 #endif
