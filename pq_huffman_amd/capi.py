@@ -155,6 +155,8 @@ SIGNATURES = [
     ("pqh_knn_blocks_info", I, [P, P, LL, LL, I, I, I, D, P, P]),
     ("pqh_knn_fast", I, [P, P, LL, LL, I, I, I, I, P, P, P, P, P]),
     ("pqh_mst_build", I, [P, P, P, LL, I, I, P, I, ctypes.c_float, P, P, P]),
+    ("pqh_knn_fast_files", I, [S, S, I, P]),
+    ("pqh_mst_files", I, [S, S, I, S, ctypes.c_float]),
 ]
 
 _lib = None
