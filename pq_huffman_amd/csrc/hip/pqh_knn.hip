@@ -299,6 +299,255 @@ knn_block_topk(const float* __restrict__ x, long long ld, int d, int num_nn,
     }
 }
 
+// ------------------------------------------------------------------ block kNN, MFMA screen
+// The default in-block kNN (PQH_KNN_IMPL=valu: knn_block_topk above).  Three steps:
+//  knn_split     every row once: x = hi + lo as two bf16 rows zero-padded to DP dimensions
+//                (DP = d rounded up to 16) and ||x||^2 in fp32.
+//  knn_screen    one wave per 32 queries of a block (v_mfma_f32_32x32x16_bf16, A = 32
+//                candidate rows, B = the 32 queries, K = 16 dimensions; hi*hi + lo*hi +
+//                hi*lo per 16 dimensions): the approximate distance
+//                d' = ||q||^2 + ||c||^2 - 2 q.c  of every (query, candidate) pair, twice.
+//                Pass 1 keeps, per half-wave lane, the kk smallest d' of its candidates; the
+//                smaller of the two halves' kk-th values, T, is >= the block's kk-th smallest
+//                d'.  Pass 2 lists every candidate with d' <= T + 2 E (E bounds |d' - D| for
+//                the oracle's fp32 distance D of every candidate of this query): that list
+//                holds every candidate whose D can be among the kk smallest (if D_c <= D_(kk)
+//                then d'_c <= D_(kk) + E <= T + 2 E, because kk candidates have D <= d' + E
+//                <= T + E).
+//  knn_select    one lane per query: the listed candidates' exact direct-form distances and
+//                the kk smallest by (distance, block position); a list that overflowed its
+//                CH slots makes the lane scan the whole block instead.
+// E = (3 2^-18 + (3 DP + 3 d + 8) 2^-24) (||q||^2 + Cmax) * 1.25, Cmax = the block's largest
+// ||c||^2: the bf16 split drops ql.cl + (qh + ql).rc + rq.c (each <= 2^-18 |q||c| summed,
+// Cauchy-Schwarz), the fp32 accumulation of 3 DP products, the fp32 norms (d + 1 roundings)
+// and the final fma, and the oracle's own direct-form rounding ((d + 2) 2^-24 D, D <=
+// 2 (||q||^2 + ||c||^2)); every term is <= its coefficient times ||q||^2 + Cmax.
+typedef __bf16 kbf16x8 __attribute__((ext_vector_type(8)));
+typedef float kf32x16 __attribute__((ext_vector_type(16)));
+constexpr int kScreenQ = 32;   // queries per screening wave (the MFMA's columns)
+
+__device__ __forceinline__ float raw_min(float a, float b) {   // (no canonicalising maxes)
+    float r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float raw_max(float a, float b) {
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+template <int DP>
+__global__ void __launch_bounds__(256)
+knn_split(const float* __restrict__ x, long long n, long long ld, int d,
+          kbf16x8* __restrict__ xhi, kbf16x8* __restrict__ xlo, float* __restrict__ norm,
+          float* __restrict__ xpad) {
+    const long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= n) return;
+    const float* xr = x + v * ld;
+    float nn = 0.0f;
+#pragma unroll
+    for (int g = 0; g < DP / 8; ++g) {
+        kbf16x8 hi, lo;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int c = 8 * g + j;
+            const float f = c < d ? xr[c] : 0.0f;
+            xpad[v * DP + c] = f;
+            nn = __fadd_rn(nn, __fmul_rn(f, f));
+            const __bf16 h = (__bf16)f;
+            hi[j] = h;
+            lo[j] = (__bf16)(f - (float)h);
+        }
+        xhi[v * (DP / 8) + g] = hi;
+        xlo[v * (DP / 8) + g] = lo;
+    }
+    norm[v] = nn;
+}
+
+// cmax[b] = the largest ||c||^2 of block b (non-negative floats order as their bits)
+__global__ void __launch_bounds__(256)
+knn_block_cmax(const uint32_t* __restrict__ keys_sorted, const uint32_t* __restrict__ rows,
+               long long np, const float* __restrict__ norm, uint32_t* __restrict__ cmax) {
+    const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= np) return;
+    atomicMax(&cmax[keys_sorted[p]], __float_as_uint(norm[rows[p]]));
+}
+
+template <int DP, int KMAX>
+__global__ void __launch_bounds__(64)
+knn_screen(const kbf16x8* __restrict__ xhi, const kbf16x8* __restrict__ xlo,
+           const float* __restrict__ norm, const uint32_t* __restrict__ rows,
+           const long long* __restrict__ boff, const uint32_t* __restrict__ cmax_bits,
+           const long long* __restrict__ tile_block, const long long* __restrict__ tile_q0,
+           int num_nn, int d, int ch, uint32_t* __restrict__ cand, uint32_t* __restrict__ ccount) {
+    constexpr int NSTEP = DP / 16;
+    constexpr int G = DP / 8;   // bf16x8 groups per row
+    __shared__ __attribute__((aligned(16))) float tnorm[kScreenQ];
+    const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
+    const long long b = tile_block[blockIdx.x];
+    const long long base = boff[b];
+    const int S = (int)(boff[b + 1] - base);
+    const int q = (int)tile_q0[blockIdx.x] + r;
+    const bool valid = q < S;
+    const int kk = (num_nn < S - 1 ? num_nn : S - 1) + 1;
+    const uint32_t* brows = rows + base;
+    const uint32_t qrow = brows[valid ? q : 0];
+    kbf16x8 bh[NSTEP], bl[NSTEP];
+#pragma unroll
+    for (int s = 0; s < NSTEP; ++s) {
+        bh[s] = xhi[(long long)qrow * G + 2 * s + h];
+        bl[s] = xlo[(long long)qrow * G + 2 * s + h];
+    }
+    const float nq = norm[qrow];
+    const float cmax = __uint_as_float(cmax_bits[b]);
+    auto tile = [&](int c0, kf32x16& acc, float* nc) {
+        const int cr = c0 + r < S ? c0 + r : S - 1;   // this lane's A row (clamped)
+        const uint32_t crow = brows[cr];
+        __syncthreads();
+        if (h == 0) tnorm[r] = norm[crow];
+        acc = kf32x16{};
+#pragma unroll
+        for (int s = 0; s < NSTEP; ++s) {
+            const kbf16x8 ah = xhi[(long long)crow * G + 2 * s + h];
+            const kbf16x8 al = xlo[(long long)crow * G + 2 * s + h];
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[s], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[s], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[s], acc, 0, 0, 0);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {   // rows 8g + 4h .. +4 of the tile
+            const float4 v4 = *reinterpret_cast<const float4*>(tnorm + 8 * g + 4 * h);
+            nc[4 * g] = v4.x; nc[4 * g + 1] = v4.y; nc[4 * g + 2] = v4.z; nc[4 * g + 3] = v4.w;
+        }
+    };
+    // pass 1: the KMAX smallest d' of this lane's candidates (values only)
+    float lst[KMAX];
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) lst[j] = INFINITY;
+    for (int c0 = 0; c0 < S; c0 += kScreenQ) {
+        kf32x16 acc;
+        float nc[16];
+        tile(c0, acc, nc);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int row = c0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+            const float dp = fmaf(-2.0f, acc[i], nq + nc[i]);
+            float cd = (valid && row < S && dp < lst[KMAX - 1]) ? dp : INFINITY;
+            if (__any(cd < INFINITY)) {
+#pragma unroll
+                for (int j = 0; j < KMAX; ++j) {
+                    const float lo = raw_min(lst[j], cd), hi = raw_max(lst[j], cd);
+                    lst[j] = lo;
+                    cd = hi;
+                }
+            }
+        }
+    }
+    float tloc = INFINITY;
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) tloc = j == kk - 1 ? lst[j] : tloc;
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(tloc), __float_as_uint(tloc),
+                                                     false, false);
+    const float T = raw_min(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+    const float E = (3.0f * 0x1p-18f + (float)(3 * DP + 3 * d + 8) * 0x1p-24f) * (nq + cmax) * 1.25f;
+    const float U = T + 2.0f * E;   // (T = +inf: every candidate is listed)
+    // pass 2: list the candidates with d' <= U (block positions, ascending per half)
+    uint32_t cnt = 0;
+    uint32_t* my = cand + ((long long)(base + q) * 2 + h) * ch;
+    for (int c0 = 0; c0 < S; c0 += kScreenQ) {
+        kf32x16 acc;
+        float nc[16];
+        tile(c0, acc, nc);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int row = c0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+            const float dp = fmaf(-2.0f, acc[i], nq + nc[i]);
+            if (valid && row < S && !(dp > U)) {
+                if (cnt < (uint32_t)ch) my[cnt] = (uint32_t)row;
+                ++cnt;
+            }
+        }
+    }
+    if (valid) ccount[(base + q) * 2 + h] = cnt;
+}
+
+// one lane per (block, query) pair: exact distances of the listed candidates (or of the whole
+// block after an overflow), the kk smallest by (distance, position), in the output lists
+template <int DP, int KMAX>
+__global__ void __launch_bounds__(64)
+knn_select(const float* __restrict__ xpad, int num_nn,
+           const uint32_t* __restrict__ rows, const uint32_t* __restrict__ keys_sorted,
+           const long long* __restrict__ boff, long long np, int ch,
+           const uint32_t* __restrict__ cand, const uint32_t* __restrict__ ccount, int stride,
+           float* __restrict__ out_dist, uint32_t* __restrict__ out_row) {
+    const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= np) return;
+    const long long b = keys_sorted[p];
+    const long long base = boff[b];
+    const int S = (int)(boff[b + 1] - base);
+    const int kk = (num_nn < S - 1 ? num_nn : S - 1) + 1;
+    const uint32_t* brows = rows + base;
+    float qv[DP];   // (rows zero-padded to DP: a zero term adds +0, exact)
+    {
+        const float4* xq = reinterpret_cast<const float4*>(xpad + (long long)rows[p] * DP);
+#pragma unroll
+        for (int j = 0; j < DP / 4; ++j) {
+            const float4 v4 = xq[j];
+            qv[4 * j] = v4.x; qv[4 * j + 1] = v4.y; qv[4 * j + 2] = v4.z; qv[4 * j + 3] = v4.w;
+        }
+    }
+    float ld_[KMAX];
+    uint32_t lp_[KMAX];
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) {
+        ld_[j] = INFINITY;
+        lp_[j] = 0xFFFFFFFFu;
+    }
+    const uint32_t n0 = ccount[p * 2], n1 = ccount[p * 2 + 1];
+    const bool full = n0 > (uint32_t)ch || n1 > (uint32_t)ch;
+    const int total = full ? S : (int)(n0 + n1);
+    for (int t = 0; t < total; ++t) {
+        const uint32_t pos = full ? (uint32_t)t
+                                  : cand[(p * 2 + (t < (int)n0 ? 0 : 1)) * ch + (t < (int)n0 ? t : t - n0)];
+        const float4* xc = reinterpret_cast<const float4*>(xpad + (long long)brows[pos] * DP);
+        float acc = 0.0f;   // get_real_dist, dimension order
+#pragma unroll
+        for (int j = 0; j < DP / 4; ++j) {
+            const float4 c4 = xc[j];
+            float tt = __fsub_rn(qv[4 * j], c4.x);
+            acc = __fadd_rn(acc, __fmul_rn(tt, tt));
+            tt = __fsub_rn(qv[4 * j + 1], c4.y);
+            acc = __fadd_rn(acc, __fmul_rn(tt, tt));
+            tt = __fsub_rn(qv[4 * j + 2], c4.z);
+            acc = __fadd_rn(acc, __fmul_rn(tt, tt));
+            tt = __fsub_rn(qv[4 * j + 3], c4.w);
+            acc = __fadd_rn(acc, __fmul_rn(tt, tt));
+            if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+        }
+        float cd = acc;   // carried up the list in (distance, position) order
+        uint32_t cp = pos;
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
+            const bool sw = ld_[j] > cd || (ld_[j] == cd && lp_[j] > cp);
+            const float dj = ld_[j];
+            const uint32_t pj = lp_[j];
+            ld_[j] = sw ? cd : dj;
+            lp_[j] = sw ? cp : pj;
+            cd = sw ? dj : cd;
+            cp = sw ? pj : cp;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) {
+        if (j < kk) {
+            out_dist[p * stride + j] = ld_[j];
+            out_row[p * stride + j] = brows[lp_[j]];
+        }
+    }
+}
+
 // ------------------------------------------------------------------ merge
 struct NnItem {
     uint32_t index;
@@ -618,27 +867,38 @@ int pqh_knn_fast(pqh_ctx_t* ctx, const float* d_x, long long n, long long ld_x, 
     PQH_HIP(ctx, hipMemcpyAsync(hb.data(), boff, sizeof(long long) * (nblocks + 1),
                                 hipMemcpyDeviceToHost, ctx->stream));
     PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    std::vector<long long> tb, tq;
     long long max_s = 0;
     for (long long b = 0; b < nblocks; ++b) {
         const long long S = hb[b + 1] - hb[b];
         if (h_block_sizes) h_block_sizes[b] = S;
         max_s = S > max_s ? S : max_s;
-        for (long long q0 = 0; q0 < S; q0 += kQ) {
-            tb.push_back(b);
-            tq.push_back(q0);
-        }
     }
-    const long long tiles = (long long)tb.size();
-    if (tiles > 0) {
-        long long* dtb = buf.get<long long>(tiles);
-        long long* dtq = buf.get<long long>(tiles);
-        if (!dtb || !dtq) return pqh_set_error(ctx, PQH_ERR_NOMEM, "knn_fast: tiles");
-        PQH_HIP(ctx, hipMemcpyAsync(dtb, tb.data(), sizeof(long long) * tiles, hipMemcpyHostToDevice,
-                                    ctx->stream));
-        PQH_HIP(ctx, hipMemcpyAsync(dtq, tq.data(), sizeof(long long) * tiles, hipMemcpyHostToDevice,
-                                    ctx->stream));
-        const int kmax = (int)((num_nn < max_s - 1 ? num_nn : max_s - 1) + 1);
+    const int kmax = (int)((num_nn < max_s - 1 ? num_nn : max_s - 1) + 1);
+    // the tile list: (block, first query) of every tq queries of every block
+    auto tiles_of = [&](int tqn, std::vector<long long>& tb, std::vector<long long>& tq) {
+        for (long long b = 0; b < nblocks; ++b)
+            for (long long q0 = 0; q0 < hb[b + 1] - hb[b]; q0 += tqn) {
+                tb.push_back(b);
+                tq.push_back(q0);
+            }
+    };
+    auto upload = [&](const std::vector<long long>& v, long long** dv) -> int {
+        *dv = buf.get<long long>(v.size());
+        if (!*dv) return pqh_set_error(ctx, PQH_ERR_NOMEM, "knn_fast: tiles");
+        PQH_HIP(ctx, hipMemcpyAsync(*dv, v.data(), sizeof(long long) * v.size(),
+                                    hipMemcpyHostToDevice, ctx->stream));
+        return PQH_OK;
+    };
+    static const bool valu_impl = [] {
+        const char* e = std::getenv("PQH_KNN_IMPL");
+        return e && std::strcmp(e, "valu") == 0;
+    }();
+    if (np > 0 && valu_impl) {   // exact VALU distances for every pair (knn_block_topk)
+        std::vector<long long> tb, tq;
+        tiles_of(kQ, tb, tq);
+        const long long tiles = (long long)tb.size();
+        long long *dtb = nullptr, *dtq = nullptr;
+        if ((rc = upload(tb, &dtb)) || (rc = upload(tq, &dtq))) return rc;
         if (d <= 8)
             launch_topk_k<8>(ctx, kmax, tiles, d_x, ld_x, d, num_nn, rows, boff, dtb, dtq, stride, ldist, lrow);
         else if (d <= 16)
@@ -651,6 +911,73 @@ int pqh_knn_fast(pqh_ctx_t* ctx, const float* d_x, long long n, long long ld_x, 
             launch_topk_k<96>(ctx, kmax, tiles, d_x, ld_x, d, num_nn, rows, boff, dtb, dtq, stride, ldist, lrow);
         else
             launch_topk_k<128>(ctx, kmax, tiles, d_x, ld_x, d, num_nn, rows, boff, dtb, dtq, stride, ldist, lrow);
+        PQH_LAUNCH_CHECK(ctx);
+    } else if (np > 0) {   // MFMA screen + exact selection
+        const int dp = d <= 16 ? 16 : d <= 32 ? 32 : d <= 64 ? 64 : 128;
+        const int ch = 2 * kmax + 16;   // listed candidates per half-wave lane before a full scan
+        kbf16x8* xhi = buf.get<kbf16x8>((size_t)n * (dp / 8));
+        kbf16x8* xlo = buf.get<kbf16x8>((size_t)n * (dp / 8));
+        float* nrm = buf.get<float>(n);
+        float* xpad = buf.get<float>((size_t)n * dp);
+        uint32_t* cmx = buf.get<uint32_t>(nblocks);
+        uint32_t* cand = buf.get<uint32_t>((size_t)np * 2 * ch);
+        uint32_t* ccnt = buf.get<uint32_t>((size_t)np * 2);
+        if (!xhi || !xlo || !nrm || !xpad || !cmx || !cand || !ccnt)
+            return pqh_set_error(ctx, PQH_ERR_NOMEM, "knn_fast: screen buffers (%lld pairs)", np);
+        std::vector<long long> tb, tq;
+        tiles_of(kScreenQ, tb, tq);
+        const long long tiles = (long long)tb.size();
+        long long *dtb = nullptr, *dtq = nullptr;
+        if ((rc = upload(tb, &dtb)) || (rc = upload(tq, &dtq))) return rc;
+        PQH_HIP(ctx, hipMemsetAsync(cmx, 0, sizeof(uint32_t) * nblocks, ctx->stream));
+        const unsigned gn = (unsigned)((n + 255) / 256);
+#define PQH_KNN_SPLIT(DP_)                                                                       \
+    hipLaunchKernelGGL(knn_split<DP_>, dim3(gn), dim3(256), 0, ctx->stream, d_x, n, ld_x, d, xhi,   \
+                       xlo, nrm, xpad)
+        if (dp == 16) PQH_KNN_SPLIT(16);
+        else if (dp == 32) PQH_KNN_SPLIT(32);
+        else if (dp == 64) PQH_KNN_SPLIT(64);
+        else PQH_KNN_SPLIT(128);
+#undef PQH_KNN_SPLIT
+        PQH_LAUNCH_CHECK(ctx);
+        hipLaunchKernelGGL(knn_block_cmax, dim3(gp), dim3(256), 0, ctx->stream, keys_s, rows, np, nrm, cmx);
+        PQH_LAUNCH_CHECK(ctx);
+#define PQH_KNN_SCREEN(DP_, K_)                                                                  \
+    hipLaunchKernelGGL((knn_screen<DP_, K_>), dim3((unsigned)tiles), dim3(64), 0, ctx->stream, xhi, \
+                       xlo, nrm, rows, boff, cmx, dtb, dtq, num_nn, d, ch, cand, ccnt)
+#define PQH_KNN_SCREEN_K(DP_)                                                                    \
+    do {                                                                                         \
+        if (kmax <= 8) PQH_KNN_SCREEN(DP_, 8);                                                    \
+        else if (kmax <= 16) PQH_KNN_SCREEN(DP_, 16);                                             \
+        else if (kmax <= 32) PQH_KNN_SCREEN(DP_, 32);                                             \
+        else if (kmax <= 52) PQH_KNN_SCREEN(DP_, 52);                                             \
+        else PQH_KNN_SCREEN(DP_, 64);                                                             \
+    } while (0)
+        if (dp == 16) PQH_KNN_SCREEN_K(16);
+        else if (dp == 32) PQH_KNN_SCREEN_K(32);
+        else if (dp == 64) PQH_KNN_SCREEN_K(64);
+        else PQH_KNN_SCREEN_K(128);
+#undef PQH_KNN_SCREEN_K
+#undef PQH_KNN_SCREEN
+        PQH_LAUNCH_CHECK(ctx);
+        const unsigned gs = (unsigned)((np + 63) / 64);
+#define PQH_KNN_SELECT(DM_, K_)                                                                  \
+    hipLaunchKernelGGL((knn_select<DM_, K_>), dim3(gs), dim3(64), 0, ctx->stream, xpad, num_nn,    \
+                       rows, keys_s, boff, np, ch, cand, ccnt, stride, ldist, lrow)
+#define PQH_KNN_SELECT_K(DM_)                                                                    \
+    do {                                                                                         \
+        if (kmax <= 8) PQH_KNN_SELECT(DM_, 8);                                                    \
+        else if (kmax <= 16) PQH_KNN_SELECT(DM_, 16);                                             \
+        else if (kmax <= 32) PQH_KNN_SELECT(DM_, 32);                                             \
+        else if (kmax <= 52) PQH_KNN_SELECT(DM_, 52);                                             \
+        else PQH_KNN_SELECT(DM_, 64);                                                             \
+    } while (0)
+        if (dp == 16) PQH_KNN_SELECT_K(16);
+        else if (dp == 32) PQH_KNN_SELECT_K(32);
+        else if (dp == 64) PQH_KNN_SELECT_K(64);
+        else PQH_KNN_SELECT_K(128);
+#undef PQH_KNN_SELECT_K
+#undef PQH_KNN_SELECT
         PQH_LAUNCH_CHECK(ctx);
     }
     hipLaunchKernelGGL(knn_merge, dim3((unsigned)((n + kQ - 1) / kQ)), dim3(kQ),
