@@ -21,9 +21,10 @@
 //                 (fast_nn_temp_file.c:11-63): one lane per row replays its blocks' lists
 //                 in block order into its max-heap (LDS), then heap-sorts it.
 //  mst            load_mst_edges_from_nn_files + minimum_spanning_tree (mst.c:80-236): PQ
-//                 penalty re-scoring and the per-row sort on the device, the global edge
-//                 sort by distance as a stable radix sort, Kruskal's union-find on the host
-//                 (a sequential scan), adjacency by a stable counting sort by source.
+//                 penalty re-scoring and the per-row sort, the global edge sort by distance as
+//                 a stable radix sort, Boruvka under that order (= Kruskal's forest, see
+//                 "minimum spanning forest"), the adjacency by a stable sort by source --
+//                 all on the device.
 //
 // Near-equal values: the reference sorts with comparators that call two floats equal when
 // they differ by less than 1e-9 (fast_nn_blocks_info.c:41-50, mst.c:15-26).  For any array
@@ -668,6 +669,105 @@ gather_pairs(const uint32_t* __restrict__ order, long long ne, const uint32_t* _
     out[e] = make_uint2(src[q], dst[q]);
 }
 
+// ------------------------------------------------------------------ minimum spanning forest
+// Boruvka over the edges in rank order (rank = position in the stable distance sort, i.e.
+// the order Kruskal scans them, mst.c:191-201): under that strict order the forest is
+// unique, so the edges Boruvka keeps are exactly Kruskal's, and listed by rank they are in
+// Kruskal's acceptance order.  Components are labelled by a root vertex; every round each
+// component takes its smallest-rank outgoing edge (atomicMin of the rank), hooks to the
+// other side's component, a mutual pair keeps its smaller root, and pointer jumping
+// relabels every vertex.
+__global__ void __launch_bounds__(256)
+bv_reset(long long n, uint32_t* __restrict__ best, uint32_t* __restrict__ hook) {
+    const long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= n) return;
+    best[v] = 0xFFFFFFFFu;
+    hook[v] = (uint32_t)v;
+}
+
+__global__ void __launch_bounds__(256)
+bv_iota(long long n, uint32_t* __restrict__ a) {
+    const long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v < n) a[v] = (uint32_t)v;
+}
+
+__global__ void __launch_bounds__(256)
+bv_edges(const uint2* __restrict__ pairs, long long ne, const uint32_t* __restrict__ comp,
+         uint32_t* __restrict__ best, int* __restrict__ any) {
+    const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= ne) return;
+    const uint2 pr = pairs[e];
+    const uint32_t ca = comp[pr.x], cb = comp[pr.y];
+    if (ca == cb) return;
+    atomicMin(&best[ca], (uint32_t)e);
+    atomicMin(&best[cb], (uint32_t)e);
+    *any = 1;   // (a plain store of the same value from every such lane)
+}
+
+__global__ void __launch_bounds__(256)
+bv_hook(const uint2* __restrict__ pairs, long long n, const uint32_t* __restrict__ comp,
+        const uint32_t* __restrict__ best, uint32_t* __restrict__ hook, uint32_t* __restrict__ kept) {
+    const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n || comp[c] != (uint32_t)c || best[c] == 0xFFFFFFFFu) return;
+    const uint32_t e = best[c];
+    const uint2 pr = pairs[e];
+    const uint32_t ca = comp[pr.x];
+    hook[c] = ca == (uint32_t)c ? comp[pr.y] : ca;
+    kept[e] = 1u;
+}
+
+// two components that chose the same edge hook to each other: the smaller root stays a root
+__global__ void __launch_bounds__(256)
+bv_mutual(long long n, uint32_t* __restrict__ hook) {
+    const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    const uint32_t h = hook[c];
+    if (h != (uint32_t)c && hook[h] == (uint32_t)c && (uint32_t)c < h) hook[c] = (uint32_t)c;
+}
+
+__global__ void __launch_bounds__(256)
+bv_jump(long long n, uint32_t* __restrict__ hook, int* __restrict__ changed) {
+    const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    const uint32_t h = hook[c], hh = hook[h];
+    if (hh != h) {
+        hook[c] = hh;
+        *changed = 1;
+    }
+}
+
+__global__ void __launch_bounds__(256)
+bv_relabel(long long n, const uint32_t* __restrict__ hook, uint32_t* __restrict__ comp) {
+    const long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v < n) comp[v] = hook[comp[v]];
+}
+
+// kept edge k (rank order): forward copy k (key = source), reversed copy K + k (key = target)
+__global__ void __launch_bounds__(256)
+bv_emit(const uint2* __restrict__ pairs, long long ne, const uint32_t* __restrict__ kept,
+        const uint32_t* __restrict__ kidx, uint32_t K, uint32_t* __restrict__ keys,
+        uint32_t* __restrict__ vals, uint32_t* __restrict__ other, int* __restrict__ counts) {
+    const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= ne || !kept[e]) return;
+    const uint32_t k = kidx[e];
+    const uint2 pr = pairs[e];
+    keys[k] = pr.x;
+    vals[k] = k;
+    other[k] = pr.y;
+    keys[K + k] = pr.y;
+    vals[K + k] = K + k;
+    other[K + k] = pr.x;
+    atomicAdd(&counts[pr.x], 1);
+    atomicAdd(&counts[pr.y], 1);
+}
+
+__global__ void __launch_bounds__(256)
+bv_targets(const uint32_t* __restrict__ vals_sorted, long long m, const uint32_t* __restrict__ other,
+           uint32_t* __restrict__ targets) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) targets[i] = other[vals_sorted[i]];
+}
+
 // ------------------------------------------------------------------ host helpers
 int radix_sort_u32(pqh_ctx* ctx, DevBuf& buf, uint32_t* k_in, uint32_t* k_out, uint32_t* v_in,
                    uint32_t* v_out, long long n) {
@@ -696,17 +796,6 @@ int edge_dist_cmp_ref(const void* a, const void* b) {   // mst.c:15-26
     const float diff = ((const HostEdge*)a)->dist - ((const HostEdge*)b)->dist;
     if (fabs(diff) < 1e-9) return 0;
     return diff < 0 ? -1 : 1;
-}
-
-uint32_t dsu_find(std::vector<uint32_t>& parent, uint32_t v) {
-    uint32_t r = v;
-    while (parent[r] != r) r = parent[r];
-    while (parent[v] != r) {
-        const uint32_t nx = parent[v];
-        parent[v] = r;
-        v = nx;
-    }
-    return r;
 }
 
 template <int DMAX, int KMAX>
@@ -1023,9 +1112,7 @@ int pqh_mst_build(pqh_ctx_t* ctx, const uint32_t* d_indices, const float* d_dist
     hipLaunchKernelGGL(gather_pairs, dim3(ge), dim3(256), 0, ctx->stream, vals_s, ne, src, dst, pairs);
     PQH_LAUNCH_CHECK(ctx);
     int hflag[2] = {0, 0};
-    std::vector<uint2> ed((size_t)ne);
     PQH_HIP(ctx, hipMemcpyAsync(hflag, flag, sizeof(hflag), hipMemcpyDeviceToHost, ctx->stream));
-    PQH_HIP(ctx, hipMemcpyAsync(ed.data(), pairs, sizeof(uint2) * ne, hipMemcpyDeviceToHost, ctx->stream));
     PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
     if (hflag[0] & 1) return pqh_set_error(ctx, PQH_ERR_ARG, "mst: a neighbour id outside the rows");
     if ((hflag[0] & 2) || hflag[1]) {
@@ -1057,30 +1144,85 @@ int pqh_mst_build(pqh_ctx_t* ctx, const uint32_t* d_indices, const float* d_dist
             for (int j = 0; j < take; ++j) all[(size_t)v * take + j] = row[j];
         }
         qsort(all.data(), (size_t)ne, sizeof(HostEdge), edge_dist_cmp_ref);
+        std::vector<uint2> ed((size_t)ne);
         for (long long e = 0; e < ne; ++e) ed[e] = make_uint2(all[e].source, all[e].target);
+        PQH_HIP(ctx, hipMemcpyAsync(pairs, ed.data(), sizeof(uint2) * ne, hipMemcpyHostToDevice, ctx->stream));
+        PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));   // (ed goes out of scope)
     }
-    // Kruskal (mst.c:185-201): kept edges in sorted order; then both directions, stably by
-    // source (:204-214) -- a counting sort
-    std::vector<uint32_t> parent((size_t)n);
-    for (long long v = 0; v < n; ++v) {
-        parent[v] = (uint32_t)v;
-        h_counts[v] = 0;
+    // Boruvka on the device (the same forest as Kruskal's scan, mst.c:185-201)
+    uint32_t* comp = buf.get<uint32_t>(n);
+    uint32_t* best = buf.get<uint32_t>(n);
+    uint32_t* hook = buf.get<uint32_t>(n);
+    uint32_t* kept = buf.get<uint32_t>(ne + 1);
+    uint32_t* kidx = buf.get<uint32_t>(ne + 1);
+    int* fl = buf.get<int>(2);
+    if (!comp || !best || !hook || !kept || !kidx || !fl)
+        return pqh_set_error(ctx, PQH_ERR_NOMEM, "mst: forest buffers");
+    const unsigned gn = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(bv_iota, dim3(gn), dim3(256), 0, ctx->stream, n, comp);
+    PQH_LAUNCH_CHECK(ctx);
+    PQH_HIP(ctx, hipMemsetAsync(kept, 0, sizeof(uint32_t) * (ne + 1), ctx->stream));
+    for (int round = 0; round < 64; ++round) {
+        PQH_HIP(ctx, hipMemsetAsync(fl, 0, 2 * sizeof(int), ctx->stream));
+        hipLaunchKernelGGL(bv_reset, dim3(gn), dim3(256), 0, ctx->stream, n, best, hook);
+        hipLaunchKernelGGL(bv_edges, dim3(ge), dim3(256), 0, ctx->stream, pairs, ne, comp, best, fl);
+        hipLaunchKernelGGL(bv_hook, dim3(gn), dim3(256), 0, ctx->stream, pairs, n, comp, best, hook, kept);
+        hipLaunchKernelGGL(bv_mutual, dim3(gn), dim3(256), 0, ctx->stream, n, hook);
+        PQH_LAUNCH_CHECK(ctx);
+        int any = 0;
+        PQH_HIP(ctx, hipMemcpyAsync(&any, fl, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+        PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        if (!any) break;
+        for (int j = 0; j < 64; ++j) {   // pointer jumping to the roots
+            PQH_HIP(ctx, hipMemsetAsync(fl + 1, 0, sizeof(int), ctx->stream));
+            hipLaunchKernelGGL(bv_jump, dim3(gn), dim3(256), 0, ctx->stream, n, hook, fl + 1);
+            PQH_LAUNCH_CHECK(ctx);
+            int changed = 0;
+            PQH_HIP(ctx, hipMemcpyAsync(&changed, fl + 1, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+            PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            if (!changed) break;
+        }
+        hipLaunchKernelGGL(bv_relabel, dim3(gn), dim3(256), 0, ctx->stream, n, hook, comp);
+        PQH_LAUNCH_CHECK(ctx);
     }
-    std::vector<uint2> kept;
-    kept.reserve((size_t)(n > 1 ? n - 1 : 0));
-    for (long long e = 0; (long long)kept.size() + 1 < n && e < ne; ++e) {
-        const uint32_t a = dsu_find(parent, ed[e].x), b = dsu_find(parent, ed[e].y);
-        if (a == b) continue;
-        parent[b] = a;
-        ++h_counts[ed[e].x];
-        kept.push_back(ed[e]);
+    {   // kidx = exclusive scan of the kept flags (kidx[ne] = K)
+        size_t temp = 0;
+        PQH_HIP(ctx, rocprim::exclusive_scan(nullptr, temp, kept, kidx, 0u, (size_t)ne + 1,
+                                             rocprim::plus<uint32_t>(), ctx->stream));
+        void* t = buf.get<char>(temp);
+        if (!t) return pqh_set_error(ctx, PQH_ERR_NOMEM, "mst: scan temp");
+        PQH_HIP(ctx, rocprim::exclusive_scan(t, temp, kept, kidx, 0u, (size_t)ne + 1,
+                                             rocprim::plus<uint32_t>(), ctx->stream));
     }
-    for (const uint2& e : kept) ++h_counts[e.y];
-    std::vector<long long> first((size_t)n + 1, 0);
-    for (long long v = 0; v < n; ++v) first[v + 1] = first[v] + h_counts[v];
-    for (const uint2& e : kept) h_targets[first[e.x]++] = e.y;   // forward copies first ...
-    for (const uint2& e : kept) h_targets[first[e.y]++] = e.x;   // ... then the reversed ones
-    *num_edges = 2 * (long long)kept.size();
+    uint32_t K = 0;
+    PQH_HIP(ctx, hipMemcpyAsync(&K, kidx + ne, 4, hipMemcpyDeviceToHost, ctx->stream));
+    PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    const long long m2 = 2 * (long long)K;
+    uint32_t* akeys = buf.get<uint32_t>(m2);
+    uint32_t* akeys_s = buf.get<uint32_t>(m2);
+    uint32_t* avals = buf.get<uint32_t>(m2);
+    uint32_t* avals_s = buf.get<uint32_t>(m2);
+    uint32_t* other = buf.get<uint32_t>(m2);
+    uint32_t* tg = buf.get<uint32_t>(m2);
+    int* cnt = buf.get<int>(n);
+    if (!akeys || !akeys_s || !avals || !avals_s || !other || !tg || !cnt)
+        return pqh_set_error(ctx, PQH_ERR_NOMEM, "mst: adjacency buffers");
+    PQH_HIP(ctx, hipMemsetAsync(cnt, 0, sizeof(int) * n, ctx->stream));
+    hipLaunchKernelGGL(bv_emit, dim3(ge), dim3(256), 0, ctx->stream, pairs, ne, kept, kidx, K, akeys,
+                       avals, other, cnt);
+    PQH_LAUNCH_CHECK(ctx);
+    if (m2 > 0) {
+        // both directions stably by source (mst.c:204-214): forward copies first, then the
+        // reversed ones, each in acceptance order
+        if ((rc = radix_sort_u32(ctx, buf, akeys, akeys_s, avals, avals_s, m2))) return rc;
+        hipLaunchKernelGGL(bv_targets, dim3((unsigned)((m2 + 255) / 256)), dim3(256), 0, ctx->stream,
+                           avals_s, m2, other, tg);
+        PQH_LAUNCH_CHECK(ctx);
+        PQH_HIP(ctx, hipMemcpyAsync(h_targets, tg, sizeof(uint32_t) * m2, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    PQH_HIP(ctx, hipMemcpyAsync(h_counts, cnt, sizeof(int) * n, hipMemcpyDeviceToHost, ctx->stream));
+    PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    *num_edges = m2;
     return PQH_OK;
 }
 
