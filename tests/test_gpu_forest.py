@@ -72,6 +72,7 @@ def _dups(n, d, seed):
     ("tiny_blocks", lambda: datagen.sift_like(400, 8, seed=44), 3, 4, 0.0, 30),
     ("d1_split1", lambda: datagen.sift_like(700, 1, seed=45), 1, 7, 0.2, 6),
     ("d40_kmax32", lambda: datagen.sift_like(1500, 40, seed=46), 2, 2, 0.3, 25),
+    ("n100k_runsh", lambda: datagen.sift_like(100_000, 32, seed=47), 3, 10, 0.01, 20),
 ], ids=lambda c: c[0])
 def test_knn_and_mst_vs_oracle(gpu, oracle, case):
     torch, forest, ctx = gpu
