@@ -385,6 +385,7 @@ knn_screen(const kbf16x8* __restrict__ xhi, const kbf16x8* __restrict__ xlo,
     constexpr int NSTEP = DP / 16;
     constexpr int G = DP / 8;   // bf16x8 groups per row
     __shared__ __attribute__((aligned(16))) float tnorm[kScreenQ];
+    __shared__ float pbuf[64 * 16];   // pass 1: a tile's values below the lane's threshold
     const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
     const long long b = tile_block[blockIdx.x];
     const long long base = boff[b];
@@ -431,18 +432,23 @@ knn_screen(const kbf16x8* __restrict__ xhi, const kbf16x8* __restrict__ xlo,
         kf32x16 acc;
         float nc[16];
         tile(c0, acc, nc);
+        // the tile's values below the lane's current KMAX-th go to its LDS buffer; the
+        // network then runs once per entry of the fullest lane (not once per register)
+        const float thr = lst[KMAX - 1];
+        int cnt = 0;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             const int row = c0 + (i & 3) + 8 * (i >> 2) + 4 * h;
             const float dp = fmaf(-2.0f, acc[i], nq + nc[i]);
-            float cd = (valid && row < S && dp < lst[KMAX - 1]) ? dp : INFINITY;
-            if (__any(cd < INFINITY)) {
+            if (valid && row < S && dp < thr) pbuf[lane * 16 + cnt++] = dp;
+        }
+        for (int e = 0; __any(e < cnt); ++e) {
+            float cd = e < cnt ? pbuf[lane * 16 + e] : INFINITY;
 #pragma unroll
-                for (int j = 0; j < KMAX; ++j) {
-                    const float lo = raw_min(lst[j], cd), hi = raw_max(lst[j], cd);
-                    lst[j] = lo;
-                    cd = hi;
-                }
+            for (int j = 0; j < KMAX; ++j) {
+                const float lo = raw_min(lst[j], cd), hi = raw_max(lst[j], cd);
+                lst[j] = lo;
+                cd = hi;
             }
         }
     }
@@ -549,6 +555,95 @@ knn_select(const float* __restrict__ xpad, int num_nn,
     }
 }
 
+// knn_select's wave form (the default): one wave per (block, query) pair, a lane per listed
+// candidate (64 at a time): the exact direct-form distances in parallel (the query row is
+// wave-uniform), then a bitonic sort of the 64 (distance, position) keys across the lanes,
+// merged into the running 64 smallest (min with the reversed new list, then a bitonic
+// clean), so after the last round lanes 0 .. kk-1 hold the kk smallest in order.
+__device__ __forceinline__ bool key_less(float da, uint32_t pa, float db, uint32_t pb) {
+    return da < db || (da == db && pa < pb);
+}
+
+// one compare-exchange stage of a bitonic network across the wave: partner = lane ^ j; the
+// lane keeps the smaller key when (lane & j) == 0 and the block is ascending
+__device__ __forceinline__ void bitonic_step(float& d, uint32_t& p, int lane, int j, bool up) {
+    const float od = __shfl_xor(d, j);
+    const uint32_t op = (uint32_t)__shfl_xor((int)p, j);
+    const bool lower = (lane & j) == 0;
+    const bool other_less = key_less(od, op, d, p);
+    const bool take = (lower == up) ? other_less : !other_less && !(od == d && op == p);
+    if (take) {
+        d = od;
+        p = op;
+    }
+}
+
+template <int DP>
+__global__ void __launch_bounds__(256)
+knn_select_wave(const float* __restrict__ xpad, int num_nn, const uint32_t* __restrict__ rows,
+                const uint32_t* __restrict__ keys_sorted, const long long* __restrict__ boff,
+                long long np, int ch, const uint32_t* __restrict__ cand,
+                const uint32_t* __restrict__ ccount, int stride, float* __restrict__ out_dist,
+                uint32_t* __restrict__ out_row) {
+    const int lane = threadIdx.x & 63;
+    const long long p = (long long)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (p >= np) return;
+    const long long b = keys_sorted[p];
+    const long long base = boff[b];
+    const int S = (int)(boff[b + 1] - base);
+    const int kk = (num_nn < S - 1 ? num_nn : S - 1) + 1;
+    const uint32_t* brows = rows + base;
+    const float4* xq = reinterpret_cast<const float4*>(xpad + (long long)rows[p] * DP);
+    const uint32_t n0 = ccount[p * 2], n1 = ccount[p * 2 + 1];
+    const bool full = n0 > (uint32_t)ch || n1 > (uint32_t)ch;
+    const int total = full ? S : (int)(n0 + n1);
+    float kd = INFINITY;          // the running 64 smallest keys, ascending by lane
+    uint32_t kp = 0xFFFFFFFFu;
+    for (int t0 = 0; t0 < total; t0 += 64) {
+        const int t = t0 + lane;
+        float d = INFINITY;
+        uint32_t pos = 0xFFFFFFFFu;
+        if (t < total) {
+            pos = full ? (uint32_t)t
+                       : cand[(p * 2 + (t < (int)n0 ? 0 : 1)) * ch + (t < (int)n0 ? t : t - (int)n0)];
+            const float4* xc = reinterpret_cast<const float4*>(xpad + (long long)brows[pos] * DP);
+            float acc = 0.0f;   // get_real_dist, dimension order
+#pragma unroll
+            for (int j = 0; j < DP / 4; ++j) {
+                const float4 q4 = xq[j], c4 = xc[j];
+                float tt = __fsub_rn(q4.x, c4.x);
+                acc = __fadd_rn(acc, __fmul_rn(tt, tt));
+                tt = __fsub_rn(q4.y, c4.y);
+                acc = __fadd_rn(acc, __fmul_rn(tt, tt));
+                tt = __fsub_rn(q4.z, c4.z);
+                acc = __fadd_rn(acc, __fmul_rn(tt, tt));
+                tt = __fsub_rn(q4.w, c4.w);
+                acc = __fadd_rn(acc, __fmul_rn(tt, tt));
+            }
+            d = acc;
+        }
+        // sort the 64 new keys ascending (bitonic)
+        for (int k = 2; k <= 64; k <<= 1)
+            for (int j = k >> 1; j > 0; j >>= 1) bitonic_step(d, pos, lane, j, (lane & k) == 0);
+        if (t0 == 0) {
+            kd = d;
+            kp = pos;
+        } else {   // the 64 smallest of both: min with the reversed new list (bitonic), clean
+            const float rd = __shfl(d, 63 - lane);
+            const uint32_t rp = (uint32_t)__shfl((int)pos, 63 - lane);
+            if (key_less(rd, rp, kd, kp)) {
+                kd = rd;
+                kp = rp;
+            }
+            for (int j = 32; j > 0; j >>= 1) bitonic_step(kd, kp, lane, j, true);
+        }
+    }
+    if (lane < kk) {
+        out_dist[p * stride + lane] = kd;
+        out_row[p * stride + lane] = brows[kp];
+    }
+}
+
 // ------------------------------------------------------------------ merge
 struct NnItem {
     uint32_t index;
@@ -584,6 +679,9 @@ knn_merge(long long n, int num_nn, const unsigned long long* __restrict__ off,
     if (v >= n) return;
     NnItem* h = heaps + threadIdx.x * num_nn;
     for (int j = 0; j < num_nn; ++j) h[j] = NnItem{0xFFFFFFFFu, INFINITY};
+    // a row in one block gets distinct indices only: the reference's duplicate scan never
+    // fires for it
+    const bool single = off[v + 1] - off[v] == 1;
     for (unsigned long long e = off[v]; e < off[v + 1]; ++e) {
         const long long p = inv[e];
         const long long b = keys_sorted[p];
@@ -593,7 +691,8 @@ knn_merge(long long n, int num_nn, const unsigned long long* __restrict__ off,
             const NnItem it{lrow[p * stride + j], ldist[p * stride + j]};
             if (!(it.dist < h[0].dist)) continue;
             bool dup = false;
-            for (int q = 0; q < num_nn; ++q) dup |= h[q].index == it.index;
+            if (!single)
+                for (int q = 0; q < num_nn; ++q) dup |= h[q].index == it.index;
             if (!dup) nn_sift(h, it, num_nn);
         }
     }
@@ -1050,6 +1149,22 @@ int pqh_knn_fast(pqh_ctx_t* ctx, const float* d_x, long long n, long long ld_x, 
 #undef PQH_KNN_SCREEN
         PQH_LAUNCH_CHECK(ctx);
         const unsigned gs = (unsigned)((np + 63) / 64);
+        static const bool lane_select = [] {
+            const char* e = std::getenv("PQH_KNN_SELECT");
+            return e && std::strcmp(e, "lane") == 0;
+        }();
+        if (!lane_select) {   // one wave per query (default)
+            const unsigned gw = (unsigned)((np + 3) / 4);
+#define PQH_KNN_SELECT_W(DP_)                                                                    \
+    hipLaunchKernelGGL((knn_select_wave<DP_>), dim3(gw), dim3(256), 0, ctx->stream, xpad, num_nn,  \
+                       rows, keys_s, boff, np, ch, cand, ccnt, stride, ldist, lrow)
+            if (dp == 16) PQH_KNN_SELECT_W(16);
+            else if (dp == 32) PQH_KNN_SELECT_W(32);
+            else if (dp == 64) PQH_KNN_SELECT_W(64);
+            else PQH_KNN_SELECT_W(128);
+#undef PQH_KNN_SELECT_W
+            PQH_LAUNCH_CHECK(ctx);
+        } else {
 #define PQH_KNN_SELECT(DM_, K_)                                                                  \
     hipLaunchKernelGGL((knn_select<DM_, K_>), dim3(gs), dim3(64), 0, ctx->stream, xpad, num_nn,    \
                        rows, keys_s, boff, np, ch, cand, ccnt, stride, ldist, lrow)
@@ -1068,6 +1183,7 @@ int pqh_knn_fast(pqh_ctx_t* ctx, const float* d_x, long long n, long long ld_x, 
 #undef PQH_KNN_SELECT_K
 #undef PQH_KNN_SELECT
         PQH_LAUNCH_CHECK(ctx);
+        }
     }
     hipLaunchKernelGGL(knn_merge, dim3((unsigned)((n + kQ - 1) / kQ)), dim3(kQ),
                        sizeof(NnItem) * kQ * num_nn, ctx->stream, n, num_nn, off, inv, keys_s, boff,
