@@ -327,6 +327,15 @@ int pqh_mst_files(const char* nn_template, const char* out_template, int take,
 int pqh_tree_order(long long num_vertices, long long num_edges, const uint32_t* edge_targets,
                    const int* children_counts, uint32_t* vertices, int* num_children,
                    long long* parents);
+/* pqh_tree_order on the device, for a forest (no self-loop, every edge stored in both
+ * directions once, no cycle): device counts/targets in, device vertices / num_children /
+ * parents (may be NULL) out, *num_roots on the host.  PQH_ERR_UNSUPPORTED for a graph that is
+ * not such a forest (nothing written; pqh_tree_order walks any graph), PQH_ERR_ARG for
+ * counts that are negative or do not sum to num_edges.  Synchronises. */
+int pqh_tree_order_device(pqh_ctx_t* ctx, long long num_vertices, long long num_edges,
+                          const uint32_t* d_edge_targets, const int* d_children_counts,
+                          uint32_t* d_vertices, int* d_num_children, long long* d_parents,
+                          int* num_roots);
 /* d_rows[p] = d_codes[d_vertices[p]] (stream order) and d_tree_prev[p][i] =
  * d_codes[d_parents[p]][i], 0xFFFF for a root.  Ids outside [0, n) are reported by
  * pqh_tree_status (nothing is read for them). */

@@ -456,6 +456,29 @@ def tree_order(targets, counts):
     return vert[:n], nch[:n], par[:n], roots
 
 
+def tree_order_device(ctx: Context, targets, counts):
+    """tree_order on the device (pqh_tree_order_device): targets / counts as host arrays or
+    device tensors.  Returns (vertices i32, num_children i32, parents i64) device tensors and
+    num_roots, or None when the graph is not a forest (tree_order walks any graph)."""
+    torch = _torch()
+    dev = torch.device("cuda", ctx.device)
+    t = torch.as_tensor(np.asarray(targets, np.uint32).view(np.int32)
+                        if not torch.is_tensor(targets) else targets).to(dev, torch.int32)
+    c = torch.as_tensor(np.asarray(counts, np.int32) if not torch.is_tensor(counts)
+                        else counts).to(dev, torch.int32)
+    n = c.numel()
+    vert = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    nch = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    par = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    roots = ctypes.c_int(0)
+    rc = lib().pqh_tree_order_device(ctx.ptr, n, t.numel(), _ptr(t), _ptr(c), _ptr(vert),
+                                     _ptr(nch), _ptr(par), ctypes.byref(roots))
+    if rc == -4:   # PQH_ERR_UNSUPPORTED
+        return None
+    check(rc, "pqh_tree_order_device: " + ctx.last_error())
+    return vert[:n], nch[:n], par[:n], roots.value
+
+
 @dataclass
 class TreeEncoded:
     stream: object             # device uint8 (huffman_indices.bin payload), padded to 4 B
@@ -494,7 +517,8 @@ def tree_ext_index(num_children, chunk_vectors: int):
 
 def tree_encode(ctx: Context, codes, targets, counts, chunk_vectors: int = 16) -> TreeEncoded:
     """Tree mode of huffman_encoder (huffman_encoder.c:321-375, encode_tree_data :240-286)
-    on device uint8 codes [n, m]: host DFS order -> device gather of the rows in stream order
+    on device uint8 codes [n, m]: DFS order (device Euler tour; the host walk for a graph
+    that is not a forest) -> device gather of the rows in stream order
     beside their parents' codes -> parent/child pair histogram -> GPU code tables -> one-pass
     encode with explicit contexts; plus the children-count stream (non-context code book of
     tree_collect_num_children_stats, mst.c:407-440, coded by the GPU encoder).
@@ -503,10 +527,15 @@ def tree_encode(ctx: Context, codes, targets, counts, chunk_vectors: int = 16) -
     n, m = codes.shape
     if len(counts) != n:
         raise ValueError(f"tree has {len(counts)} vertices for {n} rows")
-    vert, nch, par, roots = tree_order(targets, counts)
     dev = codes.device
-    d_vert = torch.from_numpy(vert.astype(np.int32)).to(dev)
-    d_par = torch.from_numpy(par).to(dev)
+    order = tree_order_device(ctx, targets, counts)
+    if order is not None:
+        d_vert, d_nch, d_par, roots = order
+        vert, nch = d_vert.cpu().numpy().view(np.uint32), d_nch.cpu().numpy()
+    else:   # not a forest: the host walk reproduces the reference's DFS on any graph
+        vert, nch, par, roots = tree_order(targets, counts)
+        d_vert = torch.from_numpy(vert.astype(np.int32)).to(dev)
+        d_par = torch.from_numpy(par).to(dev)
     rows = torch.empty((n, m), dtype=torch.uint8, device=dev)
     prev = torch.empty((n, m), dtype=torch.int16, device=dev)
     check(lib().pqh_tree_gather(ctx.ptr, _ptr(codes), n, m, 256, _ptr(d_vert), _ptr(d_par),

@@ -273,7 +273,7 @@ extern "C" int pqh_decode_files(const char* in_prefix, unsigned char** codes_out
 }
 
 // huffman_encoder --tree <mst.tree> (huffman_encoder.c:321-375, :398-428): tree order and
-// contexts on the host (pqh_tree_order), rows gathered, counted and coded on the GPU, the
+// contexts on the device (pqh_tree_order_device; the host walk for a non-forest), rows gathered, counted and coded on the GPU, the
 // children stream coded by the GPU encoder with the host-built children code book.
 // Writes huffman_codebooks.bin, huffman_indices.bin, huffman_stats.txt (appended),
 // huffman_children_codebooks.bin, huffman_children.bin, huffman_children_stats.txt.
@@ -292,12 +292,7 @@ extern "C" int pqh_encode_tree_files(const unsigned char* codes, long long n, in
          fread(adj.data(), 4, (size_t)nv, tf) == (size_t)nv;
     fclose(tf);
     if (!ok) return PQH_ERR_ARG;
-    std::vector<uint32_t> vert(n);
     std::vector<int> nch(n);
-    std::vector<long long> par(n);
-    const int roots = pqh_tree_order(n, ne, targets.data(), adj.data(), vert.data(), nch.data(),
-                                     par.data());
-    if (roots < 0) return roots;
 
     CtxGuard g;
     int rc = pqh_ctx_create(&g.ctx, 0);
@@ -306,15 +301,46 @@ extern "C" int pqh_encode_tree_files(const unsigned char* codes, long long n, in
     const long long items = (long long)k * k;
     DevBuf<unsigned char> d_codes, d_rows;
     DevBuf<uint16_t> d_prev;
-    DevBuf<uint32_t> d_vert, d_counts;
+    DevBuf<uint32_t> d_vert, d_counts, d_targets;
     DevBuf<long long> d_par;
+    DevBuf<int> d_adj, d_nch;
     if ((rc = d_codes.alloc(ctx, (size_t)n * m)) || (rc = d_rows.alloc(ctx, (size_t)n * m)) ||
         (rc = d_prev.alloc(ctx, (size_t)n * m)) || (rc = d_vert.alloc(ctx, n)) ||
         (rc = d_par.alloc(ctx, n)) || (rc = d_counts.alloc(ctx, (size_t)m * items)))
         return rc;
     PQH_HIP(ctx, hipMemcpyAsync(d_codes.p, codes, (size_t)n * m, hipMemcpyHostToDevice, ctx->stream));
-    PQH_HIP(ctx, hipMemcpyAsync(d_vert.p, vert.data(), (size_t)n * 4, hipMemcpyHostToDevice, ctx->stream));
-    PQH_HIP(ctx, hipMemcpyAsync(d_par.p, par.data(), (size_t)n * 8, hipMemcpyHostToDevice, ctx->stream));
+    // tree order (tree_collect_vertices_dfs + the traverser's parents) on the device; a file
+    // that is not a forest (a cycle, a repeated edge) takes the host walk, which reproduces
+    // the reference's DFS on any graph.  PQH_TREE_ORDER=host forces the host walk.
+    int roots = -1;
+    const char* tmode = getenv("PQH_TREE_ORDER");
+    if (!(tmode && !strcmp(tmode, "host"))) {
+        if ((rc = d_targets.alloc(ctx, ne > 0 ? ne : 1)) || (rc = d_adj.alloc(ctx, n)) ||
+            (rc = d_nch.alloc(ctx, n)))
+            return rc;
+        if (ne > 0)
+            PQH_HIP(ctx, hipMemcpyAsync(d_targets.p, targets.data(), (size_t)ne * 4,
+                                        hipMemcpyHostToDevice, ctx->stream));
+        PQH_HIP(ctx, hipMemcpyAsync(d_adj.p, adj.data(), (size_t)n * 4, hipMemcpyHostToDevice, ctx->stream));
+        int r = 0;
+        rc = pqh_tree_order_device(ctx, n, ne, d_targets.p, d_adj.p, d_vert.p, d_nch.p, d_par.p, &r);
+        if (rc == PQH_OK) {
+            roots = r;
+            PQH_HIP(ctx, hipMemcpyAsync(nch.data(), d_nch.p, (size_t)n * 4, hipMemcpyDeviceToHost,
+                                        ctx->stream));
+        } else if (rc != PQH_ERR_UNSUPPORTED) {
+            return rc;
+        }
+    }
+    if (roots < 0) {
+        std::vector<uint32_t> vert(n);
+        std::vector<long long> par(n);
+        roots = pqh_tree_order(n, ne, targets.data(), adj.data(), vert.data(), nch.data(), par.data());
+        if (roots < 0) return roots;
+        PQH_HIP(ctx, hipMemcpyAsync(d_vert.p, vert.data(), (size_t)n * 4, hipMemcpyHostToDevice, ctx->stream));
+        PQH_HIP(ctx, hipMemcpyAsync(d_par.p, par.data(), (size_t)n * 8, hipMemcpyHostToDevice, ctx->stream));
+        PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    }
     if (sort) {   // the CLI sorts before applying the tree (huffman_encoder.c:313-325)
         DevBuf<unsigned char> tmp;
         if ((rc = tmp.alloc(ctx, (size_t)n * m))) return rc;

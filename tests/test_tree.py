@@ -220,9 +220,11 @@ def test_tree_ext_index_vs_oracle(oracle, n, roots, c):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("order", ["device", "host"])
 @pytest.mark.parametrize("mode,flags", [("tree_nosort", ["--no-sort"]), ("tree_sort", [])])
-def test_cli_encoder_tree_matches_reference_files(tmp_path, mode, flags):
-    """huffman_encoder --tree (pqh_encode_tree_files) writes the reference's six files."""
+def test_cli_encoder_tree_matches_reference_files(tmp_path, mode, flags, order):
+    """huffman_encoder --tree (pqh_encode_tree_files) writes the reference's six files, with
+    the device tree order and with the host walk (PQH_TREE_ORDER=host)."""
     import os
     import subprocess
     from conftest import ROOT
@@ -235,7 +237,8 @@ def test_cli_encoder_tree_matches_reference_files(tmp_path, mode, flags):
     datagen.write_tree(str(tree), 1000, g["targets"], g["counts"])
     r = subprocess.run([os.path.join(ROOT, "pq_huffman_amd", "bin", "huffman_encoder"),
                         str(pqdir) + "/", str(out) + "/", "8", "--tree", str(tree)] + flags,
-                       capture_output=True, text=True)
+                       capture_output=True, text=True,
+                       env=dict(os.environ, PQH_TREE_ORDER=order))
     assert r.returncode == 0, r.stdout + r.stderr
     for f in FILES + ["huffman_stats", "huffman_children_stats"]:
         ext = ".txt" if f.endswith("stats") else ".bin"
@@ -252,3 +255,99 @@ def test_cli_encoder_tree_matches_reference_files(tmp_path, mode, flags):
                         str(out) + "/", "--tree", "--output-file", str(dec)],
                        capture_output=True, text=True)
     assert r.returncode != 0
+
+
+# ------------------------------------------------- device DFS order (Euler tour)
+def _path_forest(n, seed):
+    """One path through a random permutation of the ids (depth n - 1)."""
+    rng = np.random.default_rng(seed)
+    p = rng.permutation(n)
+    adj = [[] for _ in range(n)]
+    for a, b in zip(p[:-1], p[1:]):
+        adj[a].append(b)
+        adj[b].append(a)
+    return (np.array([t for a in adj for t in a], np.uint32),
+            np.array([len(a) for a in adj], np.int32))
+
+
+def _star_forest(n, centre):
+    adj = [[] for _ in range(n)]
+    for v in range(n):
+        if v != centre:
+            adj[centre].append(v)
+            adj[v].append(centre)
+    return (np.array([t for a in adj for t in a], np.uint32),
+            np.array([len(a) for a in adj], np.int32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,n,roots", [
+    ("random", 1, 1), ("random", 2, 1), ("random", 64, 64), ("random", 1000, 3),
+    ("random", 200_000, 17), ("random", 1_000_000, 1000), ("random", 300_000, 1),
+    ("path", 100_000, 1), ("star", 50_000, 1), ("two", 4, 2)])
+def test_gpu_tree_order_device_vs_host(gpu, shape, n, roots):
+    """pqh_tree_order_device equals the host walk (tree_collect_vertices_dfs + traverser
+    parents): preorder from each tree's lowest id, children in reverse adjacency order."""
+    from pq_huffman_amd import codec
+    if shape == "random":
+        targets, counts = datagen.random_forest(n, roots=roots, seed=n + roots)
+    elif shape == "path":
+        targets, counts = _path_forest(n, seed=5)
+    elif shape == "star":
+        targets, counts = _star_forest(n, centre=n // 3)
+    else:                                      # second tree's root is not the lowest id
+        targets, counts = np.array([3, 2, 1, 0], np.uint32), np.array([1, 1, 1, 1], np.int32)
+    vert, nch, par, nroots = codec.tree_order(targets, counts)
+    got = codec.tree_order_device(gpu, targets, counts)
+    assert got is not None
+    dv, dn, dp, droots = got
+    assert droots == nroots == roots
+    np.testing.assert_array_equal(dv.cpu().numpy().view(np.uint32), vert)
+    np.testing.assert_array_equal(dn.cpu().numpy(), nch)
+    np.testing.assert_array_equal(dp.cpu().numpy(), par)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("targets,counts", [
+    ([1, 2, 0, 2, 0, 1], [2, 2, 2]),          # a cycle
+    ([0, 1, 1, 0], [2, 1, 1]),                # self loops
+    ([1, 1], [2, 0, 0]),                      # a repeated edge stored in one direction
+    ([1, 2, 0, 2, 0, 1, 3, 2], [2, 2, 3, 1]),  # a triangle 0-1-2 with a pendant edge 2-3
+])
+def test_gpu_tree_order_device_declines_non_forests(gpu, targets, counts):
+    """A graph that is not a forest is declined (None), and the encoder's host walk takes it."""
+    from pq_huffman_amd import codec
+    t, c = np.array(targets, np.uint32), np.array(counts, np.int32)
+    assert codec.tree_order_device(gpu, t, c) is None
+
+
+@pytest.mark.gpu
+def test_gpu_tree_order_device_large_cycle(gpu):
+    """A forest plus one long cycle (every vertex has an edge down into it from the tour
+    pass, but the edge count exceeds a forest's): declined."""
+    from pq_huffman_amd import codec
+    n = 10_000
+    adj = [[] for _ in range(n)]
+    for v in range(n):
+        w = (v + 1) % n
+        adj[v].append(w)
+        adj[w].append(v)
+    t = np.array([x for a in adj for x in a], np.uint32)
+    c = np.array([len(a) for a in adj], np.int32)
+    assert codec.tree_order_device(gpu, t, c) is None
+
+
+@pytest.mark.gpu
+def test_gpu_tree_order_device_rejects_bad_counts(gpu):
+    from pq_huffman_amd import codec
+    from pq_huffman_amd.capi import PqhError
+    targets, counts = datagen.random_forest(50, roots=2, seed=7)
+    with pytest.raises(PqhError):             # counts do not sum to the edge count
+        codec.tree_order_device(gpu, targets[:-1], counts)
+    bad = counts.copy()
+    bad[0], bad[1] = bad[0] + 3, -3           # right sum, a negative count
+    with pytest.raises(PqhError):
+        codec.tree_order_device(gpu, targets, bad)
+    bad_t = targets.copy()
+    bad_t[0] = 50                             # target outside the vertices: not a forest
+    assert codec.tree_order_device(gpu, bad_t, counts) is None

@@ -1,6 +1,7 @@
 """Tree-mode timing (huffman_encoder/huffman_decoder --tree) at SIFT1M shape: 1M rows, M=8,
 K=256, on one GPU.  Prints one JSON line: wall-clock ms per tree_encode / tree_decode call
-(host DFS + traverser included, inputs resident in HBM) and the host walk alone; run under
+(DFS order + traverser included, inputs resident in HBM), the host walk alone and the
+device order (pqh_tree_order_device, forest already in HBM) alone; run under
 `rocprofv3 --kernel-trace --stats` for the per-kernel device times.  Synthetic skewed codes
 and a seeded random forest in the mst.tree layout (tests/datagen.py)."""
 import json
@@ -31,6 +32,14 @@ def main():
     for _ in range(reps):
         codec.tree_order(targets, counts)
     host_ms = (time.perf_counter() - t0) / reps * 1e3
+    dt, dc = torch.from_numpy(targets.view(np.int32)).cuda(), torch.from_numpy(counts).cuda()
+    codec.tree_order_device(ctx, dt, dc)
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        codec.tree_order_device(ctx, dt, dc)
+    ctx.sync()
+    dev_order_ms = (time.perf_counter() - t0) / reps * 1e3
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(reps):
@@ -45,6 +54,7 @@ def main():
     print(json.dumps({"workload": f"tree mode, {n} x {m} u8 codes, K=256, 100-root forest",
                       "encode_ms": round(enc_ms, 3), "decode_ms": round(dec_ms, 3),
                       "host_tree_order_ms": round(host_ms, 3),
+                      "device_tree_order_ms": round(dev_order_ms, 3),
                       "bits_per_vector": round(enc.bits / n, 3),
                       "ext_rows": int(enc.ext_rows.shape[0]),
                       "roundtrip_mvec_s": round(n / (enc_ms + dec_ms) / 1e3, 2)}))
