@@ -7,44 +7,49 @@
 // trees come in root-id order and the children of a vertex in reverse adjacency order; the
 // traverser's active parent of a row (mst.c:366-405) is the vertex's tree parent.  Computed
 // without a sequential walk:
-//   twins      every directed edge u->v paired with v->u (a stable radix sort of the
-//              undirected keys); a self-loop, a repeated edge or an unpaired edge is not a
-//              forest -- PQH_ERR_UNSUPPORTED, and the caller walks on the host (pqh_tree_order)
-//   tour       succ(u->v) = the edge after v->u in v's list (cyclic): one Euler tour per tree
-//   roots      the minimum vertex over each tour (pointer jumping); the tour is cut before
-//              the root's first edge and list-ranked (pointer jumping)
-//   parents    u->v is a tree edge down when it precedes v->u in the tour; subtree sizes from
-//              the two ranks; a graph with a cycle leaves a vertex without exactly one edge
-//              down into it, or more tours than the forest count allows -> not a forest
-//   preorder   pre(c) = pre(v) + 1 + the sizes of the children after c in v's list (a scan
-//              over the edges), accumulated to the root by pointer jumping, plus the sizes of
-//              the trees with smaller roots
+//   twins      every directed edge u->v paired with v->u (a radix sort of the undirected
+//              keys); a self-loop, a repeated edge or an unpaired edge is not a forest --
+//              PQH_ERR_UNSUPPORTED, and the caller walks on the host (pqh_tree_order)
+//   tours      succ(u->v) = the edge after v->u in v's list (cyclic): the faces of the
+//              graph's rotation system, one Euler tour per tree of a forest
+//   ranking    pointer jumping on (the tour's smallest edge id m, distance to it) keys: m is
+//              the first edge of the component's smallest vertex; pos(e) = distance from m
+//   forest?    every vertex's edges on one tour (then tours = components) and
+//              edges / 2 = vertices - isolated - tours (then every component is a tree)
+//   parents    u->v goes down when it precedes v->u on the tour; subtree size = half the
+//              distance between the two
+//   preorder   off(c) = 1 + sizes of the children after c in its parent's list (a scan over
+//              the edges); pre(v) = the tree's offset + the sum of off over v's ancestors --
+//              a prefix sum along the tours (+off at the edge down, -off at the edge back)
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 
-#include <vector>
+#include <algorithm>
 
 #include "pqh_internal.h"
 
 namespace {
 
-constexpr uint32_t kNil = 0xFFFFFFFFu;
-
-struct DevBuf {
-    std::vector<void*> ptrs;
-    ~DevBuf() {
-        for (void* p : ptrs) (void)hipFree(p);
-    }
-    template <typename T>
-    T* get(size_t count) {
-        void* p = nullptr;
-        if (hipMalloc(&p, count ? count * sizeof(T) : 16) != hipSuccess) return nullptr;
-        ptrs.push_back(p);
-        return static_cast<T*>(p);
-    }
-};
-
 #define G1(n) dim3((unsigned)(((n) + 255) / 256)), dim3(256)
+
+// one atomic per wave for a count of lanes
+__device__ inline void wave_count(bool pred, int* ctr) {
+    const unsigned long long b = __ballot(pred);
+    if (b && (int)(threadIdx.x & 63) == __ffsll((unsigned long long)b) - 1) atomicAdd(ctr, __popcll(b));
+}
+
+__global__ void __launch_bounds__(256)
+td_vertex_init(long long n, const int* __restrict__ counts, uint32_t* __restrict__ parent,
+               uint32_t* __restrict__ rootL, int* __restrict__ flags) {
+    const long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool in = v < n;
+    const int c = in ? counts[v] : 1;
+    if (c < 0) flags[0] = 1;
+    wave_count(in && c == 0, flags + 2);   // isolated vertices
+    if (!in) return;
+    parent[v] = (uint32_t)v;
+    rootL[v] = 0;
+}
 
 // the source of every edge (CSR rows), and the undirected key of every edge
 __global__ void __launch_bounds__(256)
@@ -61,7 +66,7 @@ td_edges(const uint32_t* __restrict__ first, long long n, const uint32_t* __rest
     }
 }
 
-// twins from the sorted keys: keys must come in pairs of opposite directions
+// twins from the sorted keys: every key exactly twice, from two different sources
 __global__ void __launch_bounds__(256)
 td_twins(const unsigned long long* __restrict__ ks, const uint32_t* __restrict__ is, long long ne,
          const uint32_t* __restrict__ src, uint32_t* __restrict__ twin, int* __restrict__ bad) {
@@ -81,189 +86,170 @@ td_twins(const unsigned long long* __restrict__ ks, const uint32_t* __restrict__
     }
 }
 
+// succ(u->v) = the edge after v->u in v's list, cyclic; key = (own id, distance 0)
 __global__ void __launch_bounds__(256)
 td_succ(const uint32_t* __restrict__ first, const uint32_t* __restrict__ tg,
         const uint32_t* __restrict__ twin, long long ne, uint32_t* __restrict__ succ,
-        uint32_t* __restrict__ mn, uint32_t* __restrict__ src) {
+        uint32_t* __restrict__ jmp, unsigned long long* __restrict__ key) {
     const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= ne) return;
     const uint32_t v = tg[e], t = twin[e];
-    const uint32_t deg = first[v + 1] - first[v];
-    const uint32_t i = t - first[v];
-    succ[e] = first[v] + (i + 1 == deg ? 0 : i + 1);
-    mn[e] = src[e];
+    const uint32_t s = t + 1 == first[v + 1] ? first[v] : t + 1;
+    succ[e] = s;
+    jmp[e] = s;
+    key[e] = (unsigned long long)e << 32;
 }
 
-// one pointer-jumping round of the minimum over a tour (cycles): mn'[e] = min(mn[e], mn[j[e]]),
-// j'[e] = j[j[e]]
+// one pointer-jumping round: the window [e, e + 2 span) from [e, e + span) and
+// [j, j + span), j = e + span; key = (smallest edge id, distance to its first occurrence)
 __global__ void __launch_bounds__(256)
-td_min_round(long long ne, const uint32_t* __restrict__ j0, const uint32_t* __restrict__ m0,
-             uint32_t* __restrict__ j1, uint32_t* __restrict__ m1) {
+td_jump(long long ne, unsigned span, const uint32_t* __restrict__ j0,
+        const unsigned long long* __restrict__ k0, uint32_t* __restrict__ j1,
+        unsigned long long* __restrict__ k1) {
     const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= ne) return;
     const uint32_t j = j0[e];
-    m1[e] = min(m0[e], m0[j]);
+    const unsigned long long a = k0[e], b = k0[j] + span;
+    k1[e] = a < b ? a : b;
     j1[e] = j0[j];
 }
 
-// cut each tour before its root's first edge: the edge into the root that precedes it
+// forest test: all edges of a vertex on one tour; tours counted (edges at distance 0)
 __global__ void __launch_bounds__(256)
-td_cut(const uint32_t* __restrict__ first, const uint32_t* __restrict__ twin,
-       const uint32_t* __restrict__ root, long long ne, uint32_t* __restrict__ succ,
-       uint32_t* __restrict__ rank) {
+td_verify(const uint32_t* __restrict__ first, const uint32_t* __restrict__ src,
+          const unsigned long long* __restrict__ key, long long ne, int* __restrict__ flags) {
     const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= ne) return;
-    const uint32_t r = root[e];
-    const uint32_t last_in = twin[first[r + 1] - 1];   // (r's last edge reversed)
-    if ((uint32_t)e == last_in) succ[e] = kNil;
-    rank[e] = succ[e] == kNil ? 0u : 1u;
-}
-
-// list ranking: distance to the tour's end
-__global__ void __launch_bounds__(256)
-td_rank_round(long long ne, const uint32_t* __restrict__ j0, const uint32_t* __restrict__ r0,
-              uint32_t* __restrict__ j1, uint32_t* __restrict__ r1, int* __restrict__ more) {
-    const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= ne) return;
-    const uint32_t j = j0[e];
-    if (j == kNil) {
-        j1[e] = kNil;
-        r1[e] = r0[e];
-        return;
+    const bool in = e < ne;
+    unsigned long long k = 1;
+    if (in) {
+        k = key[e];
+        if ((k >> 32) != (key[first[src[e]]] >> 32)) flags[0] = 1;
     }
-    r1[e] = r0[e] + r0[j];
-    j1[e] = j0[j];
-    if (j0[j] != kNil) *more = 1;
+    wave_count(in && (uint32_t)k == 0u, flags + 3);
 }
 
-// per vertex: parent, the number of edges down into it, subtree size; the tree's edge count
-// and root; isolated vertices are roots of their own tree
+// position on the tour from its smallest edge m: L - d, with L - 1 = d(succ(m))
+__device__ inline uint32_t tour_pos(const unsigned long long* __restrict__ key,
+                                    const uint32_t* __restrict__ succ, uint32_t e) {
+    const unsigned long long k = key[e];
+    const uint32_t d = (uint32_t)k;
+    if (!d) return 0u;
+    return (uint32_t)key[succ[(uint32_t)(k >> 32)]] + 1u - d;
+}
+
+// parents (the edge down), subtree sizes, tour lengths of the roots
 __global__ void __launch_bounds__(256)
-td_parents(const uint32_t* __restrict__ first, const uint32_t* __restrict__ tg,
-           const uint32_t* __restrict__ src, const uint32_t* __restrict__ twin,
-           const uint32_t* __restrict__ rank, const uint32_t* __restrict__ root, long long ne,
-           uint32_t* __restrict__ parent, uint32_t* __restrict__ size, uint32_t* __restrict__ downs,
-           uint32_t* __restrict__ tedges) {
+td_parents(const uint32_t* __restrict__ tg, const uint32_t* __restrict__ src,
+           const uint32_t* __restrict__ twin, const uint32_t* __restrict__ succ,
+           const unsigned long long* __restrict__ key, long long ne, uint32_t* __restrict__ parent,
+           uint32_t* __restrict__ size, uint32_t* __restrict__ posdown, uint32_t* __restrict__ rootof,
+           uint32_t* __restrict__ rootL) {
     const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= ne) return;
-    const uint32_t t = twin[e];
-    // positions from the tour start: pos = (tour edges - 1) - rank; compare ranks instead
-    if (rank[e] > rank[t]) {   // e = u->v comes first: v's parent is u
+    const uint32_t pe = tour_pos(key, succ, (uint32_t)e), pt = tour_pos(key, succ, twin[e]);
+    if (pe < pt) {   // e = u->v comes first: v's parent is u
         const uint32_t v = tg[e];
         parent[v] = src[e];
-        size[v] = (rank[e] - rank[t] + 1) / 2;
-        atomicAdd(&downs[v], 1u);
+        size[v] = (pt - pe + 1) / 2;
+        posdown[v] = pe;
+        rootof[v] = src[(uint32_t)(key[e] >> 32)];
     }
-    if ((uint32_t)e == first[root[e]]) tedges[root[e]] = rank[e] + 1;   // the tour's length
+    if (pe == 0) rootL[src[e]] = (uint32_t)key[succ[e]] + 1u;
 }
 
+// per root: (vertex count << 32) | tour length, scanned into the trees' offsets
 __global__ void __launch_bounds__(256)
-td_vertex_init(long long n, const int* __restrict__ counts, uint32_t* __restrict__ parent,
-               uint32_t* __restrict__ size, uint32_t* __restrict__ downs, uint32_t* __restrict__ tedges,
-               int* __restrict__ bad) {
+td_roots(long long n, const uint32_t* __restrict__ parent, const uint32_t* __restrict__ rootL,
+         uint32_t* __restrict__ size, unsigned long long* __restrict__ rinfo) {
     const long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= n) return;
-    if (counts[v] < 0) *bad = 1;
-    parent[v] = (uint32_t)v;
-    size[v] = 0;
-    downs[v] = 0;
-    tedges[v] = 0;
-}
-
-// vertex checks and the per-edge weight for the children offsets: w(e) = size of the child
-// below a down edge, 0 for the edge to the parent
-__global__ void __launch_bounds__(256)
-td_check(long long n, const uint32_t* __restrict__ first, const uint32_t* __restrict__ parent,
-         const uint32_t* __restrict__ downs, const uint32_t* __restrict__ tedges,
-         uint32_t* __restrict__ size, uint32_t* __restrict__ isroot, int* __restrict__ bad,
-         int* __restrict__ roots) {
-    const long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= n) return;
-    const bool deg0 = first[v + 1] == first[v];
-    const bool rt = parent[v] == (uint32_t)v;
-    if (rt) {
-        atomicAdd(roots, 1);
-        if (downs[v] != 0) *bad = 1;
-        // a root heads a tour over its whole tree: 2 (size - 1) edges
-        size[v] = deg0 ? 1u : tedges[v] / 2 + 1;
-        if (!deg0 && tedges[v] == 0) *bad = 1;   // (a vertex that is no tour's minimum)
-    } else if (downs[v] != 1) {
-        *bad = 1;
+    if (v > n) return;
+    unsigned long long x = 0ull;
+    if (v < n && parent[v] == (uint32_t)v) {
+        const uint32_t len = rootL[v];
+        size[v] = len / 2 + 1;
+        x = ((unsigned long long)(len / 2 + 1) << 32) | len;
     }
-    isroot[v] = rt ? size[v] : 0u;
+    rinfo[v] = x;
 }
 
+// w(e) = size of the child below a down edge, 0 for the edge to the parent
 __global__ void __launch_bounds__(256)
 td_weights(const uint32_t* __restrict__ tg, const uint32_t* __restrict__ src,
            const uint32_t* __restrict__ parent, const uint32_t* __restrict__ size, long long ne,
-           unsigned long long* __restrict__ w) {
+           uint32_t* __restrict__ w) {
     const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= ne) return;
     const uint32_t c = tg[e];
-    w[e] = (parent[c] == src[e] && c != src[e]) ? size[c] : 0ull;
+    w[e] = parent[c] == src[e] ? size[c] : 0u;
 }
 
-// off(c) = 1 + sizes of the children after c in its parent's list (incl. prefix sums W)
+// off(c) = 1 + sizes of the children after c in its parent's list (W = inclusive sums;
+// differences mod 2^32 are exact, each below n)
 __global__ void __launch_bounds__(256)
 td_offsets(const uint32_t* __restrict__ first, const uint32_t* __restrict__ tg,
            const uint32_t* __restrict__ src, const uint32_t* __restrict__ parent,
-           const unsigned long long* __restrict__ W, long long ne, unsigned long long* __restrict__ acc) {
+           const uint32_t* __restrict__ W, long long ne, uint32_t* __restrict__ offc) {
     const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= ne) return;
     const uint32_t c = tg[e], v = src[e];
-    if (parent[c] != v || c == v) return;
-    const uint32_t end = first[v + 1] - 1;
-    acc[c] = 1ull + (W[end] - W[e]);
+    if (parent[c] != v) return;
+    offc[c] = 1u + (W[first[v + 1] - 1] - W[e]);
 }
 
+// the tours laid out one after another (trees in root-id order): +off(child) at the edge
+// down, -off(child) at the edge back up
 __global__ void __launch_bounds__(256)
-td_acc_init(long long n, const uint32_t* __restrict__ parent, unsigned long long* __restrict__ acc,
-            uint32_t* __restrict__ up) {
-    const long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= n) return;
-    up[v] = parent[v];
-    if (parent[v] == (uint32_t)v) acc[v] = 0ull;
-}
-
-__global__ void __launch_bounds__(256)
-td_acc_round(long long n, const uint32_t* __restrict__ u0, const unsigned long long* __restrict__ a0,
-             uint32_t* __restrict__ u1, unsigned long long* __restrict__ a1, int* __restrict__ more) {
-    const long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= n) return;
-    const uint32_t u = u0[v];
-    if (u == u0[u]) {   // u is a root: done (its acc is 0)
-        u1[v] = u;
-        a1[v] = a0[v];
-        return;
-    }
-    a1[v] = a0[v] + a0[u];
-    u1[v] = u0[u];
-    *more = 1;
+td_tour(const uint32_t* __restrict__ tg, const uint32_t* __restrict__ src,
+        const uint32_t* __restrict__ twin, const uint32_t* __restrict__ succ,
+        const unsigned long long* __restrict__ key, const unsigned long long* __restrict__ rbase,
+        const uint32_t* __restrict__ offc, long long ne, int* __restrict__ val) {
+    const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= ne) return;
+    const uint32_t pe = tour_pos(key, succ, (uint32_t)e), pt = tour_pos(key, succ, twin[e]);
+    const uint32_t r = src[(uint32_t)(key[e] >> 32)];
+    val[(uint32_t)rbase[r] + pe] = pe < pt ? (int)offc[tg[e]] : -(int)offc[src[e]];
 }
 
 __global__ void __launch_bounds__(256)
 td_output(long long n, const uint32_t* __restrict__ first, const uint32_t* __restrict__ parent,
-          const uint32_t* __restrict__ up, const unsigned long long* __restrict__ acc,
-          const unsigned long long* __restrict__ toff, uint32_t* __restrict__ vertices,
-          int* __restrict__ num_children, long long* __restrict__ parents) {
+          const uint32_t* __restrict__ posdown, const uint32_t* __restrict__ rootof,
+          const unsigned long long* __restrict__ rbase, const int* __restrict__ S,
+          uint32_t* __restrict__ vertices, int* __restrict__ num_children,
+          long long* __restrict__ parents) {
     const long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (v >= n) return;
     const bool rt = parent[v] == (uint32_t)v;
-    const uint32_t r = rt ? (uint32_t)v : up[v];
-    const long long pre = (long long)(toff[r] + acc[v]);
+    long long pre;
+    if (rt) {
+        pre = (long long)(rbase[v] >> 32);
+    } else {
+        const unsigned long long b = rbase[rootof[v]];
+        pre = (long long)(b >> 32) + S[(uint32_t)b + posdown[v]];
+    }
     const int deg = (int)(first[v + 1] - first[v]);
     vertices[pre] = (uint32_t)v;
     num_children[pre] = rt ? deg : deg - 1;
     if (parents) parents[pre] = rt ? -1ll : (long long)parent[v];
 }
 
-}  // namespace
+struct Arena {
+    char* base = nullptr;
+    size_t used = 0;
+    template <typename T>
+    T* take(size_t count) {
+        T* p = reinterpret_cast<T*>(base ? base + used : nullptr);
+        used += (count * sizeof(T) + 255) & ~size_t(255);
+        return p;
+    }
+};
 
-static int ceil_log2(long long x) {
+int ceil_log2(long long x) {
     int r = 0;
     while ((1ll << r) < x) ++r;
     return r;
 }
+
+}  // namespace
 
 extern "C" int pqh_tree_order_device(pqh_ctx_t* ctx, long long n, long long ne,
                                      const uint32_t* d_targets, const int* d_counts,
@@ -275,162 +261,132 @@ extern "C" int pqh_tree_order_device(pqh_ctx_t* ctx, long long n, long long ne,
     int rc = pqh_use_device(ctx);
     if (rc) return rc;
     hipStream_t st = ctx->stream;
-    DevBuf buf;
-    uint32_t* first = buf.get<uint32_t>(n + 1);
-    uint32_t* parent = buf.get<uint32_t>(n);
-    uint32_t* size = buf.get<uint32_t>(n);
-    uint32_t* downs = buf.get<uint32_t>(n);
-    uint32_t* tedges = buf.get<uint32_t>(n);
-    uint32_t* isroot = buf.get<uint32_t>(n + 1);
-    unsigned long long* toff = buf.get<unsigned long long>(n + 1);
-    unsigned long long* acc = buf.get<unsigned long long>(n);
-    unsigned long long* acc2 = buf.get<unsigned long long>(n);
-    uint32_t* up = buf.get<uint32_t>(n);
-    uint32_t* up2 = buf.get<uint32_t>(n);
-    int* cnt1 = buf.get<int>(n + 1);
-    // flags: [0] bad input or not a forest, [1] list ranking unfinished, [2] root count,
-    // [3] parent chains unfinished
-    int* flags = buf.get<int>(8);
-    if (!first || !parent || !size || !downs || !tedges || !isroot || !toff || !acc || !acc2 ||
-        !up || !up2 || !cnt1 || !flags)
-        return pqh_set_error(ctx, PQH_ERR_NOMEM, "tree order: %lld vertices", n);
+    const size_t en = ne > 0 ? (size_t)ne : 1;
+    // temporary storage of the library calls
+    size_t t_scan32 = 0, t_sort = 0, t_scanw = 0, t_scan64 = 0, t_scanv = 0;
+    PQH_HIP(ctx, rocprim::exclusive_scan(nullptr, t_scan32, (const int*)nullptr, (uint32_t*)nullptr,
+                                         0u, (size_t)n + 1, rocprim::plus<uint32_t>(), st));
+    PQH_HIP(ctx, rocprim::radix_sort_pairs(nullptr, t_sort, (unsigned long long*)nullptr,
+                                           (unsigned long long*)nullptr, (uint32_t*)nullptr,
+                                           (uint32_t*)nullptr, en, 0u, 64u, st));
+    PQH_HIP(ctx, rocprim::inclusive_scan(nullptr, t_scanw, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                         en, rocprim::plus<uint32_t>(), st));
+    PQH_HIP(ctx, rocprim::exclusive_scan(nullptr, t_scan64, (const unsigned long long*)nullptr,
+                                         (unsigned long long*)nullptr, 0ull, (size_t)n + 1,
+                                         rocprim::plus<unsigned long long>(), st));
+    PQH_HIP(ctx, rocprim::inclusive_scan(nullptr, t_scanv, (const int*)nullptr, (int*)nullptr, en,
+                                         rocprim::plus<int>(), st));
+    const size_t t_max = std::max({t_scan32, t_sort, t_scanw, t_scan64, t_scanv});
+    // one scratch block (the context's grow-only workspace), carved twice: once to size it
+    uint32_t *first, *parent, *size, *posdown, *rootof, *rootL, *offc;
+    int *cnt1, *flags;
+    unsigned long long *rinfo, *rbase;
+    uint32_t *src, *idx, *idx2, *twin, *succ;
+    unsigned long long *key, *key2;
+    void* temp;
+    auto carve = [&](Arena& a) {
+        first = a.take<uint32_t>(n + 1);
+        cnt1 = a.take<int>(n + 1);
+        parent = a.take<uint32_t>(n);
+        size = a.take<uint32_t>(n);
+        posdown = a.take<uint32_t>(n);
+        rootof = a.take<uint32_t>(n);
+        rootL = a.take<uint32_t>(n);
+        offc = a.take<uint32_t>(n);
+        rinfo = a.take<unsigned long long>(n + 1);
+        rbase = a.take<unsigned long long>(n + 1);
+        flags = a.take<int>(8);
+        src = a.take<uint32_t>(en);
+        idx = a.take<uint32_t>(en);
+        idx2 = a.take<uint32_t>(en);
+        twin = a.take<uint32_t>(en);
+        succ = a.take<uint32_t>(en);
+        key = a.take<unsigned long long>(en);
+        key2 = a.take<unsigned long long>(en);
+        temp = a.take<char>(t_max);
+    };
+    Arena sizing;
+    carve(sizing);
+    if ((rc = pqh_ensure_ws(ctx, sizing.used))) return rc;
+    Arena arena;
+    arena.base = static_cast<char*>(ctx->ws);
+    carve(arena);
+    // flags: [0] bad counts / not a forest, [2] isolated vertices, [3] tours
     int hb[8] = {0};
     auto read_flags = [&]() -> int {
         PQH_HIP(ctx, hipMemcpyAsync(hb, flags, sizeof(hb), hipMemcpyDeviceToHost, st));
         PQH_HIP(ctx, hipStreamSynchronize(st));
         return PQH_OK;
     };
-    // CSR offsets (restore_tree_edges_pointers, mst.c:52-61); counts must be >= 0 and sum to ne
+    // CSR offsets (restore_tree_edges_pointers, mst.c:52-61); counts >= 0 summing to ne
     PQH_HIP(ctx, hipMemsetAsync(flags, 0, sizeof(hb), st));
     PQH_HIP(ctx, hipMemcpyAsync(cnt1, d_counts, sizeof(int) * n, hipMemcpyDeviceToDevice, st));
     PQH_HIP(ctx, hipMemsetAsync(cnt1 + n, 0, sizeof(int), st));
-    {
-        size_t temp = 0;
-        PQH_HIP(ctx, rocprim::exclusive_scan(nullptr, temp, cnt1, first, 0u, (size_t)n + 1,
-                                             rocprim::plus<uint32_t>(), st));
-        void* t = buf.get<char>(temp);
-        if (!t) return pqh_set_error(ctx, PQH_ERR_NOMEM, "tree order: scan");
-        PQH_HIP(ctx, rocprim::exclusive_scan(t, temp, cnt1, first, 0u, (size_t)n + 1,
-                                             rocprim::plus<uint32_t>(), st));
-    }
-    hipLaunchKernelGGL(td_vertex_init, G1(n), 0, st, n, d_counts, parent, size, downs, tedges, flags);
+    size_t tb = t_max;
+    PQH_HIP(ctx, rocprim::exclusive_scan(temp, tb, cnt1, first, 0u, (size_t)n + 1,
+                                         rocprim::plus<uint32_t>(), st));
+    hipLaunchKernelGGL(td_vertex_init, G1(n), 0, st, n, d_counts, parent, rootL, flags);
     PQH_LAUNCH_CHECK(ctx);
     uint32_t total = 0;
     PQH_HIP(ctx, hipMemcpyAsync(&total, first + n, 4, hipMemcpyDeviceToHost, st));
     if ((rc = read_flags())) return rc;
     if (hb[0] || (long long)total != ne) return PQH_ERR_ARG;
+    const int isolated = hb[2];
+    unsigned long long* kf = key;
+    int* val = reinterpret_cast<int*>(idx2);   // (both free once the jumping is done)
+    uint32_t* W = idx;
     if (ne > 0) {
-        uint32_t* src = buf.get<uint32_t>(ne);
-        unsigned long long* key = buf.get<unsigned long long>(ne);
-        unsigned long long* key2 = buf.get<unsigned long long>(ne);
-        uint32_t* idx = buf.get<uint32_t>(ne);
-        uint32_t* idx2 = buf.get<uint32_t>(ne);
-        uint32_t* twin = buf.get<uint32_t>(ne);
-        uint32_t* succ = buf.get<uint32_t>(ne);
-        uint32_t* j2 = buf.get<uint32_t>(ne);
-        uint32_t* mn = buf.get<uint32_t>(ne);
-        uint32_t* mn2 = buf.get<uint32_t>(ne);
-        unsigned long long* W = buf.get<unsigned long long>(ne);
-        if (!src || !key || !key2 || !idx || !idx2 || !twin || !succ || !j2 || !mn || !mn2 || !W)
-            return pqh_set_error(ctx, PQH_ERR_NOMEM, "tree order: %lld edges", ne);
         hipLaunchKernelGGL(td_edges, G1(n), 0, st, first, n, d_targets, src, key, idx);
         PQH_LAUNCH_CHECK(ctx);
-        {
-            size_t temp = 0;
-            PQH_HIP(ctx, rocprim::radix_sort_pairs(nullptr, temp, key, key2, idx, idx2, (size_t)ne,
-                                                   0u, 64u, st));
-            void* t = buf.get<char>(temp);
-            if (!t) return PQH_ERR_NOMEM;
-            PQH_HIP(ctx, rocprim::radix_sort_pairs(t, temp, key, key2, idx, idx2, (size_t)ne, 0u, 64u, st));
-        }
+        tb = t_max;
+        PQH_HIP(ctx, rocprim::radix_sort_pairs(temp, tb, key, key2, idx, idx2, (size_t)ne, 0u, 64u, st));
         // twins; an out-of-range target never pairs (no edge leaves it), so every target is
         // a vertex once this passes
         hipLaunchKernelGGL(td_twins, G1(ne), 0, st, key2, idx2, ne, src, twin, flags);
         PQH_LAUNCH_CHECK(ctx);
         if ((rc = read_flags())) return rc;
         if (hb[0]) return PQH_ERR_UNSUPPORTED;   // not a simple graph of paired edges
-        hipLaunchKernelGGL(td_succ, G1(ne), 0, st, first, d_targets, twin, ne, succ, mn, src);
+        hipLaunchKernelGGL(td_succ, G1(ne), 0, st, first, d_targets, twin, ne, succ, idx, key);
         PQH_LAUNCH_CHECK(ctx);
-        // the minimum vertex of every tour (its tree's root): pointer jumping
-        PQH_HIP(ctx, hipMemcpyAsync(j2, succ, sizeof(uint32_t) * ne, hipMemcpyDeviceToDevice, st));
-        uint32_t *ja = j2, *ma = mn, *jb = idx, *mb = mn2;   // (idx is free now)
+        uint32_t *ja = idx, *jb = idx2;
+        unsigned long long *ka = key, *kb = key2;
         for (int round = 0, rounds = ceil_log2(ne); round < rounds; ++round) {
-            hipLaunchKernelGGL(td_min_round, G1(ne), 0, st, ne, ja, ma, jb, mb);
+            hipLaunchKernelGGL(td_jump, G1(ne), 0, st, ne, 1u << round, ja, ka, jb, kb);
             std::swap(ja, jb);
-            std::swap(ma, mb);
+            std::swap(ka, kb);
         }
         PQH_LAUNCH_CHECK(ctx);
-        uint32_t* root = ma;
-        // cut every tour before its root's first edge and rank the edges to the tour's end
-        uint32_t* rank = mb;
-        hipLaunchKernelGGL(td_cut, G1(ne), 0, st, first, twin, root, ne, succ, rank);
+        kf = ka;
+        hipLaunchKernelGGL(td_verify, G1(ne), 0, st, first, src, kf, ne, flags);
         PQH_LAUNCH_CHECK(ctx);
-        uint32_t *jr = succ, *jr2 = ja, *ra = rank, *rb = jb;   // (the jump buffers are free)
-        for (int round = 0, rounds = ceil_log2(ne) + 1; round < rounds; ++round) {
-            if (round + 1 == rounds) PQH_HIP(ctx, hipMemsetAsync(flags + 1, 0, sizeof(int), st));
-            hipLaunchKernelGGL(td_rank_round, G1(ne), 0, st, ne, jr, ra, jr2, rb, flags + 1);
-            std::swap(jr, jr2);
-            std::swap(ra, rb);
-        }
+        if ((rc = read_flags())) return rc;
+        // every component on a tour of its own, and a tree: E = V - 1 for each
+        if (hb[0] || ne / 2 != n - isolated - hb[3]) return PQH_ERR_UNSUPPORTED;
+        hipLaunchKernelGGL(td_parents, G1(ne), 0, st, d_targets, src, twin, succ, kf, ne, parent,
+                           size, posdown, rootof, rootL);
         PQH_LAUNCH_CHECK(ctx);
-        hipLaunchKernelGGL(td_parents, G1(ne), 0, st, first, d_targets, src, twin, ra, root, ne,
-                           parent, size, downs, tedges);
-        PQH_LAUNCH_CHECK(ctx);
-        hipLaunchKernelGGL(td_check, G1(n), 0, st, n, first, parent, downs, tedges, size, isroot,
-                           flags, flags + 2);
-        PQH_LAUNCH_CHECK(ctx);
+    }
+    hipLaunchKernelGGL(td_roots, G1(n + 1), 0, st, n, parent, rootL, size, rinfo);
+    PQH_LAUNCH_CHECK(ctx);
+    tb = t_max;
+    PQH_HIP(ctx, rocprim::exclusive_scan(temp, tb, rinfo, rbase, 0ull, (size_t)n + 1,
+                                         rocprim::plus<unsigned long long>(), st));
+    if (ne > 0) {
         hipLaunchKernelGGL(td_weights, G1(ne), 0, st, d_targets, src, parent, size, ne, W);
         PQH_LAUNCH_CHECK(ctx);
-        {   // W = inclusive prefix sums of the weights
-            size_t temp = 0;
-            PQH_HIP(ctx, rocprim::inclusive_scan(nullptr, temp, W, W, (size_t)ne,
-                                                 rocprim::plus<unsigned long long>(), st));
-            void* t = buf.get<char>(temp);
-            if (!t) return PQH_ERR_NOMEM;
-            PQH_HIP(ctx, rocprim::inclusive_scan(t, temp, W, W, (size_t)ne,
-                                                 rocprim::plus<unsigned long long>(), st));
-        }
-        hipLaunchKernelGGL(td_offsets, G1(ne), 0, st, first, d_targets, src, parent, W, ne, acc);
+        tb = t_max;
+        PQH_HIP(ctx, rocprim::inclusive_scan(temp, tb, W, W, (size_t)ne, rocprim::plus<uint32_t>(), st));
+        hipLaunchKernelGGL(td_offsets, G1(ne), 0, st, first, d_targets, src, parent, W, ne, offc);
         PQH_LAUNCH_CHECK(ctx);
-    } else {
-        hipLaunchKernelGGL(td_check, G1(n), 0, st, n, first, parent, downs, tedges, size, isroot,
-                           flags, flags + 2);
+        hipLaunchKernelGGL(td_tour, G1(ne), 0, st, d_targets, src, twin, succ, kf, rbase, offc, ne, val);
         PQH_LAUNCH_CHECK(ctx);
+        tb = t_max;
+        PQH_HIP(ctx, rocprim::inclusive_scan(temp, tb, val, val, (size_t)ne, rocprim::plus<int>(), st));
     }
-    if ((rc = read_flags())) return rc;
-    // a forest: every tour cut once, one edge down into each non-root, and exactly the
-    // non-roots' parent edges in the graph (then parent chains are checked acyclic below)
-    if (hb[0] || hb[1] || 2ll * (n - hb[2]) != ne) return PQH_ERR_UNSUPPORTED;
-    // tree offsets in root-id order; preorder by accumulating the offsets up to the root
-    PQH_HIP(ctx, hipMemsetAsync(isroot + n, 0, sizeof(uint32_t), st));
-    {
-        size_t temp = 0;
-        PQH_HIP(ctx, rocprim::exclusive_scan(nullptr, temp, isroot, toff, 0ull, (size_t)n + 1,
-                                             rocprim::plus<unsigned long long>(), st));
-        void* t = buf.get<char>(temp);
-        if (!t) return PQH_ERR_NOMEM;
-        PQH_HIP(ctx, rocprim::exclusive_scan(t, temp, isroot, toff, 0ull, (size_t)n + 1,
-                                             rocprim::plus<unsigned long long>(), st));
-    }
-    unsigned long long all = 0;
-    PQH_HIP(ctx, hipMemcpyAsync(&all, toff + n, 8, hipMemcpyDeviceToHost, st));
-    hipLaunchKernelGGL(td_acc_init, G1(n), 0, st, n, parent, acc, up);
+    hipLaunchKernelGGL(td_output, G1(n), 0, st, n, first, parent, posdown, rootof, rbase, val,
+                       d_vertices, d_num_children, d_parents);
     PQH_LAUNCH_CHECK(ctx);
-    unsigned long long *aa = acc, *ab = acc2;
-    uint32_t *ua = up, *ub = up2;
-    for (int round = 0, rounds = ceil_log2(n) + 1; round < rounds; ++round) {
-        if (round + 1 == rounds) PQH_HIP(ctx, hipMemsetAsync(flags + 3, 0, sizeof(int), st));
-        hipLaunchKernelGGL(td_acc_round, G1(n), 0, st, n, ua, aa, ub, ab, flags + 3);
-        std::swap(ua, ub);
-        std::swap(aa, ab);
-    }
-    PQH_LAUNCH_CHECK(ctx);
-    if ((rc = read_flags())) return rc;
-    if (hb[3] || (long long)all != n) return PQH_ERR_UNSUPPORTED;
-    hipLaunchKernelGGL(td_output, G1(n), 0, st, n, first, parent, ua, aa, toff, d_vertices,
-                       d_num_children, d_parents);
-    PQH_LAUNCH_CHECK(ctx);
-    PQH_HIP(ctx, hipStreamSynchronize(st));   // (before the scratch is freed)
-    *num_roots = hb[2];
+    PQH_HIP(ctx, hipStreamSynchronize(st));
+    *num_roots = isolated + hb[3];
     return PQH_OK;
 }
