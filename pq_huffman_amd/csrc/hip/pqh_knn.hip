@@ -338,41 +338,59 @@ __device__ __forceinline__ float raw_max(float a, float b) {
     return r;
 }
 
+// one lane per (row, 8-column group): a wave reads and writes contiguous rows.  ||x||^2 is
+// summed as 8-term sequential partials combined by a butterfly -- any order is within the
+// screen's bound E (|error| <= (d - 1) u sum x^2 for every summation order)
 template <int DP>
 __global__ void __launch_bounds__(256)
 knn_split(const float* __restrict__ x, long long n, long long ld, int d,
           kbf16x8* __restrict__ xhi, kbf16x8* __restrict__ xlo, float* __restrict__ norm,
           float* __restrict__ xpad) {
-    const long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= n) return;
-    const float* xr = x + v * ld;
+    constexpr int G = DP / 8;   // lanes per row (2..16, a power of two)
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long v = t / G;
+    const int g = (int)(t % G);
+    const bool in = v < n;
+    const float* xr = x + (in ? v : 0) * ld;
+    float f[8];
     float nn = 0.0f;
+    kbf16x8 hi, lo;
 #pragma unroll
-    for (int g = 0; g < DP / 8; ++g) {
-        kbf16x8 hi, lo;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int c = 8 * g + j;
-            const float f = c < d ? xr[c] : 0.0f;
-            xpad[v * DP + c] = f;
-            nn = __fadd_rn(nn, __fmul_rn(f, f));
-            const __bf16 h = (__bf16)f;
-            hi[j] = h;
-            lo[j] = (__bf16)(f - (float)h);
-        }
-        xhi[v * (DP / 8) + g] = hi;
-        xlo[v * (DP / 8) + g] = lo;
+    for (int j = 0; j < 8; ++j) {
+        const int c = 8 * g + j;
+        f[j] = in && c < d ? xr[c] : 0.0f;
+        nn = __fadd_rn(nn, __fmul_rn(f[j], f[j]));
+        const __bf16 h = (__bf16)f[j];
+        hi[j] = h;
+        lo[j] = (__bf16)(f[j] - (float)h);
     }
-    norm[v] = nn;
+#pragma unroll
+    for (int o = 1; o < G; o <<= 1) nn = __fadd_rn(nn, __shfl_xor(nn, o, G));
+    if (!in) return;
+    float4* xp = reinterpret_cast<float4*>(xpad + v * DP + 8 * g);
+    xp[0] = make_float4(f[0], f[1], f[2], f[3]);
+    xp[1] = make_float4(f[4], f[5], f[6], f[7]);
+    xhi[v * G + g] = hi;
+    xlo[v * G + g] = lo;
+    if (g == 0) norm[v] = nn;
 }
 
-// cmax[b] = the largest ||c||^2 of block b (non-negative floats order as their bits)
+// cmax[b] = the largest ||c||^2 of block b (non-negative floats order as their bits); the
+// pairs are sorted by block, so a wave reduces its runs and each run head does one atomic
 __global__ void __launch_bounds__(256)
 knn_block_cmax(const uint32_t* __restrict__ keys_sorted, const uint32_t* __restrict__ rows,
                long long np, const float* __restrict__ norm, uint32_t* __restrict__ cmax) {
     const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= np) return;
-    atomicMax(&cmax[keys_sorted[p]], __float_as_uint(norm[rows[p]]));
+    const bool in = p < np;
+    const uint32_t key = in ? keys_sorted[p] : 0xFFFFFFFFu;
+    uint32_t val = in ? __float_as_uint(norm[rows[p]]) : 0u;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t k2 = __shfl_down(key, o), v2 = __shfl_down(val, o);
+        if (k2 == key) val = v2 > val ? v2 : val;
+    }
+    const uint32_t kprev = __shfl_up(key, 1);
+    if (in && ((threadIdx.x & 63) == 0 || kprev != key)) atomicMax(&cmax[key], val);
 }
 
 template <int DP, int KMAX>
@@ -794,13 +812,20 @@ __global__ void __launch_bounds__(256)
 bv_edges(const uint2* __restrict__ pairs, long long ne, const uint32_t* __restrict__ comp,
          uint32_t* __restrict__ best, int* __restrict__ any) {
     const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= ne) return;
-    const uint2 pr = pairs[e];
-    const uint32_t ca = comp[pr.x], cb = comp[pr.y];
-    if (ca == cb) return;
-    atomicMin(&best[ca], (uint32_t)e);
-    atomicMin(&best[cb], (uint32_t)e);
-    *any = 1;   // (a plain store of the same value from every such lane)
+    bool cross = false;
+    if (e < ne) {
+        const uint2 pr = pairs[e];
+        const uint32_t ca = comp[pr.x], cb = comp[pr.y];
+        if (ca != cb) {
+            cross = true;
+            // (best only decreases: an edge above the current value cannot win; edges come
+            // in rank order, so most lanes skip the atomic)
+            if ((uint32_t)e < best[ca]) atomicMin(&best[ca], (uint32_t)e);
+            if ((uint32_t)e < best[cb]) atomicMin(&best[cb], (uint32_t)e);
+        }
+    }
+    const unsigned long long b = __ballot(cross);
+    if (b && (int)(threadIdx.x & 63) == __ffsll((unsigned long long)b) - 1) *any = 1;
 }
 
 __global__ void __launch_bounds__(256)
@@ -1118,7 +1143,7 @@ int pqh_knn_fast(pqh_ctx_t* ctx, const float* d_x, long long n, long long ld_x, 
         long long *dtb = nullptr, *dtq = nullptr;
         if ((rc = upload(tb, &dtb)) || (rc = upload(tq, &dtq))) return rc;
         PQH_HIP(ctx, hipMemsetAsync(cmx, 0, sizeof(uint32_t) * nblocks, ctx->stream));
-        const unsigned gn = (unsigned)((n + 255) / 256);
+        const unsigned gn = (unsigned)((n * (dp / 8) + 255) / 256);
 #define PQH_KNN_SPLIT(DP_)                                                                       \
     hipLaunchKernelGGL(knn_split<DP_>, dim3(gn), dim3(256), 0, ctx->stream, d_x, n, ld_x, d, xhi,   \
                        xlo, nrm, xpad)

@@ -77,7 +77,7 @@ def main():
             oc.mst(oi, od, a.take)
         c1 = time.perf_counter()
         out["cpu_baseline"] = {"kind": "port", "rows": a.cpu_sample, "ms": round((c1 - c0) * 1e3, 1),
-                               "threads": os.cpu_count(),
+                               "threads": int(os.environ.get("OMP_NUM_THREADS", os.cpu_count())),
                                "note": "oracle pipeline on the first rows (block sizes scale "
                                        "with n, so per-row cost grows with n)"}
     print(json.dumps(out), flush=True)
