@@ -140,6 +140,7 @@ int pqh_ctx_destroy(pqh_ctx_t* ctx) {
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->d_diag) (void)hipFree(ctx->d_diag);
     if (ctx->lb_state) (void)hipFree(ctx->lb_state);
+    if (ctx->sort_state) (void)hipFree(ctx->sort_state);
     if (ctx->d_sched) (void)hipFree(ctx->d_sched);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;

@@ -34,6 +34,11 @@ struct pqh_ctx {
     // other re-rank counter, d_diag[0] / d_diag[4]) for the next one -- no memset dispatches
     uint32_t* d_sched = nullptr;
     unsigned long long assign_launches = 0;
+    // radix sort look-back state: [sort_cap * 256] per-(block, digit) status words, ticket
+    unsigned long long* sort_state = nullptr;
+    long long sort_cap = 0;
+    unsigned sort_epoch = 0;
+    unsigned long long sort_ticket_base = 0;
     int rerank_slot = 0;              // d_diag slot of the last assignment's re-rank count
 };
 constexpr int kSchedMax = 64;      // subspaces with a work queue (more: static schedule)

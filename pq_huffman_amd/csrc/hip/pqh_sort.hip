@@ -7,12 +7,26 @@
 // compared as an unsigned big-endian byte string (verified by the oracle's
 // orc_sort_rows against reference-built fixtures).
 //
-// GPU: LSD over 8-byte key chunks, least significant chunk first.  Each pass builds the
-// chunk's big-endian u64 key for every row (through the current permutation) and runs a
-// stable radix sort of (key, row index) pairs (rocPRIM onesweep radix sort -- a library
-// primitive, like a plain GEMM); stability of every pass makes the composition a stable
-// sort by the whole key.  A final gather permutes the rows.  M = 8: one pass.
+// GPU, 2 <= M <= 8 (the CLI's M = 8 among them): a hand-written LSD radix sort, one pass
+// per key byte, least significant first (stable passes compose into a stable sort by the
+// whole key).  Each element carries its big-endian key and the row itself (both u64), so
+// the first pass reads the codes and the last writes the sorted rows in place -- no index
+// permutation and no gather.  One kernel counts the digits
+// of the first pass's byte (`sort_digits`); each pass (`sort_pass`) is one kernel over
+// 8,192-row tiles taken in ticket order: a wave ranks its rows among equal digits with 8
+// ballots per 64 rows (stable: rows are ranked in index order), counts the next pass's
+// digits, chains the workgroup's per-digit counts across tiles by a decoupled look-back (one
+// lane per digit, 16 tiles per round), and scatters every row to digit base + earlier tiles
+// + earlier waves + its rank.  Measured (1M x 8, alone): 0.25 ms, as the rocPRIM path
+// (PQH_SORT_IMPL=rocprim); a pass is ~29 us, of which the look-back ~11 and the scatter ~8
+// (PQH_SORT_DIAG timing runs).
+// Other M: LSD over 8-byte key chunks, each a stable rocPRIM radix sort of (key, row index)
+// pairs, then a gather of the rows.
 #include <rocprim/device/device_radix_sort.hpp>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
 
 #include "pqh_internal.h"
 
@@ -63,9 +77,318 @@ gather_rows(const uint8_t* __restrict__ src, long long n, int m, const uint32_t*
     }
 }
 
+// ---------------------------------------------------------------- 2 <= m <= 8
+#ifndef PQH_SORT_THREADS
+#define PQH_SORT_THREADS 512
+#endif
+#ifndef PQH_SORT_ITEMS
+#define PQH_SORT_ITEMS 16
+#endif
+#ifndef PQH_SORT_WIN
+#define PQH_SORT_WIN 16
+#endif
+constexpr int kSortThreads = PQH_SORT_THREADS;
+constexpr int kSortWaves = kSortThreads / 64;
+constexpr int kSortItems = PQH_SORT_ITEMS;                 // rows per lane
+constexpr int kSortTile = kSortThreads * kSortItems;       // rows per workgroup (8,192)
+constexpr int kLookWin = PQH_SORT_WIN;                     // tiles read per look-back round
+constexpr unsigned long long kStAgg = 1ull << 46, kStPre = 1ull << 47;
+constexpr unsigned long long kStVal = (1ull << 46) - 1;
+
+// row v's bytes (byte j at bits 8j) and its strncmp key: bytes after the first 0 cleared,
+// big-endian (byte 0 most significant); bytes >= m are absent (0)
+__device__ __forceinline__ void sort_row_key(const uint8_t* __restrict__ codes, long long v, int m,
+                                             unsigned long long& key, unsigned long long& row) {
+    unsigned long long r = 0;
+    if (m == 8) {
+        r = reinterpret_cast<const unsigned long long*>(codes)[v];
+    } else {
+        for (int j = 0; j < m; ++j) r |= (unsigned long long)codes[v * m + j] << (8 * j);
+    }
+    // the lowest zero byte is flagged exactly (only bytes above a zero can be false hits)
+    const unsigned long long zb = (r - 0x0101010101010101ull) & ~r & 0x8080808080808080ull;
+    const int z = zb ? (__ffsll((long long)zb) - 1) >> 3 : 8;
+    const unsigned long long keep = z >= 7 ? ~0ull : ((1ull << (8 * (z + 1))) - 1);
+    key = __builtin_bswap64(r & keep);
+    row = r;
+}
+
+__device__ __forceinline__ unsigned key_digit(unsigned long long key, int j) {
+    return (unsigned)(key >> (56 - 8 * j)) & 0xFFu;
+}
+
+// lanes (among `valid`) holding the same 8-bit value as this lane
+__device__ __forceinline__ unsigned long long match_digit(unsigned d, bool valid) {
+    unsigned long long match = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        const unsigned long long bal = __ballot((d >> b) & 1u);
+        match &= ((d >> b) & 1u) ? bal : ~bal;
+    }
+    return match;
+}
+
+__device__ __forceinline__ uint32_t lanes_below(unsigned long long match) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(match >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((uint32_t)match, 0u));
+}
+
+// digit counts of the first pass's byte position j (counts[256], zeroed by the caller); the
+// passes count the next pass's byte as they go
+__global__ void __launch_bounds__(256)
+sort_digits(const uint8_t* __restrict__ codes, long long n, int m, int j, uint32_t* __restrict__ counts) {
+    __shared__ uint32_t h[4][256];   // one histogram per wave
+    for (int i = threadIdx.x; i < 4 * 256; i += blockDim.x) (&h[0][0])[i] = 0;
+    __syncthreads();
+    const int wave = threadIdx.x >> 6;
+    constexpr int kPer = 8;   // rows per thread, loaded together
+    for (long long v0 = (long long)blockIdx.x * blockDim.x * kPer + threadIdx.x; v0 < n;
+         v0 += (long long)gridDim.x * blockDim.x * kPer) {
+        unsigned long long key[kPer];
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+            const long long v = v0 + (long long)i * blockDim.x;
+            unsigned long long row;
+            key[i] = 0;
+            if (v < n) sort_row_key(codes, v, m, key[i], row);
+        }
+#pragma unroll
+        for (int i = 0; i < kPer; ++i)
+            if (v0 + (long long)i * blockDim.x < n) atomicAdd(&h[wave][key_digit(key[i], j)], 1u);
+    }
+    __syncthreads();
+    const uint32_t c = h[0][threadIdx.x] + h[1][threadIdx.x] + h[2][threadIdx.x] + h[3][threadIdx.x];
+    if (c) atomicAdd(counts + threadIdx.x, c);
+}
+
+// the last pass's u64 rows -> m bytes per row (m < 8)
+__global__ void __launch_bounds__(256)
+sort_unpack(const unsigned long long* __restrict__ rows, long long n, int m, uint8_t* __restrict__ codes) {
+    const long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= n) return;
+    const unsigned long long r = rows[v];
+    for (int q = 0; q < m; ++q) codes[v * m + q] = (uint8_t)(r >> (8 * q));
+}
+
+__device__ __forceinline__ void st_store(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long st_load(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// one stable counting pass by byte position j (digit counts of j in `counts`, the next
+// pass's byte jn counted into `counts_next`).  FIRST: rows come from the codes; LAST: the
+// rows go to the codes (never both in one launch: m >= 2)
+template <bool FIRST, bool LAST>
+__global__ void __launch_bounds__(kSortThreads)
+sort_pass(const uint8_t* __restrict__ codes_in, uint8_t* __restrict__ codes_out, long long n, int m,
+          int j, const unsigned long long* __restrict__ kin, const unsigned long long* __restrict__ rin,
+          unsigned long long* __restrict__ kout, unsigned long long* __restrict__ rout,
+          const uint32_t* __restrict__ counts, uint32_t* __restrict__ counts_next,
+          unsigned long long* __restrict__ state, unsigned long long* __restrict__ ticket,
+          unsigned long long ticket_base, unsigned epoch, int diag) {
+    __shared__ uint32_t wcnt[kSortWaves][256];   // per-wave digit counters, then bases
+    __shared__ uint32_t hnext[LAST ? 1 : 2][256];   // the next pass's digit counts
+    __shared__ uint32_t wsum[4];
+    __shared__ long long s_tile;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid == 0) s_tile = (long long)(atomicAdd(ticket, 1ull) - ticket_base);
+    for (int i = tid; i < kSortWaves * 256; i += kSortThreads) (&wcnt[0][0])[i] = 0;
+    if (!LAST)
+        for (int i = tid; i < 2 * 256; i += kSortThreads) (&hnext[0][0])[i] = 0;
+    __syncthreads();
+    const long long tile = s_tile;
+    const long long base = tile * kSortTile + (long long)wave * 64 * kSortItems;
+    unsigned long long key[kSortItems], row[kSortItems];
+    uint32_t rank[kSortItems];
+    // every load first (the ranking below needs each key; issuing them all up front keeps
+    // the tile's reads in flight together)
+#pragma unroll
+    for (int it = 0; it < kSortItems; ++it) {
+        const long long v = base + it * 64 + lane;
+        key[it] = 0;
+        row[it] = 0;
+        if (v < n) {
+            if (FIRST) {
+                sort_row_key(codes_in, v, m, key[it], row[it]);
+            } else {
+                key[it] = kin[v];
+                row[it] = rin[v];
+            }
+        }
+    }
+#pragma unroll
+    for (int it = 0; it < kSortItems; ++it) {
+        const bool valid = base + it * 64 + lane < n;
+        if (!LAST && valid) atomicAdd(&hnext[wave & 1][key_digit(key[it], j - 1)], 1u);
+        // lanes with this lane's digit, among the valid ones, in lane order
+        const unsigned d = key_digit(key[it], j);
+        const unsigned long long match = match_digit(d, valid);
+        const uint32_t below = lanes_below(match);
+        // every lane reads the counter, then the group's lowest lane adds the group's size
+        // (one wave: its LDS operations complete in order)
+        const uint32_t old = wcnt[wave][d];
+        if (valid && below == 0) wcnt[wave][d] = old + (uint32_t)__popcll(match);
+        rank[it] = old + below;
+    }
+    __syncthreads();
+    // one lane per digit (the first 4 waves): wave prefixes, the tile's count, the look-back
+    // over earlier tiles (kLookWin of them per round), the digit base
+    const unsigned dg = (unsigned)tid & 255u;
+    uint32_t c[kSortWaves], tot = 0;
+    unsigned long long excl = 0;
+    uint32_t x = 0;
+    if (tid < 256) {
+#pragma unroll
+        for (int w = 0; w < kSortWaves; ++w) {
+            c[w] = wcnt[w][dg];
+            tot += c[w];
+        }
+        if (!LAST) {
+            const uint32_t hn = hnext[0][dg] + hnext[1][dg];
+            if (hn) atomicAdd(counts_next + dg, hn);
+        }
+        unsigned long long* my = state + tile * 256 + dg;
+        if (diag & 1) {
+        } else if (tile == 0) {
+            st_store(my, ((unsigned long long)epoch << 48) | kStPre | tot);
+        } else {
+            st_store(my, ((unsigned long long)epoch << 48) | kStAgg | tot);
+            long long p = tile - 1;
+            for (;;) {
+                unsigned long long sw[kLookWin];
+#pragma unroll
+                for (int i = 0; i < kLookWin; ++i)
+                    sw[i] = p - i >= 0 ? st_load(state + (p - i) * 256 + dg)
+                                       : (((unsigned long long)epoch << 48) | kStPre);
+                int i = 0;
+                bool done = false;
+                for (; i < kLookWin; ++i) {
+                    const unsigned long long st = sw[i];
+                    if ((unsigned)(st >> 48) != epoch || !(st & (kStAgg | kStPre))) break;
+                    excl += st & kStVal;
+                    if (st & kStPre) {
+                        done = true;
+                        break;
+                    }
+                }
+                if (done) break;
+                p -= i;
+                if (i < kLookWin) __builtin_amdgcn_s_sleep(1);
+            }
+            st_store(my, ((unsigned long long)epoch << 48) | kStPre | (excl + tot));
+        }
+        x = counts[dg];
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wsum[wave] = x;
+    }
+    __syncthreads();   // (also: every wave has read its counters)
+    if (tid < 256) {
+        uint32_t gb = x - counts[dg];
+        for (int w = 0; w < wave; ++w) gb += wsum[w];
+        uint32_t run = gb + (uint32_t)excl;
+#pragma unroll
+        for (int w = 0; w < kSortWaves; ++w) {
+            wcnt[w][dg] = run;
+            run += c[w];
+        }
+    }
+    __syncthreads();
+    if (diag & 2) {   // (diagnostic: no scatter)
+        if (rank[0] == 0xFFFFFFFFu) kout[0] = key[0] + key[kSortItems - 1];
+        return;
+    }
+#pragma unroll
+    for (int it = 0; it < kSortItems; ++it) {
+        const long long v = base + it * 64 + lane;
+        if (v >= n) continue;
+        long long dst = (long long)wcnt[wave][key_digit(key[it], j)] + rank[it];
+        if (diag) dst = dst < n ? dst : n - 1;   // (diagnostic runs: bases are wrong, stay in range)
+        if (LAST && m == 8) {
+            reinterpret_cast<unsigned long long*>(codes_out)[dst] = row[it];
+        } else if (LAST) {   // (m < 8: the rows are unpacked by sort_unpack)
+            rout[dst] = row[it];
+        } else {
+            kout[dst] = key[it];
+            rout[dst] = row[it];
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" {
+
+static int sort_rows_radix(pqh_ctx_t* ctx, uint8_t* codes, long long n, int m) {
+    const long long tiles = (n + kSortTile - 1) / kSortTile;
+    if (tiles > ctx->sort_cap) {
+        PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));   // no launch may still use it
+        if (ctx->sort_state) (void)hipFree(ctx->sort_state);
+        ctx->sort_state = nullptr;
+        const long long cap = tiles + tiles / 4 + 16;
+        PQH_HIP(ctx, hipMalloc(&ctx->sort_state, (size_t)(cap * 256 + 1) * 8));
+        PQH_HIP(ctx, hipMemsetAsync(ctx->sort_state, 0, (size_t)(cap * 256 + 1) * 8, ctx->stream));
+        ctx->sort_cap = cap;
+        ctx->sort_epoch = 0;
+        ctx->sort_ticket_base = 0;
+    }
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t eb = al((size_t)n * 8);
+    int rc = pqh_ensure_ws(ctx, 4 * eb + al(8 * 256 * 4));
+    if (rc) return rc;
+    char* w = static_cast<char*>(ctx->ws);
+    unsigned long long* k0 = reinterpret_cast<unsigned long long*>(w);
+    unsigned long long* r0 = reinterpret_cast<unsigned long long*>(w + eb);
+    unsigned long long* k1 = reinterpret_cast<unsigned long long*>(w + 2 * eb);
+    unsigned long long* r1 = reinterpret_cast<unsigned long long*>(w + 3 * eb);
+    uint32_t* dcnt = reinterpret_cast<uint32_t*>(w + 4 * eb);
+    PQH_HIP(ctx, hipMemsetAsync(dcnt, 0, (size_t)m * 256 * 4, ctx->stream));
+    const unsigned dgrid = (unsigned)std::min<long long>((n + 2047) / 2048, 1024);
+    hipLaunchKernelGGL(sort_digits, dim3(dgrid), dim3(256), 0, ctx->stream, codes, n, m, m - 1,
+                       dcnt + (m - 1) * 256);
+    PQH_LAUNCH_CHECK(ctx);
+    unsigned long long* ticket = ctx->sort_state + ctx->sort_cap * 256;
+    static const int diag = [] {   // PQH_SORT_DIAG (timing diagnostics only: wrong results)
+        const char* e = std::getenv("PQH_SORT_DIAG");
+        return e ? std::atoi(e) : 0;
+    }();
+    for (int p = 0; p < m; ++p) {   // byte m - 1 first
+        const int j = m - 1 - p;
+        if (++ctx->sort_epoch >= 0xFFFF) {   // wrap: clear the tags
+            PQH_HIP(ctx, hipMemsetAsync(ctx->sort_state, 0, (size_t)ctx->sort_cap * 256 * 8, ctx->stream));
+            ctx->sort_epoch = 1;
+        }
+        const bool first = p == 0, last = p == m - 1;
+        // (first: codes -> k0/r0; middle: ping-pong; last: -> codes)
+        const unsigned long long* kin = (p & 1) ? k0 : k1;
+        const unsigned long long* rin = (p & 1) ? r0 : r1;
+        unsigned long long* kout = (p & 1) ? k1 : k0;
+        unsigned long long* rout = (p & 1) ? r1 : r0;
+#define PQH_SORT_PASS(F, L)                                                                       \
+    hipLaunchKernelGGL((sort_pass<F, L>), dim3((unsigned)tiles), dim3(kSortThreads), 0, ctx->stream, \
+                       codes, codes, n, m, j, kin, rin, kout, rout, dcnt + j * 256,                \
+                       dcnt + (j > 0 ? j - 1 : 0) * 256, ctx->sort_state, ticket,                  \
+                       ctx->sort_ticket_base, ctx->sort_epoch, diag)
+        if (first) PQH_SORT_PASS(true, false);
+        else if (last) PQH_SORT_PASS(false, true);
+        else PQH_SORT_PASS(false, false);
+#undef PQH_SORT_PASS
+        PQH_LAUNCH_CHECK(ctx);
+        ctx->sort_ticket_base += (unsigned long long)tiles;
+        if (last && m < 8) {
+            hipLaunchKernelGGL(sort_unpack, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                               ctx->stream, rout, n, m, codes);
+            PQH_LAUNCH_CHECK(ctx);
+        }
+    }
+    return PQH_OK;
+}
+
 
 int pqh_sort_rows(pqh_ctx_t* ctx, void* d_codes, long long n, int m, void* d_tmp) {
     if (!ctx || n < 0 || m <= 0 || (n > 0 && !d_codes)) return PQH_ERR_ARG;
@@ -73,6 +396,13 @@ int pqh_sort_rows(pqh_ctx_t* ctx, void* d_codes, long long n, int m, void* d_tmp
     int rc = pqh_use_device(ctx);
     if (rc) return rc;
     if (n <= 1) return PQH_OK;
+    static const bool force_lib = [] {
+        const char* e = std::getenv("PQH_SORT_IMPL");
+        return e && !std::strcmp(e, "rocprim");
+    }();
+    if (m >= 2 && m <= 8 && n < (1ll << 31) && !force_lib &&
+        (m != 8 || (reinterpret_cast<uintptr_t>(d_codes) & 7) == 0))
+        return sort_rows_radix(ctx, static_cast<uint8_t*>(d_codes), n, m);
     // workspace: keys in/out (u64), index in/out (u32), rocPRIM temp, row buffer if no d_tmp
     size_t temp = 0;
     if (rocprim::radix_sort_pairs(nullptr, temp, (unsigned long long*)nullptr,

@@ -320,14 +320,40 @@ def _zero_heavy_rows(n, m, seed):
 
 
 @pytest.mark.parametrize("n,m", [(1, 8), (2, 8), (1000, 8), (1000, 16), (777, 3), (513, 12),
-                                 (300, 1), (2000, 24)])
+                                 (300, 1), (2000, 24), (2048, 8), (2049, 8), (4097, 2),
+                                 (50_000, 8), (30_001, 7), (100_000, 4), (300_000, 8)])
 def test_gpu_sort_rows_vs_oracle(gpu, oracle, n, m):
+    """2 <= m <= 8 runs the hand-written radix passes (tiles of 2,048 rows chained by the
+    look-back: the sizes straddle tile edges), other m the rocPRIM chunk sort."""
     torch, codec, ctx = gpu
     for seed in (1, 2):
         a = _zero_heavy_rows(n, m, seed)
         d = torch.from_numpy(a.copy()).cuda()
         codec.sort_rows(ctx, d)
         assert np.array_equal(d.cpu().numpy(), oracle.sort_rows(a))
+
+
+def test_gpu_sort_rows_radix_vs_rocprim(gpu):
+    """The radix passes and the rocPRIM path (PQH_SORT_IMPL=rocprim) give the same rows, on
+    skewed full-alphabet codes and on heavy ties spread over many tiles."""
+    import sys
+    import tempfile
+    torch, codec, ctx = gpu
+    a = datagen.skewed_codes(200_000, 8, 256, seed=11)
+    a[::3] = a[0]                                  # one row repeated across every tile
+    d = torch.from_numpy(a.copy()).cuda()
+    codec.sort_rows(ctx, d)
+    code = ("import numpy as np, torch, sys; sys.path.insert(0, %r); "
+            "from pq_huffman_amd import codec; c = codec.Context(0); "
+            "a = np.load(sys.argv[1]); d = torch.from_numpy(a).cuda(); codec.sort_rows(c, d); "
+            "np.save(sys.argv[1], d.cpu().numpy())") % ROOT
+    with tempfile.TemporaryDirectory() as td:
+        f = os.path.join(td, "a.npy")
+        np.save(f, a)
+        r = subprocess.run([sys.executable, "-c", code, f], capture_output=True, text=True,
+                           env=dict(os.environ, PQH_SORT_IMPL="rocprim"), timeout=300)
+        assert r.returncode == 0, r.stderr
+        np.testing.assert_array_equal(d.cpu().numpy(), np.load(f))
 
 
 def test_gpu_sort_full_size_vs_oracle(gpu, oracle):
