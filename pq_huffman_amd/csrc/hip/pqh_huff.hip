@@ -34,21 +34,29 @@ __device__ __forceinline__ unsigned ld_code(const CodeT* c, long long i) { retur
 // the chunk's private partial -- plain coalesced stores, no global atomics.  split = 2
 // halves the LDS (64 KB at K = 256), so a workgroup fits on a CU beside the assignment's and
 // the code-table builds' workgroups; every split re-reads the chunk's rows (L2 hits).
+// The grid is 1-D and XCD-aware: workgroup L runs on XCD L % 8, and the m * split workgroups
+// of a chunk all get L % 8 = chunk % 8, so the chunk's rows are fetched from HBM into one
+// XCD's L2 once instead of once per XCD.
 template <typename CodeT>
 __global__ void __launch_bounds__(1024)
 hist_ctx(const CodeT* __restrict__ codes, long long n, int m_total, int k,
-         const CodeT* __restrict__ prev_row, uint32_t* __restrict__ partial, int split) {
+         const CodeT* __restrict__ prev_row, uint32_t* __restrict__ partial, int split, int chunks) {
     extern __shared__ uint32_t pairs[];   // (k / split) * k u16 counters packed two per word
-    const int m = blockIdx.y;
+    const int per_chunk = m_total * split;
+    const int q = (int)(blockIdx.x >> 3);
+    const int chunk = (q / per_chunk) * 8 + (int)(blockIdx.x & 7);
+    if (chunk >= chunks) return;   // (uniform: the XCD's list is shorter)
+    const int m = (q % per_chunk) / split;
+    const int zs = q % split;
     const int prows = k / split;
-    const unsigned plo = (unsigned)(blockIdx.z * prows);
+    const unsigned plo = (unsigned)(zs * prows);
     const int all_words = (k * k + 1) / 2;
     const int words = split == 1 ? all_words : prows * k / 2;
     for (int w = threadIdx.x; w < words; w += blockDim.x) pairs[w] = 0;
     constexpr int kRun = kHistChunk / 1024;   // consecutive vectors per thread
     constexpr int kSub = 20;                  // ... taken kSub at a time (registers)
     static_assert(kRun % kSub == 0 && kSub % 2 == 0, "whole 16-byte row pairs per group");
-    const long long v0 = (long long)blockIdx.x * kHistChunk + (long long)threadIdx.x * kRun;
+    const long long v0 = (long long)chunk * kHistChunk + (long long)threadIdx.x * kRun;
     auto count = [&](unsigned prev, unsigned cur) {
         if (prev >= (unsigned)k || cur >= (unsigned)k) return;   // absent / out of alphabet
         const unsigned pr = prev - plo;
@@ -87,8 +95,7 @@ hist_ctx(const CodeT* __restrict__ codes, long long n, int m_total, int k,
         }
     }
     __syncthreads();
-    uint32_t* out = partial + ((long long)m * gridDim.x + blockIdx.x) * all_words +
-                    (long long)blockIdx.z * words;
+    uint32_t* out = partial + ((long long)m * chunks + chunk) * all_words + (long long)zs * words;
     if ((words & 3) == 0) {
         const uint4* src = reinterpret_cast<const uint4*>(pairs);
         uint4* dst = reinterpret_cast<uint4*>(out);
@@ -553,9 +560,10 @@ static int histogram_impl(pqh_ctx_t* ctx, const void* d_codes, long long n, int 
         uint32_t* partial = static_cast<uint32_t*>(ctx->ws);
         PQH_HIP(ctx, hipFuncSetAttribute((const void*)hist_ctx<uint8_t>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL(hist_ctx<uint8_t>, dim3(chunks, m, split), dim3(1024), lds,
-                           ctx->stream, static_cast<const uint8_t*>(d_codes), n, m, k,
-                           static_cast<const uint8_t*>(d_prev_row), partial, split);
+        const unsigned grid = 8u * ((chunks + 7u) / 8u) * (unsigned)(m * split);
+        hipLaunchKernelGGL(hist_ctx<uint8_t>, dim3(grid), dim3(1024), lds, ctx->stream,
+                           static_cast<const uint8_t*>(d_codes), n, m, k,
+                           static_cast<const uint8_t*>(d_prev_row), partial, split, (int)chunks);
         PQH_LAUNCH_CHECK(ctx);
         hipLaunchKernelGGL(hist_ctx_reduce, dim3((unsigned)((words + 255) / 256), m), dim3(256), 0,
                            ctx->stream, partial, (int)chunks, words, (long long)k * k, d_counts,
