@@ -717,6 +717,190 @@ huff_trees(const uint32_t* __restrict__ counts, int k, long long trees,
     }
 }
 
+// ---- one wavefront per large tree (K > 256), the heap in LDS, each sift read in parallel --
+// The per-lane builds serialise every heap level on an LDS round trip (a K = 4,096 tree:
+// ~3 ms of its 4,095 merges' pops).  Here the wave owns one tree and reads a whole stretch of
+// a sift at once:
+//   push  lane l reads ancestor l + 1 of the new slot (<= 12 levels: one round trip); the
+//         ancestors the entry passes are exactly the lanes whose weight is strictly above
+//         it (monotone along the path, so a ballot's popcount), and they move down one
+//         level in one write;
+//   pop   lane q (subtree position q = 1..63 below the current slot, 6 levels) reads its
+//         node's two children (adjacent slots, one ds_read2) and picks the reference's
+//         candidate (left unless the right is strictly lighter); a scalar chase down the
+//         lanes' choices finds how far the last entry sinks, and the lanes on the path move
+//         their candidates up in one write.
+// Keys as SentinelHeap's, u64: weight << 16 | tie << 15 | node; slots past the heap hold all
+// ones.  Same results as huff_trees / huff_trees_small (tie rules of huffman_encode.c:33-76).
+struct ParHeap {
+    using Key = unsigned long long;
+    static constexpr Key kTie = 1ull << 15, kLow = (1ull << 16) - 1, kMaxKey = ~0ull;
+    Key* h;     // slots [0, cap]; slot cap and every slot >= size hold kMaxKey
+    int cap;
+    int size;
+    __device__ __forceinline__ void push(Key e, int lane) {
+        const int i = size++;
+        const int anc = ((i + 1) >> (lane + 1)) - 1;   // lane l: ancestor l + 1 (-1: none)
+        const bool va = lane < 16 && anc >= 0;
+        const Key av = va ? h[anc] : 0ull;
+        const bool mv = va && e < (av & ~kLow);       // strictly lighter than that ancestor
+        const int s = __popcll(__ballot(mv));
+        if (lane < s) h[((i + 1) >> lane) - 1] = av;   // ancestor l + 1 moves down to slot l
+        if (lane == 0) h[((i + 1) >> s) - 1] = e;
+    }
+    __device__ __forceinline__ Key pop(int lane) {
+        --size;
+        // this lane's subtree position q = lane (1..63: six levels below the current slot)
+        const int q = lane;
+        const int d = q ? 31 - __clz(q) : 0;
+        int i = 0;
+        Key top = 0, last = 0, lw = 0;
+        for (int round = 0;; ++round) {
+            const int g = ((i + 1) << d) + (q - (1 << d)) - 1;
+            const int c0 = 2 * g + 1;
+            if (round == 0) {   // (the first stretch's reads go out with these two)
+                top = h[0];
+                last = h[size];
+            }
+            Key kl = kMaxKey, kr = kMaxKey;
+            if (q >= 1 && c0 < cap) {
+                kl = h[c0];
+                kr = h[c0 + 1];
+            }
+            asm volatile("" : "+v"(kl), "+v"(kr), "+v"(top), "+v"(last));   // one wait for all
+            if (round == 0) {
+                lw = last & ~kLow;
+                if (lane == 0) h[size] = kMaxKey;   // the vacated slot becomes a sentinel
+            }
+            if (c0 == size) kl = kMaxKey;           // (read before the sentinel landed)
+            if (c0 + 1 == size) kr = kMaxKey;
+            const Key kc = kl < (kr | kTie) ? kl : (kr | kTie);
+            const bool mv = q >= 1 && kc < lw;
+            const int ch = 2 * q + ((kc & kTie) ? 1 : 0);
+            const int packed = mv ? (256 | ch) : 0;
+            // reached: every ancestor of q in the stretch moved toward q (independent
+            // shuffles instead of a serial chase)
+            int pa[6];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) pa[j] = __shfl(packed, q >> (j + 1));
+            asm volatile("" : "+v"(pa[0]), "+v"(pa[1]), "+v"(pa[2]), "+v"(pa[3]), "+v"(pa[4]),
+                         "+v"(pa[5]));   // all six shuffles in flight together
+            bool reached = q >= 1;
+#pragma unroll
+            for (int j = 0; j < 6; ++j) reached &= (j >= d) | (pa[j] == (256 | (q >> j)));
+            if (reached && mv) h[g] = kc & ~kTie;   // the candidates move up one level
+            const unsigned long long stop = __ballot(reached && !mv);
+            if (stop) {                              // `last` settles where the path ends
+                if (reached && !mv) h[g] = last;
+                break;
+            }
+            // the path left the stretch below its depth-5 position: continue there
+            const unsigned long long deep = __ballot(reached && mv && q >= 32);
+            const int pq = __builtin_amdgcn_readlane(packed, __ffsll((long long)deep) - 1) & 255;
+            i = ((i + 1) << 6) + (pq - 64) - 1;
+        }
+        return top;
+    }
+};
+
+template <int KMAX>
+__global__ void __launch_bounds__(64)
+huff_trees_par(const uint32_t* __restrict__ counts, int k, long long trees,
+               unsigned long long* __restrict__ enc, uint32_t* __restrict__ err) {
+    using Key = ParHeap::Key;
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    Key* heap = reinterpret_cast<Key*>(lds);                              // [KMAX + 1]
+    unsigned long long* ncode = heap + (KMAX + 1);                       // [2 KMAX]
+    uint32_t* kid = reinterpret_cast<uint32_t*>(ncode + 2 * KMAX);       // [KMAX]
+    uint16_t* lsym = reinterpret_cast<uint16_t*>(kid + KMAX);            // [KMAX]
+    uint16_t* par = lsym + KMAX;                                         // [2 KMAX]
+    const int lane = threadIdx.x;
+    const long long tree = blockIdx.x;
+    if (tree >= trees) return;
+    const uint32_t* cnt = counts + tree * k;
+    unsigned long long* out = enc + tree * k;
+    const bool stamp = tree == 0 && lane == 0;
+    if (stamp) g_tree_stamps[0] = __builtin_amdgcn_s_memtime();
+    for (int s = lane; s <= KMAX; s += 64) heap[s] = ParHeap::kMaxKey;
+    // nonzero symbols in symbol order (their counts parked in ncode); no code for the rest
+    int nz = 0;
+    for (int s0 = 0; s0 < k; s0 += 64) {
+        const int s = s0 + lane;
+        const uint32_t c = s < k ? cnt[s] : 0u;
+        const unsigned long long b = __ballot(c != 0u);
+        if (c) {
+            const int pos = nz + (int)__builtin_amdgcn_mbcnt_hi(
+                                     (uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+            lsym[pos] = (uint16_t)s;
+            ncode[pos] = c;
+        } else if (s < k) {
+            out[s] = 0ull;
+        }
+        nz += __popcll(b);
+    }
+    if (nz == 0) return;
+    ParHeap hp{heap, KMAX, 0};
+    constexpr Key kNode = ParHeap::kTie - 1;
+    if (stamp) g_tree_stamps[1] = __builtin_amdgcn_s_memtime();
+    for (int j = 0; j < nz; ++j) hp.push((ncode[j] << 16) | (Key)j, lane);
+    if (stamp) g_tree_stamps[2] = __builtin_amdgcn_s_memtime();
+    int next = nz;
+    if (hp.size == 1) {   // lone symbol: code "0" (huffman_encode.c:168-177)
+        const Key e = hp.pop(lane);
+        if (lane == 0) kid[0] = (uint32_t)(e & kNode) | 0xFFFF0000u;
+        hp.push((e & ~ParHeap::kLow) | (Key)next, lane);
+        ++next;
+    }
+    while (hp.size > 1) {
+        const Key a = hp.pop(lane);
+        const Key b = hp.pop(lane);
+        if (lane == 0) kid[next - nz] = (uint32_t)(a & kNode) | ((uint32_t)(b & kNode) << 16);
+        hp.push(((a & ~ParHeap::kLow) + (b & ~ParHeap::kLow)) | (Key)next, lane);
+        ++next;
+    }
+    if (stamp) g_tree_stamps[3] = __builtin_amdgcn_s_memtime();
+    // codes (huffman_encode.c:100-132: child 0 appends bit 0) by pointer jumping over the
+    // parent links: e[v] = len << 56 | the path's bits from par[v] down to v (len saturates
+    // at 255; any len > 56 is reported, so a truncated code never reaches a table)
+    for (int q = nz + lane; q < next; q += 64) {
+        const uint32_t kk = kid[q - nz];
+        par[kk & 0xFFFFu] = (uint16_t)q;
+        ncode[kk & 0xFFFFu] = 1ull << 56;
+        if ((kk >> 16) != 0xFFFFu) {
+            par[kk >> 16] = (uint16_t)q;
+            ncode[kk >> 16] = (1ull << 56) | 1ull;
+        }
+    }
+    if (lane == 0) {
+        par[next - 1] = (uint16_t)(next - 1);   // the root: its own parent, empty path
+        ncode[next - 1] = 0;
+    }
+    for (int span = 1; span < next; span <<= 1) {   // (in place: a node's link and path
+        for (int v = lane; v < next; v += 64) {      //  are read before either is rewritten)
+            const int u = par[v];
+            const unsigned long long ev = ncode[v], eu = ncode[u];
+            const int pu = par[u];
+            const unsigned lv = (unsigned)(ev >> 56), lu = (unsigned)(eu >> 56);
+            const unsigned long long hi = lv < 56 ? ((eu & kCodeMask) << lv) : 0ull;
+            const unsigned long long len = min((unsigned long long)(lv + lu), 255ull);
+            ncode[v] = (len << 56) | ((hi | (ev & kCodeMask)) & kCodeMask);
+            par[v] = (uint16_t)pu;
+        }
+    }
+    if (stamp) {
+        g_tree_stamps[4] = __builtin_amdgcn_s_memtime();
+        g_tree_stamps[5] = (unsigned long long)nz;
+        g_tree_stamps[6] = (unsigned long long)next;
+    }
+    bool too_long = false;
+    for (int j = lane; j < nz; j += 64) {
+        const unsigned long long e = ncode[j];
+        if ((e >> 56) > (unsigned long long)kMaxCodeLen) too_long = true;
+        else out[lsym[j]] = e;
+    }
+    if (too_long) atomicOr(err, 1u);
+}
+
 // Two-level decode tables, one block per alphabet.
 //   L1: 2^W1 u16 entries per alphabet, W1 fixed for the table set (9 in context mode, 11
 //       otherwise) so a lookup never waits for per-alphabet metadata:
@@ -1319,7 +1503,14 @@ int pqh_tables_build(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts) 
            : tpw_env == 32 ? launch(std::integral_constant<int, 32>{})
                            : launch(std::integral_constant<int, 16>{});
         if (rc) return rc;
-    } else {
+    } else if (!(impl && std::strcmp(impl, "lane") == 0)) {
+        // K > 256: one wavefront per tree, sifts read in parallel (huff_trees_par)
+        const size_t lds = (size_t)(4096 + 1) * 8 + (size_t)4096 * (16 + 4 + 2 + 4);
+        PQH_HIP(ctx, hipFuncSetAttribute((const void*)huff_trees_par<4096>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL((huff_trees_par<4096>), dim3((unsigned)trees), dim3(64), lds, ctx->stream,
+                           d_counts, t->k, trees, t->d_enc, t->d_err);
+    } else {   // (PQH_TREE_IMPL=lane: one lane per tree through LDS)
         constexpr int TPW = 1;
         const size_t lds = (size_t)4096 * TPW * (16 + 4 + 4 + 2);
         PQH_HIP(ctx, hipFuncSetAttribute((const void*)huff_trees<4096, TPW>,

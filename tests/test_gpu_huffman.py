@@ -260,6 +260,35 @@ def test_gpu_tree_builder_heavy_and_rebuilt(gpu, ctxm, impl, monkeypatch):
         assert tabs.codebooks().file_bytes() == host.file_bytes()
 
 
+@pytest.mark.parametrize("impl", ["lane", "par"])
+def test_gpu_tree_builder_k4096_vs_host(gpu, impl, monkeypatch):
+    """K = 4096 trees (huff_trees_par: one wave per tree, sifts read in parallel; and the
+    one-lane build, PQH_TREE_IMPL=lane): tie-heavy, heavy (64-bit weights), skewed,
+    one-symbol and empty parts, then a sparser rebuild -- GPU tables == host codebooks."""
+    monkeypatch.setenv("PQH_TREE_IMPL", impl)
+    torch, codec, ctx = gpu
+    rng = np.random.default_rng(41)
+    k = 4096
+    a = rng.integers(0, 4, (8, k)).astype(np.int64)
+    a[0] *= rng.integers(0, 50, k)                            # ties among small counts
+    a[1] = rng.integers(0, 3, k) * 3_000_000 + (np.arange(k) % 7 == 0) * 5   # heavy + light
+    a[2] = 0
+    a[2, 4000] = 11                                           # one symbol
+    a[3] = 0                                                  # empty part
+    a[4] = np.floor(1e6 / (np.arange(k) + 1) ** 1.1).astype(np.int64)   # Zipf-like
+    a[5] = 1                                                  # all equal
+    a[6, ::3] = 0
+    a[7] = rng.integers(1, 2 ** 20, k)
+    b = np.zeros_like(a)
+    b[:, ::9] = rng.integers(1, 5, (8, len(range(0, k, 9))))
+    tabs = codec.Tables(ctx, 8, k, False)
+    for counts in (a, b):
+        assert counts.max() < 2 ** 31
+        tabs.build(torch.from_numpy(counts.astype(np.int32)).cuda())
+        host = codec.Codebooks(counts.astype(np.float64), k, False)
+        assert tabs.codebooks().file_bytes() == host.file_bytes()
+
+
 def _run(args, cwd=None):
     r = subprocess.run(args, capture_output=True, text=True, cwd=cwd)
     assert r.returncode == 0, r.stdout + r.stderr

@@ -21,7 +21,11 @@ def main():
     skew = (torch.rand((n, m), generator=g, device=dev) ** 3 * k).long()
     codes = ((base // 16) * 16 + skew % 16).clamp(0, k - 1).to(torch.uint8)
     ctx = codec.Context(0)
-    for mode in (True, False):
+    if os.environ.get("K") == "4096":   # configs[4]: 8 plain alphabets of 4,096 symbols
+        k = 4096
+        codes = ((torch.rand((n, m), generator=g, device=dev) ** 4) * k).long().clamp(0, k - 1)
+        codes = codes.to(torch.int16)
+    for mode in ((False,) if k > 256 else (True, False)):
         items = k * k if mode else k
         counts = torch.zeros((m, items), dtype=torch.int32, device=dev)
         codec.histogram(ctx, codes, k, mode, counts=counts)
