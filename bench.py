@@ -88,6 +88,10 @@ def parse():
     ap.add_argument("--elanes", type=int, default=1,
                     help="> 0: encode + decode on this many streams of their own; the --lanes "
                          "streams then build code tables only")
+    ap.add_argument("--drain-trees", choices=["wave", "lane"], default="wave",
+                    help="tree builder of the run's last batch, built after the assignment "
+                         "stream is done: one wavefront per tree (lower latency) or the "
+                         "default one lane per tree")
     ap.add_argument("--hist-on", choices=["assign", "lanes"], default="assign",
                     help="stream of the context histogram: the assignment's, or the batch's "
                          "lane (before its code tables)")
@@ -429,7 +433,11 @@ def main():
             if elanes is not lanes:              # tabs[ti] free: its last decode is done
                 sL.wait_event(ev_dec[ti])
             e = rec("codebook", sL)
-            tabs[ti].build(counts[s], c)         # GPU trees + lookup tables, no host trip
+            # GPU trees + lookup tables, no host trip.  The run's last batch builds while
+            # the assignment stream has nothing left to do: there the one-wavefront-per-tree
+            # build (lower latency, more waves) shortens the drain (--drain-trees).
+            last = i == state["nsteps"] - 1 and args.drain_trees == "wave"
+            tabs[ti].build(counts[s], c, trees="wave" if last else None)
             done(e, sL)
             ev_tab[s].record(sL)
 
@@ -478,6 +486,7 @@ def main():
     lag = 0 if world == 1 or serial else nl * nbuf - 1
 
     def run(steps):
+        state["nsteps"] = steps
         for i in range(steps):
             front(i)
             if i >= lag:

@@ -125,6 +125,13 @@ int pqh_tables_destroy(pqh_tables_t* tables);
  * Codes longer than 56 bits set an error reported by pqh_tables_status.  `ctx` may be any
  * context on the tables' device; the build is ordered on ctx's stream. */
 int pqh_tables_build(pqh_ctx_t* ctx, pqh_tables_t* tables, const uint32_t* d_counts);
+/* pqh_tables_build with the tree builder chosen by the caller (PQH_TREES_DEFAULT: the
+ * PQH_TREE_IMPL environment choice).  K <= 256: LANE = one lane per tree (the default: few
+ * waves beside concurrent kernels), WAVE = one wavefront per tree (lower latency on an
+ * otherwise idle GPU); K > 256: LANE = one lane per tree, otherwise one wavefront per tree.
+ * Every choice builds the same tables. */
+enum { PQH_TREES_DEFAULT = 0, PQH_TREES_LANE = 1, PQH_TREES_WAVE = 2 };
+int pqh_tables_build_impl(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts, int which);
 /* Load codes from m host codebooks (e.g. huffman_codebooks.bin read by huffman_codebook_load). */
 int pqh_tables_upload(pqh_ctx_t* ctx, pqh_tables_t* tables, const huffman_codebook_t* codebooks);
 /* alloc + upload */

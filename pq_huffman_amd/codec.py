@@ -267,11 +267,17 @@ class Tables:
             raise PqhError(st, "pqh_tables_upload: " + ctx.last_error())
         return t
 
-    def build(self, counts, ctx: Context = None) -> "Tables":
+    TREES = {None: 0, "lane": 1, "wave": 2}
+
+    def build(self, counts, ctx: Context = None, trees: str = None) -> "Tables":
         """GPU codebook construction from device counts (async, on `ctx`'s stream: any
-        context of the same device, default the one the tables were allocated with)."""
+        context of the same device, default the one the tables were allocated with).
+        trees: the tree builder (pqh_tables_build_impl) -- None = the library default,
+        "lane" (one lane per tree) or "wave" (one wavefront per tree); all build the same
+        tables."""
         c = ctx or self.ctx
-        check(lib().pqh_tables_build(c.ptr, self.ptr, _ptr(counts)), "pqh_tables_build")
+        check(lib().pqh_tables_build_impl(c.ptr, self.ptr, _ptr(counts), self.TREES[trees]),
+              "pqh_tables_build")
         return self
 
     def status(self) -> None:

@@ -1455,9 +1455,14 @@ static int launch_luts(pqh_ctx* ctx, pqh_tables* t) {
 }
 
 int pqh_tables_build(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts) {
+    return pqh_tables_build_impl(ctx, t, d_counts, PQH_TREES_DEFAULT);
+}
+
+int pqh_tables_build_impl(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts, int which) {
     // any context of the tables' device may run the build (on its own stream), so the
     // builds of consecutive batches can overlap on different streams
     if (!ctx || !t || !d_counts || !t->ctx || t->ctx->device != ctx->device) return PQH_ERR_ARG;
+    if (which < PQH_TREES_DEFAULT || which > PQH_TREES_WAVE) return PQH_ERR_ARG;
     int rc = pqh_use_device(ctx);
     if (rc) return rc;
     PQH_HIP(ctx, hipMemsetAsync(t->d_err, 0, 4, ctx->stream));
@@ -1471,7 +1476,8 @@ int pqh_tables_build(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts) 
     //    PQH_TREE_IMPL=wave): half the latency alone (0.40 vs 0.70 ms with the decode
     //    tables), but its 2,048 wavefronts take wave slots and issue cycles from the
     //    concurrent assignment (bench 1,610-1,880 Mvec/s against 2,270).
-    const char* impl = std::getenv("PQH_TREE_IMPL");
+    const char* impl = which == PQH_TREES_WAVE ? "wave"
+                     : which == PQH_TREES_LANE ? "lane" : std::getenv("PQH_TREE_IMPL");
     if (t->k <= 256 && impl && std::strcmp(impl, "wave") == 0) {
         // writes every entry (0 for symbols that never occur): no memset
         hipLaunchKernelGGL(huff_trees_wave, dim3((unsigned)((trees + kTreeWaves - 1) / kTreeWaves)),
