@@ -487,7 +487,9 @@ def main():
 
     def run(steps):
         state["nsteps"] = steps
+        state["issue_t"] = []
         for i in range(steps):
+            state["issue_t"].append(time.perf_counter())
             front(i)
             if i >= lag:
                 back(i - lag)
@@ -622,6 +624,10 @@ def main():
             "roundtrip_read_roofline_frac": round(
                 vec_read * n * world * args.steps / elapsed / 1e9 / HBM_PEAK_GBS / world, 4),
             "host_issue_ms_per_step": round(t_issue / args.steps * 1e3, 3),
+            # the longest pause between two steps' issue (a host stall starves the GPU)
+            "host_issue_max_gap_ms": round(max((b - a for a, b in zip(state["issue_t"],
+                                                                      state["issue_t"][1:])),
+                                               default=0.0) * 1e3, 3),
             "bits_per_vector": round(bits_per_vec, 3),
             "rerank_fraction": round(rerank / (n * m), 6),
         }
