@@ -359,10 +359,13 @@ def main():
     acc = {s: 0.0 for s in list(stages) + ["collectives"]}
     state = {"timed": False}
 
+    ev_pool = []         # timing events made before the timed region (not while issuing)
+
     def rec(name, stream):
         if not state["timed"]:
             return None
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0, e1 = ev_pool.pop() if ev_pool else (torch.cuda.Event(enable_timing=True),
+                                                torch.cuda.Event(enable_timing=True))
         e0.record(stream)
         events.append((name, e0, e1))
         return e1
@@ -503,6 +506,8 @@ def main():
             torch.cuda.synchronize()
 
     run(args.warmup)
+    ev_pool.extend((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                   for _ in range(args.steps * len(stages)))
     barrier()
     state["timed"] = True
     t0 = time.perf_counter()
