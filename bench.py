@@ -83,11 +83,13 @@ def parse():
                          "tables, encode and decode on one of --lanes streams (overlapped); "
                          "'serial': every stage in order on one stream")
     ap.add_argument("--no-overlap", action="store_true", help="same as --sched serial")
-    ap.add_argument("--lanes", type=int, default=2,
-                    help="streams taking batches round robin for tables + encode + decode")
-    ap.add_argument("--elanes", type=int, default=1,
+    ap.add_argument("--lanes", type=int, default=None,
+                    help="streams taking batches round robin for tables + encode + decode "
+                         "(default 2; 3 for --config k4096, whose tree builds are the long "
+                         "stage: 230 vs 219 Mvec/s)")
+    ap.add_argument("--elanes", type=int, default=None,
                     help="> 0: encode + decode on this many streams of their own; the --lanes "
-                         "streams then build code tables only")
+                         "streams then build code tables only (default 1; 0 for k4096)")
     ap.add_argument("--drain-trees", choices=["wave", "lane"], default="wave",
                     help="tree builder of the run's last batch, built after the assignment "
                          "stream is done: one wavefront per tree (lower latency) or the "
@@ -309,6 +311,10 @@ def main():
     ctx = (codec.Context(local, stream=torch.cuda.Stream(device=dev, priority=-1))
            if args.a_priority else codec.Context(local))
     sA = ctx.stream
+    if args.lanes is None:   # 1 + lanes + elanes <= 4 streams: one hardware queue each
+        args.lanes = 3 if args.config == "k4096" else 2
+    if args.elanes is None:
+        args.elanes = 0 if args.config == "k4096" else 1
     nl = 1 if serial else max(1, args.lanes)
     # Lane streams are the library's own (pqh_ctx_create_cu_split; cus >= the device's CU
     # count: no CU mask).  (torch.cuda.Stream lanes measured 1,107 vs 2,250 Mvec/s: torch's
