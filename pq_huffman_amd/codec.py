@@ -582,11 +582,29 @@ def tree_encode(ctx: Context, codes, targets, counts, chunk_vectors: int = 16) -
                        coff, ext_rows)
 
 
+def tree_ext_index_device(ctx: Context, num_children, chunk_vectors: int):
+    """tree_ext_index on the device (pqh_tree_ext_index_device) from a device tensor of child
+    counts (uint8, int16-as-u16 or int32): (parent_pos i64[n], ext_offsets i64[chunks + 1])
+    device tensors and the ext count."""
+    torch = _torch()
+    nch = num_children.contiguous()
+    n = nch.numel()
+    nbytes = {torch.uint8: 1, torch.int16: 2, torch.int32: 4}[nch.dtype]
+    chunks = (n + chunk_vectors - 1) // chunk_vectors
+    pp = torch.empty(max(n, 1), dtype=torch.int64, device=nch.device)
+    eo = torch.empty(chunks + 1, dtype=torch.int64, device=nch.device)
+    ext = lib().pqh_tree_ext_index_device(ctx.ptr, n, _ptr(nch), nbytes, chunk_vectors,
+                                          _ptr(pp), _ptr(eo))
+    if ext < 0:
+        raise PqhError(int(ext), "pqh_tree_ext_index_device: " + ctx.last_error())
+    return pp[:n], eo, int(ext)
+
+
 def tree_decode(ctx: Context, enc: TreeEncoded, tables: Tables = None, out=None,
                 stream_bytes: int = None):
     """huffman_decoder --tree on the GPU (huffman_decoder.c:214-247): the children stream
-    first (GPU decode of its non-context book), then the host traverser over the decoded
-    child counts, then one lane per chunk with the encoder's sidecar.  Rows come back in
+    first (GPU decode of its non-context book), then the traverser's index over the decoded
+    child counts (on the device), then one lane per chunk with the encoder's sidecar.  Rows come back in
     stream (DFS) order, as the reference decoder writes them.  stream_bytes (default: the
     encoded length) bounds the bits the decoder may consume: a stream shorter than its
     sidecar says raises PqhError (PQH_ERR_CORRUPT)."""
@@ -595,13 +613,11 @@ def tree_decode(ctx: Context, enc: TreeEncoded, tables: Tables = None, out=None,
     ctab = Tables.from_codebooks(ctx, enc.children_codebook)
     nch = decode(ctx, ctab, enc.children)
     decode_status(ctx)
-    nch = nch.cpu().numpy().reshape(-1).view(np.uint8 if ctab.k <= 256 else np.int16)
-    pp, eo, _ = tree_ext_index(nch.astype(np.int32), enc.chunk_vectors)
+    # the traverser's index on the device, from the decoded child counts in place
+    d_pp, d_eo, _ = tree_ext_index_device(ctx, nch.reshape(-1), enc.chunk_vectors)
     dev = enc.stream.device
     if out is None:
         out = torch.empty((enc.n, t.m), dtype=torch.uint8, device=dev)
-    d_pp = torch.from_numpy(pp).to(dev)
-    d_eo = torch.from_numpy(eo).to(dev)
     nb = enc.nbytes if stream_bytes is None else stream_bytes
     check(lib().pqh_decode_tree(ctx.ptr, t.ptr, _ptr(enc.stream), nb, enc.n,
                                 enc.chunk_vectors, _ptr(enc.chunk_offsets), _ptr(d_pp),

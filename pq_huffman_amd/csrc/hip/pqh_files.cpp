@@ -623,18 +623,14 @@ extern "C" int pqh_decode_tree_files(const char* in_prefix, unsigned char** code
                     d_cc.p);
     if (!rc) rc = pqh_decode_status(ctx);
     if (rc) return fail(rc);
-    std::vector<unsigned char> ccodes(n * cesz);
-    PQH_HIP(ctx, hipMemcpy(ccodes.data(), d_cc.p, ccodes.size(), hipMemcpyDeviceToHost));
-    std::vector<int> nch(n);
-    for (unsigned long long p = 0; p < n; ++p)
-        nch[p] = cesz == 1 ? ccodes[p] : reinterpret_cast<const uint16_t*>(ccodes.data())[p];
-    // traverser index; its ext count must agree with the sidecar's
+    // the traverser's index on the device from the decoded child counts; its ext count must
+    // agree with the sidecar's
     const int C = (int)h.chunk_vectors;
-    std::vector<long long> pp(n), eo(h.chunks + 1);
-    const long long ext = pqh_tree_ext_index((long long)n, nch.data(), C, pp.data(), eo.data(), nullptr);
+    if ((rc = d_pp.alloc(ctx, n)) || (rc = d_eo.alloc(ctx, h.chunks + 1))) return fail(rc);
+    const long long ext = pqh_tree_ext_index_device(ctx, (long long)n, d_cc.p, (int)cesz, C,
+                                                    d_pp.p, d_eo.p);
     if (ext < 0 || (unsigned long long)ext != h.ext) return fail(PQH_ERR_CORRUPT);
     if ((rc = d_stream.alloc(ctx, stream.size())) || (rc = d_coff.alloc(ctx, h.chunks + 1)) ||
-        (rc = d_pp.alloc(ctx, n)) || (rc = d_eo.alloc(ctx, h.chunks + 1)) ||
         (rc = d_ext.alloc(ctx, h.ext * m + 1)) || (rc = d_rows.alloc(ctx, n * m)))
         return fail(rc);
     const unsigned char* sp = side.data() + sizeof(h);
@@ -642,8 +638,6 @@ extern "C" int pqh_decode_tree_files(const char* in_prefix, unsigned char** code
     PQH_HIP(ctx, hipMemcpyAsync(d_coff.p, sp, h.chunks * 8, hipMemcpyHostToDevice, ctx->stream));
     if (h.ext)
         PQH_HIP(ctx, hipMemcpyAsync(d_ext.p, sp + h.chunks * 8, h.ext * m, hipMemcpyHostToDevice, ctx->stream));
-    PQH_HIP(ctx, hipMemcpyAsync(d_pp.p, pp.data(), n * 8, hipMemcpyHostToDevice, ctx->stream));
-    PQH_HIP(ctx, hipMemcpyAsync(d_eo.p, eo.data(), (h.chunks + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
     rc = pqh_decode_tree(ctx, tab, d_stream.p, bytes, (long long)n, C, d_coff.p, d_pp.p,
                          d_eo.p, d_ext.p, d_rows.p);
     if (!rc) rc = pqh_decode_status(ctx);

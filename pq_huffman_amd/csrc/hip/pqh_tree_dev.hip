@@ -21,10 +21,21 @@
 //   preorder   off(c) = 1 + sizes of the children after c in its parent's list (a scan over
 //              the edges); pre(v) = the tree's offset + the sum of off over v's ancestors --
 //              a prefix sum along the tours (+off at the edge down, -off at the edge back)
+//
+// pqh_tree_ext_index_device: the decoder's traverser (huffman_decoder.c:214-247) over the
+// decoded child counts, without a walk.  Row p pops one slot of the stack's top entry (its
+// context) unless the stack is empty (a root), then pushes nch[p] slots.  With
+// E(p) = sum_{q<=p} (nch[q] - 1), p is a root exactly when E(p - 1) is a new strict minimum
+// below 0 (E falls by at most one per row); the stack depth is D(p) = E(p) + roots so far,
+// and the depth after p's pop is L(p) = D(p) - nch[p].  The slot p pops sits at depth
+// D(p - 1) = L(p) + 1 and was pushed by the last row q < p with L(q) < D(p - 1): p's context
+// is the nearest earlier row with L(q) <= L(p) (a min-tree search).
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
+#include <climits>
+#include <vector>
 
 #include "pqh_internal.h"
 
@@ -243,6 +254,86 @@ struct Arena {
     }
 };
 
+// ---------------------------------------------------------------- decoder's traverser
+template <typename T>
+__global__ void __launch_bounds__(256)
+tx_vals(const T* __restrict__ nch, long long n, long long* __restrict__ val) {
+    const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < n) val[p] = (long long)nch[p] - 1;
+}
+
+// roots (E(p-1) a new strict minimum below 0), as 0/1 for a sum scan
+__global__ void __launch_bounds__(256)
+tx_roots(const long long* __restrict__ E, const long long* __restrict__ PM, long long n,
+         long long* __restrict__ root) {
+    const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const long long before = p >= 2 && PM[p - 2] < 0 ? PM[p - 2] : 0;   // min(0, E(0..p-2))
+    root[p] = (p == 0 || E[p - 1] < before) ? 1 : 0;
+}
+
+// L(p) = E(p) + R(p) - nch[p] (level 0 of the min tree); roots marked for the query
+template <typename T>
+__global__ void __launch_bounds__(256)
+tx_levels0(const T* __restrict__ nch, const long long* __restrict__ E,
+           const long long* __restrict__ R, long long n, long long* __restrict__ L) {
+    const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < n) L[p] = E[p] + R[p] - (long long)nch[p];
+}
+
+__global__ void __launch_bounds__(256)
+tx_level_up(const long long* __restrict__ lo, long long nlo, long long* __restrict__ hi, long long nhi) {
+    const long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nhi) return;
+    const long long a = lo[2 * j];
+    const long long b = 2 * j + 1 < nlo ? lo[2 * j + 1] : LLONG_MAX;
+    hi[j] = a < b ? a : b;
+}
+
+// context row of p: the nearest earlier row with L <= L(p) (climb to the first block holding
+// one, then descend to its rightmost); roots have none.  Ext flag: a context before p's chunk.
+__global__ void __launch_bounds__(256)
+tx_query(const long long* __restrict__ levels, const long long* __restrict__ loff, int nlev,
+         const long long* __restrict__ rootflag, long long n, int C,
+         long long* __restrict__ parent_pos, long long* __restrict__ ext) {
+    const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    long long q = -1;
+    if (!rootflag[p]) {
+        const long long x = levels[p];
+        int k = 0;
+        long long j = p - 1;
+        while (j >= 0 && levels[loff[k] + j] > x) {
+            if (j & 1) {
+                j -= 1;
+            } else {
+                j = j / 2 - 1;
+                ++k;
+                if (k >= nlev) { j = -1; break; }
+            }
+        }
+        if (j >= 0) {
+            while (k > 0) {
+                --k;
+                j = 2 * j + 1;   // the right child, unless it is past the level's end
+                if (j >= loff[k + 1] - loff[k] || levels[loff[k] + j] > x) j -= 1;
+            }
+            q = j;
+        }
+    }
+    parent_pos[p] = q;
+    ext[p] = (q >= 0 && q < p - p % C) ? 1 : 0;
+}
+
+__global__ void __launch_bounds__(256)
+tx_offsets(const long long* __restrict__ S, long long n, int C, long long chunks,
+           long long* __restrict__ eo) {
+    const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c > chunks) return;
+    const long long end = c * C < n ? c * C : n;   // rows before chunk c
+    eo[c] = end > 0 ? S[end - 1] : 0;
+}
+
 int ceil_log2(long long x) {
     int r = 0;
     while ((1ll << r) < x) ++r;
@@ -389,4 +480,103 @@ extern "C" int pqh_tree_order_device(pqh_ctx_t* ctx, long long n, long long ne,
     PQH_HIP(ctx, hipStreamSynchronize(st));
     *num_roots = isolated + hb[3];
     return PQH_OK;
+}
+
+extern "C" long long pqh_tree_ext_index_device(pqh_ctx_t* ctx, long long n,
+                                               const void* d_num_children, int child_bytes,
+                                               int chunk_vectors, long long* d_parent_pos,
+                                               long long* d_ext_offsets) {
+    if (!ctx || n < 0 || chunk_vectors <= 0 || (child_bytes != 1 && child_bytes != 2 && child_bytes != 4) ||
+        (n > 0 && (!d_num_children || !d_parent_pos || !d_ext_offsets)))
+        return PQH_ERR_ARG;
+    int rc = pqh_use_device(ctx);
+    if (rc) return rc;
+    hipStream_t st = ctx->stream;
+    const long long chunks = (n + chunk_vectors - 1) / chunk_vectors;
+    if (n == 0) {
+        PQH_HIP(ctx, hipMemsetAsync(d_ext_offsets, 0, 8, st));
+        PQH_HIP(ctx, hipStreamSynchronize(st));
+        return 0;
+    }
+    size_t t_sum = 0, t_min = 0;
+    PQH_HIP(ctx, rocprim::inclusive_scan(nullptr, t_sum, (const long long*)nullptr, (long long*)nullptr,
+                                         (size_t)n, rocprim::plus<long long>(), st));
+    PQH_HIP(ctx, rocprim::inclusive_scan(nullptr, t_min, (const long long*)nullptr, (long long*)nullptr,
+                                         (size_t)n, rocprim::minimum<long long>(), st));
+    const size_t t_max = std::max(t_sum, t_min);
+    int nlev = 1;
+    long long tot = n;
+    std::vector<long long> loff(1, 0);   // level k at loff[k], loff[nlev] = the total
+    for (long long len = n; len > 1; len = (len + 1) / 2) {
+        loff.push_back(tot);
+        tot += (len + 1) / 2;
+        ++nlev;
+    }
+    loff.push_back(tot);
+    long long *E, *PM, *R, *lev, *ext, *S, *dloff;
+    void* temp;
+    auto carve = [&](Arena& a) {
+        E = a.take<long long>(n);
+        PM = a.take<long long>(n);
+        R = a.take<long long>(n);
+        lev = a.take<long long>(tot);
+        ext = a.take<long long>(n);
+        S = a.take<long long>(n);
+        dloff = a.take<long long>(nlev + 1);
+        temp = a.take<char>(t_max);
+    };
+    Arena sizing;
+    carve(sizing);
+    if ((rc = pqh_ensure_ws(ctx, sizing.used))) return rc;
+    Arena arena;
+    arena.base = static_cast<char*>(ctx->ws);
+    carve(arena);
+    PQH_HIP(ctx, hipMemcpyAsync(dloff, loff.data(), sizeof(long long) * (nlev + 1), hipMemcpyHostToDevice, st));
+#define PQH_TX(T)                                                                                \
+    do {                                                                                         \
+        const T* nc = static_cast<const T*>(d_num_children);                                    \
+        hipLaunchKernelGGL(tx_vals<T>, G1(n), 0, st, nc, n, E);                                  \
+        size_t tb = t_max;                                                                       \
+        PQH_HIP(ctx, rocprim::inclusive_scan(temp, tb, E, E, (size_t)n, rocprim::plus<long long>(), st)); \
+        tb = t_max;                                                                              \
+        PQH_HIP(ctx, rocprim::inclusive_scan(temp, tb, E, PM, (size_t)n,                         \
+                                             rocprim::minimum<long long>(), st));               \
+        hipLaunchKernelGGL(tx_roots, G1(n), 0, st, E, PM, n, R);                                  \
+    } while (0)
+    if (child_bytes == 1) PQH_TX(uint8_t);
+    else if (child_bytes == 2) PQH_TX(uint16_t);
+    else PQH_TX(int32_t);
+#undef PQH_TX
+    PQH_LAUNCH_CHECK(ctx);
+    // PM <- the root flags (kept for the query), R <- their running count; then level 0
+    PQH_HIP(ctx, hipMemcpyAsync(PM, R, sizeof(long long) * n, hipMemcpyDeviceToDevice, st));
+    {
+        size_t tb = t_max;
+        PQH_HIP(ctx, rocprim::inclusive_scan(temp, tb, R, R, (size_t)n, rocprim::plus<long long>(), st));
+    }
+    if (child_bytes == 1)
+        hipLaunchKernelGGL(tx_levels0<uint8_t>, G1(n), 0, st, static_cast<const uint8_t*>(d_num_children), E, R, n, lev);
+    else if (child_bytes == 2)
+        hipLaunchKernelGGL(tx_levels0<uint16_t>, G1(n), 0, st, static_cast<const uint16_t*>(d_num_children), E, R, n, lev);
+    else
+        hipLaunchKernelGGL(tx_levels0<int32_t>, G1(n), 0, st, static_cast<const int32_t*>(d_num_children), E, R, n, lev);
+    PQH_LAUNCH_CHECK(ctx);
+    for (int k = 1; k < nlev; ++k) {
+        const long long nlo = loff[k] - loff[k - 1];
+        const long long nhi = loff[k + 1] - loff[k];
+        hipLaunchKernelGGL(tx_level_up, G1(nhi), 0, st, lev + loff[k - 1], nlo, lev + loff[k], nhi);
+    }
+    PQH_LAUNCH_CHECK(ctx);
+    hipLaunchKernelGGL(tx_query, G1(n), 0, st, lev, dloff, nlev, PM, n, chunk_vectors, d_parent_pos, ext);
+    PQH_LAUNCH_CHECK(ctx);
+    {
+        size_t tb = t_max;
+        PQH_HIP(ctx, rocprim::inclusive_scan(temp, tb, ext, S, (size_t)n, rocprim::plus<long long>(), st));
+    }
+    hipLaunchKernelGGL(tx_offsets, G1(chunks + 1), 0, st, S, n, chunk_vectors, chunks, d_ext_offsets);
+    PQH_LAUNCH_CHECK(ctx);
+    long long total = 0;
+    PQH_HIP(ctx, hipMemcpyAsync(&total, S + n - 1, 8, hipMemcpyDeviceToHost, st));
+    PQH_HIP(ctx, hipStreamSynchronize(st));
+    return total;
 }

@@ -351,3 +351,44 @@ def test_gpu_tree_order_device_rejects_bad_counts(gpu):
     bad_t = targets.copy()
     bad_t[0] = 50                             # target outside the vertices: not a forest
     assert codec.tree_order_device(gpu, bad_t, counts) is None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,n,c", [("forest", 1, 16), ("forest", 2, 1), ("forest", 1000, 7),
+                                      ("forest", 200_000, 16), ("forest", 1_000_000, 64),
+                                      ("path", 100_000, 16), ("star", 50_000, 16),
+                                      ("arbitrary", 5000, 3), ("arbitrary", 300_000, 16),
+                                      ("wide", 70_000, 16)])
+@pytest.mark.parametrize("width", [1, 2, 4])
+def test_gpu_tree_ext_index_device_vs_host(gpu, kind, n, c, width):
+    """The decoder's traverser index on the device (pqh_tree_ext_index_device) equals the
+    host walk (pqh_tree_ext_index) -- for forests' DFS child counts and for arbitrary counts
+    (truncated trees, slots left open at the end), read as u8 / u16 / i32."""
+    import torch
+    from pq_huffman_amd import codec
+    rng = np.random.default_rng(n + c + width)
+    if kind == "forest":
+        t, cnt = datagen.random_forest(n, roots=max(1, n // 5000), seed=n)
+        nch = codec.tree_order(t, cnt)[1]
+    elif kind == "path":
+        nch = codec.tree_order(*_path_forest(n, seed=3))[1]
+    elif kind == "star":
+        nch = codec.tree_order(*_star_forest(n, centre=7))[1]
+    elif kind == "wide":                       # child counts past 255 (u16 / i32 only)
+        nch = np.zeros(n, np.int32)
+        nch[::1000] = rng.integers(0, 3000, len(nch[::1000]))
+    else:
+        nch = rng.integers(0, 4, n).astype(np.int32)
+        nch[rng.random(n) < 0.55] = 0
+    nch = np.asarray(nch, np.int32)
+    if width == 1 and nch.max() > 255:
+        pytest.skip("u8 counts cannot hold this forest's widest vertex")
+    pp, eo, ep = codec.tree_ext_index(nch, c)
+    dt = {1: torch.uint8, 2: torch.int16, 4: torch.int32}[width]
+    d = torch.from_numpy(nch.astype({1: np.uint8, 2: np.uint16, 4: np.int32}[width])
+                         .view({1: np.uint8, 2: np.int16, 4: np.int32}[width])).cuda()
+    assert d.dtype == dt
+    dpp, deo, ext = codec.tree_ext_index_device(gpu, d, c)
+    assert ext == len(ep)
+    np.testing.assert_array_equal(dpp.cpu().numpy(), pp)
+    np.testing.assert_array_equal(deo.cpu().numpy(), eo)
