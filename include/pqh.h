@@ -371,11 +371,12 @@ long long pqh_tree_ext_index(long long n, const int* num_children, int chunk_vec
                              long long* parent_pos, long long* ext_offsets,
                              long long* ext_positions);
 /* pqh_tree_ext_index on the device, from device child counts (child_bytes 1, 2 or 4: u8,
- * u16 or i32): d_parent_pos[n] and d_ext_offsets[chunks + 1]; returns the ext count or a
- * negative status.  Same results as the host walk for any counts.  Synchronises. */
+ * u16 or i32): d_parent_pos[n], d_ext_offsets[chunks + 1] and, unless NULL,
+ * d_ext_positions (room for n); returns the ext count or a negative status.  Same results
+ * as the host walk for any counts.  Synchronises. */
 long long pqh_tree_ext_index_device(pqh_ctx_t* ctx, long long n, const void* d_num_children,
                                     int child_bytes, int chunk_vectors, long long* d_parent_pos,
-                                    long long* d_ext_offsets);
+                                    long long* d_ext_offsets, long long* d_ext_positions);
 /* huffman_decoder --tree on the GPU: rows in stream order.  One lane per chunk (offsets
  * from pqh_encode_tree_write); a context inside the chunk is read from the chunk's own
  * decoded rows, one before it from d_ext_rows[d_ext_offsets[j]...] (m codes each, the rows

@@ -144,7 +144,7 @@ SIGNATURES = [
     ("pqh_shard_halo_source", I, [P, I, I, P, P]),
     ("pqh_tree_order", I, [LL, LL, P, P, P, P, P]),
     ("pqh_tree_order_device", I, [P, LL, LL, P, P, P, P, P, P]),
-    ("pqh_tree_ext_index_device", LL, [P, LL, P, I, I, P, P]),
+    ("pqh_tree_ext_index_device", LL, [P, LL, P, I, I, P, P, P]),
     ("pqh_tree_gather", I, [P, P, LL, I, I, P, P, P, P]),
     ("pqh_tree_status", I, [P]),
     ("pqh_histogram_tree", I, [P, P, P, LL, I, I, P]),

@@ -542,6 +542,7 @@ def tree_encode(ctx: Context, codes, targets, counts, chunk_vectors: int = 16) -
         vert, nch, par, roots = tree_order(targets, counts)
         d_vert = torch.from_numpy(vert.astype(np.int32)).to(dev)
         d_par = torch.from_numpy(par).to(dev)
+        d_nch = torch.from_numpy(np.ascontiguousarray(nch, np.int32)).to(dev)
     rows = torch.empty((n, m), dtype=torch.uint8, device=dev)
     prev = torch.empty((n, m), dtype=torch.int16, device=dev)
     check(lib().pqh_tree_gather(ctx.ptr, _ptr(codes), n, m, 256, _ptr(d_vert), _ptr(d_par),
@@ -562,8 +563,8 @@ def tree_encode(ctx: Context, codes, targets, counts, chunk_vectors: int = 16) -
                                       _ptr(total)),
           "pqh_encode_tree_write: " + ctx.last_error())
     # decode sidecar: the contexts each chunk needs from before it (the encoder has them)
-    _, _, ext_pos = tree_ext_index(nch, chunk_vectors)
-    ext_rows = rows.index_select(0, torch.from_numpy(ext_pos).to(dev))
+    _, _, _, ext_pos = tree_ext_index_device(ctx, d_nch, chunk_vectors, positions=True)
+    ext_rows = rows.index_select(0, ext_pos)
     encode_status(ctx)
     bits = int(total.item())
     # children stream: one non-context part over the child counts
@@ -573,19 +574,17 @@ def tree_encode(ctx: Context, codes, targets, counts, chunk_vectors: int = 16) -
     ccounts = np.bincount(nch, minlength=alphabet).astype(np.float64)[None]
     cbook = Codebooks(ccounts, alphabet, False)
     ctab = Tables.from_codebooks(ctx, cbook)
-    cdt = torch.uint8 if alphabet <= 256 else torch.int16
-    ccodes = torch.from_numpy(nch.astype(np.uint8 if alphabet <= 256 else np.int16)
-                              .reshape(n, 1)).to(dev)
-    assert ccodes.dtype == cdt
+    ccodes = d_nch.to(torch.uint8 if alphabet <= 256 else torch.int16).reshape(n, 1)
     children = encode(ctx, ctab, ccodes, chunk_vectors=64, raw_first=1)
     return TreeEncoded(out, bits, n, roots, tables, vert, nch, cbook, children, chunk_vectors,
                        coff, ext_rows)
 
 
-def tree_ext_index_device(ctx: Context, num_children, chunk_vectors: int):
+def tree_ext_index_device(ctx: Context, num_children, chunk_vectors: int,
+                          positions: bool = False):
     """tree_ext_index on the device (pqh_tree_ext_index_device) from a device tensor of child
     counts (uint8, int16-as-u16 or int32): (parent_pos i64[n], ext_offsets i64[chunks + 1])
-    device tensors and the ext count."""
+    device tensors and the ext count -- plus ext_positions i64[ext] with positions=True."""
     torch = _torch()
     nch = num_children.contiguous()
     n = nch.numel()
@@ -593,10 +592,13 @@ def tree_ext_index_device(ctx: Context, num_children, chunk_vectors: int):
     chunks = (n + chunk_vectors - 1) // chunk_vectors
     pp = torch.empty(max(n, 1), dtype=torch.int64, device=nch.device)
     eo = torch.empty(chunks + 1, dtype=torch.int64, device=nch.device)
+    ep = torch.empty(max(n, 1), dtype=torch.int64, device=nch.device) if positions else None
     ext = lib().pqh_tree_ext_index_device(ctx.ptr, n, _ptr(nch), nbytes, chunk_vectors,
-                                          _ptr(pp), _ptr(eo))
+                                          _ptr(pp), _ptr(eo), _ptr(ep) if positions else None)
     if ext < 0:
         raise PqhError(int(ext), "pqh_tree_ext_index_device: " + ctx.last_error())
+    if positions:
+        return pp[:n], eo, int(ext), ep[:ext]
     return pp[:n], eo, int(ext)
 
 

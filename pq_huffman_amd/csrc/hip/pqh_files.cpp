@@ -628,7 +628,7 @@ extern "C" int pqh_decode_tree_files(const char* in_prefix, unsigned char** code
     const int C = (int)h.chunk_vectors;
     if ((rc = d_pp.alloc(ctx, n)) || (rc = d_eo.alloc(ctx, h.chunks + 1))) return fail(rc);
     const long long ext = pqh_tree_ext_index_device(ctx, (long long)n, d_cc.p, (int)cesz, C,
-                                                    d_pp.p, d_eo.p);
+                                                    d_pp.p, d_eo.p, nullptr);
     if (ext < 0 || (unsigned long long)ext != h.ext) return fail(PQH_ERR_CORRUPT);
     if ((rc = d_stream.alloc(ctx, stream.size())) || (rc = d_coff.alloc(ctx, h.chunks + 1)) ||
         (rc = d_ext.alloc(ctx, h.ext * m + 1)) || (rc = d_rows.alloc(ctx, n * m)))

@@ -325,6 +325,14 @@ tx_query(const long long* __restrict__ levels, const long long* __restrict__ lof
     ext[p] = (q >= 0 && q < p - p % C) ? 1 : 0;
 }
 
+// the contexts before their chunk, in row order (the encoder gathers these rows)
+__global__ void __launch_bounds__(256)
+tx_compact(const long long* __restrict__ ext, const long long* __restrict__ S,
+           const long long* __restrict__ parent_pos, long long n, long long* __restrict__ pos) {
+    const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < n && ext[p]) pos[S[p] - 1] = parent_pos[p];
+}
+
 __global__ void __launch_bounds__(256)
 tx_offsets(const long long* __restrict__ S, long long n, int C, long long chunks,
            long long* __restrict__ eo) {
@@ -485,7 +493,8 @@ extern "C" int pqh_tree_order_device(pqh_ctx_t* ctx, long long n, long long ne,
 extern "C" long long pqh_tree_ext_index_device(pqh_ctx_t* ctx, long long n,
                                                const void* d_num_children, int child_bytes,
                                                int chunk_vectors, long long* d_parent_pos,
-                                               long long* d_ext_offsets) {
+                                               long long* d_ext_offsets,
+                                               long long* d_ext_positions) {
     if (!ctx || n < 0 || chunk_vectors <= 0 || (child_bytes != 1 && child_bytes != 2 && child_bytes != 4) ||
         (n > 0 && (!d_num_children || !d_parent_pos || !d_ext_offsets)))
         return PQH_ERR_ARG;
@@ -574,6 +583,8 @@ extern "C" long long pqh_tree_ext_index_device(pqh_ctx_t* ctx, long long n,
         PQH_HIP(ctx, rocprim::inclusive_scan(temp, tb, ext, S, (size_t)n, rocprim::plus<long long>(), st));
     }
     hipLaunchKernelGGL(tx_offsets, G1(chunks + 1), 0, st, S, n, chunk_vectors, chunks, d_ext_offsets);
+    if (d_ext_positions)
+        hipLaunchKernelGGL(tx_compact, G1(n), 0, st, ext, S, d_parent_pos, n, d_ext_positions);
     PQH_LAUNCH_CHECK(ctx);
     long long total = 0;
     PQH_HIP(ctx, hipMemcpyAsync(&total, S + n - 1, 8, hipMemcpyDeviceToHost, st));

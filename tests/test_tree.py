@@ -388,7 +388,8 @@ def test_gpu_tree_ext_index_device_vs_host(gpu, kind, n, c, width):
     d = torch.from_numpy(nch.astype({1: np.uint8, 2: np.uint16, 4: np.int32}[width])
                          .view({1: np.uint8, 2: np.int16, 4: np.int32}[width])).cuda()
     assert d.dtype == dt
-    dpp, deo, ext = codec.tree_ext_index_device(gpu, d, c)
+    dpp, deo, ext, dep = codec.tree_ext_index_device(gpu, d, c, positions=True)
     assert ext == len(ep)
     np.testing.assert_array_equal(dpp.cpu().numpy(), pp)
     np.testing.assert_array_equal(deo.cpu().numpy(), eo)
+    np.testing.assert_array_equal(dep.cpu().numpy(), ep)
