@@ -669,19 +669,22 @@ struct NnItem {
 };
 
 // fast_nn_heap_push_impl (fast_nn_temp_file.c:23-46): the item replaces the root and sinks
-// while a child is strictly heavier (the right one when it is the heavier of the two)
+// while a child is strictly heavier (the right one when it is the heavier of the two).
+// Heap slot i at h[i * S] (S = kQ in the merge: the lanes' heaps interleaved, so lanes at the
+// same slot read consecutive words).
+template <int S>
 __device__ __forceinline__ void nn_sift(NnItem* h, NnItem it, int k) {
     int i = 0;
     for (;;) {
         const int l = 2 * i + 1, r = 2 * i + 2;
         int sw;
-        if (r < k && h[r].dist > h[l].dist && h[r].dist > it.dist) sw = r;
-        else if (l < k && h[l].dist > it.dist) sw = l;
+        if (r < k && h[r * S].dist > h[l * S].dist && h[r * S].dist > it.dist) sw = r;
+        else if (l < k && h[l * S].dist > it.dist) sw = l;
         else break;
-        h[i] = h[sw];
+        h[i * S] = h[sw * S];
         i = sw;
     }
-    h[i] = it;
+    h[i * S] = it;
 }
 
 // one lane per row: its blocks' lists (entries 1 .. kk-1) in block order into the heap, then
@@ -695,8 +698,8 @@ knn_merge(long long n, int num_nn, const unsigned long long* __restrict__ off,
     extern __shared__ NnItem heaps[];
     const long long v = (long long)blockIdx.x * kQ + threadIdx.x;
     if (v >= n) return;
-    NnItem* h = heaps + threadIdx.x * num_nn;
-    for (int j = 0; j < num_nn; ++j) h[j] = NnItem{0xFFFFFFFFu, INFINITY};
+    NnItem* h = heaps + threadIdx.x;   // slot j at h[j * kQ]
+    for (int j = 0; j < num_nn; ++j) h[j * kQ] = NnItem{0xFFFFFFFFu, INFINITY};
     // a row in one block gets distinct indices only: the reference's duplicate scan never
     // fires for it
     const bool single = off[v + 1] - off[v] == 1;
@@ -705,19 +708,31 @@ knn_merge(long long n, int num_nn, const unsigned long long* __restrict__ off,
         const long long b = keys_sorted[p];
         const long long S = boff[b + 1] - boff[b];
         const int kk = (int)((num_nn < S - 1 ? num_nn : S - 1) + 1);
-        for (int j = 1; j < kk; ++j) {
-            const NnItem it{lrow[p * stride + j], ldist[p * stride + j]};
-            if (!(it.dist < h[0].dist)) continue;
-            bool dup = false;
-            if (!single)
-                for (int q = 0; q < num_nn; ++q) dup |= h[q].index == it.index;
-            if (!dup) nn_sift(h, it, num_nn);
+        // the list's entries eight at a time, their loads issued together (the merge is
+        // bound by these loads' latency, not by the heap work)
+        for (int j0 = 1; j0 < kk; j0 += 8) {
+            NnItem its[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int j = j0 + u < kk ? j0 + u : j0;
+                its[u] = NnItem{lrow[p * stride + j], ldist[p * stride + j]};
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                if (j0 + u >= kk) break;
+                const NnItem it = its[u];
+                if (!(it.dist < h[0].dist)) continue;
+                bool dup = false;
+                if (!single)
+                    for (int q = 0; q < num_nn; ++q) dup |= h[q * kQ].index == it.index;
+                if (!dup) nn_sift<kQ>(h, it, num_nn);
+            }
         }
     }
     for (int k = num_nn - 1; k >= 0; --k) {
         out_idx[v * num_nn + k] = h[0].index;
         out_dist[v * num_nn + k] = h[0].dist;
-        nn_sift(h, h[k], k);
+        nn_sift<kQ>(h, h[k * kQ], k);
     }
 }
 
