@@ -198,10 +198,16 @@ __device__ __forceinline__ unsigned partner32(unsigned v) {
 // upper, so both halves round the same sum; a VALU lane swap, no LDS round trip).  The main
 // loop and the re-rank tail both use this, so their biases are bitwise the same.
 template <int D>
-__device__ __forceinline__ float norm_x(const float* xs) {
+__device__ __forceinline__ float norm_part(const float* xs) {
     float X = 0.0f;
 #pragma unroll
     for (int j = 0; j < Slice<D>::XD; ++j) X = fmaf(xs[j], xs[j], X);
+    return X;
+}
+
+template <int D>
+__device__ __forceinline__ float norm_x(const float* xs) {
+    float X = norm_part<D>(xs);
     if constexpr (Slice<D>::HALF) {
         const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(X), __float_as_uint(X),
                                                          false, false);
@@ -483,6 +489,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     const unsigned xlane_off = __umul24((unsigned)r, ldx4) + xh_off;
     const char* const xm = reinterpret_cast<const char*>(x + (long long)m * D);
     const unsigned code_lane_off = (unsigned)r * (unsigned)m_total * (unsigned)sizeof(CodeT);
+    const unsigned code_pair_off = (unsigned)lane * (unsigned)m_total * (unsigned)sizeof(CodeT);
     auto load_x = [&](long long b, float* dst) {
 #ifdef PQH_ASSIGN_NOMEM   // diagnostic: every chunk re-reads the first 64 blocks (cache hits)
         b &= 63;
@@ -523,19 +530,12 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     // straight from x by packed conversions, the lo pass is decided once per chunk (a lo pass
     // over bf16-exact x adds exact zeros, so the blocks without a remainder keep their exact
     // scores and their tighter bound), and the winner's tile rides in its key.
-    auto body = [&](auto lo_c, long long blk0, float (*xs)[XD], const float* X,
-                    const bool* any_lo, const bool* finite_x) {
+    auto body = [&](auto lo_c, long long blk0, float (*xs)[XD], const float* Xg,
+                    const bool* any_lo) {
         constexpr bool LO = decltype(lo_c)::value;
-        long long row0[kNB];   // (uniform) the block's first row
-        bool valid[kNB];
         bf16x8 Bm[kNB][P::PM], Bl[kNB][P::PL];
 #pragma unroll
-        for (int b = 0; b < kNB; ++b) {
-            row0[b] = (blk0 + b) * 32;
-            // rows past n hold row n - 1 (clamped loads), never stored
-            valid[b] = row0[b] + 32 <= n || (long long)r < n - row0[b];
-            make_b<D, LO>(xs[b], h, Bm[b], Bl[b]);
-        }
+        for (int b = 0; b < kNB; ++b) make_b<D, LO>(xs[b], h, Bm[b], Bl[b]);
         // The lane's 128 scores of a block form an 8 x 16 grid: tile t (row) x accumulator
         // register i (column).  Instead of ranking every score with its index attached, two
         // partitions of the grid are reduced on the raw score bits:
@@ -644,62 +644,84 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
                 }
             }
         }
+        // the lane's 128 centroids per block: keyed group minima, top two of each partition,
+        // and the winner's row bits from its two keys
+        unsigned own1[kNB], own2[kNB], cbits[kNB];
 #pragma unroll
         for (int b = 0; b < kNB; ++b) {
-            // the lane's 128 centroids: keyed group minima, top two of each partition ...
             unsigned qk[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) qk[j] = (qg[b][j] & ~15u) | q_code_bits(j);
-            const unsigned p1 = pm1[b], p2 = pm2[b];
             unsigned q1, q2;
             top2_8(qk, q1, q2);
-            const unsigned own1 = p1;
-            const unsigned own2 = minu(p2, q2);
-            // ... then the two half-waves (lanes l and l^32 hold the same vector): after the
-            // swap, s[0] holds the lower half's value and s[1] the upper half's, in every lane
-            const auto s1 = __builtin_amdgcn_permlane32_swap(own1, own1, false, false);
-            const auto s2 = __builtin_amdgcn_permlane32_swap(own2, own2, false, false);
+            own1[b] = pm1[b];
+            own2[b] = minu(pm2[b], q2);
+            // the winner's row (tile_row): 16 (2t + g) from its P key, the rest from its Q key
+            cbits[b] = ((pm1[b] & PMASK) << 4) | (q1 & 15u) | ((unsigned)h << 2);
+        }
+        // The two half-waves hold the two halves of a vector's centroids.  Blocks are merged
+        // in pairs by one v_permlane32_swap per value: swap(block b0's, block b0 + 1's) leaves
+        // both halves of block b0's vector r in lane r and both halves of block b0 + 1's in
+        // lane r + 32 (s[0]: the lower half's value, s[1]: the upper's), so everything after
+        // the merge -- gap test, re-rank decision, store, histogram -- runs once per vector
+        // on all 64 lanes.  (An odd block count merges its last block with itself: both
+        // halves then hold the same vector and the lower half stores.)
+        constexpr int NG = (kNB + 1) / 2;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            const int ba = 2 * g, bb = 2 * g + 1 < kNB ? 2 * g + 1 : 2 * g;
+            const bool pair = ba != bb;
+            const auto s1 = __builtin_amdgcn_permlane32_swap(own1[ba], own1[bb], false, false);
+            const auto s2 = __builtin_amdgcn_permlane32_swap(own2[ba], own2[bb], false, false);
+            const auto sc = __builtin_amdgcn_permlane32_swap(cbits[ba], cbits[bb], false, false);
             const unsigned b1 = minu((unsigned)s1[0], (unsigned)s1[1]);
             const unsigned b2 = minu(minu((unsigned)s2[0], (unsigned)s2[1]),
                                      maxu((unsigned)s1[0], (unsigned)s1[1]));
-            const bool mine = own1 == b1;   // this half holds the winner (both: a tie -> slow)
-            // the winner's row (tile_row): 16 (2t + g) from its P key, the rest from its Q key
-            int code = (int)(((p1 & PMASK) << 4) | (q1 & 15u)) | (h << 2);
-            const float tau = screen_tau(X[b], any_lo[b], tq);
+            // (equal keys in the two halves: K2 = K1, the gap test fails, the slow path decides)
+            // (keys order as floats: the lower half won iff its key is the minimum)
+            int code = (int)((unsigned)s1[0] == b1 ? (unsigned)sc[0] : (unsigned)sc[1]);
+            // the lane's vector: block ba + h (pair) or ba, row r
+            const long long rowl = (blk0 + ba) * 32 + (pair ? lane : r);
+            const bool valid = rowl < n;   // rows past n hold row n - 1 (clamped loads)
+            const bool own_lane = pair || h == 0;
+            const float Xl = Xg[g];
+            const bool finite = isfinite(Xl);
+            const float tau = screen_tau(Xl, pair && h ? any_lo[bb] : any_lo[ba], tq);
             // a key differs from its score by less than 2^PB ulp (2^(PB-23) relative):
             // 2^(PB-21) of the larger magnitude covers both keys of the gap (and the rounding
             // of K2 - K1)
             constexpr float kKeySlack = PB == 4 ? 0x1p-17f : 0x1p-13f;
             const float K1 = __uint_as_float(b1), K2 = __uint_as_float(b2);
             const float KA = max_abs(K1, K2);
-            const bool slow = !(K2 - K1 > fmaf(kKeySlack, KA, tau)) || !finite_x[b];
+            const bool slow = !(K2 - K1 > fmaf(kKeySlack, KA, tau)) || !finite;
 
-            unsigned long long need = __ballot(slow && valid[b] && h == 0);
+            unsigned long long need = __ballot(slow && valid && own_lane);
             bool deferred = false;
             if (need) {
                 slow_count += __popcll(need);
                 // finite vectors go to the queue with their candidate window: every centroid
                 // that can be the fp32 argmin (or tie with it) screens below
                 // K1 + tau + 2^-16 |K1| -- see the tail; non-finite ones stay inline
-                const unsigned long long fin = need & __ballot(finite_x[b]);
+                const unsigned long long fin = need & __ballot(finite);
                 const unsigned cnt = (unsigned)__popcll(fin);
                 if (PQH_ASSIGN_DEFER && cnt && qn + cnt <= (unsigned)kRqLds) {
-                    if (slow && valid[b] && h == 0 && finite_x[b]) {
+                    if (slow && valid && own_lane && finite) {
                         const float thr = fmaf(2.0f * kKeySlack, fabsf(K1), K1 + tau);
                         rqs[wave][qn + __builtin_amdgcn_mbcnt_hi((unsigned)(fin >> 32),
                                       __builtin_amdgcn_mbcnt_lo((unsigned)fin, 0u))] =
-                            make_uint2((uint32_t)row0[b] + (uint32_t)r, __float_as_uint(thr));
+                            make_uint2((uint32_t)rowl, __float_as_uint(thr));
                     }
                     qn += cnt;
-                    deferred = finite_x[b];
+                    deferred = finite;
                     need &= ~fin;
                 }
                 unsigned long long todo = need;
-                while (todo) {   // inline exact re-rank: non-finite x, or a full segment
+                while (todo) {   // inline exact re-rank: non-finite x, or a full queue
                     const int rs = __ffsll((long long)todo) - 1;
                     todo &= todo - 1;
                     float xv[D];   // the vector's slice, re-read (a uniform address)
-                    const float* xr = x + ((blk0 + b) * 32 + rs) * ldx + (long long)m * D;
+                    const long long vrow = (blk0 + ba) * 32 + (pair ? rs : (rs & 31));
+                    const float* xr = x + vrow * ldx + (long long)m * D;
 #pragma unroll
                     for (int j = 0; j < D; ++j) xv[j] = xr[j];
                     float best = INFINITY;
@@ -719,11 +741,11 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
                     if (lane == rs) code = bidx == 0x7FFFFFFF ? 0 : bidx;
                 }
             }
-            // fast path: the winner's half stores; slow path: the lower half (inline code),
-            // unless the vector waits in the queue
-            if (valid[b] && (slow ? (h == 0 && !deferred) : mine)) {
-                *reinterpret_cast<CodeT*>(reinterpret_cast<char*>(codes + (row0[b] * m_total + m)) +
-                                          code_lane_off) = (CodeT)code;
+            // every lane stores its vector's code (the lower half only for a self-merged
+            // block), unless the vector waits in the queue
+            if (valid && own_lane && !(slow && deferred)) {
+                *reinterpret_cast<CodeT*>(reinterpret_cast<char*>(codes + ((blk0 + ba) * 32 * m_total + m)) +
+                                          (pair ? code_pair_off : code_lane_off)) = (CodeT)code;
                 if (kLdsA && counts) atomicAdd(&hist[wave][code], 1u);
             }
         }
@@ -742,20 +764,36 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         }
         return;
 #endif
-        float X[kNB];
-        bool any_lo[kNB], finite_x[kNB];
+        // ||x||^2 of the lane's vector after the block merge (see body): a pair's partial sums
+        // are merged by the same swap as the keys (lower + upper, bitwise norm_x's sum)
+        constexpr int NG = (kNB + 1) / 2;
+        float Xg[NG];
+        bool any_lo[kNB];
         bool chunk_lo = false;
 #pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            const int ba = 2 * g, bb = 2 * g + 1 < kNB ? 2 * g + 1 : 2 * g;
+            if (ba == bb) {
+                Xg[g] = norm_x<D>(xs[ba]);
+            } else if constexpr (Slice<D>::HALF) {
+                const auto sw = __builtin_amdgcn_permlane32_swap(
+                    __float_as_uint(norm_part<D>(xs[ba])), __float_as_uint(norm_part<D>(xs[bb])),
+                    false, false);
+                Xg[g] = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+            } else {
+                const float xa_ = norm_x<D>(xs[ba]), xb_ = norm_x<D>(xs[bb]);
+                Xg[g] = h ? xb_ : xa_;
+            }
+        }
+#pragma unroll
         for (int b = 0; b < kNB; ++b) {
-            X[b] = norm_x<D>(xs[b]);
             any_lo[b] = __any(has_lo<D>(xs[b]));
-            finite_x[b] = isfinite(X[b]);
             chunk_lo |= any_lo[b];
         }
         if (chunk_lo)
-            body(std::true_type{}, blk0, xs, X, any_lo, finite_x);
+            body(std::true_type{}, blk0, xs, Xg, any_lo);
         else
-            body(std::false_type{}, blk0, xs, X, any_lo, finite_x);
+            body(std::false_type{}, blk0, xs, Xg, any_lo);
     };
 
     // Chunk schedule (a chunk = kNB blocks = one step).  Wave w of the subspace (w = bx
