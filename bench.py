@@ -108,6 +108,8 @@ def parse():
                          "multi-rank schedule with every rank on one GPU, --one-device)")
     ap.add_argument("--one-device", action="store_true",
                     help="every rank uses GPU 0 (schedule rehearsal on a one-GPU box)")
+    ap.add_argument("--timeline", action="store_true",
+                    help="(diagnostic) print every timed stage's start/end in ms from the first")
     ap.add_argument("--dump", default="",
                     help="write the last batch's stitched stream and all ranks' codes to this "
                          ".npz on rank 0 (parity tests)")
@@ -524,6 +526,11 @@ def main():
     state["timed"] = False
     for name, e0, e1 in events:
         acc[name] += e0.elapsed_time(e1) / 1e3
+    if args.timeline and rank == 0 and events:
+        f0 = events[0][1]
+        for i, (name, e0, e1) in enumerate(events):
+            print(f"TL {i:3d} {name:9s} {f0.elapsed_time(e0):8.3f} {f0.elapsed_time(e1):8.3f}",
+                  file=sys.stderr)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

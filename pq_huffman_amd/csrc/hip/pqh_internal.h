@@ -96,8 +96,7 @@ struct pqh_tables {
     uint16_t* d_lut1 = nullptr;
     uint16_t* d_lut2 = nullptr;
     uint32_t* d_meta = nullptr;
-    uint32_t* d_scratch = nullptr;   // per-table sizes for the allocation scan
     pqh_long_code* d_long = nullptr;
     uint32_t* d_long_cnt = nullptr;
-    uint32_t* d_err = nullptr;       // [0] code too long
+    uint32_t* d_err = nullptr;       // [0] code too long; [2..3] the LUT pool head (u64)
 };

@@ -9,9 +9,9 @@
 //               carry (weight << 16 | node) so a comparison is one LDS read; all per-tree
 //               arrays are interleaved tree-minor so the 32 lanes of a wave hit 32
 //               consecutive LDS words.
-//  lut_plan/alloc/fill  two-level decode tables per alphabet: a first level of up to 2^11
+//  lut_build    two-level decode tables per alphabet: a first level of up to 2^11
 //               entries (2^9 in context mode, where there are K*m alphabets), second-level
-//               subtables for the prefixes of longer codes, allocated by a device scan.
+//               subtables for the prefixes of longer codes, ranges taken from a pool head.
 //  dec_chunks   huffman_decoder.c:211-255: one lane per chunk of C vectors; a symbol costs
 //               one table load instead of one trie step per bit (huffman_decode.c:137-191).
 #include <algorithm>
@@ -909,8 +909,7 @@ huff_trees_par(const uint32_t* __restrict__ counts, int k, long long trees,
 //   L2: per alphabet `nsub` subtables of one width w2 (the widest prefix needs, <= 8):
 //       entry (rem << 12) | sym, or 15 << 12 for codes longer than W1 + w2 (long list).
 //   meta[alphabet] = l2base << 9 | noL2 << 8 | w2 << 4 | W1   (l2base < 2^23)
-// lut_plan sizes every alphabet, lut_alloc (one workgroup) scans the sizes into pool
-// offsets, lut_fill writes the entries.
+// lut_build sizes every alphabet, takes its L2 range from the pool and writes the entries.
 constexpr int kL1Max = 11;
 constexpr long long kL2BaseMax = 1ll << 23;
 
@@ -930,94 +929,23 @@ __device__ void block_w2max(const unsigned long long* e, int k, int w1, int l2_b
     __syncthreads();
 }
 
-__device__ __forceinline__ uint32_t block_sum_u32(uint32_t v, uint32_t* red /* LDS [4] */) {
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-    __syncthreads();
-    return red[0] + red[1] + red[2] + red[3];
-}
-
-__device__ __forceinline__ uint32_t block_max_u32(uint32_t v, uint32_t* red /* LDS [4] */) {
-    for (int off = 32; off >= 1; off >>= 1) v = max(v, (uint32_t)__shfl_xor(v, off));
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-    __syncthreads();
-    return max(max(red[0], red[1]), max(red[2], red[3]));
-}
-
+// One workgroup per alphabet: size its second level, take the pool range with one atomic
+// on the build's pool head (zeroed with the error word before the trees), write both levels.
+// (Pool ranges are taken in completion order, so two builds may place an alphabet's
+// subtables differently; the tables they describe are the same.  An alphabet whose range
+// would pass the pool's end keeps only L1: its long codes go to the long list.)
 __global__ void __launch_bounds__(256)
-lut_plan(const unsigned long long* __restrict__ enc, int k, int w1, int l2_bits,
-         uint32_t* __restrict__ meta, uint32_t* __restrict__ sizes) {
-    __shared__ uint32_t w2max[1 << kL1Max];
-    __shared__ uint32_t red[4];
-    const long long t = blockIdx.x;
-    block_w2max(enc + t * k, k, w1, l2_bits, w2max);
-    uint32_t nsub = 0, w2 = 0;
-    for (int i = threadIdx.x; i < (1 << w1); i += blockDim.x)
-        if (w2max[i]) {
-            ++nsub;
-            w2 = max(w2, w2max[i]);
-        }
-    nsub = block_sum_u32(nsub, red);
-    w2 = block_max_u32(w2, red);
-    if (threadIdx.x == 0) {
-        meta[t] = (w2 << 4) | (uint32_t)w1;
-        sizes[t] = nsub < 4095 ? nsub << w2 : 0xFFFFFFFFu;   // sub ids must fit 12 bits
-    }
-}
-
-// one workgroup: exclusive scan of the L2 entry counts; an alphabet that does not fit (or
-// has too many subtables) keeps only L1 (noL2 flag: its long codes go to the long list)
-__global__ void __launch_bounds__(1024)
-lut_alloc(long long tables, long long lut2_cap, uint32_t* __restrict__ meta,
-          uint32_t* __restrict__ sizes) {
-    __shared__ unsigned long long ws[16];
-    __shared__ unsigned long long carry;
-    if (threadIdx.x == 0) carry = 0;
-    __syncthreads();
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (long long base = 0; base < tables; base += blockDim.x) {
-        const long long i = base + threadIdx.x;
-        const uint32_t sz = i < tables ? sizes[i] : 0u;
-        const unsigned long long b = sz == 0xFFFFFFFFu ? 0ull : sz;
-        unsigned long long inc = b;
-        for (int off = 1; off < 64; off <<= 1) {
-            const unsigned long long y = __shfl_up(inc, off);
-            if (lane >= off) inc += y;
-        }
-        if (lane == 63) ws[wid] = inc;
-        __syncthreads();
-        unsigned long long before = carry;
-        for (int q = 0; q < wid; ++q) before += ws[q];
-        if (i < tables) {
-            const unsigned long long l0 = before + inc - b;
-            const bool fits = sz != 0xFFFFFFFFu && l0 + b <= (unsigned long long)lut2_cap;
-            const uint32_t low = meta[i] & 0xFFu;
-            meta[i] = fits ? (uint32_t)((l0 << 9) | low) : (0x100u | low);
-        }
-        __syncthreads();
-        if (threadIdx.x == blockDim.x - 1) carry = before + inc;
-        __syncthreads();
-    }
-}
-
-__global__ void __launch_bounds__(256)
-lut_fill(const unsigned long long* __restrict__ enc, uint32_t* __restrict__ enc32, int k,
-         int l2_bits, const uint32_t* __restrict__ meta, uint16_t* __restrict__ lut1,
-         uint16_t* __restrict__ lut2, long long lut2_cap, pqh_long_code* __restrict__ longs,
-         uint32_t* __restrict__ long_cnt) {
+lut_build(const unsigned long long* __restrict__ enc, uint32_t* __restrict__ enc32, int k, int w1,
+          int l2_bits, uint32_t* __restrict__ meta, uint16_t* __restrict__ lut1,
+          uint16_t* __restrict__ lut2, long long lut2_cap, pqh_long_code* __restrict__ longs,
+          uint32_t* __restrict__ long_cnt, unsigned long long* __restrict__ pool_head) {
     __shared__ uint32_t w2max[1 << kL1Max];
     __shared__ uint32_t sub_id[1 << kL1Max];
-    __shared__ uint32_t nlong, nsub;
+    __shared__ uint32_t nlong, nsub, w2s;
+    __shared__ unsigned long long base_s;
     __shared__ uint32_t part[256];
     const long long t = blockIdx.x;
     const unsigned long long* e = enc + t * k;
-    const uint32_t mt = meta[t];
-    const int w1 = (int)(mt & 15u);
-    const int w2 = (int)((mt >> 4) & 15u);
-    const bool subs = !(mt & 0x100u) && w2 > 0;
-    const long long l2base = (long long)(mt >> 9);
     uint16_t* L1 = lut1 + (t << kL1Max);
     block_w2max(e, k, w1, l2_bits, w2max);
     // subtable ids in prefix order: per-thread chunk counts, then a block-wide exclusive
@@ -1048,7 +976,31 @@ lut_fill(const unsigned long long* __restrict__ enc, uint32_t* __restrict__ enc3
         }
         c_id = before + incl - c_id;
     }
+    {   // the widest remainder over the prefixes: the subtables' width
+        uint32_t w = 0;
+        for (int p = p0; p < p1; ++p) w = max(w, w2max[p]);
+        for (int off = 32; off >= 1; off >>= 1) w = max(w, (uint32_t)__shfl_xor(w, off));
+        __syncthreads();   // (part[] was read above)
+        if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = w;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t w2 = 0;
+            for (int q = 0; q < (int)blockDim.x / 64; ++q) w2 = max(w2, part[q]);
+            w2s = w2;
+            // sub ids must fit 12 bits; an alphabet without long codes takes no range
+            const bool ok = nsub < 4095;
+            const unsigned long long size = ok ? (unsigned long long)nsub << w2 : 0ull;
+            const unsigned long long l0 = size ? atomicAdd(pool_head, size) : 0ull;
+            const bool fits = ok && l0 + size <= (unsigned long long)lut2_cap;
+            base_s = fits ? l0 : ~0ull;
+            meta[t] = fits ? (uint32_t)((l0 << 9) | (w2 << 4) | (uint32_t)w1)
+                           : (0x100u | (w2 << 4) | (uint32_t)w1);
+        }
+    }
     __syncthreads();
+    const int w2 = (int)w2s;
+    const bool subs = base_s != ~0ull && w2 > 0;
+    const long long l2base = subs ? (long long)base_s : 0;
     for (int p = p0; p < p1; ++p)
         if (w2max[p]) sub_id[p] = c_id++;
     for (int i = threadIdx.x; i < np; i += blockDim.x) L1[i] = 0;
@@ -1415,7 +1367,6 @@ int pqh_tables_alloc(pqh_ctx_t* ctx, int m, int k, int context, pqh_tables_t** o
         hipMalloc(&t->d_lut1, (size_t)(t->tables << kL1Max) * 2) != hipSuccess ||
         hipMalloc(&t->d_lut2, (size_t)t->lut2_cap * 2) != hipSuccess ||
         hipMalloc(&t->d_meta, (size_t)t->tables * 4 + 16) != hipSuccess ||
-        hipMalloc(&t->d_scratch, (size_t)t->tables * 8 + 16) != hipSuccess ||
         hipMalloc(&t->d_long, (size_t)t->tables * k * sizeof(pqh_long_code)) != hipSuccess ||
         hipMalloc(&t->d_long_cnt, (size_t)t->tables * 4) != hipSuccess ||
         hipMalloc(&t->d_err, 16) != hipSuccess) {
@@ -1432,8 +1383,8 @@ int pqh_tables_destroy(pqh_tables_t* t) {
         (void)hipSetDevice(t->ctx->device);
         (void)hipStreamSynchronize(t->ctx->stream);
     }
-    void* bufs[] = {t->d_enc, t->d_enc32, t->d_lut1, t->d_lut2, t->d_meta, t->d_scratch,
-                    t->d_long, t->d_long_cnt, t->d_err};
+    void* bufs[] = {t->d_enc, t->d_enc32, t->d_lut1, t->d_lut2, t->d_meta, t->d_long,
+                    t->d_long_cnt, t->d_err};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     delete t;
@@ -1441,15 +1392,11 @@ int pqh_tables_destroy(pqh_tables_t* t) {
 }
 
 static int launch_luts(pqh_ctx* ctx, pqh_tables* t) {
-    hipLaunchKernelGGL(lut_plan, dim3((unsigned)t->tables), dim3(256), 0, ctx->stream, t->d_enc,
-                       t->k, t->l1_bits, t->l2_bits, t->d_meta, t->d_scratch);
-    PQH_LAUNCH_CHECK(ctx);
-    hipLaunchKernelGGL(lut_alloc, dim3(1), dim3(1024), 0, ctx->stream, t->tables, t->lut2_cap,
-                       t->d_meta, t->d_scratch);
-    PQH_LAUNCH_CHECK(ctx);
-    hipLaunchKernelGGL(lut_fill, dim3((unsigned)t->tables), dim3(256), 0, ctx->stream, t->d_enc,
-                       t->d_enc32, t->k, t->l2_bits, t->d_meta, t->d_lut1, t->d_lut2, t->lut2_cap, t->d_long,
-                       t->d_long_cnt);
+    // (the pool head, d_err[2..3], was zeroed with the error word before the trees)
+    hipLaunchKernelGGL(lut_build, dim3((unsigned)t->tables), dim3(256), 0, ctx->stream, t->d_enc,
+                       t->d_enc32, t->k, t->l1_bits, t->l2_bits, t->d_meta, t->d_lut1, t->d_lut2,
+                       t->lut2_cap, t->d_long, t->d_long_cnt,
+                       reinterpret_cast<unsigned long long*>(t->d_err + 2));
     PQH_LAUNCH_CHECK(ctx);
     return PQH_OK;
 }
@@ -1465,7 +1412,7 @@ int pqh_tables_build_impl(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_cou
     if (which < PQH_TREES_DEFAULT || which > PQH_TREES_WAVE) return PQH_ERR_ARG;
     int rc = pqh_use_device(ctx);
     if (rc) return rc;
-    PQH_HIP(ctx, hipMemsetAsync(t->d_err, 0, 4, ctx->stream));
+    PQH_HIP(ctx, hipMemsetAsync(t->d_err, 0, 16, ctx->stream));   // error word + LUT pool head
     if (reinterpret_cast<uintptr_t>(d_counts) & 15u) return PQH_ERR_ARG;
     const long long trees = t->tables;
     // Two builds of the same trees:
@@ -1553,7 +1500,7 @@ int pqh_tables_upload(pqh_ctx_t* ctx, pqh_tables_t* t, const huffman_codebook_t*
             for (int b = 0; b < c.bit_length; ++b) v = (v << 1) | ((c.code[b >> 3] >> (7 - (b & 7))) & 1u);
             h[(size_t)i * t->items + it] = ((unsigned long long)c.bit_length << 56) | v;
         }
-    PQH_HIP(ctx, hipMemsetAsync(t->d_err, 0, 4, ctx->stream));
+    PQH_HIP(ctx, hipMemsetAsync(t->d_err, 0, 16, ctx->stream));   // error word + LUT pool head
     PQH_HIP(ctx, hipMemcpyAsync(t->d_enc, h.data(), h.size() * 8, hipMemcpyHostToDevice, ctx->stream));
     rc = launch_luts(ctx, t);
     if (rc) return rc;
