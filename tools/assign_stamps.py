@@ -14,7 +14,7 @@ from pq_huffman_amd.capi import lib  # noqa: E402
 
 def main():
     dev = torch.device("cuda", 0)
-    n, d, m, k = 1_000_000, 128, 8, 256
+    n, d, m, k = int(os.environ.get("BENCH_ASSIGN_N", 1_000_000)), 128, 8, 256
     x = bench.make_data(torch, n, d, 1234, 0, dev)
     cent = bench.train_centroids(torch, x, m, k)
     ctx = codec.Context(0)

@@ -34,7 +34,7 @@ def centroids_from_rows(x, m, k, seed):
 def run(reps, name):
     d, m, k = CONFIGS[name]
     dev = torch.device("cuda", 0)
-    n = 1_000_000
+    n = int(os.environ.get("BENCH_ASSIGN_N", 1_000_000))
     x = bench.make_data(torch, n, d, 1234, 0, dev) if name != "deep" else \
         torch.nn.functional.normalize(torch.randn((n, d), device=dev,
                                                   generator=torch.Generator(device=dev).manual_seed(7)), dim=1)
