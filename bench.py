@@ -108,6 +108,10 @@ def parse():
                          "multi-rank schedule with every rank on one GPU, --one-device)")
     ap.add_argument("--one-device", action="store_true",
                     help="every rank uses GPU 0 (schedule rehearsal on a one-GPU box)")
+    ap.add_argument("--lut-on", choices=["lanes", "assign"], default="lanes",
+                    help="where a batch's decode tables are built: on its table lane after the "
+                         "trees, or on the assignment stream --lut-lag batches later")
+    ap.add_argument("--lut-lag", type=int, default=2)
     ap.add_argument("--timeline", action="store_true",
                     help="(diagnostic) print every timed stage's start/end in ms from the first")
     ap.add_argument("--dump", default="",
@@ -341,6 +345,10 @@ def main():
     ev_hist = [torch.cuda.Event() for _ in range(slots)]
     ev_tab = [torch.cuda.Event() for _ in range(slots)]
     ev_enc = [torch.cuda.Event() for _ in range(slots)]
+    ev_trees = [torch.cuda.Event() for _ in range(slots)]
+    lut_a = args.lut_on == "assign" and not serial
+    dl = max(1, min(args.lut_lag, nl * (1 if elanes is lanes else max(1, args.tbufs)) - 1)) \
+        if lut_a else 0
     used = [False] * slots    # slot s has held a batch (its events were recorded)
     chunks = (n + args.chunk - 1) // args.chunk
     # code tables: one set per lane; two per table lane when encode/decode have streams of
@@ -359,7 +367,7 @@ def main():
            for _ in elanes]
     tot_dev = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in elanes]
     raw_first = shard.raw_first(rank)
-    stages = ("assign", "sort", "hist", "codebook", "encode", "decode")
+    stages = ("assign", "sort", "hist", "codebook", "lut", "encode", "decode")
     if args.sort and (k > 256 or world > 1):
         raise SystemExit("--sort: one rank, K <= 256 (the distributed sort is shard.py's)")
     sort_tmp = torch.empty((n, m), dtype=torch.uint8, device=dev) if args.sort else None
@@ -448,9 +456,27 @@ def main():
             # the assignment stream has nothing left to do: there the one-wavefront-per-tree
             # build (lower latency, more waves) shortens the drain (--drain-trees).
             last = i == state["nsteps"] - 1 and args.drain_trees == "wave"
-            tabs[ti].build(counts[s], c, trees="wave" if last else None)
-            done(e, sL)
-            ev_tab[s].record(sL)
+            if lut_a:   # trees here, the decode tables on A dl batches later (lut())
+                tabs[ti].build_trees(counts[s], c, trees="wave" if last else None)
+                done(e, sL)
+                ev_trees[s].record(sL)
+            else:
+                tabs[ti].build(counts[s], c, trees="wave" if last else None)
+                done(e, sL)
+                ev_tab[s].record(sL)
+        if lut_a and i >= dl:
+            lut(i - dl)
+
+    def lut(i):
+        """batch i's decode tables on the assignment stream (which has slack: it waits for
+        free code buffers), after its trees on the lane"""
+        s = i % slots
+        with torch.cuda.stream(sA):
+            sA.wait_event(ev_trees[s])
+            e = rec("lut", sA)
+            tabs[tab_index(i)].build_luts(ctx)
+            done(e, sA)
+            ev_tab[s].record(sA)
 
     def back(i):
         """batch i: encode + decode on its lane (queued behind its tables) or on its
@@ -495,6 +521,7 @@ def main():
     # histogram collectives of batch i + lag, so those never queue behind a table build.
     # (back(i) must be issued before front(i + lanes * nbuf) waits for its decode)
     lag = 0 if world == 1 or serial else nl * nbuf - 1
+    lag = max(lag, dl)   # (back(i) is issued after lut(i))
 
     def run(steps):
         state["nsteps"] = steps
@@ -504,6 +531,8 @@ def main():
             front(i)
             if i >= lag:
                 back(i - lag)
+        for i in range(max(0, steps - dl), steps) if lut_a else ():
+            lut(i)
         for i in range(max(0, steps - lag), steps):
             back(i)
 
@@ -568,7 +597,7 @@ def main():
         vec_read, vec_write = 4 * d, m * code_bytes
         achieved = (vec_read + vec_write) * n / t_assign / 1e9
         traffic, traffic_src, prof_avg_us = pmc_traffic("pq_assign_mfma")
-        t_enc = (acc["assign"] + acc["hist"] + acc["codebook"] + acc["encode"]) / args.steps
+        t_enc = (acc["assign"] + acc["hist"] + acc["codebook"] + acc["lut"] + acc["encode"]) / args.steps
         tf = 2.0 * k * d * n / t_assign / 1e12   # algorithmic: 2 K D flop per vector
         workload = {
             "sift": f"SIFT1M-shaped: {n:,} x 128-d fp32 per GPU, M=8, K=256, ",

@@ -132,6 +132,11 @@ int pqh_tables_build(pqh_ctx_t* ctx, pqh_tables_t* tables, const uint32_t* d_cou
  * Every choice builds the same tables. */
 enum { PQH_TREES_DEFAULT = 0, PQH_TREES_LANE = 1, PQH_TREES_WAVE = 2 };
 int pqh_tables_build_impl(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts, int which);
+/* The two halves of pqh_tables_build_impl, for callers that run them on different streams:
+ * the Huffman trees (code table) on ctx's stream, then -- after the caller orders it behind
+ * the trees (an event) -- the decode tables and the encoder's gather copy on ctx's stream. */
+int pqh_tables_build_trees(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts, int which);
+int pqh_tables_build_luts(pqh_ctx_t* ctx, pqh_tables_t* t);
 /* Load codes from m host codebooks (e.g. huffman_codebooks.bin read by huffman_codebook_load). */
 int pqh_tables_upload(pqh_ctx_t* ctx, pqh_tables_t* tables, const huffman_codebook_t* codebooks);
 /* alloc + upload */

@@ -280,6 +280,20 @@ class Tables:
               "pqh_tables_build")
         return self
 
+    def build_trees(self, counts, ctx: Context = None, trees: str = None) -> "Tables":
+        """The first half of build(): the Huffman trees only (on `ctx`'s stream)."""
+        c = ctx or self.ctx
+        check(lib().pqh_tables_build_trees(c.ptr, self.ptr, _ptr(counts), self.TREES[trees]),
+              "pqh_tables_build_trees")
+        return self
+
+    def build_luts(self, ctx: Context = None) -> "Tables":
+        """The second half of build(): decode tables + the encoder's gather copy, on
+        `ctx`'s stream, which the caller has ordered behind build_trees (an event)."""
+        c = ctx or self.ctx
+        check(lib().pqh_tables_build_luts(c.ptr, self.ptr), "pqh_tables_build_luts")
+        return self
+
     def status(self) -> None:
         st = lib().pqh_tables_status(self.ctx.ptr, self.ptr)
         if st:

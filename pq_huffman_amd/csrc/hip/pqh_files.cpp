@@ -111,10 +111,15 @@ extern "C" int pqh_encode_files(const unsigned char* codes, long long n, int m,
         return pqh_set_error(ctx, PQH_ERR_ARG, "cannot write codebooks");
     }
     uint32_t mu = (uint32_t)m;
-    fwrite(&mu, 4, 1, cf);
+    bool cok = fwrite(&mu, 4, 1, cf) == 1;
     for (int i = 0; i < m; ++i) huffman_codebook_save(&cbs[i], cf);
-    fclose(cf);
+    cok = !ferror(cf) && cok;
+    cok = fclose(cf) == 0 && cok;
     for (auto& cb : cbs) huffman_codebook_destroy(&cb);
+    if (!cok) {
+        pqh_tables_destroy(tab);
+        return pqh_set_error(ctx, PQH_ERR_ARG, "cannot write codebooks");
+    }
 
     DevBuf<unsigned long long> d_total;
     const long long chunks = (n + opt.chunk_vectors - 1) / opt.chunk_vectors;
@@ -154,10 +159,13 @@ extern "C" int pqh_encode_files(const unsigned char* codes, long long n, int m,
     FILE* ef = fopen(path_of(out_prefix, "huffman_indices.bin").c_str(), "wb");
     if (!ef) return pqh_set_error(ctx, PQH_ERR_ARG, "cannot write indices");
     unsigned long long nn = (unsigned long long)n;
-    fwrite(&nn, 8, 1, ef);
-    fwrite(stream.data(), 1, bytes, ef);
-    fclose(ef);
+    bool wok = fwrite(&nn, 8, 1, ef) == 1;
+    wok = fwrite(stream.data(), 1, bytes, ef) == bytes && wok;
+    wok = fclose(ef) == 0 && wok;
+    if (!wok) return pqh_set_error(ctx, PQH_ERR_ARG, "cannot write indices");
 
+    // the sidecar is optional (the decoder rebuilds the chunk index without it), but a
+    // partly written one is an error
     FILE* sf = fopen(path_of(out_prefix, "huffman_chunks.bin").c_str(), "wb");
     if (sf) {
         Sidecar h;
@@ -170,10 +178,11 @@ extern "C" int pqh_encode_files(const unsigned char* codes, long long n, int m,
         h.raw_first = 1;
         h.n = n;
         h.chunks = chunks;
-        fwrite(&h, sizeof(h), 1, sf);
-        fwrite(coff.data(), 8, chunks, sf);
-        if (opt.context) fwrite(cprev.data(), 1, (size_t)chunks * m, sf);
-        fclose(sf);
+        bool sok = fwrite(&h, sizeof(h), 1, sf) == 1;
+        sok = (long long)fwrite(coff.data(), 8, chunks, sf) == chunks && sok;
+        if (opt.context) sok = fwrite(cprev.data(), 1, (size_t)chunks * m, sf) == (size_t)chunks * m && sok;
+        sok = fclose(sf) == 0 && sok;
+        if (!sok) return pqh_set_error(ctx, PQH_ERR_ARG, "cannot write huffman_chunks.bin");
     }
     return PQH_OK;
 }

@@ -1405,7 +1405,25 @@ int pqh_tables_build(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts) 
     return pqh_tables_build_impl(ctx, t, d_counts, PQH_TREES_DEFAULT);
 }
 
+static int build_trees(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts, int which);
+
 int pqh_tables_build_impl(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts, int which) {
+    const int rc = build_trees(ctx, t, d_counts, which);
+    return rc ? rc : launch_luts(ctx, t);
+}
+
+int pqh_tables_build_trees(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts, int which) {
+    return build_trees(ctx, t, d_counts, which);
+}
+
+int pqh_tables_build_luts(pqh_ctx_t* ctx, pqh_tables_t* t) {
+    if (!ctx || !t || !t->ctx || t->ctx->device != ctx->device) return PQH_ERR_ARG;
+    const int rc = pqh_use_device(ctx);
+    return rc ? rc : launch_luts(ctx, t);
+}
+
+// the code tables' trees (d_enc) on ctx's stream; the decode tables follow (launch_luts)
+static int build_trees(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts, int which) {
     // any context of the tables' device may run the build (on its own stream), so the
     // builds of consecutive batches can overlap on different streams
     if (!ctx || !t || !d_counts || !t->ctx || t->ctx->device != ctx->device) return PQH_ERR_ARG;
@@ -1431,7 +1449,7 @@ int pqh_tables_build_impl(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_cou
                            dim3(64 * kTreeWaves), 0, ctx->stream, d_counts, t->k, trees, t->d_enc,
                            t->d_err);
         PQH_LAUNCH_CHECK(ctx);
-        return launch_luts(ctx, t);
+        return PQH_OK;
     }
     // (every build writes every entry, 0 for symbols that never occur: no memset)
     if (t->k <= 256) {
@@ -1472,7 +1490,7 @@ int pqh_tables_build_impl(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_cou
                            lds, ctx->stream, d_counts, t->k, trees, t->d_enc, t->d_err);
     }
     PQH_LAUNCH_CHECK(ctx);
-    return launch_luts(ctx, t);
+    return PQH_OK;
 }
 
 // diagnostics only: phase stamps (s_memtime) of tree 0 of the last huff_trees launch
