@@ -112,6 +112,9 @@ def parse():
                     help="where a batch's decode tables are built: on its table lane after the "
                          "trees, or on the assignment stream --lut-lag batches later")
     ap.add_argument("--lut-lag", type=int, default=2)
+    ap.add_argument("--pair-tables", action="store_true",
+                    help="a table lane builds two consecutive batches' code tables in one "
+                         "tree launch (pqh_tables_build_pair)")
     ap.add_argument("--timeline", action="store_true",
                     help="(diagnostic) print every timed stage's start/end in ms from the first")
     ap.add_argument("--dump", default="",
@@ -354,10 +357,18 @@ def main():
     # code tables: one set per lane; two per table lane when encode/decode have streams of
     # their own, so a lane builds batch i + lanes's tables while batch i's are still read
     nbuf = 1 if elanes is lanes else max(1, args.tbufs)
+    pair = args.pair_tables and not serial and elanes is not lanes
+    if pair:
+        nbuf = 2 * max(1, args.tbufs)   # two batches per build, double-buffered
     tabs = [codec.Tables(c, m, k, ctxm) for c in lanes for _ in range(nbuf)]
     ev_dec = [torch.cuda.Event() for _ in tabs]    # last decode that read tabs[t]
 
+    def lane_of(i):
+        return (i // 2) % nl if pair else i % nl
+
     def tab_index(i):
+        if pair:   # lane (i // 2) % nl, pair buffer (i // 2 // nl) % (nbuf / 2), member i % 2
+            return lane_of(i) * nbuf + ((i // 2) // nl) % (nbuf // 2) * 2 + i % 2
         return (i % nl) * nbuf + (i // nl) % nbuf
     dec = [torch.empty((n, m), dtype=code_t, device=dev) for _ in elanes]
     coff = [torch.empty(chunks, dtype=torch.int64, device=dev) for _ in elanes]
@@ -413,7 +424,7 @@ def main():
 
     def front(i):
         """batch i: assignment + histogram on A, then its code tables on its lane"""
-        s, j = i % slots, i % nl
+        s, j = i % slots, lane_of(i)
         c = lanes[j]
         sL = c.stream
         cF, sF = ctx, sA             # the stream of assignment + histogram
@@ -447,6 +458,23 @@ def main():
                               accumulate=True)
             reduce(s)
         used[s] = True
+        if pair and i % 2 == 0 and i != state["nsteps"] - 1:
+            return                   # built with batch i + 1 (its partner)
+        if pair and i % 2 == 1:
+            with torch.cuda.stream(sL):
+                s0, t0i, ti = (i - 1) % slots, tab_index(i - 1), tab_index(i)
+                sL.wait_event(ev_dec[t0i])
+                sL.wait_event(ev_dec[ti])
+                e = rec("codebook", sL)
+                if i == state["nsteps"] - 1 and args.drain_trees == "wave":
+                    tabs[t0i].build(counts[s0], c, trees="wave")   # the drain: lower latency
+                    tabs[ti].build(counts[s], c, trees="wave")
+                else:
+                    tabs[t0i].build_pair(counts[s0], tabs[ti], counts[s], c)
+                done(e, sL)
+                ev_tab[s0].record(sL)
+                ev_tab[s].record(sL)
+            return
         with torch.cuda.stream(sL):
             ti = tab_index(i)
             if elanes is not lanes:              # tabs[ti] free: its last decode is done
@@ -522,6 +550,8 @@ def main():
     # (back(i) must be issued before front(i + lanes * nbuf) waits for its decode)
     lag = 0 if world == 1 or serial else nl * nbuf - 1
     lag = max(lag, dl)   # (back(i) is issued after lut(i))
+    if pair:
+        lag = max(lag, 1)    # (back(i) is issued after its pair's build)
 
     def run(steps):
         state["nsteps"] = steps

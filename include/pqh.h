@@ -137,6 +137,11 @@ int pqh_tables_build_impl(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_cou
  * the trees (an event) -- the decode tables and the encoder's gather copy on ctx's stream. */
 int pqh_tables_build_trees(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts, int which);
 int pqh_tables_build_luts(pqh_ctx_t* ctx, pqh_tables_t* t);
+/* Two table sets (same m, K <= 256, mode) built by one launch of the one-lane-per-tree
+ * build: twice the trees in one latency-bound pass, for a caller whose table builds are the
+ * bound; then both sets' decode tables.  Same tables as two pqh_tables_build calls. */
+int pqh_tables_build_pair(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts,
+                          pqh_tables_t* t2, const uint32_t* d_counts2);
 /* Load codes from m host codebooks (e.g. huffman_codebooks.bin read by huffman_codebook_load). */
 int pqh_tables_upload(pqh_ctx_t* ctx, pqh_tables_t* tables, const huffman_codebook_t* codebooks);
 /* alloc + upload */

@@ -287,6 +287,14 @@ class Tables:
               "pqh_tables_build_trees")
         return self
 
+    def build_pair(self, counts, other: "Tables", counts2, ctx: Context = None) -> "Tables":
+        """This table set from `counts` and `other` from `counts2` in one tree launch
+        (pqh_tables_build_pair: the same tables as two build() calls)."""
+        c = ctx or self.ctx
+        check(lib().pqh_tables_build_pair(c.ptr, self.ptr, _ptr(counts), other.ptr, _ptr(counts2)),
+              "pqh_tables_build_pair")
+        return self
+
     def build_luts(self, ctx: Context = None) -> "Tables":
         """The second half of build(): decode tables + the encoder's gather copy, on
         `ctx`'s stream, which the caller has ordered behind build_trees (an event)."""

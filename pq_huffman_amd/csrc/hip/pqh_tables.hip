@@ -33,12 +33,29 @@ constexpr unsigned long long kCodeMask = (1ull << 56) - 1;
 // the lanes of a wave touch consecutive words.  Keys are (weight << NB | node): a 32-bit key
 // (NB = 9) when the tree's total weight is below 2^23, else 64-bit (NB = 16).  Comparisons
 // use the weight only, exactly as the reference heap does.
-template <typename Key, int NB, int TPW, int CAP>
+// SPLIT (64-bit keys in a u32 column): entry i is the words [2i * TPW] (low) and
+// [(2i + 1) * TPW] (high) of the lane's own u32 column, so a 64-bit heap touches only the
+// slots of its own tree and the u32 sentinel heaps of the other lanes of the workgroup --
+// whose branch may run after this one -- keep their sentinels.
+template <typename Key, int NB, int TPW, int CAP, bool SPLIT = false>
 struct LdsHeap {
-    Key* h;
+    using Word = typename std::conditional<SPLIT, uint32_t, Key>::type;
+    Word* h;
     int size;
-    __device__ __forceinline__ Key get(int i) const { return h[i * TPW]; }
-    __device__ __forceinline__ void set(int i, Key v) { h[i * TPW] = v; }
+    __device__ __forceinline__ Key get(int i) const {
+        if constexpr (SPLIT)
+            return (Key)h[2 * i * TPW] | ((Key)h[(2 * i + 1) * TPW] << 32);
+        else
+            return h[i * TPW];
+    }
+    __device__ __forceinline__ void set(int i, Key v) {
+        if constexpr (SPLIT) {
+            h[2 * i * TPW] = (uint32_t)v;
+            h[(2 * i + 1) * TPW] = (uint32_t)(v >> 32);
+        } else {
+            h[i * TPW] = v;
+        }
+    }
     // huffman_encode.c:33-46: sift up while strictly lighter than the parent.  The first
     // three ancestors are read in one round trip (most pushes stop within them).
     __device__ __forceinline__ void push(Key e) {
@@ -134,10 +151,10 @@ __device__ __forceinline__ void scan_counts(const uint32_t* __restrict__ cnt, in
 // Merge loop of huffman_codebook_init_encoder (huffman_encode.c:150-190) on one lane's heap:
 // the nz leaves (counts lcnt, in symbol order) are pushed, then pop two / push their sum
 // until one node is left.  Returns the node count; kid[q - nz] = children of internal node q.
-template <typename Key, int NB, int TPW, int CAP>
-__device__ __forceinline__ int merge_tree(Key* heap_base, const uint32_t* lcnt, int nz,
-                                          uint32_t* kid) {
-    LdsHeap<Key, NB, TPW, CAP> hp{heap_base, 0};
+template <typename Key, int NB, int TPW, int CAP, bool SPLIT = false>
+__device__ __forceinline__ int merge_tree(typename LdsHeap<Key, NB, TPW, CAP, SPLIT>::Word* heap_base,
+                                          const uint32_t* lcnt, int nz, uint32_t* kid) {
+    LdsHeap<Key, NB, TPW, CAP, SPLIT> hp{heap_base, 0};
     for (int j = 0; j < nz; ++j) hp.push(((Key)lcnt[j * TPW] << NB) | (Key)j);
     int next = nz;
     const Key nmask = ((Key)1 << NB) - 1;
@@ -529,7 +546,22 @@ huff_trees_wave(const uint32_t* __restrict__ counts, int k, long long trees,
 template <int TPW>
 __global__ void __launch_bounds__(64)
 huff_trees_small(const uint32_t* __restrict__ counts, int k, long long trees,
-                 unsigned long long* __restrict__ enc, uint32_t* __restrict__ err) {
+                 unsigned long long* __restrict__ enc, uint32_t* __restrict__ err,
+                 long long trees2, const uint32_t* __restrict__ counts2,
+                 unsigned long long* __restrict__ enc2, uint32_t* __restrict__ err2) {
+    // trees [0, trees) from counts -> enc; a paired build (pqh_tables_build_pair) adds trees
+    // [trees, trees + trees2) of a second table set
+    if ((long long)blockIdx.x * TPW >= trees) {
+        const long long b = (long long)blockIdx.x - (trees + TPW - 1) / TPW;
+        counts = counts2 + b * TPW * k;
+        enc = enc2 + b * TPW * k;
+        err = err2;
+        trees = trees2 - b * TPW;
+    } else {
+        trees -= (long long)blockIdx.x * TPW;
+        counts += (long long)blockIdx.x * TPW * k;
+        enc += (long long)blockIdx.x * TPW * k;
+    }
     extern __shared__ __attribute__((aligned(16))) char lds[];
     uint32_t* heap_all = reinterpret_cast<uint32_t*>(lds);
     uint32_t* kid_all = heap_all + 512 * TPW;
@@ -541,11 +573,10 @@ huff_trees_small(const uint32_t* __restrict__ counts, int k, long long trees,
         __syncthreads();
     }
     if (t >= TPW) return;  // no barriers below
-    const long long tree = (long long)blockIdx.x * TPW + t;
-    if (tree >= trees) return;
-    const uint32_t* cnt = counts + tree * k;
-    unsigned long long* out = enc + tree * k;
-    const bool stamp = tree == 0;
+    if (t >= trees) return;   // (counts / enc / trees are this workgroup's, above)
+    const uint32_t* cnt = counts + (long long)t * k;
+    unsigned long long* out = enc + (long long)t * k;
+    const bool stamp = blockIdx.x == 0 && t == 0;
 #ifdef PQH_LAT_PRIO   // (experiment) latency-bound waves first in issue arbitration
     __builtin_amdgcn_s_setprio(PQH_LAT_PRIO);
 #endif
@@ -582,9 +613,8 @@ huff_trees_small(const uint32_t* __restrict__ counts, int k, long long trees,
             hp.push(((a & ~1023u) + (b & ~1023u)) | (uint32_t)next);
             ++next;
         }
-    } else {   // heavy tree: 64-bit keys (u64 [256] in the heap's 2 KB)
-        next = merge_tree<unsigned long long, 16, TPW, 256>(
-            reinterpret_cast<unsigned long long*>(heap_all) + t, lcnt, nz, kid);
+    } else {   // heavy tree: 64-bit keys (u64 [256] as word pairs of the lane's own column)
+        next = merge_tree<unsigned long long, 16, TPW, 256, true>(heap_all + t, lcnt, nz, kid);
     }
     if (stamp) g_tree_stamps[3] = __builtin_amdgcn_s_memtime();
     // codes top-down in reverse creation order (parents are created after their children):
@@ -1405,7 +1435,8 @@ int pqh_tables_build(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts) 
     return pqh_tables_build_impl(ctx, t, d_counts, PQH_TREES_DEFAULT);
 }
 
-static int build_trees(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts, int which);
+static int build_trees(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts, int which,
+                       pqh_tables_t* t2 = nullptr, const uint32_t* d_counts2 = nullptr);
 
 int pqh_tables_build_impl(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts, int which) {
     const int rc = build_trees(ctx, t, d_counts, which);
@@ -1416,6 +1447,17 @@ int pqh_tables_build_trees(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_co
     return build_trees(ctx, t, d_counts, which);
 }
 
+int pqh_tables_build_pair(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts,
+                          pqh_tables_t* t2, const uint32_t* d_counts2) {
+    if (!t || !t2 || t == t2 || !d_counts2 || t2->k != t->k || t2->m != t->m ||
+        t2->context != t->context || !t2->ctx || t2->ctx->device != t->ctx->device ||
+        t->k > 256 || (reinterpret_cast<uintptr_t>(d_counts2) & 15u))
+        return PQH_ERR_ARG;
+    int rc = build_trees(ctx, t, d_counts, PQH_TREES_LANE, t2, d_counts2);
+    if (!rc) rc = launch_luts(ctx, t);
+    return rc ? rc : launch_luts(ctx, t2);
+}
+
 int pqh_tables_build_luts(pqh_ctx_t* ctx, pqh_tables_t* t) {
     if (!ctx || !t || !t->ctx || t->ctx->device != ctx->device) return PQH_ERR_ARG;
     const int rc = pqh_use_device(ctx);
@@ -1423,7 +1465,8 @@ int pqh_tables_build_luts(pqh_ctx_t* ctx, pqh_tables_t* t) {
 }
 
 // the code tables' trees (d_enc) on ctx's stream; the decode tables follow (launch_luts)
-static int build_trees(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts, int which) {
+static int build_trees(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts, int which,
+                       pqh_tables_t* t2, const uint32_t* d_counts2) {
     // any context of the tables' device may run the build (on its own stream), so the
     // builds of consecutive batches can overlap on different streams
     if (!ctx || !t || !d_counts || !t->ctx || t->ctx->device != ctx->device) return PQH_ERR_ARG;
@@ -1431,6 +1474,7 @@ static int build_trees(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts
     int rc = pqh_use_device(ctx);
     if (rc) return rc;
     PQH_HIP(ctx, hipMemsetAsync(t->d_err, 0, 16, ctx->stream));   // error word + LUT pool head
+    if (t2) PQH_HIP(ctx, hipMemsetAsync(t2->d_err, 0, 16, ctx->stream));
     if (reinterpret_cast<uintptr_t>(d_counts) & 15u) return PQH_ERR_ARG;
     const long long trees = t->tables;
     // Two builds of the same trees:
@@ -1443,7 +1487,7 @@ static int build_trees(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts
     //    concurrent assignment (bench 1,610-1,880 Mvec/s against 2,270).
     const char* impl = which == PQH_TREES_WAVE ? "wave"
                      : which == PQH_TREES_LANE ? "lane" : std::getenv("PQH_TREE_IMPL");
-    if (t->k <= 256 && impl && std::strcmp(impl, "wave") == 0) {
+    if (t->k <= 256 && impl && std::strcmp(impl, "wave") == 0 && !t2) {
         // writes every entry (0 for symbols that never occur): no memset
         hipLaunchKernelGGL(huff_trees_wave, dim3((unsigned)((trees + kTreeWaves - 1) / kTreeWaves)),
                            dim3(64 * kTreeWaves), 0, ctx->stream, d_counts, t->k, trees, t->d_enc,
@@ -1466,8 +1510,11 @@ static int build_trees(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts
             const size_t lds = (size_t)TPW * (512 * 4 + 256 * 4 + 256 * 2);
             PQH_HIP(ctx, hipFuncSetAttribute((const void*)huff_trees_small<TPW>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            hipLaunchKernelGGL((huff_trees_small<TPW>), dim3((unsigned)((trees + TPW - 1) / TPW)),
-                               dim3(64), lds, ctx->stream, d_counts, t->k, trees, t->d_enc, t->d_err);
+            const long long blocks = (trees + TPW - 1) / TPW + (t2 ? (t2->tables + TPW - 1) / TPW : 0);
+            hipLaunchKernelGGL((huff_trees_small<TPW>), dim3((unsigned)blocks), dim3(64), lds,
+                               ctx->stream, d_counts, t->k, trees, t->d_enc, t->d_err,
+                               t2 ? t2->tables : 0ll, t2 ? d_counts2 : d_counts,
+                               t2 ? t2->d_enc : t->d_enc, t2 ? t2->d_err : t->d_err);
             return PQH_OK;
         };
         rc = tpw_env == 8 ? launch(std::integral_constant<int, 8>{})

@@ -237,6 +237,45 @@ def test_gpu_tree_builder_vs_host_builder_ties(gpu, ctxm, impl, monkeypatch):
     assert dev.codebooks().file_bytes() == host.file_bytes()
 
 
+@pytest.mark.parametrize("impl", ["lane", "wave"])
+def test_gpu_tree_builder_mixed_heavy_light(gpu, impl, monkeypatch):
+    """Context alphabets of one workgroup that take different heaps: frequent previous
+    symbols give trees past 2^22 (64-bit keys), rare ones stay on the u32 sentinel heap.
+    (Regression: the 64-bit heap once overwrote its neighbours' sentinels.)"""
+    monkeypatch.setenv("PQH_TREE_IMPL", impl)
+    torch, codec, ctx = gpu
+    rng = np.random.default_rng(31)
+    codes = torch.from_numpy(rng.zipf(1.3, (20000, 8)).clip(1, 256).astype(np.uint8) - 1).cuda()
+    c = codec.histogram(ctx, codes, 256, True)
+    c = c * 1000 + (c > 0).to(c.dtype) * 5
+    tabs = codec.Tables(ctx, 8, 256, True).build(c)
+    host = codec.Codebooks(c.cpu().numpy().astype(np.float64), 256, True)
+    assert tabs.codebooks().file_bytes() == host.file_bytes()
+
+
+@pytest.mark.parametrize("ctxm", [True, False])
+def test_gpu_tree_builder_pair(gpu, ctxm):
+    """pqh_tables_build_pair: two table sets from two histograms (tie-heavy, and heavy with
+    64-bit keys) in one tree launch == each set's host codebooks; the pair's decode tables
+    decode both sets' streams."""
+    torch, codec, ctx = gpu
+    rng = np.random.default_rng(29)
+    codes = torch.from_numpy(rng.zipf(1.3, (20000, 8)).clip(1, 256).astype(np.uint8) - 1).cuda()
+    c1 = codec.histogram(ctx, codes, 256, ctxm)                 # tie-heavy small counts
+    c2 = c1 * 1000 + (c1 > 0).to(c1.dtype) * 5                  # totals past 2^22: 64-bit keys
+    t1 = codec.Tables(ctx, 8, 256, ctxm)
+    t2 = codec.Tables(ctx, 8, 256, ctxm)
+    t1.build_pair(c1, t2, c2)
+    t1.status()
+    t2.status()
+    for t, c in ((t1, c1), (t2, c2)):
+        host = codec.Codebooks(c.cpu().numpy().astype(np.float64), 256, ctxm)
+        assert t.codebooks().file_bytes() == host.file_bytes()
+        enc = codec.encode(ctx, t, codes, chunk_vectors=8)
+        assert torch.equal(codec.decode(ctx, t, enc), codes)
+    codec.decode_status(ctx)
+
+
 @pytest.mark.parametrize("ctxm", [True, False])
 @pytest.mark.parametrize("impl", ["lane", "wave"])
 def test_gpu_tree_builder_heavy_and_rebuilt(gpu, ctxm, impl, monkeypatch):
