@@ -94,6 +94,9 @@ def parse():
                     help="tree builder of the run's last batch, built after the assignment "
                          "stream is done: one wavefront per tree (lower latency) or the "
                          "default one lane per tree")
+    ap.add_argument("--fill-trees", choices=["wave", "lane"], default="lane",
+                    help="tree builder of the first batch on each table lane (the pipeline's "
+                         "fill: the lanes start their back-to-back builds earlier)")
     ap.add_argument("--hist-on", choices=["assign", "lanes"], default="assign",
                     help="stream of the context histogram: the assignment's, or the batch's "
                          "lane (before its code tables)")
@@ -483,7 +486,8 @@ def main():
             # GPU trees + lookup tables, no host trip.  The run's last batch builds while
             # the assignment stream has nothing left to do: there the one-wavefront-per-tree
             # build (lower latency, more waves) shortens the drain (--drain-trees).
-            last = i == state["nsteps"] - 1 and args.drain_trees == "wave"
+            last = (i == state["nsteps"] - 1 and args.drain_trees == "wave") or \
+                (i < nl and args.fill_trees == "wave")
             if lut_a:   # trees here, the decode tables on A dl batches later (lut())
                 tabs[ti].build_trees(counts[s], c, trees="wave" if last else None)
                 done(e, sL)
@@ -690,7 +694,7 @@ def main():
                          "profile_avg_ms": (round(prof_avg_us / 1e3, 4)
                                             if prof_avg_us is not None else None)},
             "stages_ms": {s: round(v / args.steps * 1e3, 4) for s, v in acc.items()
-                          if s != "sort" or args.sort},
+                          if (s != "sort" or args.sort) and (s != "lut" or lut_a)},
             "stages_note": ("per-stage HIP-event times on their own streams" +
                             ("" if serial else "; the stages of consecutive batches run "
                              "concurrently, so they sum to more than ms_per_step")),
