@@ -595,22 +595,25 @@ huff_trees_small(const uint32_t* __restrict__ counts, int k, long long trees,
     if (nz == 0) return;
     if (stamp) g_tree_stamps[1] = __builtin_amdgcn_s_memtime();
     int next;
-    if (total < (1ull << 22)) {
+    // u32 heap: key payloads are the leaf's symbol (< 256) or 256 + the internal node's
+    // creation index, so the code pass reads no symbol table; the 64-bit heap's are node ids
+    const bool symp = total < (1ull << 22);
+    if (symp) {
         SentinelHeap<TPW> hp{heap_all + t, 0};
-        for (int j = 0; j < nz; ++j) hp.push((lcnt[j * TPW] << 10) | (uint32_t)j);
+        for (int j = 0; j < nz; ++j) hp.push((lcnt[j * TPW] << 10) | (uint32_t)lsym[j * TPW]);
         if (stamp) g_tree_stamps[2] = __builtin_amdgcn_s_memtime();
         next = nz;
         if (hp.size == 1) {  // lone symbol: code "0" (huffman_encode.c:168-177)
             const uint32_t e = hp.pop();
             kid[0] = (e & 511u) | 0xFFFF0000u;
-            hp.push((e & ~1023u) | (uint32_t)next);
+            hp.push((e & ~1023u) | (uint32_t)(256 + next - nz));
             ++next;
         }
         while (hp.size > 1) {
             const uint32_t a = hp.pop();
             const uint32_t b = hp.pop();
             kid[(next - nz) * TPW] = (a & 511u) | ((b & 511u) << 16);
-            hp.push(((a & ~1023u) + (b & ~1023u)) | (uint32_t)next);
+            hp.push(((a & ~1023u) + (b & ~1023u)) | (uint32_t)(256 + next - nz));
             ++next;
         }
     } else {   // heavy tree: 64-bit keys (u64 [256] as word pairs of the lane's own column)
@@ -634,12 +637,13 @@ huff_trees_small(const uint32_t* __restrict__ counts, int k, long long trees,
             const uint32_t ch = b ? kk >> 16 : kk & 0xFFFFu;
             if (ch == 0xFFFFu) continue;
             const unsigned long long v = (d << 56) | ((c | (unsigned long long)b) & kMask);
-            if ((int)ch >= nz) {
-                icode[(ch - nz) * TPW] = v;
+            const int base = symp ? 256 : nz;   // first internal payload
+            if ((int)ch >= base) {
+                icode[((int)ch - base) * TPW] = v;
             } else if (d > (unsigned long long)kMaxCodeLen) {
                 too_long = true;
             } else {
-                out[lsym[ch * TPW]] = v;
+                out[symp ? ch : lsym[ch * TPW]] = v;
             }
         }
     }
