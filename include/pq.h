@@ -41,9 +41,19 @@ int centroids_codebook_load(centroids_codebook_t* codebook, const char* filename
 int fvecs_load_meta(const char* filename, long long* num_vectors, int* num_dimensions);
 float* fvecs_load(const char* filename, long long* num_vectors, int* num_dimensions);
 
-/* codes: n x M, uint8 when K <= 256 else uint16 (row-major, pq_indices.bvecsl order). */
+/* codes: n x M, uint8 when K <= 256 else uint16 (row-major, pq_indices.bvecsl order).
+ * Streams: the rows go to the GPU a chunk at a time (PQH_ENCODE_CHUNK rows, default 2^18)
+ * through two pinned buffers, so device memory is bounded for any n. */
 int pq_encode(const centroids_codebook_t* codebook, const float* x, long long n, int d,
               void* codes);
+/* pq_encode over rows produced by the caller: read(user, row0, rows, dst) fills rows
+ * [row0, row0 + rows) as rows x d floats into dst (a pinned buffer) and returns 0; the
+ * reader for chunk i + 1 runs while chunk i is copied and assigned (the pq_encoder CLI reads
+ * its .fvecs file this way, as the reference does in 128K-row batches, pq_encoder.c:43,58-80).
+ * chunk_rows <= 0: the default. */
+typedef int (*pq_rows_fn)(void* user, long long row0, long long rows, float* dst);
+int pq_encode_rows(const centroids_codebook_t* codebook, int d, long long n, pq_rows_fn read,
+                   void* user, void* codes, long long chunk_rows);
 /* Train the codebook in place on the GPU: `iters` deterministic Lloyd iterations
  * (pqh_kmeans_train) from the centroids it holds -- the build's replacement for the
  * training done by yael kmeans at pq_encoder.c:265-274. */

@@ -39,7 +39,8 @@ typedef enum {
     PQH_ERR_CODE_TOO_LONG = -5,  /* a Huffman code longer than 56 bits (needs N >= F(58)) */
     PQH_ERR_CORRUPT = -6,        /* invalid code in a stream */
     PQH_ERR_NOMEM = -7,
-    PQH_ERR_CAPACITY = -8        /* output buffer too small */
+    PQH_ERR_CAPACITY = -8,       /* output buffer too small */
+    PQH_ERR_REMOTE = -9          /* another rank's part of a sharded call failed */
 } pqh_status_t;
 
 typedef struct pqh_ctx pqh_ctx_t;
@@ -126,18 +127,19 @@ int pqh_tables_destroy(pqh_tables_t* tables);
  * context on the tables' device; the build is ordered on ctx's stream. */
 int pqh_tables_build(pqh_ctx_t* ctx, pqh_tables_t* tables, const uint32_t* d_counts);
 /* pqh_tables_build with the tree builder chosen by the caller (PQH_TREES_DEFAULT: the
- * PQH_TREE_IMPL environment choice).  K <= 256: LANE = one lane per tree (the default: few
- * waves beside concurrent kernels), WAVE = one wavefront per tree (lower latency on an
- * otherwise idle GPU); K > 256: LANE = one lane per tree, otherwise one wavefront per tree.
- * Every choice builds the same tables. */
-enum { PQH_TREES_DEFAULT = 0, PQH_TREES_LANE = 1, PQH_TREES_WAVE = 2 };
+ * PQH_TREE_IMPL environment choice, "lane" | "wave" | "grp").  K <= 256: GROUP = 16 lanes per
+ * tree, four trees per wavefront, at most 32 VGPRs so it runs beside the assignment grid (the
+ * default); LANE = one lane per tree; WAVE = one wavefront per tree with the heap in
+ * registers.  K > 256: LANE = one lane per tree, otherwise one wavefront per tree.  Every
+ * choice builds the same tables. */
+enum { PQH_TREES_DEFAULT = 0, PQH_TREES_LANE = 1, PQH_TREES_WAVE = 2, PQH_TREES_GROUP = 3 };
 int pqh_tables_build_impl(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts, int which);
 /* The two halves of pqh_tables_build_impl, for callers that run them on different streams:
  * the Huffman trees (code table) on ctx's stream, then -- after the caller orders it behind
  * the trees (an event) -- the decode tables and the encoder's gather copy on ctx's stream. */
 int pqh_tables_build_trees(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts, int which);
 int pqh_tables_build_luts(pqh_ctx_t* ctx, pqh_tables_t* t);
-/* Two table sets (same m, K <= 256, mode) built by one launch of the one-lane-per-tree
+/* Two table sets (same m, K <= 256, mode) built by one launch of the default K <= 256
  * build: twice the trees in one latency-bound pass, for a caller whose table builds are the
  * bound; then both sets' decode tables.  Same tables as two pqh_tables_build calls. */
 int pqh_tables_build_pair(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts,
@@ -247,24 +249,33 @@ typedef struct {
 long long pqh_shard_scratch_bytes(int world, int m);
 
 /* One rank's encode of its shard (uint8 codes, K <= 256 -- context mode needs K = 256):
- *   context mode: all-gather of every rank's (non-empty flag, last row) -> the halo of this
- *     shard = the last row of the nearest non-empty rank before it, and the raw first row
- *     (huffman_encoder.c:234) belongs to the first non-empty rank (one host read of the
- *     flags: a shard may be empty, e.g. a slice of the distributed sort);
+ *   context mode: all-gather of every rank's (non-empty flag, last row) -> on the device,
+ *     the halo of this shard = the last row of the nearest non-empty rank before it, and the
+ *     raw first row (huffman_encoder.c:234) belongs to the first non-empty rank (a shard may
+ *     be empty, e.g. a slice of the distributed sort);
  *   histogram of the shard (+ the halo pair) -> all_reduce_sum_u32 -> GPU code tables
  *   (identical on every rank: no broadcast) -> the shard's exact bit length -> all_gather
  *   of the lengths -> exclusive scan on the device -> pqh_encode_write_at.
+ * Asynchronous: no host round trip (unless raw_first is non-NULL, which reads back at the
+ * end whether this shard wrote the raw first row).
  * Outputs: d_counts [m][items] the GLOBAL histogram; tables built from it; d_out holds the
  * shard's bits at (global offset % 32) with word 0 = the global stream's word offset / 32
  * (buffers compose by OR-ing boundary words: pqh_shard_stitch); d_offsets[2] (device u64) =
  * {this shard's global bit offset, the global stream's length in bits}; the chunk index
- * (optional, chunk_vectors > 0) is relative to d_out bit 0.  *raw_first (may be NULL)
- * reports whether this shard wrote the raw first row. */
+ * (optional, chunk_vectors > 0) is relative to d_out bit 0.
+ * Errors: PQH_ERR_ARG at once (before any collective) when ctx, comm, m, k, context,
+ * d_counts, d_offsets or d_scratch are unusable -- the arguments the collectives need.  Any
+ * other failure of this rank (its shard, tables or output arguments, or a library call)
+ * keeps the rank in the collective sequence with an empty contribution and the sentinel
+ * length ~0, and is returned here; every rank's d_offsets then reads {0, ~0}, which
+ * pqh_shard_status reports as PQH_ERR_REMOTE -- no rank is left waiting in a collective. */
 int pqh_shard_encode(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm, const block_t* shard,
                      const void* d_codes, int m, int k, int context, pqh_tables_t* tables,
                      uint32_t* d_counts, unsigned char* d_out, unsigned long long out_bytes,
                      int chunk_vectors, unsigned long long* d_chunk_offsets, void* d_chunk_prev,
                      unsigned long long* d_offsets, void* d_scratch, int* raw_first);
+/* Synchronises; PQH_ERR_REMOTE if some rank's pqh_shard_encode behind d_offsets failed. */
+int pqh_shard_status(pqh_ctx_t* ctx, const unsigned long long* d_offsets);
 
 /* Host: (this rank's global bit offset, the global length) from every rank's bit length. */
 int pqh_shard_offsets(const unsigned long long* lengths, int world, int rank,

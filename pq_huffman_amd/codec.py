@@ -267,7 +267,7 @@ class Tables:
             raise PqhError(st, "pqh_tables_upload: " + ctx.last_error())
         return t
 
-    TREES = {None: 0, "lane": 1, "wave": 2}
+    TREES = {None: 0, "lane": 1, "wave": 2, "grp": 3}
 
     def build(self, counts, ctx: Context = None, trees: str = None) -> "Tables":
         """GPU codebook construction from device counts (async, on `ctx`'s stream: any

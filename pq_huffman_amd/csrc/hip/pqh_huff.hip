@@ -40,8 +40,10 @@ __device__ __forceinline__ unsigned ld_code(const CodeT* c, long long i) { retur
 template <typename CodeT>
 __global__ void __launch_bounds__(1024)
 hist_ctx(const CodeT* __restrict__ codes, long long n, int m_total, int k,
-         const CodeT* __restrict__ prev_row, uint32_t* __restrict__ partial, int split, int chunks) {
+         const CodeT* __restrict__ prev_row, const int* __restrict__ d_rawf,
+         uint32_t* __restrict__ partial, int split, int chunks) {
     extern __shared__ uint32_t pairs[];   // (k / split) * k u16 counters packed two per word
+    if (d_rawf && *d_rawf) prev_row = nullptr;   // decided on the device (pqh_shard_encode)
     const int per_chunk = m_total * split;
     const int q = (int)(blockIdx.x >> 3);
     const int chunk = (q / per_chunk) * 8 + (int)(blockIdx.x & 7);
@@ -179,10 +181,12 @@ __device__ __forceinline__ unsigned long long sym_entry(const CodeT* codes, long
 template <typename CodeT>
 __global__ void __launch_bounds__(kEncBlock)
 enc_size(const CodeT* __restrict__ codes, long long n, int m_total, int k, int context,
-         int raw_first, const CodeT* __restrict__ prev_row, const unsigned long long* __restrict__ enc,
+         int raw_first, const CodeT* __restrict__ prev_row, const int* __restrict__ d_rawf,
+         const unsigned long long* __restrict__ enc,
          long long items, uint32_t* __restrict__ block_bits,
          const uint16_t* __restrict__ tree_prev) {
     __shared__ uint32_t red[kEncBlock / 64];
+    if (d_rawf) raw_first = *d_rawf;   // decided on the device (pqh_shard_encode)
     const long long v = (long long)blockIdx.x * kEncBlock + threadIdx.x;
     uint32_t bits = 0;
     if (v < n)
@@ -336,7 +340,7 @@ __device__ unsigned long long g_enc_stamps[8];
 template <typename CodeT, int MAXM>
 __global__ void __launch_bounds__(kEncBlock)
 enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, int context,
-            int raw_first, const CodeT* __restrict__ prev_row,
+            int raw_first, const CodeT* __restrict__ prev_row, const int* __restrict__ d_rawf,
             const unsigned long long* __restrict__ enc, const uint32_t* __restrict__ enc32,
             long long items,
             unsigned long long bit_offset_arg,
@@ -354,6 +358,7 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
     __shared__ unsigned long long s_excl;
     __shared__ uint32_t s_head;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    if (d_rawf) raw_first = *d_rawf;   // decided on the device (pqh_shard_encode)
     // d_bit_offset: the shard's GLOBAL bit offset, produced on the device (multi-GPU, no host
     // round trip); the shard's own buffer starts at its word, so only offset % 32 matters
     const unsigned long long bit_offset = d_bit_offset ? (*d_bit_offset & 31ull) : bit_offset_arg;
@@ -535,7 +540,8 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
 extern "C" {
 
 static int histogram_impl(pqh_ctx_t* ctx, const void* d_codes, long long n, int m, int k,
-                          int context, const void* d_prev_row, uint32_t* d_counts, int set) {
+                          int context, const void* d_prev_row, uint32_t* d_counts, int set,
+                          const int* d_rawf = nullptr) {
     if (!ctx || m <= 0 || k <= 0 || n < 0 || !d_counts || (n > 0 && !d_codes)) return PQH_ERR_ARG;
     if (context && k > 256) return PQH_ERR_UNSUPPORTED;
     int rc = pqh_use_device(ctx);
@@ -563,7 +569,8 @@ static int histogram_impl(pqh_ctx_t* ctx, const void* d_codes, long long n, int 
         const unsigned grid = 8u * ((chunks + 7u) / 8u) * (unsigned)(m * split);
         hipLaunchKernelGGL(hist_ctx<uint8_t>, dim3(grid), dim3(1024), lds, ctx->stream,
                            static_cast<const uint8_t*>(d_codes), n, m, k,
-                           static_cast<const uint8_t*>(d_prev_row), partial, split, (int)chunks);
+                           static_cast<const uint8_t*>(d_prev_row), d_rawf, partial, split,
+                           (int)chunks);
         PQH_LAUNCH_CHECK(ctx);
         hipLaunchKernelGGL(hist_ctx_reduce, dim3((unsigned)((words + 255) / 256), m), dim3(256), 0,
                            ctx->stream, partial, (int)chunks, words, (long long)k * k, d_counts,
@@ -603,7 +610,8 @@ static int enc_ws(pqh_ctx* ctx, long long n, uint32_t** bb, unsigned long long**
 }
 
 static int run_size(pqh_ctx* ctx, const pqh_tables* t, const void* d_codes, long long n,
-                    int raw_first, const void* d_prev_row, unsigned long long* d_total) {
+                    int raw_first, const void* d_prev_row, unsigned long long* d_total,
+                    const int* d_rawf = nullptr) {
     uint32_t* bb;
     unsigned long long* bo;
     int rc = enc_ws(ctx, n, &bb, &bo);
@@ -612,13 +620,13 @@ static int run_size(pqh_ctx* ctx, const pqh_tables* t, const void* d_codes, long
     if (t->k <= 256)
         hipLaunchKernelGGL(enc_size<uint8_t>, dim3((unsigned)nb), dim3(kEncBlock), 0, ctx->stream,
                            static_cast<const uint8_t*>(d_codes), n, t->m, t->k, t->context,
-                           raw_first, static_cast<const uint8_t*>(d_prev_row), t->d_enc, t->items, bb,
-                           nullptr);
+                           raw_first, static_cast<const uint8_t*>(d_prev_row), d_rawf, t->d_enc,
+                           t->items, bb, nullptr);
     else
         hipLaunchKernelGGL(enc_size<uint16_t>, dim3((unsigned)nb), dim3(kEncBlock), 0, ctx->stream,
                            static_cast<const uint16_t*>(d_codes), n, t->m, t->k, t->context,
-                           raw_first, static_cast<const uint16_t*>(d_prev_row), t->d_enc, t->items, bb,
-                           nullptr);
+                           raw_first, static_cast<const uint16_t*>(d_prev_row), d_rawf, t->d_enc,
+                           t->items, bb, nullptr);
     PQH_LAUNCH_CHECK(ctx);
     hipLaunchKernelGGL(scan_blocks, dim3(1), dim3(1024), 0, ctx->stream, bb, nb, bo, d_total);
     PQH_LAUNCH_CHECK(ctx);
@@ -644,7 +652,7 @@ static int encode_write_impl(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* 
                              unsigned long long out_bytes, int chunk_vectors,
                              unsigned long long* d_chunk_offsets, void* d_chunk_prev,
                              unsigned long long* d_total_bits,
-                             const uint16_t* tree_prev = nullptr) {
+                             const uint16_t* tree_prev = nullptr, const int* d_rawf = nullptr) {
     if (!ctx || !t || n < 0 || (n > 0 && (!d_codes || !d_out))) return PQH_ERR_ARG;
     if ((reinterpret_cast<uintptr_t>(d_out) & 3u) || (out_bytes & 3u))
         return pqh_set_error(ctx, PQH_ERR_ARG, "stream buffer must be 4-byte aligned and sized");
@@ -687,7 +695,8 @@ static int encode_write_impl(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* 
                                              (int)lds));                                          \
         hipLaunchKernelGGL((enc_onepass<T, MAXM>), dim3((unsigned)nb), dim3(kEncBlock), lds,       \
                            ctx->stream, static_cast<const T*>(d_codes), n, t->m, t->k,            \
-                           t->context, raw_first, static_cast<const T*>(d_prev_row), t->d_enc,    \
+                           t->context, raw_first, static_cast<const T*>(d_prev_row), d_rawf,     \
+                           t->d_enc,                                                              \
                            t->d_enc32, t->items, bit_offset, d_bit_offset, words,                 \
                            (long long)(out_bytes / 4),                                            \
                            chunk_vectors, d_chunk_offsets, static_cast<T*>(d_chunk_prev),         \
@@ -729,6 +738,38 @@ int pqh_encode_write_at(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_cod
     return encode_write_impl(ctx, t, d_codes, n, raw_first, d_prev_row, 0, d_global_bit_offset,
                              d_out, out_bytes, chunk_vectors, d_chunk_offsets, d_chunk_prev,
                              d_total_bits);
+}
+
+// pqh_shard_encode's variants: this shard's raw-first flag lives in device memory (decided
+// on the device from the all-gathered halo records); 1 = write row 0 raw and count no halo
+// pair, 0 = row 0 in the context of d_prev_row
+int pqh_histogram_set_dev(pqh_ctx_t* ctx, const void* d_codes, long long n, int m, int k,
+                          const void* d_prev_row, const int* d_rawf, uint32_t* d_counts) {
+    return histogram_impl(ctx, d_codes, n, m, k, 1, d_prev_row, d_counts, 1, d_rawf);
+}
+
+int pqh_encode_size_dev(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes, long long n,
+                        const void* d_prev_row, const int* d_rawf,
+                        unsigned long long* d_total_bits) {
+    if (!ctx || !t || n < 0 || !d_total_bits || (n > 0 && !d_codes)) return PQH_ERR_ARG;
+    int rc = pqh_use_device(ctx);
+    if (rc) return rc;
+    if (n == 0) {
+        PQH_HIP(ctx, hipMemsetAsync(d_total_bits, 0, 8, ctx->stream));
+        return PQH_OK;
+    }
+    return run_size(ctx, t, d_codes, n, 0, d_prev_row, d_total_bits, d_rawf);
+}
+
+int pqh_encode_write_at_dev(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes,
+                            long long n, const void* d_prev_row, const int* d_rawf,
+                            const unsigned long long* d_global_bit_offset, unsigned char* d_out,
+                            unsigned long long out_bytes, int chunk_vectors,
+                            unsigned long long* d_chunk_offsets, void* d_chunk_prev) {
+    if (!d_global_bit_offset) return PQH_ERR_ARG;
+    return encode_write_impl(ctx, t, d_codes, n, 0, d_prev_row, 0, d_global_bit_offset, d_out,
+                             out_bytes, chunk_vectors, d_chunk_offsets, d_chunk_prev, nullptr,
+                             nullptr, d_rawf);
 }
 
 // diagnostics only: phase stamps of the mid-grid workgroup of the last one-pass encode

@@ -50,6 +50,20 @@ int pqh_set_error(pqh_ctx* ctx, int code, const char* fmt, ...);
 int pqh_ensure_ws(pqh_ctx* ctx, size_t bytes);
 int pqh_use_device(pqh_ctx* ctx);
 int pqh_kmeans_fixed_shift(float max_abs, long long n);
+// pqh_shard_encode's histogram / size / write with this shard's raw-first flag in device
+// memory (1: row 0 raw, no halo pair; 0: row 0 in the context of d_prev_row) -- pqh_huff.hip
+extern "C" {
+int pqh_histogram_set_dev(pqh_ctx_t* ctx, const void* d_codes, long long n, int m, int k,
+                          const void* d_prev_row, const int* d_rawf, uint32_t* d_counts);
+int pqh_encode_size_dev(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes, long long n,
+                        const void* d_prev_row, const int* d_rawf,
+                        unsigned long long* d_total_bits);
+int pqh_encode_write_at_dev(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes,
+                            long long n, const void* d_prev_row, const int* d_rawf,
+                            const unsigned long long* d_global_bit_offset, unsigned char* d_out,
+                            unsigned long long out_bytes, int chunk_vectors,
+                            unsigned long long* d_chunk_offsets, void* d_chunk_prev);
+}
 
 #define PQH_HIP(ctx, expr)                                                                \
     do {                                                                                  \

@@ -18,22 +18,40 @@
 
 namespace {
 
-// d_offsets = {sum of the lengths of the ranks before `rank`, sum of all lengths}
+// d_offsets = {sum of the lengths of the ranks before `rank`, sum of all lengths}; a rank
+// that failed locally sent the sentinel length ~0: then {0, ~0} (pqh_shard_status reports it)
 __global__ void shard_prefix(const unsigned long long* __restrict__ lengths, int world, int rank,
                              unsigned long long* __restrict__ offsets) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     unsigned long long before = 0, all = 0;
+    bool failed = false;
     for (int r = 0; r < world; ++r) {
+        failed |= lengths[r] == ~0ull;
         before += r < rank ? lengths[r] : 0ull;
         all += lengths[r];
     }
-    offsets[0] = before;
-    offsets[1] = all;
+    offsets[0] = failed ? 0ull : before;
+    offsets[1] = failed ? ~0ull : all;
 }
 
 constexpr long long kHaloData = 16;   // a halo record: flag byte, pad, the row at byte 16
 
 long long halo_record_bytes(int m) { return ((kHaloData + m + 15) / 16) * 16; }
+
+// The halo of this shard, decided on the device from every rank's record (flag byte = the
+// shard is non-empty, its last row at byte 16): the last row of the nearest non-empty rank
+// before this one goes to `row`, and *rawf = 1 when there is none -- this shard then holds
+// global row 0 and writes it raw (huffman_encoder.c:234); pqh_shard_halo_source's rule.
+__global__ void shard_halo_pick(const unsigned char* __restrict__ recs, long long recb, int world,
+                                int rank, int m, unsigned char* __restrict__ row,
+                                int* __restrict__ rawf) {
+    int prev = -1;
+    for (int r = 0; r < rank && r < world; ++r)
+        if (recs[r * recb]) prev = r;
+    if (threadIdx.x == 0) *rawf = prev < 0 ? 1 : 0;
+    for (int i = threadIdx.x; i < m; i += blockDim.x)
+        row[i] = prev >= 0 ? recs[prev * recb + kHaloData + i] : (unsigned char)0;
+}
 
 }  // namespace
 
@@ -51,9 +69,11 @@ int pqh_shard_block(long long n_total, int world, int rank, block_t* block) {
     return PQH_OK;
 }
 
+// scratch: [send record][world records][halo row (a record's size)][send length]
+//          [world lengths][raw-first flag, 64 B]
 long long pqh_shard_scratch_bytes(int world, int m) {
     if (world <= 0 || m <= 0) return PQH_ERR_ARG;
-    return halo_record_bytes(m) * (world + 1) + 8ll * (world + 1) + 64;
+    return halo_record_bytes(m) * (world + 2) + 8ll * (world + 1) + 64;
 }
 
 int pqh_shard_offsets(const unsigned long long* lengths, int world, int rank,
@@ -108,71 +128,109 @@ int pqh_shard_encode(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm, const block_t
                      uint32_t* d_counts, unsigned char* d_out, unsigned long long out_bytes,
                      int chunk_vectors, unsigned long long* d_chunk_offsets, void* d_chunk_prev,
                      unsigned long long* d_offsets, void* d_scratch, int* raw_first_out) {
-    if (!ctx || !comm || !shard || !tables || !d_counts || !d_out || out_bytes < 4 ||
-        !d_offsets || !d_scratch || m <= 0 || k <= 0 || k > 256 || (context && k != 256) ||
-        shard->size < 0 || (shard->size > 0 && !d_codes) || comm->world <= 0 ||
-        comm->rank < 0 || comm->rank >= comm->world || !comm->all_gather ||
-        !comm->all_reduce_sum_u32 || (reinterpret_cast<uintptr_t>(d_scratch) & 15u))
+    // Without these the collective sequence itself cannot run (or would not match the other
+    // ranks' sizes): refuse before the first collective.
+    if (!ctx || !comm || comm->world <= 0 || comm->rank < 0 || comm->rank >= comm->world ||
+        !comm->all_gather || !comm->all_reduce_sum_u32 || m <= 0 || k <= 0 || k > 256 ||
+        (context && k != 256) || !d_counts || !d_offsets || !d_scratch ||
+        (reinterpret_cast<uintptr_t>(d_scratch) & 15u))
         return PQH_ERR_ARG;
     int rc = pqh_use_device(ctx);
     if (rc) return rc;
-    const long long n = shard->size;
+    // Any other failure is local: the rank stays in the collective sequence (an empty halo
+    // record, its histogram counting nothing, the sentinel length ~0), so no rank waits
+    // forever; every rank's d_offsets then reads {0, ~0} (pqh_shard_status) and this call
+    // returns the local error.
+    int err = PQH_OK;
+    if (!shard || shard->size < 0 || (shard->size > 0 && !d_codes) || !tables || !d_out ||
+        out_bytes < 4 || tables->m != m || tables->k != k || (tables->context ? 1 : 0) != (context ? 1 : 0))
+        err = PQH_ERR_ARG;
+    const long long n = err ? 0 : shard->size;
     const int world = comm->world, rank = comm->rank;
     unsigned char* scratch = static_cast<unsigned char*>(d_scratch);
     const long long recb = halo_record_bytes(m);
     unsigned char* halo_send = scratch;
     unsigned char* halo_recv = scratch + recb;
+    unsigned char* halo_row = scratch + recb * (world + 1);
     unsigned long long* len_send =
-        reinterpret_cast<unsigned long long*>(scratch + recb * (world + 1));
+        reinterpret_cast<unsigned long long*>(scratch + recb * (world + 2));
     unsigned long long* len_recv = len_send + 1;
+    int* d_rawf = reinterpret_cast<int*>(len_recv + world);
     void* const st = ctx->stream;
-    // 1. the halo (context mode): every rank's (non-empty flag, last row)
-    int raw_first = rank == 0 ? 1 : 0;
-    const void* d_prev = nullptr;
+    auto local = [&](int r) {   // the first local failure is kept
+        if (r && !err) err = r;
+    };
+    // 1. the halo (context mode): every rank's (non-empty flag, last row); the halo row and
+    //    the raw-first flag are picked on the device -- no host round trip
     if (context) {
-        PQH_HIP(ctx, hipMemsetAsync(halo_send, 0, recb, ctx->stream));
-        if (n > 0) {
-            PQH_HIP(ctx, hipMemsetAsync(halo_send, 1, 1, ctx->stream));
-            PQH_HIP(ctx, hipMemcpyAsync(halo_send + kHaloData,
-                                        static_cast<const unsigned char*>(d_codes) + (n - 1) * m,
-                                        m, hipMemcpyDeviceToDevice, ctx->stream));
+        local(hipMemsetAsync(halo_send, 0, recb, ctx->stream) == hipSuccess ? PQH_OK : PQH_ERR_HIP);
+        if (n > 0 && !err) {
+            local(hipMemsetAsync(halo_send, 1, 1, ctx->stream) == hipSuccess ? PQH_OK : PQH_ERR_HIP);
+            local(hipMemcpyAsync(halo_send + kHaloData,
+                                 static_cast<const unsigned char*>(d_codes) + (n - 1) * m, m,
+                                 hipMemcpyDeviceToDevice, ctx->stream) == hipSuccess
+                      ? PQH_OK : PQH_ERR_HIP);
         }
         if (comm->all_gather(comm->user, halo_send, halo_recv, recb, st))
             return pqh_set_error(ctx, PQH_ERR_ARG, "shard halo all-gather failed");
-        // which rank's row is the halo, and who writes the raw first row: the flags of
-        // every rank (one small host read; a shard may be empty)
-        std::vector<unsigned char> recs((size_t)(recb * world));
-        PQH_HIP(ctx, hipMemcpyAsync(recs.data(), halo_recv, recs.size(), hipMemcpyDeviceToHost,
-                                    ctx->stream));
-        PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
-        std::vector<int> nonempty(world);
-        for (int r = 0; r < world; ++r) nonempty[r] = recs[(size_t)(r * recb)] ? 1 : 0;
-        int prev = -1;
-        pqh_shard_halo_source(nonempty.data(), world, rank, &prev, &raw_first);
-        if (prev >= 0) d_prev = halo_recv + prev * recb + kHaloData;
+        hipLaunchKernelGGL(shard_halo_pick, dim3(1), dim3(64), 0, ctx->stream, halo_recv, recb,
+                           world, rank, m, halo_row, d_rawf);
+        local(hipGetLastError() == hipSuccess ? PQH_OK : PQH_ERR_HIP);
     }
     // 2. the shard's histogram (+ the halo pair), summed over ranks -> identical tables
-    if ((rc = pqh_histogram_set(ctx, d_codes, n, m, k, context, d_prev, d_counts))) return rc;
     const long long items = context ? (long long)k * k : k;
+    if (err) {
+        local(hipMemsetAsync(d_counts, 0, (size_t)m * items * 4, ctx->stream) == hipSuccess
+                  ? PQH_OK : PQH_ERR_HIP);
+    } else if (context) {
+        local(pqh_histogram_set_dev(ctx, d_codes, n, m, k, halo_row, d_rawf, d_counts));
+    } else {
+        local(pqh_histogram_set(ctx, d_codes, n, m, k, 0, nullptr, d_counts));
+    }
     if (comm->all_reduce_sum_u32(comm->user, d_counts, (long long)m * items, st))
         return pqh_set_error(ctx, PQH_ERR_ARG, "shard histogram all-reduce failed");
-    if ((rc = pqh_tables_build(ctx, tables, d_counts))) return rc;
+    if (!err) local(pqh_tables_build(ctx, tables, d_counts));
     // 3. place the shard: its exact length, everyone's, the exclusive scan on the device
-    if ((rc = pqh_encode_size(ctx, tables, d_codes, n, raw_first, d_prev, len_send))) return rc;
+    if (!err)
+        local(context ? pqh_encode_size_dev(ctx, tables, d_codes, n, halo_row, d_rawf, len_send)
+                      : pqh_encode_size(ctx, tables, d_codes, n, 0, nullptr, len_send));
+    if (err) (void)hipMemsetAsync(len_send, 0xFF, 8, ctx->stream);   // the sentinel length
     if (comm->all_gather(comm->user, len_send, len_recv, 8, st))
         return pqh_set_error(ctx, PQH_ERR_ARG, "shard length all-gather failed");
     hipLaunchKernelGGL(shard_prefix, dim3(1), dim3(64), 0, ctx->stream, len_recv, world, rank,
                        d_offsets);
     PQH_LAUNCH_CHECK(ctx);
+    if (err) return err;
     // 4. write it (word 0 of d_out = the global word offset / 32; the bits before the shard's
     // offset in that word belong to the previous shard and stay zero here)
     PQH_HIP(ctx, hipMemsetAsync(d_out, 0, 4, ctx->stream));
-    if ((rc = pqh_encode_write_at(ctx, tables, d_codes, n, raw_first, d_prev, d_offsets, d_out,
-                                  out_bytes, chunk_vectors, d_chunk_offsets, d_chunk_prev,
-                                  nullptr)))
-        return rc;
-    if (raw_first_out) *raw_first_out = raw_first;
+    rc = context ? pqh_encode_write_at_dev(ctx, tables, d_codes, n, halo_row, d_rawf, d_offsets,
+                                           d_out, out_bytes, chunk_vectors, d_chunk_offsets,
+                                           d_chunk_prev)
+                 : pqh_encode_write_at(ctx, tables, d_codes, n, 0, nullptr, d_offsets, d_out,
+                                       out_bytes, chunk_vectors, d_chunk_offsets, d_chunk_prev,
+                                       nullptr);
+    if (rc) return rc;
+    if (raw_first_out) {   // (optional: the one host read of the call, at its end)
+        int rf = rank == 0 ? 1 : 0;
+        if (context) {
+            PQH_HIP(ctx, hipMemcpyAsync(&rf, d_rawf, 4, hipMemcpyDeviceToHost, ctx->stream));
+            PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        }
+        *raw_first_out = rf;
+    }
     return PQH_OK;
+}
+
+int pqh_shard_status(pqh_ctx_t* ctx, const unsigned long long* d_offsets) {
+    if (!ctx || !d_offsets) return PQH_ERR_ARG;
+    int rc = pqh_use_device(ctx);
+    if (rc) return rc;
+    unsigned long long total = 0;
+    PQH_HIP(ctx, hipMemcpyAsync(&total, d_offsets + 1, 8, hipMemcpyDeviceToHost, ctx->stream));
+    PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return total == ~0ull ? pqh_set_error(ctx, PQH_ERR_REMOTE, "a rank's shard encode failed")
+                          : PQH_OK;
 }
 
 }  // extern "C"

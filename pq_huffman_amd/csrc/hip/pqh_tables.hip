@@ -27,6 +27,8 @@ namespace {
 
 constexpr int kMaxCodeLen = 56;
 constexpr unsigned long long kCodeMask = (1ull << 56) - 1;
+constexpr int kL1Max = 11;                      // decode first level: 2^W1 entries, W1 <= 11
+constexpr long long kL2BaseMax = 1ll << 23;     // (meta holds l2base in 23 bits)
 
 // ------------------------------------------------------------------- tree building
 // A tree's heap lives in LDS, interleaved tree-minor (entry i of lane t at [i * TPW + t]) so
@@ -655,6 +657,456 @@ huff_trees_small(const uint32_t* __restrict__ counts, int k, long long trees,
     }
 }
 
+// ---- sixteen lanes per tree, four trees per wavefront (K <= 256; the default build) -------
+// The heap of huffman_encode.c:33-76 in LDS, each sift read a stretch at a time by the
+// tree's 16 lanes, so a heap level costs no LDS round trip of its own:
+//   push  lane l reads ancestor l + 1 of the new slot (the whole path: one round trip); the
+//         ancestors the entry passes are those strictly heavier than it -- a prefix of the
+//         path (weights fall towards the root), so the group's ballot popcount is the stop
+//         level -- and they move down one level in one write;
+//   pop   lane q = 1..15 stands for node q of the 4-level subtree below the hole (heap
+//         numbering, q = 1 the hole itself) and reads that node's two children in one
+//         ds_read2: kc = the reference's candidate (left unless the right is strictly
+//         lighter: min(left, right | TIE)), mv = the sinking entry moves past it.  Lane q is
+//         on the sink's path iff every ancestor p of q in the stretch chose the side towards
+//         q and moved: two compares of the group's ballots against lane constants A(q) (the
+//         ancestors' bits) and E(q) (the directions towards q) -- no serial walk down the
+//         path.  Lanes on the path move their candidate up; the one whose candidate does not
+//         move takes the sinking entry.  If a depth-3 lane moved, the next stretch starts at
+//         its candidate's slot (two stretches cover a 256-entry heap).
+// Keys are the SentinelHeap's (weight << 10 | tie << 9 | payload, slots past the heap all
+// ones; payload = the leaf's symbol or 256 + the internal node's creation index), u32 when
+// every tree of the wavefront weighs < 2^22, else u64.  The codes come from the merge record
+// by pointer jumping.  At most 32 VGPRs: the persistent assignment grid (3 waves x 160 VGPRs
+// per SIMD) leaves exactly that, so the build runs beside it instead of between its launches.
+constexpr int kGrpTrees = 4;                        // trees per wavefront
+constexpr int kGrpHeapBytes = 4096;                 // heap (<= 257 slots) / codes u64 [512]
+constexpr int kGrpKidBytes = 1024;                  // kid u32 [256]
+constexpr int kGrpLeafBytes = 2048;                 // leaf keys u64 [256] / links u16 [512]
+constexpr int kGrpTreeBytes = kGrpHeapBytes + kGrpKidBytes + kGrpLeafBytes;
+
+// the 16 ballot bits of this lane's group
+__device__ __forceinline__ uint32_t grp_bits(bool pred, int gsh) {
+    return (uint32_t)(__ballot(pred) >> gsh) & 0xFFFFu;
+}
+
+// 1-based heap positions (slot s of the reference heap at h[s + 1]); h[0] = 0 makes a
+// missing ancestor read as lighter than anything, positions past the heap hold all ones.
+struct GrpHeap {
+    static constexpr uint32_t kTie = 1u << 9, kLow = 1023u, kMax = ~0u;
+    static constexpr int kDummy = 1023;   // lanes off the write set store here (never read)
+    uint32_t* h;     // this tree's positions
+    int n;           // entries
+    int gl;          // lane in the group
+    int gsh;         // the group's first bit in a ballot
+    int dq, off;     // node gl of a stretch below hole I: (I << dq) + off (lane 0: past the heap)
+    uint32_t A, E;   // ancestors of node gl in a stretch, and the directions towards gl
+    // ancestor gl + 1 of the position a push fills (0 when there is none)
+    __device__ __forceinline__ uint32_t anc() const { return h[(n + 1) >> (gl + 1)]; }
+    // huffman_encode.c:33-46 (sift up while strictly lighter), `a` = anc(): lanes below the
+    // stop level move their ancestor down, the stop level takes e -- one store, no branch
+    __device__ __forceinline__ void push(uint32_t e, uint32_t a) {
+        const int s = __popc((uint32_t)(__ballot(e < (a & ~kLow)) >> gsh) & 0xFFFFu);
+        h[gl <= s ? (n + 1) >> gl : kDummy] = gl < s ? a : e;
+        ++n;
+    }
+    // one stretch below hole I: lane gl's node, its candidate child, whether the sinking
+    // entry passes it; the lanes on the sink's path store (branch-free); returns the ballot
+    // bits of the group's path lanes
+    __device__ __forceinline__ uint32_t stretch(int G, uint32_t kl, uint32_t kr, uint32_t lw,
+                                                uint32_t last, bool act, uint32_t& mm,
+                                                uint32_t& md) {
+        const uint32_t t = kr | kTie;
+        const uint32_t kc = min(kl, t);
+        const bool mv = kc < lw;
+        mm = (uint32_t)(__ballot(mv) >> gsh);
+        md = (uint32_t)(__ballot(t < kl) >> gsh);
+        const bool on = act && (((md ^ E) | ~mm) & A) == 0;
+        h[on ? G : kDummy] = mv ? (kc & ~kTie) : last;
+        return (uint32_t)(__ballot(on) >> gsh);
+    }
+    // huffman_encode.c:48-76: the last entry sinks from the root, moving while strictly
+    // heavier than the candidate child (left unless the right one is strictly lighter).
+    // Two stretches cover every sink: the second's deepest nodes (level 7) have no children
+    // in a heap of < 256 entries, and at 256 entries position 256 is the sinking entry itself.
+    __device__ __forceinline__ uint32_t pop() {
+        // the root, the last entry and the first stretch's children in one round trip; the
+        // sentinel store sits between them in LDS order (LDS is in order)
+        const int G1 = gl ? gl : 256;   // stretch 1 below the root: node gl
+        const int g1 = min(G1, 129);     // (nodes past 128 have no children in the heap)
+        const uint32_t top = h[1];
+        const uint32_t last = h[n];
+        h[gl ? kDummy : n] = kMax;       // the vacated position becomes a sentinel
+        uint32_t kl = h[2 * g1], kr = h[2 * g1 + 1];
+        --n;
+        const uint32_t lw = last & ~kLow;
+        uint32_t mm, md;
+        const uint32_t onm = stretch(G1, kl, kr, lw, last, gl != 0, mm, md);
+        const uint32_t deep = onm & mm & 0xFF00u;   // the path left the stretch below level 3
+        if (__any(deep)) {
+            const int p = deep ? __ffs(deep) - 1 : 8;
+            const int I = 2 * p + (int)((md >> p) & 1u);   // the hole, level 4
+            const int G = (I << dq) + off;
+            const int g = min(G, 129);
+            kl = h[2 * g];
+            kr = h[2 * g + 1];
+            (void)stretch(G, kl, kr, lw, last, deep != 0u, mm, md);
+        }
+        return top;
+    }
+};
+
+// leaves (pushed in symbol order), merges; returns the internal-node count
+__device__ __forceinline__ int grp_merge(GrpHeap& hp, const unsigned long long* lkey, int nz,
+                                         uint32_t* kid, bool stamp) {
+    constexpr uint32_t kLow = GrpHeap::kLow;
+    for (int j = 0; j < nz; ++j) {
+        const uint32_t a = hp.anc();
+        const uint32_t e = (uint32_t)lkey[j];   // (read in the same round trip as the ancestors)
+        hp.push(e, a);
+    }
+    if (stamp) g_tree_stamps[2] = __builtin_amdgcn_s_memtime();
+    int next = 0;
+    if (hp.n == 1) {   // lone symbol: code "0" (huffman_encode.c:168-177)
+        const uint32_t e = hp.pop();
+        if (hp.gl == 0) kid[0] = (e & 511u) | 0xFFFF0000u;
+        hp.push((e & ~kLow) | 256u, hp.anc());
+        next = 1;
+    }
+    while (hp.n > 1) {
+        const uint32_t a = hp.pop();
+        const uint32_t b = hp.pop();
+        kid[hp.gl ? 255 : next] = (a & 511u) | ((b & 511u) << 16);   // (255: never a node)
+        hp.push(((a & ~kLow) + (b & ~kLow)) | (uint32_t)(256 + next), hp.anc());
+        ++next;
+    }
+    return next;
+}
+
+// A tree weighing 2^22 or more (counts accumulated over more than ~4M rows): the same heap
+// with u64 keys, sifted by one lane (the group's other lanes wait) -- the cooperative u64
+// sifts would take the build past its 32-VGPR budget, and such trees are rare.
+__device__ __forceinline__ int grp_merge_heavy(unsigned long long* h, const unsigned long long* lkey,
+                                               int nz, uint32_t* kid) {
+    using Key = unsigned long long;
+    constexpr Key kTie = 1ull << 9, kLow = 1023ull, kMax = ~0ull;
+    int n = 0;
+    auto push = [&](Key e) {
+        int i = n++;
+        while (i > 0) {
+            const int p = (i - 1) >> 1;
+            const Key hp = h[p];
+            if (!(e < (hp & ~kLow))) break;
+            h[i] = hp;
+            i = p;
+        }
+        h[i] = e;
+    };
+    auto pop = [&]() -> Key {
+        const Key top = h[0];
+        const Key last = h[--n];
+        h[n] = kMax;
+        const Key lw = last & ~kLow;
+        int i = 0;
+        while (i < 128) {
+            const Key kl = h[2 * i + 1], kr = h[2 * i + 2];
+            const Key kc = min(kl, kr | kTie);
+            if (!(kc < lw)) break;
+            h[i] = kc & ~kTie;
+            i = 2 * i + 1 + ((kc & kTie) ? 1 : 0);
+        }
+        h[i] = last;
+        return top;
+    };
+    for (int j = 0; j < nz; ++j) push(lkey[j]);
+    int next = 0;
+    if (n == 1) {   // lone symbol
+        const Key e = pop();
+        kid[0] = (uint32_t)(e & 511) | 0xFFFF0000u;
+        push((e & ~kLow) | 256ull);
+        next = 1;
+    }
+    while (n > 1) {
+        const Key a = pop();
+        const Key b = pop();
+        kid[next] = (uint32_t)(a & 511) | ((uint32_t)(b & 511) << 16);
+        push(((a & ~kLow) + (b & ~kLow)) | (Key)(256 + next));
+        ++next;
+    }
+    return next;
+}
+
+// Pointers of the decode tables lut_grp writes (the layout of lut_build, below).
+struct GrpLut {
+    uint32_t* enc32;
+    uint16_t* lut1;
+    uint16_t* lut2;
+    uint32_t* meta;
+    pqh_long_code* longs;
+    uint32_t* long_cnt;
+    unsigned long long* pool_head;
+    long long lut2_cap;
+    int w1, l2_bits;
+};
+
+__device__ __forceinline__ void grp_luts(const GrpLut& L, long long t, int k, int gl, int gsh,
+                                         const unsigned long long* code, char* scratch);
+
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(32)))
+huff_trees_grp(const uint32_t* __restrict__ counts, int k, long long trees,
+               unsigned long long* __restrict__ enc, uint32_t* __restrict__ err,
+               long long trees2, const uint32_t* __restrict__ counts2,
+               unsigned long long* __restrict__ enc2, uint32_t* __restrict__ err2) {
+    // trees [0, trees) from counts -> enc; a paired build adds [trees, trees + trees2)
+    const long long blocks1 = (trees + kGrpTrees - 1) / kGrpTrees;
+    if ((long long)blockIdx.x >= blocks1) {
+        const long long b = (long long)blockIdx.x - blocks1;
+        counts = counts2 + b * kGrpTrees * k;
+        enc = enc2 + b * kGrpTrees * k;
+        err = err2;
+        trees = trees2 - b * kGrpTrees;
+    } else {
+        trees -= (long long)blockIdx.x * kGrpTrees;
+        counts += (long long)blockIdx.x * kGrpTrees * k;
+        enc += (long long)blockIdx.x * kGrpTrees * k;
+    }
+    __shared__ __attribute__((aligned(16))) char lds[kGrpTrees * kGrpTreeBytes];
+    const int lane = threadIdx.x, grp = lane >> 4, gl = lane & 15, gsh = grp * 16;
+    char* base = lds + grp * kGrpTreeBytes;
+    uint32_t* kid = reinterpret_cast<uint32_t*>(base + kGrpHeapBytes);
+    unsigned long long* lkey = reinterpret_cast<unsigned long long*>(base + kGrpHeapBytes + kGrpKidBytes);
+    {   // sentinels: every heap slot all ones (u32 and u64 views alike)
+        uint4* z = reinterpret_cast<uint4*>(base);
+        for (int q = gl; q < kGrpHeapBytes / 16; q += 16) z[q] = make_uint4(~0u, ~0u, ~0u, ~0u);
+    }
+    if (grp >= trees) return;   // no workgroup barriers below
+    // latency-bound: issue ahead of the (older, VALU-bound) assignment waves on the SIMD
+    __builtin_amdgcn_s_setprio(3);
+    const bool stamp = blockIdx.x == 0 && lane == 0;
+    if (stamp) g_tree_stamps[0] = __builtin_amdgcn_s_memtime();
+    const uint32_t* cnt = counts + (long long)grp * k;
+    // nonzero counts in symbol order (huffman_encode.c:158): key count << 10 | symbol
+    int nz = 0;
+    unsigned long long total = 0;
+    for (int s0 = 0; s0 < k; s0 += 16) {
+        const int s = s0 + gl;
+        const uint32_t c = s < k ? cnt[s] : 0u;
+        const uint32_t mb = grp_bits(c != 0u, gsh);
+        if (c) lkey[nz + __popc(mb & ((1u << gl) - 1u))] = ((unsigned long long)c << 10) | (unsigned)s;
+        nz += __popc(mb);
+        total += c;
+    }
+#pragma unroll
+    for (int off = 8; off >= 1; off >>= 1) total += __shfl_xor(total, off, 16);
+    const bool heavy = total >= (1ull << 22);   // (uniform in the group)
+    if (stamp) g_tree_stamps[1] = __builtin_amdgcn_s_memtime();
+    uint16_t* par = reinterpret_cast<uint16_t*>(lkey);   // (after the leaves are pushed)
+    unsigned long long* code = reinterpret_cast<unsigned long long*>(base);   // (after the merges)
+    int nint = 0;
+    if (nz > 0 && !heavy) {
+        // lane constants of the stretch: node gl's depth, its ancestors and the directions
+        // towards it; lane 0 stands for no node (its node lies past the heap and its
+        // direction bit, 0, never matches E)
+        const int dq = gl ? 31 - __clz(gl) : 8;
+        const int off = gl ? gl - (1 << dq) : 0;
+        uint32_t A = gl ? 0u : 1u, E = gl ? 0u : 1u;
+        for (int j = 1; j <= (gl ? dq : 0); ++j) {
+            A |= 1u << (gl >> j);
+            E |= (uint32_t)((gl >> (j - 1)) & 1) << (gl >> j);
+        }
+        uint32_t* h = reinterpret_cast<uint32_t*>(base);
+        if (gl == 0) h[0] = 0u;   // position 0: the missing ancestor
+        GrpHeap hp{h, 0, gl, gsh, dq, off, A, E};
+        nint = grp_merge(hp, lkey, nz, kid, stamp);
+    } else if (nz > 0) {
+        if (gl == 0) nint = grp_merge_heavy(reinterpret_cast<unsigned long long*>(base), lkey, nz, kid);
+        nint = __shfl(nint, 0, 16);
+    }
+    wave_sync_lds();
+    if (stamp) g_tree_stamps[3] = __builtin_amdgcn_s_memtime();
+    // codes (huffman_encode.c:100-132: child 0 appends bit 0, child 1 bit 1) by pointer
+    // jumping over the parent links of node ids sym | 256 + q: code[v] = len << 56 | the bits
+    // of the path from par[v] down to v; len saturates at 255 and any len > 56 is reported
+    for (int v = gl; v < 512; v += 16) par[v] = 0xFFFFu;
+    wave_sync_lds();
+    const int root = 256 + nint - 1;
+    for (int q = gl; q < nint; q += 16) {
+        const uint32_t kk = kid[q];
+        par[kk & 0xFFFFu] = (uint16_t)(256 + q);
+        code[kk & 0xFFFFu] = 1ull << 56;
+        if ((kk >> 16) != 0xFFFFu) {
+            par[kk >> 16] = (uint16_t)(256 + q);
+            code[kk >> 16] = (1ull << 56) | 1ull;
+        }
+    }
+    wave_sync_lds();
+    for (bool live = nint > 0; __any(live);) {
+        live = false;
+        for (int v = gl; v < 256 + nint; v += 16) {
+            const int u = par[v];
+            if (u == 0xFFFF || u == root) continue;   // absent leaf / the root's child (done)
+            const unsigned long long ev = code[v], eu = code[u];
+            const int pu = par[u];
+            const unsigned lv = (unsigned)(ev >> 56), lu = (unsigned)(eu >> 56);
+            const unsigned long long hi = lv < 56 ? ((eu & kCodeMask) << lv) : 0ull;
+            const unsigned long long len = min((unsigned long long)(lv + lu), 255ull);
+            code[v] = (len << 56) | ((hi | (ev & kCodeMask)) & kCodeMask);
+            par[v] = (uint16_t)pu;
+            live = true;
+        }
+        wave_sync_lds();
+    }
+    // (the group index made opaque, so the pointers below are formed here and not kept
+    // live across the merges: the build stays within the VGPRs the assignment grid leaves)
+    int grp2 = grp;
+    asm volatile("" : "+v"(grp2));
+    unsigned long long* out = enc + (long long)grp2 * k;
+    bool too_long = false;
+    for (int s = gl; s < k; s += 16) {
+        unsigned long long e = 0;
+        if (par[s] != 0xFFFFu) {
+            e = code[s];
+            if ((e >> 56) > (unsigned long long)kMaxCodeLen) {
+                too_long = true;
+                e = 0;
+            }
+        }
+        out[s] = e;
+    }
+    if (too_long) atomicOr(err, 1u);
+    if (stamp) {
+        g_tree_stamps[4] = __builtin_amdgcn_s_memtime();
+        g_tree_stamps[5] = (unsigned long long)nz;
+        g_tree_stamps[6] = (unsigned long long)(nz + nint);
+    }
+}
+
+// The decode tables of lut_build for four alphabets per 64-thread workgroup (16 lanes each):
+// the same tables from <= 32 VGPRs and 20 KB of LDS, so -- like huff_trees_grp -- it runs
+// beside the assignment grid instead of waiting for its end (context mode, W1 <= 9).
+__global__ void __launch_bounds__(64)
+lut_grp(const unsigned long long* __restrict__ enc, int k, long long tables, GrpLut lut) {
+    __shared__ __attribute__((aligned(16))) char lds[kGrpTrees * (2048 + 3072 + 16)];
+    const int lane = threadIdx.x, grp = lane >> 4, gl = lane & 15, gsh = grp * 16;
+    const long long t = (long long)blockIdx.x * kGrpTrees + grp;
+    if (t >= tables) return;   // no workgroup barriers below
+    __builtin_amdgcn_s_setprio(3);
+    char* base = lds + grp * (2048 + 3072 + 16);
+    unsigned long long* code = reinterpret_cast<unsigned long long*>(base);
+    const unsigned long long* e = enc + t * k;
+#pragma unroll 1
+    for (int s = gl; s < k; s += 16) code[s] = e[s];
+    wave_sync_lds();
+    grp_luts(lut, t, k, gl, gsh, code, base + 2048);
+}
+
+// lut_build's tables for alphabet t from its k code entries `code` (LDS), by the tree's 16
+// lanes; `scratch` = 3 KB of LDS (the L1 image u16 [2^w1 <= 512], the per-prefix widest
+// remainder / subtable id u32 [512]) + a counter word after them.  Same entries as
+// lut_build (whose comments give the format); only the pool ranges' placement may differ.
+__device__ __forceinline__ void grp_luts(const GrpLut& L, long long t, int k, int gl, int gsh,
+                                         const unsigned long long* code, char* scratch) {
+    const int w1 = L.w1, np = 1 << w1;                 // (w1 <= 9 here)
+    uint16_t* img = reinterpret_cast<uint16_t*>(scratch);
+    uint32_t* pre = reinterpret_cast<uint32_t*>(scratch + 1024);
+    uint32_t* nlong = reinterpret_cast<uint32_t*>(scratch + 3072);
+    for (int q = gl; q < 512 / 8; q += 16) reinterpret_cast<uint4*>(img)[q] = make_uint4(0, 0, 0, 0);
+    for (int q = gl; q < 512 / 4; q += 16) reinterpret_cast<uint4*>(pre)[q] = make_uint4(0, 0, 0, 0);
+    if (gl == 0) *nlong = 0;
+    wave_sync_lds();
+    // the widest remainder (capped at l2_bits) past W1 bits, per W1-bit prefix
+#pragma unroll 1
+    for (int s = gl; s < k; s += 16) {
+        const unsigned long long v = code[s];
+        const int len = (int)(v >> 56);
+        if (len > w1)
+            atomicMax(&pre[(unsigned)((v & kCodeMask) >> (len - w1))], (uint32_t)min(len - w1, L.l2_bits));
+    }
+    wave_sync_lds();
+    // subtable ids in prefix order: lane gl's np / 16 prefixes, a group scan of their counts
+    const int per = np / 16, p0 = gl * per;
+    uint32_t c_id = 0, w2 = 0;
+#pragma unroll 1
+    for (int p = p0; p < p0 + per; ++p) {
+        const uint32_t x = pre[p];
+        c_id += x ? 1u : 0u;
+        w2 = max(w2, x);
+    }
+    uint32_t incl = c_id;
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off, 16);
+        if (gl >= off) incl += y;
+    }
+#pragma unroll
+    for (int off = 8; off >= 1; off >>= 1) w2 = max(w2, (uint32_t)__shfl_xor(w2, off, 16));
+    const uint32_t nsub = __shfl(incl, 15, 16);
+    uint32_t id = incl - c_id;
+    // the pool range (sub ids must fit 12 bits; an alphabet without long codes takes none)
+    unsigned long long l0 = 0;
+    const bool ok = nsub < 4095;
+    const unsigned long long size = ok ? (unsigned long long)nsub << w2 : 0ull;
+    if (gl == 0 && size) l0 = atomicAdd(L.pool_head, size);
+    l0 = __shfl(l0, 0, 16);
+    const bool fits = ok && l0 + size <= (unsigned long long)L.lut2_cap;
+    if (gl == 0)
+        L.meta[t] = fits ? (uint32_t)((l0 << 9) | (w2 << 4) | (uint32_t)w1)
+                         : (0x100u | (w2 << 4) | (uint32_t)w1);
+    const bool subs = fits && w2 > 0;
+    uint16_t* const sub0 = L.lut2 + (subs ? (long long)l0 : 0);   // this alphabet's subtables
+    // (entries past the pool's end are dropped, as lut_build does)
+    const int room = subs ? (int)min((long long)nsub << w2, L.lut2_cap - (long long)l0) : 0;
+#pragma unroll 1
+    for (int p = p0; p < p0 + per; ++p) {   // long prefixes: their L1 entry, their sub id
+        if (pre[p]) {
+            img[p] = (uint16_t)((15u << 12) | (subs ? id : 0xFFFu));
+            pre[p] = id++;
+        }
+    }
+    if (subs) {   // zero the subtables (the fill below is ordered after these stores)
+#pragma clang loop unroll(disable) vectorize(disable) interleave(disable)
+        for (int q = gl; q < room; q += 16) sub0[q] = 0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    }
+    wave_sync_lds();
+    uint16_t* const L1 = L.lut1 + (t << kL1Max);
+#pragma unroll 1
+    for (int s = gl; s < k; s += 16) {
+        const unsigned long long v = code[s];
+        const int len = (int)(v >> 56);
+        L.enc32[t * k + s] = len <= 26 ? (uint32_t)(((unsigned long long)len << 26) | (v & kCodeMask)) : ~0u;
+        if (!len) continue;
+        const unsigned long long cbits = v & kCodeMask;
+        if (len <= w1) {   // replicated over the 2^(W1 - len) patterns that start with it
+            const unsigned first = (unsigned)(cbits << (w1 - len));
+            const uint16_t val = (uint16_t)((len << 12) | s);
+#pragma clang loop unroll(disable) vectorize(disable) interleave(disable)
+            for (unsigned j = 0; j < (1u << (w1 - len)); ++j) img[first + j] = val;
+            continue;
+        }
+        const unsigned p = (unsigned)(cbits >> (len - w1));
+        const int rem = len - w1;
+        if (subs) {
+            const int sb = (int)(pre[p] << w2);
+            if (rem <= (int)w2) {
+                const int b0 = sb + (int)((unsigned)(cbits & ((1ull << rem) - 1)) << (w2 - rem));
+                const uint16_t val = (uint16_t)((rem << 12) | s);
+#pragma clang loop unroll(disable) vectorize(disable) interleave(disable)
+                for (int j = b0; j < b0 + (1 << (w2 - rem)) && j < room; ++j) sub0[j] = val;
+                continue;
+            }
+            const int q = sb + (int)((cbits >> (rem - w2)) & ((1u << w2) - 1));
+            if (q < room) sub0[q] = (uint16_t)(15u << 12);
+        }
+        const uint32_t idx = atomicAdd(nlong, 1u);
+        L.longs[t * k + idx] = {cbits, (uint32_t)len, (uint32_t)s};
+    }
+    wave_sync_lds();
+#pragma unroll 1
+    for (int q = gl; q < np / 8; q += 16)   // the first level, 16 B per lane and store
+        reinterpret_cast<uint4*>(L1)[q] = reinterpret_cast<const uint4*>(img)[q];
+    if (gl == 0) L.long_cnt[t] = *nlong;
+}
 
 template <int KMAX, int TPW>
 __global__ void __launch_bounds__(64)
@@ -944,8 +1396,6 @@ huff_trees_par(const uint32_t* __restrict__ counts, int k, long long trees,
 //       entry (rem << 12) | sym, or 15 << 12 for codes longer than W1 + w2 (long list).
 //   meta[alphabet] = l2base << 9 | noL2 << 8 | w2 << 4 | W1   (l2base < 2^23)
 // lut_build sizes every alphabet, takes its L2 range from the pool and writes the entries.
-constexpr int kL1Max = 11;
-constexpr long long kL2BaseMax = 1ll << 23;
 
 // per W1-prefix: widest remainder (capped at l2_bits) of the codes longer than W1
 __device__ void block_w2max(const unsigned long long* e, int k, int w1, int l2_bits,
@@ -1425,7 +1875,23 @@ int pqh_tables_destroy(pqh_tables_t* t) {
     return PQH_OK;
 }
 
+static void launch_lut_grp(pqh_ctx* ctx, pqh_tables* t) {
+    const GrpLut lut{t->d_enc32, t->d_lut1, t->d_lut2, t->d_meta, t->d_long, t->d_long_cnt,
+                     reinterpret_cast<unsigned long long*>(t->d_err + 2), t->lut2_cap,
+                     t->l1_bits, t->l2_bits};
+    hipLaunchKernelGGL(lut_grp, dim3((unsigned)((t->tables + kGrpTrees - 1) / kGrpTrees)), dim3(64),
+                       0, ctx->stream, t->d_enc, t->k, t->tables, lut);
+}
+
 static int launch_luts(pqh_ctx* ctx, pqh_tables* t) {
+    // the 16-lane build for context tables (W1 = 9), lut_build otherwise
+    // (PQH_LUT_IMPL=block: lut_build for every table set)
+    const char* impl = std::getenv("PQH_LUT_IMPL");
+    if (!(impl && std::strcmp(impl, "block") == 0) && t->l1_bits <= 9 && t->k == 256) {
+        launch_lut_grp(ctx, t);
+        PQH_LAUNCH_CHECK(ctx);
+        return PQH_OK;
+    }
     // (the pool head, d_err[2..3], was zeroed with the error word before the trees)
     hipLaunchKernelGGL(lut_build, dim3((unsigned)t->tables), dim3(256), 0, ctx->stream, t->d_enc,
                        t->d_enc32, t->k, t->l1_bits, t->l2_bits, t->d_meta, t->d_lut1, t->d_lut2,
@@ -1457,7 +1923,7 @@ int pqh_tables_build_pair(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_cou
         t2->context != t->context || !t2->ctx || t2->ctx->device != t->ctx->device ||
         t->k > 256 || (reinterpret_cast<uintptr_t>(d_counts2) & 15u))
         return PQH_ERR_ARG;
-    int rc = build_trees(ctx, t, d_counts, PQH_TREES_LANE, t2, d_counts2);
+    int rc = build_trees(ctx, t, d_counts, PQH_TREES_DEFAULT, t2, d_counts2);
     if (!rc) rc = launch_luts(ctx, t);
     return rc ? rc : launch_luts(ctx, t2);
 }
@@ -1474,28 +1940,38 @@ static int build_trees(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts
     // any context of the tables' device may run the build (on its own stream), so the
     // builds of consecutive batches can overlap on different streams
     if (!ctx || !t || !d_counts || !t->ctx || t->ctx->device != ctx->device) return PQH_ERR_ARG;
-    if (which < PQH_TREES_DEFAULT || which > PQH_TREES_WAVE) return PQH_ERR_ARG;
+    if (which < PQH_TREES_DEFAULT || which > PQH_TREES_GROUP) return PQH_ERR_ARG;
     int rc = pqh_use_device(ctx);
     if (rc) return rc;
     PQH_HIP(ctx, hipMemsetAsync(t->d_err, 0, 16, ctx->stream));   // error word + LUT pool head
     if (t2) PQH_HIP(ctx, hipMemsetAsync(t2->d_err, 0, 16, ctx->stream));
     if (reinterpret_cast<uintptr_t>(d_counts) & 15u) return PQH_ERR_ARG;
     const long long trees = t->tables;
-    // Two builds of the same trees:
-    //  * one lane per tree through LDS (huff_trees_small, the default): 128 wavefronts of 16
-    //    trees -- a small footprint beside the next batches' assignment in the pipelined
-    //    bench (0.79 ms a batch there, 0.64 ms alone);
+    // Three builds of the same trees (K <= 256):
+    //  * 16 lanes per tree, four trees per wavefront (huff_trees_grp, the default): two LDS
+    //    round trips per pop, <= 32 VGPRs, so it runs beside the assignment grid;
+    //  * one lane per tree through LDS (huff_trees_small, PQH_TREE_IMPL=lane): 128
+    //    wavefronts of 16 trees, a heap level per LDS round trip (0.64 ms alone);
     //  * one wavefront per tree with the heap in registers (huff_trees_wave,
-    //    PQH_TREE_IMPL=wave): half the latency alone (0.40 vs 0.70 ms with the decode
-    //    tables), but its 2,048 wavefronts take wave slots and issue cycles from the
-    //    concurrent assignment (bench 1,610-1,880 Mvec/s against 2,270).
+    //    PQH_TREE_IMPL=wave): 0.40 ms alone, but 52 VGPRs.
     const char* impl = which == PQH_TREES_WAVE ? "wave"
-                     : which == PQH_TREES_LANE ? "lane" : std::getenv("PQH_TREE_IMPL");
+                     : which == PQH_TREES_LANE ? "lane"
+                     : which == PQH_TREES_GROUP ? "grp" : std::getenv("PQH_TREE_IMPL");
     if (t->k <= 256 && impl && std::strcmp(impl, "wave") == 0 && !t2) {
         // writes every entry (0 for symbols that never occur): no memset
         hipLaunchKernelGGL(huff_trees_wave, dim3((unsigned)((trees + kTreeWaves - 1) / kTreeWaves)),
                            dim3(64 * kTreeWaves), 0, ctx->stream, d_counts, t->k, trees, t->d_enc,
                            t->d_err);
+        PQH_LAUNCH_CHECK(ctx);
+        return PQH_OK;
+    }
+    if (t->k <= 256 && !(impl && std::strcmp(impl, "lane") == 0)) {
+        const long long blocks = (trees + kGrpTrees - 1) / kGrpTrees +
+                                 (t2 ? (t2->tables + kGrpTrees - 1) / kGrpTrees : 0);
+        hipLaunchKernelGGL(huff_trees_grp, dim3((unsigned)blocks), dim3(64), 0, ctx->stream, d_counts,
+                           t->k, trees, t->d_enc, t->d_err, t2 ? t2->tables : 0ll,
+                           t2 ? d_counts2 : d_counts, t2 ? t2->d_enc : t->d_enc,
+                           t2 ? t2->d_err : t->d_err);
         PQH_LAUNCH_CHECK(ctx);
         return PQH_OK;
     }

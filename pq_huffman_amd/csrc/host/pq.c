@@ -33,8 +33,8 @@ int centroids_codebook_save(const centroids_codebook_t* cb, const char* filename
     save_vecs_light_meta_file(f, (long long)cb->num_parts * cb->num_clusters, cb->num_dimensions);
     size_t cnt = (size_t)cb->num_parts * cb->num_clusters * cb->num_dimensions;
     size_t w = fwrite(cb->centroids_pool, sizeof(float), cnt, f);
-    fclose(f);
-    return w == cnt ? 0 : -1;
+    const int bad = ferror(f);
+    return fclose(f) == 0 && !bad && w == cnt ? 0 : -1;
 }
 
 int centroids_codebook_load(centroids_codebook_t* cb, const char* filename, int num_parts,

@@ -6,9 +6,13 @@
  * iterations on the GPU (pq_train: exact assignment, fixed-point centroid means) from a
  * seeded sample init (yael's time-seeded Berkeley init is not reproducible); --centroids
  * skips training.  --num-threads is accepted for compatibility. */
+#define _FILE_OFFSET_BITS 64
+#define _POSIX_C_SOURCE 200809L
+#include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/types.h>
 
 #include "misc.h"
 #include "pq.h"
@@ -20,6 +24,35 @@ static unsigned long long rng_next(void) {
     rng_state ^= rng_state >> 7;
     rng_state ^= rng_state << 17;
     return rng_state;
+}
+
+/* Streaming .fvecs reader for pq_encode_rows: rows [row0, row0 + rows) into dst, the
+ * per-row i32 dimension headers dropped (pq_encoder.c:58-80 reads 128K-row batches). */
+typedef struct {
+    FILE* f;
+    int d;
+    int32_t* raw;
+    long long cap;    /* rows of raw */
+    long long next;   /* the row the file position is at */
+} fvecs_reader_t;
+
+static int fvecs_rows(void* user, long long row0, long long rows, float* dst) {
+    fvecs_reader_t* r = (fvecs_reader_t*)user;
+    const long long rb = 4LL * (r->d + 1);
+    if (row0 != r->next && fseeko(r->f, (off_t)(row0 * rb), SEEK_SET)) return -1;
+    r->next = row0;
+    while (rows > 0) {
+        const long long want = rows < r->cap ? rows : r->cap;
+        if (fread(r->raw, (size_t)rb, (size_t)want, r->f) != (size_t)want) return -1;
+        for (long long i = 0; i < want; ++i) {
+            if (r->raw[i * (r->d + 1)] != r->d) return -1;   /* a row of another dimension */
+            memcpy(dst + i * r->d, r->raw + i * (r->d + 1) + 1, (size_t)r->d * sizeof(float));
+        }
+        dst += want * r->d;
+        rows -= want;
+        r->next += want;
+    }
+    return 0;
 }
 
 int main(int argc, const char* argv[]) {
@@ -46,13 +79,13 @@ int main(int argc, const char* argv[]) {
     }
     long long n = 0;
     int d = 0;
-    float* x = fvecs_load(input, &n, &d);
-    if (!x || m <= 0 || d % m) {
+    if (fvecs_load_meta(input, &n, &d) || m <= 0 || d % m) {
         fprintf(stderr, "cannot read %s or D %% m != 0\n", input);
         return 1;
     }
     const int ds = d / m;
     unsigned char* codes = (unsigned char*)malloc((size_t)n * m + 1);
+    float* x = NULL;   /* the whole input: only for training and the error pass */
     centroids_codebook_t cb;
     if (cfile) {
         if (centroids_codebook_load(&cb, cfile, m, k) || cb.num_dimensions != ds) {
@@ -60,6 +93,11 @@ int main(int argc, const char* argv[]) {
             return 1;
         }
     } else {
+        x = fvecs_load(input, &n, &d);
+        if (!x) {
+            fprintf(stderr, "cannot read %s\n", input);
+            return 1;
+        }
         centroids_codebook_init(&cb, m, k, ds);
         for (int c = 0; c < k; ++c) {
             long long v = n ? (long long)(rng_next() % (unsigned long long)n) : 0;
@@ -72,27 +110,51 @@ int main(int argc, const char* argv[]) {
             return 1;
         }
     }
-    int rc = pq_encode(&cb, x, n, d, codes);
+    int rc;
+    if (x) {
+        rc = pq_encode(&cb, x, n, d, codes);   /* streamed to the GPU in chunks */
+    } else {   /* fixed centroids: stream the file itself, never holding it whole */
+        fvecs_reader_t rd = {fopen(input, "rb"), d, NULL, 1 << 16, 0};
+        rd.raw = (int32_t*)malloc((size_t)rd.cap * (d + 1) * 4);
+        rc = rd.f && rd.raw ? pq_encode_rows(&cb, d, n, fvecs_rows, &rd, codes, 0) : -1;
+        if (rd.f) fclose(rd.f);
+        free(rd.raw);
+    }
     if (rc) {
         fprintf(stderr, "pq_encode failed: %d\n", rc);
         return 1;
     }
     char* pc = concat(tmpl, "pq_centroids.fvecsl");
     char* pi = concat(tmpl, "pq_indices.bvecsl");
-    centroids_codebook_save(&cb, pc);
+    if (centroids_codebook_save(&cb, pc)) {
+        fprintf(stderr, "cannot write %s\n", pc);
+        return 1;
+    }
     FILE* f = fopen(pi, "wb");
+    if (!f) {
+        fprintf(stderr, "cannot open %s\n", pi);
+        return 1;
+    }
     save_vecs_light_meta_file(f, n, m);
-    fwrite(codes, (size_t)m, (size_t)n, f);
-    fclose(f);
+    const size_t wrote = n ? fwrite(codes, (size_t)m, (size_t)n, f) : 0;
+    if (wrote != (size_t)n || ferror(f) || fclose(f)) {
+        fprintf(stderr, "cannot write %s\n", pi);
+        return 1;
+    }
     if (compute_error) {
+        if (!x) x = fvecs_load(input, &n, &d);
         double err = 0;
-        if (pq_compute_error(&cb, x, n, d, codes, &err) == 0) {
-            char* pe = concat(tmpl, "pq_error");
-            FILE* ef = fopen(pe, "a");
-            fprintf(ef, "%lf\n", err);
-            fclose(ef);
-            free(pe);
+        if (!x || pq_compute_error(&cb, x, n, d, codes, &err)) {
+            fprintf(stderr, "compute_error failed\n");
+            return 1;
         }
+        char* pe = concat(tmpl, "pq_error");
+        FILE* ef = fopen(pe, "a");
+        if (!ef || fprintf(ef, "%lf\n", err) < 0 || fclose(ef)) {
+            fprintf(stderr, "cannot write %s\n", pe);
+            return 1;
+        }
+        free(pe);
     }
     free(pc);
     free(pi);

@@ -328,6 +328,11 @@ class TorchComm:
                 self._tensors.append(t)
         return self
 
+    def clear(self):
+        """forget the registered tensors (shard_encode registers its buffers per call)"""
+        self._tensors = []
+        return self
+
     def _view(self, ptr, nbytes, dtype):
         import torch
         for t in self._tensors:
@@ -371,11 +376,14 @@ class _null:
 
 
 def shard_encode(ctx, comm: TorchComm, codes, tables, counts, out, chunk_vectors=0,
-                 chunk_offsets=None, chunk_prev=None, first_row=0):
+                 chunk_offsets=None, chunk_prev=None, first_row=0, raw_first=True):
     """This rank's encode through pqh_shard_encode (halo, histogram all-reduce, GPU code
-    tables, lengths all-gather, device offsets, write).  codes: (n, m) uint8 cuda tensor
-    (n may be 0); counts: (m, items) int32; out: uint8 buffer.  Returns (offsets, raw_first):
-    offsets a (2,) int64 device tensor {global bit offset, global length}."""
+    tables, lengths all-gather, device offsets, write) -- asynchronous on ctx's stream.
+    codes: (n, m) uint8 cuda tensor (n may be 0); counts: (m, items) int32; out: uint8
+    buffer.  Returns (offsets, raw): offsets a (2,) int64 device tensor {global bit offset,
+    global length}; raw = whether this shard wrote the raw first row (read back from the
+    device when raw_first is True -- the call's one host round trip -- else None).  A failure
+    on another rank shows in offsets[1] == -1 (status())."""
     import torch
     from .capi import Block, check
     n, m = codes.shape
@@ -383,18 +391,31 @@ def shard_encode(ctx, comm: TorchComm, codes, tables, counts, out, chunk_vectors
     scratch = torch.empty(int(_lib().pqh_shard_scratch_bytes(comm.world, m)), dtype=torch.uint8,
                           device=dev)
     offsets = torch.zeros(2, dtype=torch.int64, device=dev)
-    comm.register(counts, scratch)
     b = Block()
     b.id, b.size, b.capacity = first_row, n, n
     raw = ctypes.c_int()
     ptr = (lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None)
     comm.error = None
-    rc = _lib().pqh_shard_encode(ctx.ptr, ctypes.byref(comm.struct), ctypes.byref(b),
-                                 ptr(codes) if n else None, m, tables.k, int(tables.context),
-                                 tables.ptr, ptr(counts), ptr(out), out.numel(), chunk_vectors,
-                                 ptr(chunk_offsets), ptr(chunk_prev), ptr(offsets), ptr(scratch),
-                                 ctypes.byref(raw))
+    comm.register(counts, scratch)   # the hooks' buffers, for this call only
+    try:
+        rc = _lib().pqh_shard_encode(ctx.ptr, ctypes.byref(comm.struct), ctypes.byref(b),
+                                     ptr(codes) if n else None, m, tables.k, int(tables.context),
+                                     tables.ptr, ptr(counts), ptr(out), out.numel(), chunk_vectors,
+                                     ptr(chunk_offsets), ptr(chunk_prev), ptr(offsets),
+                                     ptr(scratch), ctypes.byref(raw) if raw_first else None)
+    finally:
+        comm.clear()
     if comm.error is not None:
         raise comm.error
     check(rc, "pqh_shard_encode")
-    return offsets, raw.value
+    if ctx.stream != torch.cuda.current_stream(dev):
+        scratch.record_stream(ctx.stream)   # (asynchronous: keep it until the stream is done)
+    return offsets, (raw.value if raw_first else None)
+
+
+def status(ctx, offsets):
+    """Synchronise; raise if any rank's pqh_shard_encode behind `offsets` failed
+    (pqh_shard_status: PQH_ERR_REMOTE)."""
+    from .capi import check
+    check(_lib().pqh_shard_status(ctx.ptr, ctypes.c_void_p(offsets.data_ptr())),
+          "pqh_shard_status")

@@ -4,8 +4,10 @@ rank on cuda:0 (a fresh process per rank).  Writes rank 0's result to --out (.np
 the stitched stream (pqh_shard_stitch of every rank's buffer), the global histogram, and
 the rows the ranks encoded, for the test to compare with the oracle's one-shot results.
 
-  --case even|ragged|sort   --mode ctx|noctx
-even: contiguous shards; ragged: rank 1 holds no rows; sort: the distributed sample sort
+  --case even|ragged|sort|fail   --mode ctx|noctx
+even: contiguous shards; ragged: rank 1 holds no rows; fail: rank 1's call fails locally
+(an output buffer too small) -- both ranks must return, rank 1 with its error and rank 0
+through pqh_shard_status; sort: the distributed sample sort
 (shard.sort_rows_distributed with the library's stable radix sort) then the sorted slices,
 whose halo also goes through shard.halo_ragged into codec.histogram / encode_size (the
 library's halo must agree)."""
@@ -54,6 +56,27 @@ def main():
     tabs = codec.Tables(ctx, m, k, ctxm)
     out = torch.zeros(n * m * 7 + 64, dtype=torch.uint8, device="cuda")
     comm = shard.TorchComm(world, rank)
+    if a.case == "fail":
+        from pq_huffman_amd.capi import PqhError
+        bad = out[:2] if rank == 1 else out            # rank 1: out_bytes < 4 (local failure)
+        try:
+            offsets, _ = shard.shard_encode(ctx, comm, mine, tabs, counts, bad, first_row=b,
+                                            raw_first=False)
+            assert rank != 1, "rank 1's bad buffer was accepted"
+            try:
+                shard.status(ctx, offsets)
+                raise AssertionError("rank 0 did not see rank 1's failure")
+            except PqhError as e:
+                assert "another rank" in str(e), str(e)
+        except PqhError as e:
+            assert rank == 1 and "invalid argument" in str(e), str(e)
+        dist.barrier()
+        if rank == 0:
+            np.savez(a.out, failed=np.int64(1))
+        tabs.close()
+        ctx.close()
+        dist.destroy_process_group()
+        return
     offsets, raw = shard.shard_encode(ctx, comm, mine, tabs, counts, out, first_row=b)
     torch.cuda.synchronize()
     goff, total = (int(v) for v in offsets.cpu().tolist())

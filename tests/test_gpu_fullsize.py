@@ -31,39 +31,48 @@ def gpu():
     return torch, codec, codec.Context(0)
 
 
-def _bench_path(gpu, x, cent, chunk=8):
-    """the bench's per-batch calls, in its order, on one stream"""
+def _bench_path(gpu, x, cent, chunk=8, ctxm=True, sort=False):
+    """the bench's per-batch calls, in its order, on one stream (bench.py front/back):
+    assignment [-> sort] -> histogram -> GPU code tables -> one-pass encode -> decode"""
     torch, codec, ctx = gpu
     n = x.shape[0]
     m, k, _ = cent.shape
     pq = codec.PQ(ctx, cent)
-    codes = torch.empty((n, m), dtype=torch.uint8, device=x.device)
+    codes = torch.empty((n, m), dtype=torch.uint8 if k <= 256 else torch.int16, device=x.device)
     pq.assign(x, codes)
-    counts = torch.empty((m, k * k), dtype=torch.int32, device=x.device)
-    codec.histogram(ctx, codes, k, True, counts=counts, accumulate=False)
-    tabs = codec.Tables(ctx, m, k, True).build(counts)
+    if sort:   # stable strncmp-key sort of the rows, in place (huffman_encoder.c:301-317)
+        codec.sort_rows(ctx, codes, torch.empty_like(codes))
+    counts = torch.empty((m, k * k if ctxm else k), dtype=torch.int32, device=x.device)
+    codec.histogram(ctx, codes, k, ctxm, counts=counts, accumulate=False)
+    tabs = codec.Tables(ctx, m, k, ctxm).build(counts)
     chunks = (n + chunk - 1) // chunk
     out = torch.empty(n * m * 56 // 8 + 64, dtype=torch.uint8, device=x.device)
     coff = torch.empty(chunks, dtype=torch.int64, device=x.device)
-    cprev = torch.empty((chunks, m), dtype=torch.uint8, device=x.device)
+    cprev = torch.empty((chunks, m), dtype=torch.uint8, device=x.device) if ctxm else None
     tot = torch.zeros(1, dtype=torch.int64, device=x.device)
-    codec.encode_write(ctx, tabs, codes, out, 0, 1, None, chunk, coff, cprev, total=tot)
+    raw_first = 1 if ctxm else 0
+    codec.encode_write(ctx, tabs, codes, out, 0, raw_first, None, chunk, coff, cprev, total=tot)
     codec.encode_status(ctx)
-    enc = codec.Encoded(out, int(tot.item()), chunk, coff, cprev, n, 1)
+    enc = codec.Encoded(out, int(tot.item()), chunk, coff, cprev, n, raw_first)
     dec = codec.decode(ctx, tabs, enc)
     codec.decode_status(ctx)
     tabs.status()
     return pq, codes, counts, tabs, enc, dec
 
 
-def _check_against_oracle(gpu, oracle, xh, cent, codes, tabs, enc, dec):
+def _check_against_oracle(gpu, oracle, xh, cent, codes, tabs, enc, dec, ctxm=True, sort=False):
     torch, codec, ctx = gpu
     assert torch.equal(dec, codes)
+    k = cent.shape[1]
     hc = codes.cpu().numpy()
+    if k > 256:
+        hc = hc.view(np.uint16)
     want, _ = oracle.pq_assign(xh, cent, threads=0)
+    if sort:
+        want = oracle.sort_rows(want)
     bad = int((hc != want).sum())
     assert bad == 0, f"{bad} PQ codes differ from the oracle"
-    ocb = oracle.build_codebooks(want, cent.shape[1], True)
+    ocb = oracle.build_codebooks(want, k, ctxm)
     assert tabs.codebooks().file_bytes() == oracle.codebooks_file(ocb)
     stream, bits = oracle.encode(want, ocb)
     assert enc.bits == bits
@@ -91,6 +100,37 @@ def test_bench_path_deep1m_all_rows(gpu, oracle):
     x = torch.from_numpy(xh).cuda()
     pq, codes, counts, tabs, enc, dec = _bench_path(gpu, x, cent)
     _check_against_oracle(gpu, oracle, xh, cent, codes, tabs, enc, dec)
+
+
+def test_bench_path_k4096_1m_all_rows(gpu, oracle):
+    """configs[4] as `bench.py --config k4096` runs it, on all 1,000,000 rows: K = 4,096
+    assignment (u16 codes, centroid tiles from L2) -> non-context histogram -> huff_trees_par
+    code tables -> one-pass encode -> chunked decode; every code, the codebook file and the
+    stream bytes against the oracle (src/huffman_encode.c:141-192, src/huffman_encoder.c:207-218)."""
+    import bench
+    torch, codec, ctx = gpu
+    dev = torch.device("cuda", 0)
+    x = bench.make_data(torch, 1_000_000, 128, 0x5EED, 0, dev)
+    cent = bench.train_centroids(torch, bench.make_data(torch, 200_000, 128, 0x5EED, 0, dev),
+                                 8, 4096)
+    pq, codes, counts, tabs, enc, dec = _bench_path(gpu, x, cent, ctxm=False)
+    assert pq.rerank_count() > 0
+    _check_against_oracle(gpu, oracle, x.cpu().numpy(), cent, codes, tabs, enc, dec, ctxm=False)
+
+
+def test_bench_path_sort_1m_all_rows(gpu, oracle):
+    """`bench.py --sort` (the reference's default sort + context mode) on all 1,000,000 rows:
+    assignment -> stable strncmp-key sort on the device -> context histogram -> GPU code tables
+    -> encode -> decode, against the oracle's sorted codes, codebooks and stream
+    (src/huffman_encoder.c:301-318, src/huffman_encode.c:235-269)."""
+    import bench
+    torch, codec, ctx = gpu
+    dev = torch.device("cuda", 0)
+    x = bench.make_data(torch, 1_000_000, 128, 0x5EED, 0, dev)
+    cent = bench.train_centroids(torch, bench.make_data(torch, 200_000, 128, 0x5EED, 0, dev),
+                                 8, 256)
+    pq, codes, counts, tabs, enc, dec = _bench_path(gpu, x, cent, sort=True)
+    _check_against_oracle(gpu, oracle, x.cpu().numpy(), cent, codes, tabs, enc, dec, sort=True)
 
 
 def test_configs2_shard_125m_rows(gpu, oracle):

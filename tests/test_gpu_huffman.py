@@ -202,7 +202,7 @@ def test_full_size_roundtrip_sift1m(gpu, oracle, ctxm):
 @pytest.mark.parametrize("case", ["enc_test_many", "enc_test_one", "enc_test_zero",
                                   "ties_small_ints", "ties_all_equal", "ties_powers",
                                   "single_symbol", "empty", "geometric"])
-@pytest.mark.parametrize("impl", ["lane", "wave"])
+@pytest.mark.parametrize("impl", ["grp", "lane", "wave"])
 def test_gpu_tree_builder_vs_reference_codebooks(gpu, case, impl, monkeypatch):
     """pqh_tables_build (GPU heap simulation, both builds) == the reference's codebook bytes."""
     monkeypatch.setenv("PQH_TREE_IMPL", impl)
@@ -216,7 +216,7 @@ def test_gpu_tree_builder_vs_reference_codebooks(gpu, case, impl, monkeypatch):
 
 
 @pytest.mark.parametrize("ctxm", [True, False])
-@pytest.mark.parametrize("impl", ["lane", "wave"])
+@pytest.mark.parametrize("impl", ["grp", "lane", "wave"])
 def test_gpu_tree_builder_vs_host_builder_ties(gpu, ctxm, impl, monkeypatch):
     """2048 tie-heavy context trees (or 8 plain ones): GPU tables == host codebooks."""
     monkeypatch.setenv("PQH_TREE_IMPL", impl)
@@ -237,7 +237,63 @@ def test_gpu_tree_builder_vs_host_builder_ties(gpu, ctxm, impl, monkeypatch):
     assert dev.codebooks().file_bytes() == host.file_bytes()
 
 
-@pytest.mark.parametrize("impl", ["lane", "wave"])
+@pytest.mark.parametrize("impl", ["grp", "lane"])
+def test_gpu_tree_builder_random_shapes(gpu, impl, monkeypatch):
+    """2048 context alphabets of random size (0 to 256 symbols) and shape -- tie-heavy small
+    counts, geometric, Zipf, a few dominant symbols, all equal -- GPU tables == host codebooks
+    (every sift depth of the 16-lane stretches, heaps of 1 to 256 entries)."""
+    monkeypatch.setenv("PQH_TREE_IMPL", impl)
+    torch, codec, ctx = gpu
+    rng = np.random.default_rng(57)
+    counts = np.zeros((8, 256 * 256), np.int64)
+    for t in range(8 * 256):
+        nzc = int(rng.choice([0, 1, 2, 3, 7, 16, 17, 31, 64, 100, 200, 255, 256]))
+        sym = rng.choice(256, nzc, replace=False)
+        kind = t % 5
+        if kind == 0:
+            w = rng.integers(1, 4, nzc)
+        elif kind == 1:
+            w = 2 ** rng.integers(0, 12, nzc)
+        elif kind == 2:
+            w = np.floor(5e4 / (np.arange(nzc) + 1) ** 1.2).astype(np.int64) + 1
+        elif kind == 3:
+            w = rng.integers(1, 6, nzc)
+            w[: max(1, nzc // 20)] = rng.integers(10_000, 20_000)
+        else:
+            w = np.full(nzc, 7)
+        counts[t // 256, (t % 256) * 256 + sym] = w
+    dev = codec.Tables(ctx, 8, 256, True).build(torch.from_numpy(counts.astype(np.int32)).cuda())
+    host = codec.Codebooks(counts.astype(np.float64), 256, True)
+    assert dev.codebooks().file_bytes() == host.file_bytes()
+
+
+@pytest.mark.parametrize("luts", ["grp", "block"])
+def test_gpu_decode_tables_long_codes(gpu, luts, monkeypatch):
+    """Context decode tables (lut_grp, the default, and lut_build, PQH_LUT_IMPL=block) for
+    alphabets whose codes reach ~30 bits: first level (W1 = 9), second-level subtables and
+    the long-code list all used; every row round-trips (huffman_decode.c:137-191)."""
+    monkeypatch.setenv("PQH_LUT_IMPL", luts)
+    torch, codec, ctx = gpu
+    rng = np.random.default_rng(61)
+    m, k, n = 8, 256, 30000
+    w = np.maximum(1, np.floor(2.0 ** 20 / 1.5 ** np.arange(k))).astype(np.int64)
+    counts = np.zeros((m, k * k), np.int64)
+    for i in range(m):
+        for c in range(k):
+            counts[i, c * k:(c + 1) * k] = np.roll(w, (7 * c + i) % k)   # every pair coded
+    tabs = codec.Tables(ctx, m, k, True).build(torch.from_numpy(counts.astype(np.int32)).cuda())
+    host = codec.Codebooks(counts.astype(np.float64), k, True)
+    assert tabs.codebooks().file_bytes() == host.file_bytes()
+    codes = torch.from_numpy(rng.integers(0, k, (n, m)).astype(np.uint8)).cuda()
+    for chunk in (1, 8, 33):
+        enc = codec.encode(ctx, tabs, codes, chunk_vectors=chunk)
+        codec.encode_status(ctx)
+        dec = codec.decode(ctx, tabs, enc)
+        codec.decode_status(ctx)
+        assert torch.equal(dec, codes)
+
+
+@pytest.mark.parametrize("impl", ["grp", "lane", "wave"])
 def test_gpu_tree_builder_mixed_heavy_light(gpu, impl, monkeypatch):
     """Context alphabets of one workgroup that take different heaps: frequent previous
     symbols give trees past 2^22 (64-bit keys), rare ones stay on the u32 sentinel heap.
@@ -277,7 +333,7 @@ def test_gpu_tree_builder_pair(gpu, ctxm):
 
 
 @pytest.mark.parametrize("ctxm", [True, False])
-@pytest.mark.parametrize("impl", ["lane", "wave"])
+@pytest.mark.parametrize("impl", ["grp", "lane", "wave"])
 def test_gpu_tree_builder_heavy_and_rebuilt(gpu, ctxm, impl, monkeypatch):
     """Trees whose total weight reaches 2^22 (64-bit heap keys) with ties, and a table set
     rebuilt from a histogram with fewer symbols: every entry is rewritten (the build does not
@@ -359,7 +415,12 @@ def test_cli_tools_match_reference_files(tmp_path, mode, flags):
     assert np.array_equal(np.fromfile(dec, np.uint8).reshape(1000, 8), want)
 
 
-def test_cli_pq_encoder_fixed_centroids(tmp_path, oracle):
+@pytest.mark.parametrize("chunk", [None, "97"])
+def test_cli_pq_encoder_fixed_centroids(tmp_path, oracle, chunk, monkeypatch):
+    """pq_encoder --centroids streams the .fvecs file to the GPU (pq_encode_rows; chunk 97:
+    eleven chunks of a 1,000-row file) and writes the reference's files."""
+    if chunk:
+        monkeypatch.setenv("PQH_ENCODE_CHUNK", chunk)
     g = golden("pq_sift_n1000_m8_k256.npz")
     bind = os.path.join(ROOT, "pq_huffman_amd", "bin")
     datagen.write_fvecs(str(tmp_path / "x.fvecs"), g["x"])

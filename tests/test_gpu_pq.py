@@ -225,3 +225,28 @@ def test_cli_pq_encoder_trains_on_gpu(gpu, oracle, tmp_path):
     codes_raw = (tmp_path / "pq_indices.bvecsl").read_bytes()
     want_codes, _ = oracle.pq_assign(x, want, threads=0)
     assert np.array_equal(np.frombuffer(codes_raw[8:], np.uint8).reshape(5000, 8), want_codes)
+
+
+def test_pq_encode_streams_in_chunks(gpu, oracle, monkeypatch):
+    """pq.h pq_encode (host pointers) on 7,777 rows through 1,000-row chunks -- two pinned
+    buffers, so device memory holds two chunks -- equals the one-shot device assignment and
+    the oracle (src/pq_encoder.c:43,58-80 reads 128K-row batches)."""
+    import ctypes
+    from pq_huffman_amd.capi import lib
+
+    class CB(ctypes.Structure):   # pq.h centroids_codebook_t
+        _fields_ = [("num_clusters", ctypes.c_int), ("num_dimensions", ctypes.c_int),
+                    ("num_parts", ctypes.c_int), ("centroids_pool", ctypes.c_void_p),
+                    ("centroids", ctypes.c_void_p)]
+
+    monkeypatch.setenv("PQH_ENCODE_CHUNK", "1000")
+    n = 7777
+    x = datagen.sift_like(n, 128, seed=5)
+    cent = np.ascontiguousarray(datagen.lloyd_centroids(x, 8, 256, iters=1, sample=4000), np.float32)
+    cb = CB(256, 16, 8, cent.ctypes.data, None)
+    codes = np.zeros((n, 8), np.uint8)
+    assert lib().pq_encode(ctypes.byref(cb), x.ctypes.data, n, 128, codes.ctypes.data) == 0
+    one_shot, _ = _assign(gpu, x, cent)
+    assert np.array_equal(codes, one_shot)
+    want, _ = oracle.pq_assign(x, cent, threads=0)
+    assert np.array_equal(codes, want)

@@ -46,3 +46,17 @@ def test_two_rank_library_shard_encode(oracle, tmp_path, case, mode):
     want, bits = oracle.encode(rows, oracle.build_codebooks(rows, 256, ctxm))
     assert int(d["total"]) == bits
     assert d["stream"].tobytes() == want
+
+
+def test_two_rank_library_shard_encode_one_rank_fails(tmp_path):
+    """A local failure on rank 1 (an output buffer too small) must not leave rank 0 waiting
+    in a collective: rank 1 gets its error, rank 0 PQH_ERR_REMOTE from pqh_shard_status."""
+    dump = tmp_path / "shard.npz"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(ROOT, "tests", "shard_worker.py"), "--case", "fail", "--mode", "ctx",
+           "--out", str(dump)]
+    r = subprocess.run(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1"), capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert int(np.load(dump, allow_pickle=False)["failed"]) == 1
