@@ -111,7 +111,7 @@ SIGNATURES = [
     ("centroids_codebook_save", I, [P, S]), ("centroids_codebook_load", I, [P, S, I, I]),
     ("fvecs_load_meta", I, [S, P, P]), ("fvecs_load", P, [S, P, P]),
     ("pq_encode", I, [P, P, LL, I, P]), ("pq_compute_error", I, [P, P, LL, I, P, P]),
-    ("pq_train", I, [P, P, LL, I, I]),
+    ("pq_train", I, [P, P, LL, I, I]), ("pq_encode_rows", I, [P, I, LL, P, P, P, LL]),
     # pqh.h
     ("pqh_ctx_create", I, [P, I]), ("pqh_ctx_destroy", I, [P]), ("pqh_ctx_set_stream", I, [P, P]),
     ("pqh_ctx_create_cu_limited", I, [P, I, I]), ("pqh_ctx_create_cu_split", I, [P, I, I, I]), ("pqh_ctx_stream", P, [P]),

@@ -37,8 +37,10 @@ __device__ __forceinline__ unsigned ld_code(const CodeT* c, long long i) { retur
 // The grid is 1-D and XCD-aware: workgroup L runs on XCD L % 8, and the m * split workgroups
 // of a chunk all get L % 8 = chunk % 8, so the chunk's rows are fetched from HBM into one
 // XCD's L2 once instead of once per XCD.
-template <typename CodeT>
-__global__ void __launch_bounds__(1024)
+// BLK = 1024 threads (20 rows per load group), or 256 threads with 8-row groups: <= 32
+// VGPRs and one wave per SIMD, so it fits on a CU beside the assignment grid's waves.
+template <typename CodeT, int BLK = 1024, int kSub = 20>
+__global__ void __launch_bounds__(BLK)
 hist_ctx(const CodeT* __restrict__ codes, long long n, int m_total, int k,
          const CodeT* __restrict__ prev_row, const int* __restrict__ d_rawf,
          uint32_t* __restrict__ partial, int split, int chunks) {
@@ -54,9 +56,9 @@ hist_ctx(const CodeT* __restrict__ codes, long long n, int m_total, int k,
     const unsigned plo = (unsigned)(zs * prows);
     const int all_words = (k * k + 1) / 2;
     const int words = split == 1 ? all_words : prows * k / 2;
+#pragma clang loop unroll_count(4) vectorize(disable) interleave(disable)
     for (int w = threadIdx.x; w < words; w += blockDim.x) pairs[w] = 0;
-    constexpr int kRun = kHistChunk / 1024;   // consecutive vectors per thread
-    constexpr int kSub = 20;                  // ... taken kSub at a time (registers)
+    constexpr int kRun = kHistChunk / BLK;    // consecutive vectors per thread, taken kSub
     static_assert(kRun % kSub == 0 && kSub % 2 == 0, "whole 16-byte row pairs per group");
     const long long v0 = (long long)chunk * kHistChunk + (long long)threadIdx.x * kRun;
     auto count = [&](unsigned prev, unsigned cur) {
@@ -75,6 +77,7 @@ hist_ctx(const CodeT* __restrict__ codes, long long n, int m_total, int k,
         // loads issued before its counter updates (8-byte rows of u8 codes: 16 B per load)
         const uint4* rows = reinterpret_cast<const uint4*>(codes + v0 * 8);
         const int sh = 8 * (m & 3);
+#pragma unroll 1
         for (int g = 0; g < kRun / kSub; ++g) {
             uint4 q[kSub / 2];
 #pragma unroll
@@ -101,8 +104,10 @@ hist_ctx(const CodeT* __restrict__ codes, long long n, int m_total, int k,
     if ((words & 3) == 0) {
         const uint4* src = reinterpret_cast<const uint4*>(pairs);
         uint4* dst = reinterpret_cast<uint4*>(out);
+#pragma clang loop unroll_count(2) vectorize(disable) interleave(disable)
         for (int w = threadIdx.x; w < words / 4; w += blockDim.x) dst[w] = src[w];
     } else {
+#pragma clang loop unroll(disable) vectorize(disable) interleave(disable)
         for (int w = threadIdx.x; w < words; w += blockDim.x) out[w] = pairs[w];
     }
 }
@@ -234,6 +239,19 @@ scan_blocks(const uint32_t* __restrict__ block_bits, long long nb,
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
+// Inclusive wave64 scan of u32 with DPP row shifts and row broadcasts (no LDS permutes, no
+// lane-address registers): rows of 16 scan by row_shr 1/2/4/8, then row 15's / 31's
+// totals are broadcast into the rows after them.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);   // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);   // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);   // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);   // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);   // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);   // row_bcast:31
+    return v;
+}
+
 // decoupled look-back state words: epoch (16 bits) | status (2) | value (46)
 constexpr unsigned long long kLbAgg = 1ull << 46, kLbPrefix = 2ull << 46;
 constexpr unsigned long long kLbValue = (1ull << 46) - 1;
@@ -282,15 +300,16 @@ __device__ __forceinline__ void load_row(const CodeT* __restrict__ codes, long l
     }
 }
 
-// The m (code, length) entries of vector v, all table loads issued together
-// (huffman_encoder.c:207-238: context index (prev << 8) + cur; context row 0 raw 8 bits)
+// The m table entries of vector v as the u32 gather copy (len << 26 | code; ~0u = a code
+// longer than 26 bits, read from the u64 table when it is emitted), all loads issued together
+// (huffman_encoder.c:207-238: context index (prev << 8) + cur; context row 0 raw 8 bits).
+// u32 entries keep a vector's m entries in m registers, not 2m.
 template <typename CodeT, int MAXM>
 __device__ __forceinline__ void gather_entries(const CodeT* __restrict__ codes, long long v, int m,
                                                int k, int context, int raw_first,
                                                const CodeT* __restrict__ prev_row,
-                                               const unsigned long long* __restrict__ enc,
                                                const uint32_t* __restrict__ enc32,
-                                               long long items, unsigned long long (&ent)[MAXM],
+                                               long long items, uint32_t (&e32)[MAXM],
                                                const uint16_t* __restrict__ tree_prev) {
     unsigned cur[MAXM], prv[MAXM];
     load_row<CodeT, MAXM>(codes, v, m, cur);
@@ -304,23 +323,15 @@ __device__ __forceinline__ void gather_entries(const CodeT* __restrict__ codes, 
 #pragma unroll
         for (int i = 0; i < MAXM; ++i) prv[i] = (context && prev_row && i < m) ? (unsigned)prev_row[i] : 0u;
     }
-    uint32_t e32[MAXM];
-    long long idx[MAXM];
 #pragma unroll
     for (int i = 0; i < MAXM; ++i) {
         const bool ok = i < m && cur[i] < (unsigned)k && (!context || prv[i] < (unsigned)k) && !raw;
-        idx[i] = ok ? (long long)i * items +
-                          (context ? (long long)prv[i] * k + cur[i] : (long long)cur[i])
-                    : -1;
-        e32[i] = ok ? enc32[idx[i]] : 0u;
+        const long long idx = i * items + (context ? (long long)prv[i] * k + cur[i] : (long long)cur[i]);
+        e32[i] = ok ? enc32[idx] : 0u;
     }
-#pragma unroll
-    for (int i = 0; i < MAXM; ++i)
-        ent[i] = e32[i] == ~0u ? enc[idx[i]]   // codes longer than 26 bits: rare
-                               : ((unsigned long long)(e32[i] >> 26) << 56) | (e32[i] & ((1u << 26) - 1));
     if (raw) {
 #pragma unroll
-        for (int i = 0; i < MAXM; ++i) ent[i] = i < m ? ((8ull << 56) | (cur[i] & 0xFFu)) : 0ull;
+        for (int i = 0; i < MAXM; ++i) e32[i] = i < m ? ((8u << 26) | (cur[i] & 0xFFu)) : 0u;
     }
 }
 
@@ -337,8 +348,8 @@ __device__ __forceinline__ void gather_entries(const CodeT* __restrict__ codes, 
 // stamps of the mid-grid workgroup, read by pqh_debug_enc_stamps.)
 __device__ unsigned long long g_enc_stamps[8];
 
-template <typename CodeT, int MAXM>
-__global__ void __launch_bounds__(kEncBlock)
+template <typename CodeT, int MAXM, int BLK, bool ROW8 = false>
+__global__ void __launch_bounds__(BLK)
 enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, int context,
             int raw_first, const CodeT* __restrict__ prev_row, const int* __restrict__ d_rawf,
             const unsigned long long* __restrict__ enc, const uint32_t* __restrict__ enc32,
@@ -353,7 +364,7 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
             unsigned epoch, long long nb, unsigned long long* __restrict__ total_out,
             const uint16_t* __restrict__ tree_prev) {
     extern __shared__ uint32_t img[];   // LDS image of this block's bit range
-    __shared__ uint32_t wsum[kEncBlock / 64];
+    __shared__ uint32_t wsum[BLK / 64];
     __shared__ long long s_id;
     __shared__ unsigned long long s_excl;
     __shared__ uint32_t s_head;
@@ -365,35 +376,67 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
     if (tid == 0) s_id = (long long)(atomicAdd(ticket, 1ull) - ticket_base);
     __syncthreads();
     const long long id = s_id;
-    const long long v = id * kEncBlock + tid;
+    const long long v = id * BLK + tid;
     const bool stamp = id == nb / 2 && tid == 0;
     if (stamp) g_enc_stamps[0] = __builtin_amdgcn_s_memtime();
 
     // code entries of this vector (gathered once)
-    unsigned long long ent[MAXM > 0 ? MAXM : 1];
+    uint32_t ent[MAXM > 0 ? MAXM : 1];
     uint32_t bits = 0;
+    if constexpr (ROW8) tree_prev = nullptr;   // (the 8-byte-row path: no tree order)
     if (v < n) {
-        if constexpr (MAXM > 0) {
-            gather_entries<CodeT, MAXM>(codes, v, m_total, k, context, raw_first, prev_row, enc,
+        if constexpr (ROW8) {
+            // m = 8 u8 codes: the row (and its context row) is one 8-byte load; entry loads
+            // are a uniform base plus a 32-bit offset (m * items * 4 B < 4 GB)
+            static_assert(MAXM == 8 && sizeof(CodeT) == 1, "8-byte rows");
+            const unsigned long long* r8 = reinterpret_cast<const unsigned long long*>(codes);
+            const unsigned long long row = r8[v];
+            unsigned long long prow = 0;
+            bool raw = false;
+            if (context) {
+                if (v > 0) {
+                    prow = r8[v - 1];
+                } else if (!raw_first && prev_row) {
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) prow |= (unsigned long long)prev_row[i] << (8 * i);
+                } else {
+                    raw = true;   // row 0 raw, 8 bits per part (huffman_encoder.c:234)
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const unsigned cur = (unsigned)(row >> (8 * i)) & 0xFFu;
+                const unsigned prv = (unsigned)(prow >> (8 * i)) & 0xFFu;
+                const bool ok = cur < (unsigned)k && (!context || prv < (unsigned)k);
+                const unsigned idx = (unsigned)i * (unsigned)items + (context ? prv * (unsigned)k + cur : cur);
+                ent[i] = raw ? ((8u << 26) | cur) : ok ? enc32[idx] : 0u;
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                bits += ent[i] != ~0u ? ent[i] >> 26
+                                      : (uint32_t)(sym_entry(codes, v, i, 8, k, context, raw_first,
+                                                             prev_row, enc, items, nullptr) >> 56);
+        } else if constexpr (MAXM > 0) {
+            gather_entries<CodeT, MAXM>(codes, v, m_total, k, context, raw_first, prev_row,
                                         enc32, items, ent, tree_prev);
 #pragma unroll
-            for (int i = 0; i < MAXM; ++i) bits += (uint32_t)(ent[i] >> 56);
+            for (int i = 0; i < MAXM; ++i)
+                bits += ent[i] != ~0u ? ent[i] >> 26
+                                      : (uint32_t)(sym_entry(codes, v, i, m_total, k, context,
+                                                             raw_first, prev_row, enc, items,
+                                                             tree_prev) >> 56);
         } else {
             for (int i = 0; i < m_total; ++i)
                 bits += (uint32_t)(sym_entry(codes, v, i, m_total, k, context, raw_first,
                                              prev_row, enc, items, tree_prev) >> 56);
         }
     }
-    uint32_t incl = bits;
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(incl, off);
-        if (lane >= off) incl += y;
-    }
+    const uint32_t incl = wave_incl_scan(bits);
     if (lane == 63) wsum[wid] = incl;
     __syncthreads();
     if (stamp) g_enc_stamps[1] = __builtin_amdgcn_s_memtime();
     uint32_t before = 0, block_bits = 0;
-    for (int w = 0; w < kEncBlock / 64; ++w) {
+    for (int w = 0; w < BLK / 64; ++w) {
         before += w < wid ? wsum[w] : 0u;
         block_bits += wsum[w];
     }
@@ -419,10 +462,16 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
                     __builtin_amdgcn_s_sleep(1);
                     continue;
                 }
-                unsigned long long v = lane <= f ? (st & kLbValue) : 0ull;
-                for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
-                excl += v;
-                if (pref) break;
+                // the aggregates before the prefix lane (block totals: < 2^23 for 64 of them)
+                // summed in 32 bits, the prefix itself read from its lane
+                const uint32_t a = (!pref || lane < f) ? (uint32_t)(st & kLbValue) : 0u;
+                excl += (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(a), 63);
+                if (pref) {
+                    const unsigned long long lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)st, f);
+                    const unsigned long long hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(st >> 32), f);
+                    excl += ((hi << 32) | lo) & kLbValue;
+                    break;
+                }
                 p -= 64;
             }
             if (lane == 0) lb_store(state + id, lb_pack(epoch, kLbPrefix, excl + block_bits));
@@ -438,7 +487,7 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
     const bool head_pred = (bs & 31) && bs > bit_offset;    // earlier blocks' bits in word wa
     const bool head_mem = (bs & 31) && bs == bit_offset;    // the caller's bits in word wa
     const bool overflow = nwords > 0 && wz >= cap_words;
-    for (long long w = tid; w < nwords; w += kEncBlock) img[w] = 0;
+    for (long long w = tid; w < nwords; w += BLK) img[w] = 0;
     __syncthreads();
 
     unsigned long long pos = bs + before + incl - bits;
@@ -446,10 +495,15 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
         if (chunk_vectors > 0 && v % chunk_vectors == 0) {
             const long long j = v / chunk_vectors;
             chunk_off[j] = pos;
-            if (context && chunk_prev)
-                for (int i = 0; i < m_total; ++i)
-                    chunk_prev[j * m_total + i] =
-                        v > 0 ? codes[(v - 1) * m_total + i] : (prev_row ? prev_row[i] : (CodeT)0);
+            if (context && chunk_prev) {
+                if (ROW8 && v > 0)   // (chunk_prev rows are 8 bytes: aligned)
+                    reinterpret_cast<unsigned long long*>(chunk_prev)[j] =
+                        reinterpret_cast<const unsigned long long*>(codes)[v - 1];
+                else
+                    for (int i = 0; i < m_total; ++i)
+                        chunk_prev[j * m_total + i] =
+                            v > 0 ? codes[(v - 1) * m_total + i] : (prev_row ? prev_row[i] : (CodeT)0);
+            }
         }
         // assemble this vector's bits in registers: words wholly inside its range are
         // plain LDS stores (no other thread touches them); only the first and the last,
@@ -483,9 +537,16 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
                 append(code, len);
             }
         };
-        if constexpr (MAXM > 0) {
+        if constexpr (MAXM > 0 || ROW8) {
 #pragma unroll
-            for (int i = 0; i < MAXM; ++i) put(ent[i]);   // length 0 past m_total
+            for (int i = 0; i < MAXM; ++i) {   // length 0 past m_total
+                if (ent[i] != ~0u) {
+                    if (ent[i] >> 26) append(ent[i] & ((1u << 26) - 1), (int)(ent[i] >> 26));
+                } else {   // a code longer than 26 bits: its u64 entry
+                    put(sym_entry(codes, v, i, m_total, k, context, raw_first, prev_row, enc,
+                                  items, tree_prev));
+                }
+            }
         } else {
             for (int i = 0; i < m_total; ++i)
                 put(sym_entry(codes, v, i, m_total, k, context, raw_first, prev_row, enc, items,
@@ -527,7 +588,7 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
     if (!overflow) {
         // words this block owns: [wa, wz], minus an open last word unless this is the last block
         const long long wend = ((be & 31) && !last) ? nwords - 1 : nwords;
-        for (long long w = tid; w < wend; w += kEncBlock)
+        for (long long w = tid; w < wend; w += BLK)
             __builtin_nontemporal_store(bswap32(w == 0 ? s_head : img[w]), out_words + wa + w);
         if (nwords == 0 && last && (be & 31) && tid == 0)   // empty last block closes the word
             out_words[wa] = bswap32(s_head);
@@ -564,13 +625,26 @@ static int histogram_impl(pqh_ctx_t* ctx, const void* d_codes, long long n, int 
         rc = pqh_ensure_ws(ctx, (size_t)m * chunks * words * 4);
         if (rc) return rc;
         uint32_t* partial = static_cast<uint32_t*>(ctx->ws);
-        PQH_HIP(ctx, hipFuncSetAttribute((const void*)hist_ctx<uint8_t>,
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         const unsigned grid = 8u * ((chunks + 7u) / 8u) * (unsigned)(m * split);
-        hipLaunchKernelGGL(hist_ctx<uint8_t>, dim3(grid), dim3(1024), lds, ctx->stream,
-                           static_cast<const uint8_t*>(d_codes), n, m, k,
-                           static_cast<const uint8_t*>(d_prev_row), d_rawf, partial, split,
-                           (int)chunks);
+        // 1024-thread workgroups; PQH_HIST_BLOCK=256: 256 threads with <= 32 VGPRs, which fit
+        // beside the assignment grid (measured: histogram 0.19 vs 0.075 ms in the bench -- a
+        // quarter of the loads in flight -- and the bench 2,119 vs 2,534 Mvec/s)
+        const char* hb = std::getenv("PQH_HIST_BLOCK");
+        if (!(hb && std::atoi(hb) == 256)) {
+            PQH_HIP(ctx, hipFuncSetAttribute((const void*)hist_ctx<uint8_t>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            hipLaunchKernelGGL(hist_ctx<uint8_t>, dim3(grid), dim3(1024), lds, ctx->stream,
+                               static_cast<const uint8_t*>(d_codes), n, m, k,
+                               static_cast<const uint8_t*>(d_prev_row), d_rawf, partial, split,
+                               (int)chunks);
+        } else {
+            PQH_HIP(ctx, hipFuncSetAttribute((const void*)hist_ctx<uint8_t, 256, 8>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            hipLaunchKernelGGL((hist_ctx<uint8_t, 256, 8>), dim3(grid), dim3(256), lds, ctx->stream,
+                               static_cast<const uint8_t*>(d_codes), n, m, k,
+                               static_cast<const uint8_t*>(d_prev_row), d_rawf, partial, split,
+                               (int)chunks);
+        }
         PQH_LAUNCH_CHECK(ctx);
         hipLaunchKernelGGL(hist_ctx_reduce, dim3((unsigned)((words + 255) / 256), m), dim3(256), 0,
                            ctx->stream, partial, (int)chunks, words, (long long)k * k, d_counts,
@@ -663,8 +737,11 @@ static int encode_write_impl(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* 
         if (d_total_bits) PQH_HIP(ctx, hipMemsetAsync(d_total_bits, 0, 8, ctx->stream));
         return PQH_OK;
     }
-    const long long nb = (n + kEncBlock - 1) / kEncBlock;
-    const size_t lds = ((size_t)kEncBlock * t->m * kMaxCodeLen / 32 + 4) * 4;
+    // m <= 8: 256-vector workgroups (one wave per SIMD, <= 32 VGPRs), which fit on a CU beside
+    // the assignment grid's waves; wider rows: 512
+    const int blk = t->m <= 8 ? 256 : kEncBlock;
+    const long long nb = (n + blk - 1) / blk;
+    const size_t lds = ((size_t)blk * t->m * kMaxCodeLen / 32 + 4) * 4;
     if (lds > 160 * 1024) return PQH_ERR_UNSUPPORTED;
     // look-back state: grow-only, epoch-tagged so it never needs clearing between calls
     if (nb > ctx->lb_cap) {
@@ -687,13 +764,14 @@ static int encode_write_impl(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* 
     unsigned long long* ticket = st + 2 * ctx->lb_cap;
     unsigned long long* total = d_total_bits ? d_total_bits : ctx->d_diag + 3;
     uint32_t* words = reinterpret_cast<uint32_t*>(d_out);
-#define PQH_ENC(T, MAXM)                                                                          \
+#define PQH_ENC(T, MAXM, R8)                                                                      \
     do {                                                                                          \
+        constexpr int B = MAXM > 0 && MAXM <= 8 ? 256 : kEncBlock;                                \
         if (lds > 64 * 1024)                                                                      \
-            PQH_HIP(ctx, hipFuncSetAttribute((const void*)(enc_onepass<T, MAXM>),                 \
+            PQH_HIP(ctx, hipFuncSetAttribute((const void*)(enc_onepass<T, MAXM, B, R8>),          \
                                              hipFuncAttributeMaxDynamicSharedMemorySize,          \
                                              (int)lds));                                          \
-        hipLaunchKernelGGL((enc_onepass<T, MAXM>), dim3((unsigned)nb), dim3(kEncBlock), lds,       \
+        hipLaunchKernelGGL((enc_onepass<T, MAXM, B, R8>), dim3((unsigned)nb), dim3(B), lds,       \
                            ctx->stream, static_cast<const T*>(d_codes), n, t->m, t->k,            \
                            t->context, raw_first, static_cast<const T*>(d_prev_row), d_rawf,     \
                            t->d_enc,                                                              \
@@ -704,13 +782,17 @@ static int encode_write_impl(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* 
                            (unsigned)ctx->lb_epoch, nb, total, tree_prev);                        \
     } while (0)
     if (t->k <= 256) {
-        if (t->m <= 8) PQH_ENC(uint8_t, 8);
-        else if (t->m <= 16) PQH_ENC(uint8_t, 16);
-        else PQH_ENC(uint8_t, 0);
+        // 8-byte rows (m = 8, aligned codes, no tree order): one load per row
+        if (t->m == 8 && !tree_prev && !(reinterpret_cast<uintptr_t>(d_codes) & 7) &&
+            !(reinterpret_cast<uintptr_t>(d_chunk_prev) & 7))
+            PQH_ENC(uint8_t, 8, true);
+        else if (t->m <= 8) PQH_ENC(uint8_t, 8, false);
+        else if (t->m <= 16) PQH_ENC(uint8_t, 16, false);
+        else PQH_ENC(uint8_t, 0, false);
     } else {
-        if (t->m <= 8) PQH_ENC(uint16_t, 8);
-        else if (t->m <= 16) PQH_ENC(uint16_t, 16);
-        else PQH_ENC(uint16_t, 0);
+        if (t->m <= 8) PQH_ENC(uint16_t, 8, false);
+        else if (t->m <= 16) PQH_ENC(uint16_t, 16, false);
+        else PQH_ENC(uint16_t, 0, false);
     }
 #undef PQH_ENC
     PQH_LAUNCH_CHECK(ctx);

@@ -1819,6 +1819,204 @@ dec_chunks(const uint32_t* __restrict__ words, long long nwords, long long n, in
     if (!ok) atomicOr(err, 1ull);
 }
 
+// ---- slim decoder for 8-part u8 rows (the bench shape): <= 32 VGPRs, so, like the table
+// builds, it runs beside the assignment grid.  One lane per chunk of C <= 32 vectors, 64
+// chunks per workgroup; the chunks' stream window in LDS (or, if it does not fit, the
+// global stream at 32-bit offsets from the window's first word); a row is decoded into one
+// u64, staged in LDS and written back as whole rows; the context row is that u64.  Table
+// lookups as dec_symbol (first level, second level, long list).
+template <bool LDS>
+struct BitRd {   // MSB-first reader over words [0, lim] (32-bit indices)
+    const uint32_t* w;
+    uint32_t lim;
+    uint32_t next;
+    unsigned long long buf;
+    int have;
+    __device__ __forceinline__ uint32_t load(uint32_t i) const { return __builtin_bswap32(w[min(i, lim)]); }
+    __device__ __forceinline__ void init(unsigned long long p) {
+        const uint32_t wi = (uint32_t)(p >> 5);
+        const int o = (int)(p & 31);
+        buf = (((unsigned long long)load(wi) << 32) | load(wi + 1)) << o;
+        have = 64 - o;
+        next = wi + 2;
+    }
+    __device__ __forceinline__ uint32_t peek(int nb) const { return (uint32_t)(buf >> (64 - nb)); }
+    __device__ __forceinline__ void skip(int nb) {   // nb <= 32
+        const uint32_t x = load(next);
+        buf <<= nb;
+        have -= nb;
+        const bool need = have <= 32;
+        buf |= need ? ((unsigned long long)x << (32 - have)) : 0ull;
+        next += need ? 1u : 0u;
+        have += need ? 32 : 0;
+    }
+    __device__ __forceinline__ unsigned long long peek56() const {   // the next 56 bits
+        const unsigned long long p = (unsigned long long)next * 32 - (unsigned long long)have;
+        const uint32_t wi = (uint32_t)(p >> 5);
+        const int o = (int)(p & 31);
+        const unsigned long long hi = ((unsigned long long)load(wi) << 32) | load(wi + 1);
+        const unsigned long long lo = load(wi + 2);
+        return (o ? ((hi << o) | (lo >> (32 - o))) : hi) >> 8;
+    }
+};
+
+// codes beyond both table levels: linear search of the alphabet's long list against the
+// next 56 stream bits; returns len << 16 | sym, or 0 if none matches (inlined: a call would
+// cost the kernel its register budget)
+__device__ __forceinline__ uint32_t dec_long(const pqh_long_code* __restrict__ longs, uint32_t cnt,
+                                          unsigned long long bits56) {
+    for (uint32_t q = 0; q < cnt; ++q) {
+        const pqh_long_code lc = longs[q];
+        if (lc.len >= 1 && lc.len <= 56 && (bits56 >> (56 - lc.len)) == lc.code)
+            return (lc.len << 16) | lc.sym;
+    }
+    return 0;
+}
+
+struct Row8Tabs {
+    const uint16_t* lut1;
+    const uint16_t* lut2;
+    const uint32_t* meta;
+    const pqh_long_code* longs;
+    const uint32_t* long_cnt;
+    long long lut2_cap;
+    int w1, k;
+};
+
+// one symbol of alphabet tab, or -1 (invalid)
+template <bool LDS>
+__device__ __forceinline__ int dec_sym8(BitRd<LDS>& br, const Row8Tabs& T, unsigned tab) {
+    const int w1 = T.w1;
+    const uint16_t e = T.lut1[(tab << kL1Max) + br.peek(w1)];
+    const int len = e >> 12;
+    unsigned sym = e & 0xFFFu;
+    if (len >= 1 && len <= w1) {
+        br.skip(len);
+        return sym < (unsigned)T.k ? (int)sym : -1;
+    }
+    if (len != 15) return -1;
+    if (sym != 0xFFFu) {   // second level
+        const uint32_t mt = T.meta[tab];
+        const int w2 = (int)((mt >> 4) & 15u);
+        const long long li = (long long)(mt >> 9) + ((long long)sym << w2) +
+                             (br.peek(w1 + w2) & ((1u << w2) - 1u));
+        if (w2 < 1 || (mt & 0x100u) || li >= T.lut2_cap) return -1;
+        const uint16_t e2 = T.lut2[li];
+        const int len2 = e2 >> 12;
+        if (len2 >= 1 && len2 <= w2) {
+            br.skip(w1 + len2);
+            sym = e2 & 0xFFFu;
+            return sym < (unsigned)T.k ? (int)sym : -1;
+        }
+        if (len2 != 15) return -1;
+    }
+    const uint32_t f = dec_long(T.longs + (long long)tab * T.k, T.long_cnt[tab], br.peek56());
+    if (!f) return -1;
+    for (int nb = (int)(f >> 16); nb > 0; nb -= 32) br.skip(nb < 32 ? nb : 32);
+    sym = f & 0xFFFFu;
+    return sym < (unsigned)T.k ? (int)sym : -1;
+}
+
+template <bool CTX, bool LDS>
+__device__ __forceinline__ bool dec_row8_lane(const uint32_t* src, uint32_t lim,
+                                              unsigned long long start, long long j, long long n,
+                                              int chunk_vectors, int raw_first,
+                                              const unsigned long long* __restrict__ chunk_prev,
+                                              const Row8Tabs& T, unsigned long long* st) {
+    BitRd<LDS> br{src, lim, 0, 0, 0};
+    br.init(start);
+    const long long v0 = j * chunk_vectors;
+    const int cnt = (int)min((long long)chunk_vectors, n - v0);
+    unsigned long long prev = 0;
+    int s = 0;
+    if (CTX) {
+        if (j == 0 && raw_first) {   // global row 0: ceil(log2 K) raw bits per part
+            int wb = 1;              // (huffman_decode.c:73-76; the encoder writes 8)
+            while ((1 << wb) < T.k) ++wb;
+#pragma unroll 1
+            for (int i = 0; i < 8; ++i) {
+                prev |= (unsigned long long)br.peek(wb) << (8 * i);
+                br.skip(wb);
+            }
+            st[0] = prev;
+            s = 1;
+        } else {
+            prev = chunk_prev[j];
+        }
+    }
+    const unsigned roots = CTX ? (unsigned)T.k : 1u;
+    for (; s < cnt; ++s) {
+        unsigned long long row = 0;
+#pragma unroll 1
+        for (int i = 0; i < 8; ++i) {   // (rolled: one copy of the lookup code, fewer registers)
+            const unsigned tab = (unsigned)i * roots + (CTX ? (unsigned)(prev >> (8 * i)) & 0xFFu : 0u);
+            const int sym = dec_sym8(br, T, tab);
+            if (sym < 0) return false;
+            row |= (unsigned long long)sym << (8 * i);
+        }
+        prev = row;
+        st[s] = row;
+    }
+    return true;
+}
+
+template <bool CTX>
+__global__ void __launch_bounds__(64)
+dec_row8(const uint32_t* __restrict__ words, long long nwords, long long n, int raw_first,
+         int chunk_vectors, const unsigned long long* __restrict__ chunk_off,
+         const unsigned long long* __restrict__ chunk_prev, Row8Tabs T,
+         unsigned long long* __restrict__ out, unsigned long long* __restrict__ err, int win_words) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    unsigned long long* stage = reinterpret_cast<unsigned long long*>(lds);   // [64][C] rows
+    uint32_t* win = reinterpret_cast<uint32_t*>(lds + 64 * 8 * chunk_vectors);
+    const int lane = threadIdx.x;
+    __builtin_amdgcn_s_setprio(3);   // latency-bound: issue ahead of the assignment's waves
+    const long long chunks = (n + chunk_vectors - 1) / chunk_vectors;
+    const long long j0 = (long long)blockIdx.x * 64;
+    const long long jn = min(chunks - j0, 64ll);
+    const unsigned long long b_lo = chunk_off[j0];
+    const unsigned long long b_hi = j0 + 64 < chunks ? chunk_off[j0 + 64] : (unsigned long long)nwords * 32;
+    const long long w_lo = (long long)(b_lo >> 5);
+    const long long w_hi = min(nwords, (long long)((b_hi + 31) >> 5) + 2);
+    const long long nw = w_hi - w_lo;
+    const bool in_lds = nw <= win_words;
+    if (in_lds) {   // streamed once: non-temporal, so the code tables keep the L2
+#pragma unroll 1
+        for (long long w0 = 0; w0 < nw; w0 += 4 * 64) {
+            uint32_t r[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const long long w = w0 + u * 64 + lane;
+                r[u] = w < nw ? __builtin_nontemporal_load(words + w_lo + w) : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const long long w = w0 + u * 64 + lane;
+                if (w < nw) win[w] = r[u];
+            }
+        }
+        if (lane < 4) win[nw + lane] = 0;   // zero pad read past the window
+    }
+    __syncthreads();
+    const long long j = j0 + lane;
+    bool ok = true;
+    if (lane < jn) {
+        const unsigned long long start = chunk_off[j] - (unsigned long long)w_lo * 32;
+        unsigned long long* st = stage + (long long)lane * chunk_vectors;
+        ok = in_lds ? dec_row8_lane<CTX, true>(win, (uint32_t)(nw + 3), start, j, n, chunk_vectors,
+                                               raw_first, chunk_prev, T, st)
+                    : dec_row8_lane<CTX, false>(words + w_lo, (uint32_t)(nwords - 1 - w_lo), start,
+                                                j, n, chunk_vectors, raw_first, chunk_prev, T, st);
+    }
+    __syncthreads();
+    // the workgroup's rows are contiguous: whole-row stores
+    const long long r0 = j0 * chunk_vectors;
+    const long long rows = min(n, (j0 + 64) * chunk_vectors) - r0;
+#pragma unroll 1
+    for (long long q = lane; q < rows; q += 64) __builtin_nontemporal_store(stage[q], out + r0 + q);
+    if (!ok) atomicOr(err, 1ull);
+}
+
 }  // namespace
 
 extern "C" {
@@ -2137,6 +2335,28 @@ int pqh_decode(pqh_ctx_t* ctx, const pqh_tables_t* t, const unsigned char* d_str
     const size_t lds = meta_bytes + (lds_l1 ? ((l1_bytes + 15) & ~(size_t)15) : 0) +
                        ((size_t)win_words + 4) * 4 + (size_t)64 * S * t->m * esz + 16;
     if (lds > 160 * 1024) return PQH_ERR_UNSUPPORTED;
+    // 8-part u8 rows (aligned, C <= 32): the slim decoder
+    if (t->k <= 256 && t->m == 8 && chunk_vectors <= 32 && nwords < (1ll << 31) &&
+        !(reinterpret_cast<uintptr_t>(d_codes) & 7) && !(reinterpret_cast<uintptr_t>(d_chunk_prev) & 7)) {
+        const int ww = (int)std::min<long long>(3072, std::max<long long>(
+            256, (64ll * chunk_vectors * 8 * 12 + 31) / 32 + 8));
+        const size_t lds8 = (size_t)64 * 8 * chunk_vectors + ((size_t)ww + 4) * 4;
+        const Row8Tabs T{t->d_lut1, t->d_lut2, t->d_meta, t->d_long, t->d_long_cnt, t->lut2_cap,
+                         t->l1_bits, t->k};
+        if (t->context)
+            hipLaunchKernelGGL(dec_row8<true>, dim3(blocks), dim3(64), lds8, ctx->stream,
+                               reinterpret_cast<const uint32_t*>(d_stream), nwords, n, raw_first,
+                               chunk_vectors, d_chunk_offsets,
+                               static_cast<const unsigned long long*>(d_chunk_prev), T,
+                               static_cast<unsigned long long*>(d_codes), ctx->d_diag + 1, ww);
+        else
+            hipLaunchKernelGGL(dec_row8<false>, dim3(blocks), dim3(64), lds8, ctx->stream,
+                               reinterpret_cast<const uint32_t*>(d_stream), nwords, n, raw_first,
+                               chunk_vectors, d_chunk_offsets, nullptr, T,
+                               static_cast<unsigned long long*>(d_codes), ctx->d_diag + 1, ww);
+        PQH_LAUNCH_CHECK(ctx);
+        return PQH_OK;
+    }
 #define PQH_DEC(MT, T, L)                                                                        \
     do {                                                                                         \
         if (lds > 64 * 1024)                                                                     \
