@@ -24,7 +24,7 @@ BINS := $(OUT)/huffman_encoder $(OUT)/huffman_decoder \
         $(OUT)/huffman_encoder_O0 $(OUT)/huffman_decoder_O0 \
         $(OUT)/bitstream_test $(OUT)/huffman_encode_test $(OUT)/huffman_decode_test \
         $(OUT)/huffman_codebook_test $(OUT)/libref.so \
-        $(OUT)/mst_builder $(OUT)/libref_knn.so
+        $(OUT)/mst_builder $(OUT)/libref_knn.so $(OUT)/prepend_vecsl_meta
 
 .PHONY: all clean
 all: $(BINS)
@@ -67,6 +67,10 @@ $(OUT)/huffman_codebook_test: $(LIBSRC) | $(OUT)
 
 $(OUT)/libref.so: oracle/ref_harness.c $(LIBSRC) | $(OUT)
 	$(CC) $(CFLAGS_O2) -fPIC -shared -o $@ $^ -lm
+
+# the light-header converter as shipped (prepend_vecsl_meta.c + vecs_io.c + misc.c)
+$(OUT)/prepend_vecsl_meta: $(REF)/prepend_vecsl_meta.c $(REF)/vecs_io.c $(REF)/misc.c | $(OUT)
+	$(CC) $(CFLAGS_O2) -o $@ $^ -lm
 
 # the forest builder's yael-free parts: mst_builder as shipped (mst_builder.c + mst.c + dsu.c
 # + the library), and the kNN block geometry / heap merge of compute_nn_fast behind

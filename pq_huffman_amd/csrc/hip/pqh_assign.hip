@@ -401,7 +401,8 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
                const float* __restrict__ cmax, const float* __restrict__ sqrt_cmax,
                CodeT* __restrict__ codes, uint32_t* __restrict__ counts,
                unsigned long long* __restrict__ rerank, uint32_t* __restrict__ sched, int gx,
-               unsigned long long* __restrict__ rerank_next, uint32_t* __restrict__ sched_next) {
+               unsigned long long* __restrict__ rerank_next, uint32_t* __restrict__ sched_next,
+               int prio) {
     using P = Plan<D>;
     constexpr int K = KT * 32;
     constexpr bool kLdsA = KT <= 8;
@@ -434,9 +435,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     const int bx = inter ? (L / (8 * m_total)) * 8 + (L & 7) : L % gx;
     const int r = lane & 31;
     const int h = lane >> 5;
-#ifdef PQH_ASSIGN_PRIO   // (experiment) wave issue priority against concurrent kernels
-    __builtin_amdgcn_s_setprio(PQH_ASSIGN_PRIO);
-#endif
+    pqh_set_prio(prio);   // (pqh_prio "ASSIGN": against the kernels running beside it)
     if (L == 0 && wave == 0) {   // the next launch's queue heads and re-rank counter
         // (agent-scope stores: written through to where the next launch's atomics act)
         if (sched_next)
@@ -1196,6 +1195,7 @@ int launch_mfma(pqh_ctx* ctx, pqh_pq* pq, const float* x, long long n, long long
 #else
     uint32_t* sched = pq->m <= kSchedMax ? ctx->d_sched + ring * kSchedSet : nullptr;
 #endif
+    const int prio = pqh_prio("ASSIGN", 0);
     // grid = the workgroups that are resident at once (persistent, grid-stride over the
     // 32-vector blocks): more would only queue behind the first wave of workgroups
 #define PQH_CASE(DD) PQH_CASE_KT(DD, 8)
@@ -1212,7 +1212,8 @@ int launch_mfma(pqh_ctx* ctx, pqh_pq* pq, const float* x, long long n, long long
         hipLaunchKernelGGL((pq_assign_mfma<DD, KTT, CodeT>), dim3((unsigned)(gx * groups)), block, \
                            0, ctx->stream, x, n, ldx, pq->m, pq->d_afrag, pq->d_cn, pq->d_cent, \
                            pq->d_cmax, pq->d_sqc, codes, counts, rr, sched, (int)gx,         \
-                           rr_next, sched ? ctx->d_sched + (1 - ring) * kSchedSet : nullptr); \
+                           rr_next, sched ? ctx->d_sched + (1 - ring) * kSchedSet : nullptr, \
+                           prio);                                                             \
         PQH_LAUNCH_CHECK(ctx);                                                              \
         break;                                                                              \
     }

@@ -182,3 +182,11 @@ const char* pqh_status_string(int s) {
 }
 
 }  // extern "C"
+
+int pqh_prio(const char* name, int def) {
+    char key[64];
+    std::snprintf(key, sizeof key, "PQH_PRIO_%s", name);
+    const char* e = std::getenv(key);
+    if (!e || e[0] < '0' || e[0] > '3') return def;
+    return e[0] - '0';
+}

@@ -43,8 +43,9 @@ template <typename CodeT, int BLK = 1024, int kSub = 20>
 __global__ void __launch_bounds__(BLK)
 hist_ctx(const CodeT* __restrict__ codes, long long n, int m_total, int k,
          const CodeT* __restrict__ prev_row, const int* __restrict__ d_rawf,
-         uint32_t* __restrict__ partial, int split, int chunks) {
+         uint32_t* __restrict__ partial, int split, int chunks, int prio) {
     extern __shared__ uint32_t pairs[];   // (k / split) * k u16 counters packed two per word
+    pqh_set_prio(prio);
     if (d_rawf && *d_rawf) prev_row = nullptr;   // decided on the device (pqh_shard_encode)
     const int per_chunk = m_total * split;
     const int q = (int)(blockIdx.x >> 3);
@@ -362,8 +363,9 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
             unsigned long long* __restrict__ state, unsigned long long* __restrict__ tails,
             unsigned long long* __restrict__ ticket, unsigned long long ticket_base,
             unsigned epoch, long long nb, unsigned long long* __restrict__ total_out,
-            const uint16_t* __restrict__ tree_prev) {
+            const uint16_t* __restrict__ tree_prev, int prio) {
     extern __shared__ uint32_t img[];   // LDS image of this block's bit range
+    pqh_set_prio(prio);
     __shared__ uint32_t wsum[BLK / 64];
     __shared__ long long s_id;
     __shared__ unsigned long long s_excl;
@@ -636,14 +638,14 @@ static int histogram_impl(pqh_ctx_t* ctx, const void* d_codes, long long n, int 
             hipLaunchKernelGGL(hist_ctx<uint8_t>, dim3(grid), dim3(1024), lds, ctx->stream,
                                static_cast<const uint8_t*>(d_codes), n, m, k,
                                static_cast<const uint8_t*>(d_prev_row), d_rawf, partial, split,
-                               (int)chunks);
+                               (int)chunks, pqh_prio("HIST", 0));
         } else {
             PQH_HIP(ctx, hipFuncSetAttribute((const void*)hist_ctx<uint8_t, 256, 8>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
             hipLaunchKernelGGL((hist_ctx<uint8_t, 256, 8>), dim3(grid), dim3(256), lds, ctx->stream,
                                static_cast<const uint8_t*>(d_codes), n, m, k,
                                static_cast<const uint8_t*>(d_prev_row), d_rawf, partial, split,
-                               (int)chunks);
+                               (int)chunks, pqh_prio("HIST", 0));
         }
         PQH_LAUNCH_CHECK(ctx);
         hipLaunchKernelGGL(hist_ctx_reduce, dim3((unsigned)((words + 255) / 256), m), dim3(256), 0,
@@ -764,6 +766,7 @@ static int encode_write_impl(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* 
     unsigned long long* ticket = st + 2 * ctx->lb_cap;
     unsigned long long* total = d_total_bits ? d_total_bits : ctx->d_diag + 3;
     uint32_t* words = reinterpret_cast<uint32_t*>(d_out);
+    const int enc_prio = pqh_prio("ENCODE", 0);
 #define PQH_ENC(T, MAXM, R8)                                                                      \
     do {                                                                                          \
         constexpr int B = MAXM > 0 && MAXM <= 8 ? 256 : kEncBlock;                                \
@@ -779,7 +782,7 @@ static int encode_write_impl(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* 
                            (long long)(out_bytes / 4),                                            \
                            chunk_vectors, d_chunk_offsets, static_cast<T*>(d_chunk_prev),         \
                            ctx->d_diag + 2, st, tails, ticket, ctx->lb_ticket_base,               \
-                           (unsigned)ctx->lb_epoch, nb, total, tree_prev);                        \
+                           (unsigned)ctx->lb_epoch, nb, total, tree_prev, enc_prio);              \
     } while (0)
     if (t->k <= 256) {
         // 8-byte rows (m = 8, aligned codes, no tree order): one load per row

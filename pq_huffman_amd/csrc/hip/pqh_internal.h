@@ -73,6 +73,19 @@ int pqh_encode_write_at_dev(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d
                                  #expr, hipGetErrorString(_e));                          \
     } while (0)
 
+// Wave issue priority of a kernel (s_setprio takes an immediate): the latency-bound kernels
+// that run beside the assignment grid raise theirs.  pqh_prio(name, default) reads the
+// PQH_PRIO_<NAME> override (0..3) -- an experiment knob; the defaults are the measured best.
+int pqh_prio(const char* name, int def);
+__device__ __forceinline__ void pqh_set_prio(int p) {
+    switch (p) {
+        case 1: __builtin_amdgcn_s_setprio(1); break;
+        case 2: __builtin_amdgcn_s_setprio(2); break;
+        case 3: __builtin_amdgcn_s_setprio(3); break;
+        default: break;
+    }
+}
+
 // PQH_DEBUG_SYNC=1: synchronise and check after every launch, so an asynchronous fault is
 // reported by the call that caused it (diagnostics only).
 bool pqh_debug_sync();

@@ -847,6 +847,7 @@ struct GrpLut {
     unsigned long long* pool_head;
     long long lut2_cap;
     int w1, l2_bits;
+    int prio;   // wave issue priority (pqh_prio)
 };
 
 __device__ __forceinline__ void grp_luts(const GrpLut& L, long long t, int k, int gl, int gsh,
@@ -856,7 +857,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(32)))
 huff_trees_grp(const uint32_t* __restrict__ counts, int k, long long trees,
                unsigned long long* __restrict__ enc, uint32_t* __restrict__ err,
                long long trees2, const uint32_t* __restrict__ counts2,
-               unsigned long long* __restrict__ enc2, uint32_t* __restrict__ err2) {
+               unsigned long long* __restrict__ enc2, uint32_t* __restrict__ err2, int prio) {
     // trees [0, trees) from counts -> enc; a paired build adds [trees, trees + trees2)
     const long long blocks1 = (trees + kGrpTrees - 1) / kGrpTrees;
     if ((long long)blockIdx.x >= blocks1) {
@@ -881,7 +882,7 @@ huff_trees_grp(const uint32_t* __restrict__ counts, int k, long long trees,
     }
     if (grp >= trees) return;   // no workgroup barriers below
     // latency-bound: issue ahead of the (older, VALU-bound) assignment waves on the SIMD
-    __builtin_amdgcn_s_setprio(3);
+    pqh_set_prio(prio);
     const bool stamp = blockIdx.x == 0 && lane == 0;
     if (stamp) g_tree_stamps[0] = __builtin_amdgcn_s_memtime();
     const uint32_t* cnt = counts + (long long)grp * k;
@@ -990,7 +991,7 @@ lut_grp(const unsigned long long* __restrict__ enc, int k, long long tables, Grp
     const int lane = threadIdx.x, grp = lane >> 4, gl = lane & 15, gsh = grp * 16;
     const long long t = (long long)blockIdx.x * kGrpTrees + grp;
     if (t >= tables) return;   // no workgroup barriers below
-    __builtin_amdgcn_s_setprio(3);
+    pqh_set_prio(lut.prio);
     char* base = lds + grp * (2048 + 3072 + 16);
     unsigned long long* code = reinterpret_cast<unsigned long long*>(base);
     const unsigned long long* e = enc + t * k;
@@ -1881,6 +1882,7 @@ struct Row8Tabs {
     const uint32_t* long_cnt;
     long long lut2_cap;
     int w1, k;
+    int prio;   // wave issue priority (pqh_prio)
 };
 
 // one symbol of alphabet tab, or -1 (invalid)
@@ -1970,7 +1972,7 @@ dec_row8(const uint32_t* __restrict__ words, long long nwords, long long n, int 
     unsigned long long* stage = reinterpret_cast<unsigned long long*>(lds);   // [64][C] rows
     uint32_t* win = reinterpret_cast<uint32_t*>(lds + 64 * 8 * chunk_vectors);
     const int lane = threadIdx.x;
-    __builtin_amdgcn_s_setprio(3);   // latency-bound: issue ahead of the assignment's waves
+    pqh_set_prio(T.prio);   // latency-bound: issue ahead of the assignment's waves
     const long long chunks = (n + chunk_vectors - 1) / chunk_vectors;
     const long long j0 = (long long)blockIdx.x * 64;
     const long long jn = min(chunks - j0, 64ll);
@@ -2076,7 +2078,7 @@ int pqh_tables_destroy(pqh_tables_t* t) {
 static void launch_lut_grp(pqh_ctx* ctx, pqh_tables* t) {
     const GrpLut lut{t->d_enc32, t->d_lut1, t->d_lut2, t->d_meta, t->d_long, t->d_long_cnt,
                      reinterpret_cast<unsigned long long*>(t->d_err + 2), t->lut2_cap,
-                     t->l1_bits, t->l2_bits};
+                     t->l1_bits, t->l2_bits, pqh_prio("LUTS", 3)};
     hipLaunchKernelGGL(lut_grp, dim3((unsigned)((t->tables + kGrpTrees - 1) / kGrpTrees)), dim3(64),
                        0, ctx->stream, t->d_enc, t->k, t->tables, lut);
 }
@@ -2169,7 +2171,7 @@ static int build_trees(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts
         hipLaunchKernelGGL(huff_trees_grp, dim3((unsigned)blocks), dim3(64), 0, ctx->stream, d_counts,
                            t->k, trees, t->d_enc, t->d_err, t2 ? t2->tables : 0ll,
                            t2 ? d_counts2 : d_counts, t2 ? t2->d_enc : t->d_enc,
-                           t2 ? t2->d_err : t->d_err);
+                           t2 ? t2->d_err : t->d_err, pqh_prio("TREES", 3));
         PQH_LAUNCH_CHECK(ctx);
         return PQH_OK;
     }
@@ -2342,7 +2344,7 @@ int pqh_decode(pqh_ctx_t* ctx, const pqh_tables_t* t, const unsigned char* d_str
             256, (64ll * chunk_vectors * 8 * 12 + 31) / 32 + 8));
         const size_t lds8 = (size_t)64 * 8 * chunk_vectors + ((size_t)ww + 4) * 4;
         const Row8Tabs T{t->d_lut1, t->d_lut2, t->d_meta, t->d_long, t->d_long_cnt, t->lut2_cap,
-                         t->l1_bits, t->k};
+                         t->l1_bits, t->k, pqh_prio("DECODE", 3)};
         if (t->context)
             hipLaunchKernelGGL(dec_row8<true>, dim3(blocks), dim3(64), lds8, ctx->stream,
                                reinterpret_cast<const uint32_t*>(d_stream), nwords, n, raw_first,
