@@ -39,21 +39,36 @@ BYTES_PER_VEC_WRITE = 8           # M=8 uint8 codes
 ROOT = os.path.dirname(os.path.abspath(__file__))
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary
-    (profiles/<round>_pmc_summary.json, written by profiles/summarize.py from a separate
-    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE pass of this same bench command)."""
+# the assignment kernel instantiation each configuration runs (its rocprof short name)
+ASSIGN_KERNEL = {"sift": "pq_assign_mfma<16, 8, unsigned char>",
+                 "deep": "pq_assign_mfma<6, 8, unsigned char>",
+                 "k4096": "pq_assign_mfma<16, 128, unsigned short>"}
+
+
+def profile_tag(config, sort):
+    """the profiles/ tag of a bench configuration (profiles/collect.sh r<N>_<tag>)"""
+    return config + ("_sort" if sort else "")
+
+
+def pmc_traffic(kernel, tag):
+    """HBM bytes per launch and the kernel-trace average of exactly `kernel` (the
+    instantiation this configuration runs) from the newest committed profile of THIS
+    configuration: profiles/r<N>_<tag>_pmc_summary.json, written by profiles/summarize.py
+    from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench command."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")),
-                   key=lambda f: int(os.path.basename(f)[1:].split("_")[0]))
-    for f in reversed(files):
+    import re
+    files = []
+    for f in glob.glob(os.path.join(ROOT, "profiles", f"r*_{tag}_pmc_summary.json")):
+        mt = re.match(r"r(\d+)_" + re.escape(tag) + r"_pmc_summary\.json$", os.path.basename(f))
+        if mt:
+            files.append((int(mt.group(1)), f))
+    for _, f in sorted(files, reverse=True):
         try:
-            ks = json.load(open(f))["kernels"]
+            e = json.load(open(f))["kernels"].get(kernel)
         except (OSError, ValueError, KeyError):
             continue
-        for name, e in ks.items():
-            if name.startswith(kernel) and "hbm_bytes" in e:
-                return e["hbm_bytes"], os.path.relpath(f, ROOT), e.get("avg_us")
+        if e and "hbm_bytes" in e:
+            return e["hbm_bytes"], os.path.relpath(f, ROOT), e.get("avg_us")
     return None, None, None
 
 
@@ -109,6 +124,9 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl",
                     help="process-group backend (nccl = RCCL; gloo only to rehearse the "
                          "multi-rank schedule with every rank on one GPU, --one-device)")
+    ap.add_argument("--shard-path", choices=["library", "python"], default="library",
+                    help="world > 1: the library's two-phase pqh_shard_encode (C ABI, RCCL "
+                         "hooks; default) or the Python composition of the same steps")
     ap.add_argument("--one-device", action="store_true",
                     help="every rank uses GPU 0 (schedule rehearsal on a one-GPU box)")
     ap.add_argument("--lut-on", choices=["lanes", "assign"], default="lanes",
@@ -381,6 +399,15 @@ def main():
            for _ in elanes]
     tot_dev = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in elanes]
     raw_first = shard.raw_first(rank)
+    # world > 1 through the C ABI (pqh_shard_encode_tables on the table lane, then
+    # pqh_shard_encode_write on the encode stream): the histogram moves off the assignment
+    # stream into phase 1; each in-flight batch keeps its scratch (halo row, raw-first flag)
+    lib_shard = world > 1 and args.shard_path == "library" and not serial and not args.sort
+    if lib_shard:
+        comm = shard.TorchComm(world, rank)
+        scratch = [shard.scratch_for(comm, m, dev) for _ in range(slots)]
+        status = [0] * slots
+        offs = [torch.zeros(2, dtype=torch.int64, device=dev) for _ in elanes]
     stages = ("assign", "sort", "hist", "codebook", "lut", "encode", "decode")
     if args.sort and (k > 256 or world > 1):
         raise SystemExit("--sort: one rank, K <= 256 (the distributed sort is shard.py's)")
@@ -425,8 +452,37 @@ def main():
         shard.reduce_counts(counts[s], world)
         acc["collectives"] += time.perf_counter() - tc if state["timed"] else 0.0
 
+    def front_lib(i):
+        """world > 1, library path: batch i's assignment on A, then phase 1 of
+        pqh_shard_encode (halo, histogram, all-reduce, code tables) on its lane"""
+        s, j = i % slots, lane_of(i)
+        c = lanes[j]
+        sL = c.stream
+        with torch.cuda.stream(sA):
+            if used[s]:              # the slot's previous batch: encoded (codes[s] free)
+                sA.wait_event(ev_enc[s])
+            e = rec("assign", sA)
+            pq.assign(x, codes[s], ctx=ctx)
+            done(e, sA)
+            ev_hist[s].record(sA)
+        with torch.cuda.stream(sL):
+            sL.wait_event(ev_hist[s])
+            ti = tab_index(i)
+            if elanes is not lanes:              # tabs[ti] free: its last decode is done
+                sL.wait_event(ev_dec[ti])
+            e = rec("codebook", sL)
+            tc = time.perf_counter()
+            status[s] = shard.shard_encode_tables(c, comm, codes[s], tabs[ti], counts[s],
+                                                  scratch[s], first_row=rank * n)
+            acc["collectives"] += time.perf_counter() - tc if state["timed"] else 0.0
+            done(e, sL)
+            ev_tab[s].record(sL)
+        used[s] = True
+
     def front(i):
         """batch i: assignment + histogram on A, then its code tables on its lane"""
+        if lib_shard:
+            return front_lib(i)
         s, j = i % slots, lane_of(i)
         c = lanes[j]
         sL = c.stream
@@ -525,7 +581,14 @@ def main():
                 halo[s].record_stream(sL)
             e = rec("encode", sL)
             tc = time.perf_counter()
-            if world > 1:   # place the shard in the global stream before writing it: sizes,
+            if lib_shard:   # phase 2 of pqh_shard_encode: length, all-gather, offsets, write
+                shard.shard_encode_write(c, comm, codes[s], tj, out[j], args.chunk, coff[j],
+                                         cprev[j], offs[j], scratch[s], status[s],
+                                         first_row=rank * n)
+                tot_dev[j].copy_(shard.scratch_shard_bits(scratch[s], world, m))
+                state["goff"] = offs[j][:1]
+                acc["collectives"] += time.perf_counter() - tc if state["timed"] else 0.0
+            elif world > 1:   # place the shard in the global stream before writing it: sizes,
                 # all-gather + prefix sum on the device, offset read by the kernel (no host sync)
                 total = codec.encode_size(c, tj, codes[s], raw_first, halo[s])
                 goff, _ = shard.bit_offsets_device(total, world, rank)
@@ -607,6 +670,8 @@ def main():
         codec.decode_status(c)
         codec.encode_status(c)
     assert torch.equal(dec[j_last], codes[s_last]), "round trip mismatch"
+    if lib_shard:   # every rank's pqh_shard_encode_write succeeded (no sentinel length)
+        shard.status(elanes[j_last], offs[j_last])
     rerank = pq.rerank_count(ctx)
     bits_per_vec = int(tot_dev[j_last].item()) / n
 
@@ -630,7 +695,8 @@ def main():
         t_assign = acc["assign"] / args.steps
         vec_read, vec_write = 4 * d, m * code_bytes
         achieved = (vec_read + vec_write) * n / t_assign / 1e9
-        traffic, traffic_src, prof_avg_us = pmc_traffic("pq_assign_mfma")
+        akern = ASSIGN_KERNEL[args.config]
+        traffic, traffic_src, prof_avg_us = pmc_traffic(akern, profile_tag(args.config, args.sort))
         t_enc = (acc["assign"] + acc["hist"] + acc["codebook"] + acc["lut"] + acc["encode"]) / args.steps
         tf = 2.0 * k * d * n / t_assign / 1e12   # algorithmic: 2 K D flop per vector
         workload = {
@@ -675,10 +741,13 @@ def main():
                                     f"i % {nl}, beside the assignment of the next batches; "
                                     "every timed step runs all five stages and the pipeline "
                                     "fills and drains inside the timed region")},
-            "roofline": {"kernel": "pq_assign_mfma", "bound": "hbm",
-                         # what actually limits the kernel (PMC): the
-                         # wave64 VALU issue of the top-2 key reduction, ~4 cycles each
-                         "limiter": "VALU issue (top-2 key reduction), not HBM",
+            "roofline": {"kernel": akern,
+                         # `bound`: the roofline the fraction is taken against (the contract's
+                         # HBM read roofline); `measured_limiter`: what the PMC counters show
+                         # limits the kernel
+                         "bound": "hbm",
+                         "measured_limiter": "VALU issue (the top-2 key reduction, ~4 cycles "
+                                             "per wave64 instruction) -- not HBM",
                          "mfma_tflops_algorithmic": round(tf, 1),
                          # of the dense bf16 peak (~2.5 PF/s); each fp32 product costs two or
                          # three bf16 MFMA passes (the hi/lo split), so issued MFMA work is 2-3x

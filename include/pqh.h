@@ -40,7 +40,8 @@ typedef enum {
     PQH_ERR_CORRUPT = -6,        /* invalid code in a stream */
     PQH_ERR_NOMEM = -7,
     PQH_ERR_CAPACITY = -8,       /* output buffer too small */
-    PQH_ERR_REMOTE = -9          /* another rank's part of a sharded call failed */
+    PQH_ERR_REMOTE = -9,         /* another rank's part of a sharded call failed */
+    PQH_ERR_COMM = -10           /* a collective hook of a sharded call failed */
 } pqh_status_t;
 
 typedef struct pqh_ctx pqh_ctx_t;
@@ -218,7 +219,14 @@ int pqh_chunk_index_host(const pqh_tables_t* t, const unsigned char* stream,
 
 /* ---- sort mode (huffman_encoder.c:301-317: qsort + strncmp) ---------------------- */
 /* Stable sort of the n rows by key(row) = row with every byte after its first 0 zeroed
- * (strncmp order), uint8 codes only.  d_tmp: n*m bytes scratch. */
+ * (strncmp order), uint8 codes only.
+ * Workspace (grown in the context, kept between calls): the in-tree radix sort (2 <= m
+ * <= 8, n < 2^31) takes 32 bytes per row + 8 KB plus a persistent 2 KB-per-8192-row
+ * tile-state array, and sorts in place (d_tmp unused, may be NULL).  Other shapes, or
+ * PQH_SORT_IMPL=rocprim, use rocPRIM's radix_sort_pairs: 24 bytes per row + its temp
+ * storage, plus n*m bytes for the gathered rows unless d_tmp (n*m bytes) is given.
+ * If the in-tree sort cannot allocate its workspace it retries on the rocPRIM path
+ * before returning PQH_ERR_NOMEM. */
 int pqh_sort_rows(pqh_ctx_t* ctx, void* d_codes, long long n, int m, void* d_tmp);
 
 /* ---- multi-GPU row shards ------------------------------------------
@@ -274,6 +282,21 @@ int pqh_shard_encode(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm, const block_t
                      uint32_t* d_counts, unsigned char* d_out, unsigned long long out_bytes,
                      int chunk_vectors, unsigned long long* d_chunk_offsets, void* d_chunk_prev,
                      unsigned long long* d_offsets, void* d_scratch, int* raw_first);
+/* pqh_shard_encode in two phases, for a caller that pipelines batches (bench.py): phase 1
+ * (halo, histogram, all-reduce, code tables) and phase 2 (length, all-gather, offsets,
+ * write) may run on different streams -- ordered by the caller -- with other batches'
+ * collectives between them.  Both take the same d_scratch; phase 2's `status` is phase 1's
+ * return value (a nonzero status sends the sentinel length).  pqh_shard_encode = phase 1 +
+ * phase 2.  A collective hook failure returns PQH_ERR_COMM. */
+int pqh_shard_encode_tables(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm, const block_t* shard,
+                            const void* d_codes, int m, int k, int context,
+                            pqh_tables_t* tables, uint32_t* d_counts, void* d_scratch);
+int pqh_shard_encode_write(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm, const block_t* shard,
+                           const void* d_codes, int m, int k, int context, pqh_tables_t* tables,
+                           unsigned char* d_out, unsigned long long out_bytes, int chunk_vectors,
+                           unsigned long long* d_chunk_offsets, void* d_chunk_prev,
+                           unsigned long long* d_offsets, void* d_scratch, int status,
+                           int* raw_first);
 /* Synchronises; PQH_ERR_REMOTE if some rank's pqh_shard_encode behind d_offsets failed. */
 int pqh_shard_status(pqh_ctx_t* ctx, const unsigned long long* d_offsets);
 

@@ -25,7 +25,8 @@ PQH_OK = 0
 STATUS = {0: "ok", -1: "invalid argument", -2: "no HIP device", -3: "HIP runtime error",
           -4: "unsupported configuration", -5: "code longer than 56 bits", -6: "corrupt stream",
           -7: "out of memory", -8: "output buffer too small",
-          -9: "another rank's part of the sharded call failed"}
+          -9: "another rank's part of the sharded call failed",
+          -10: "a collective hook failed"}
 
 
 class PqhError(RuntimeError):
@@ -143,6 +144,8 @@ SIGNATURES = [
     ("pqh_shard_block", I, [LL, I, I, P]), ("pqh_shard_scratch_bytes", LL, [I, I]),
     ("pqh_shard_encode", I, [P, P, P, P, I, I, I, P, P, P, ULL, I, P, P, P, P, P]),
     ("pqh_shard_status", I, [P, P]),
+    ("pqh_shard_encode_tables", I, [P, P, P, P, I, I, I, P, P, P]),
+    ("pqh_shard_encode_write", I, [P, P, P, P, I, I, I, P, P, ULL, I, P, P, P, P, I, P]),
     ("pqh_shard_offsets", I, [P, I, I, P, P]),
     ("pqh_shard_stitch", I, [I, P, P, P, P, ULL]),
     ("pqh_shard_halo_source", I, [P, I, I, P, P]),

@@ -46,13 +46,21 @@ int pqh_ensure_ws(pqh_ctx* ctx, size_t bytes) {
     if (bytes <= ctx->ws_bytes) return PQH_OK;
     if (ctx->ws) {
         PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        ctx->ws_bytes = 0;
         PQH_HIP(ctx, hipFree(ctx->ws));
         ctx->ws = nullptr;
     }
-    size_t want = bytes + bytes / 4 + 4096;
-    PQH_HIP(ctx, hipMalloc(&ctx->ws, want));
-    ctx->ws_bytes = want;
-    return PQH_OK;
+    // 25% slack so that slowly growing requests do not reallocate every call; the exact
+    // size when the slack does not fit
+    for (size_t want : {bytes + bytes / 4 + 4096, bytes}) {
+        if (hipMalloc(&ctx->ws, want) == hipSuccess) {
+            ctx->ws_bytes = want;
+            return PQH_OK;
+        }
+        ctx->ws = nullptr;
+        (void)hipGetLastError();
+    }
+    return pqh_set_error(ctx, PQH_ERR_NOMEM, "workspace: cannot allocate %zu bytes", bytes);
 }
 
 extern "C" {

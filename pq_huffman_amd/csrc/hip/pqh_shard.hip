@@ -123,103 +123,161 @@ int pqh_shard_halo_source(const int* nonempty, int world, int rank, int* prev_ra
     return PQH_OK;
 }
 
-int pqh_shard_encode(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm, const block_t* shard,
-                     const void* d_codes, int m, int k, int context, pqh_tables_t* tables,
-                     uint32_t* d_counts, unsigned char* d_out, unsigned long long out_bytes,
-                     int chunk_vectors, unsigned long long* d_chunk_offsets, void* d_chunk_prev,
-                     unsigned long long* d_offsets, void* d_scratch, int* raw_first_out) {
-    // Without these the collective sequence itself cannot run (or would not match the other
-    // ranks' sizes): refuse before the first collective.
-    if (!ctx || !comm || comm->world <= 0 || comm->rank < 0 || comm->rank >= comm->world ||
-        !comm->all_gather || !comm->all_reduce_sum_u32 || m <= 0 || k <= 0 || k > 256 ||
-        (context && k != 256) || !d_counts || !d_offsets || !d_scratch ||
-        (reinterpret_cast<uintptr_t>(d_scratch) & 15u))
-        return PQH_ERR_ARG;
+namespace {
+// the scratch layout (pqh_shard_scratch_bytes)
+struct ShardScratch {
+    unsigned char* halo_send;
+    unsigned char* halo_recv;
+    unsigned char* halo_row;
+    unsigned long long* len_send;
+    unsigned long long* len_recv;
+    int* rawf;
+    long long recb;
+    ShardScratch(void* d, int world, int m) {
+        unsigned char* p = static_cast<unsigned char*>(d);
+        recb = halo_record_bytes(m);
+        halo_send = p;
+        halo_recv = p + recb;
+        halo_row = p + recb * (world + 1);
+        len_send = reinterpret_cast<unsigned long long*>(p + recb * (world + 2));
+        len_recv = len_send + 1;
+        rawf = reinterpret_cast<int*>(len_recv + world);
+    }
+};
+
+// Without these the collective sequence itself cannot run (or would not match the other
+// ranks' sizes): refused before the first collective.
+bool shard_fatal(const pqh_ctx_t* ctx, const pqh_shard_comm_t* comm, int m, int k, int context,
+                 const void* d_scratch) {
+    return !ctx || !comm || comm->world <= 0 || comm->rank < 0 || comm->rank >= comm->world ||
+           !comm->all_gather || !comm->all_reduce_sum_u32 || m <= 0 || k <= 0 || k > 256 ||
+           (context && k != 256) || !d_scratch || (reinterpret_cast<uintptr_t>(d_scratch) & 15u);
+}
+
+bool shard_local_bad(const block_t* shard, const void* d_codes, const pqh_tables_t* tables, int m,
+                     int k, int context) {
+    return !shard || shard->size < 0 || (shard->size > 0 && !d_codes) || !tables ||
+           tables->m != m || tables->k != k || (tables->context ? 1 : 0) != (context ? 1 : 0);
+}
+}  // namespace
+
+// Phase 1: halo, histogram, all-reduce, code tables.  Any failure after the fatal checks is
+// local: the rank stays in the collective sequence (an empty halo record, a histogram
+// counting nothing), the error is returned and must be handed to phase 2 (status), which
+// then sends the sentinel length so every rank sees it (pqh_shard_status).
+int pqh_shard_encode_tables(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm, const block_t* shard,
+                            const void* d_codes, int m, int k, int context,
+                            pqh_tables_t* tables, uint32_t* d_counts, void* d_scratch) {
+    if (shard_fatal(ctx, comm, m, k, context, d_scratch) || !d_counts) return PQH_ERR_ARG;
     int rc = pqh_use_device(ctx);
     if (rc) return rc;
-    // Any other failure is local: the rank stays in the collective sequence (an empty halo
-    // record, its histogram counting nothing, the sentinel length ~0), so no rank waits
-    // forever; every rank's d_offsets then reads {0, ~0} (pqh_shard_status) and this call
-    // returns the local error.
-    int err = PQH_OK;
-    if (!shard || shard->size < 0 || (shard->size > 0 && !d_codes) || !tables || !d_out ||
-        out_bytes < 4 || tables->m != m || tables->k != k || (tables->context ? 1 : 0) != (context ? 1 : 0))
-        err = PQH_ERR_ARG;
-    const long long n = err ? 0 : shard->size;
-    const int world = comm->world, rank = comm->rank;
-    unsigned char* scratch = static_cast<unsigned char*>(d_scratch);
-    const long long recb = halo_record_bytes(m);
-    unsigned char* halo_send = scratch;
-    unsigned char* halo_recv = scratch + recb;
-    unsigned char* halo_row = scratch + recb * (world + 1);
-    unsigned long long* len_send =
-        reinterpret_cast<unsigned long long*>(scratch + recb * (world + 2));
-    unsigned long long* len_recv = len_send + 1;
-    int* d_rawf = reinterpret_cast<int*>(len_recv + world);
-    void* const st = ctx->stream;
+    int err = shard_local_bad(shard, d_codes, tables, m, k, context) ? PQH_ERR_ARG : PQH_OK;
     auto local = [&](int r) {   // the first local failure is kept
         if (r && !err) err = r;
     };
-    // 1. the halo (context mode): every rank's (non-empty flag, last row); the halo row and
-    //    the raw-first flag are picked on the device -- no host round trip
+    const long long n = err ? 0 : shard->size;
+    const int world = comm->world, rank = comm->rank;
+    ShardScratch sc(d_scratch, world, m);
+    void* const st = ctx->stream;
+    // the halo (context mode): every rank's (non-empty flag, last row); the halo row and the
+    // raw-first flag are picked on the device -- no host round trip
     if (context) {
-        local(hipMemsetAsync(halo_send, 0, recb, ctx->stream) == hipSuccess ? PQH_OK : PQH_ERR_HIP);
+        local(hipMemsetAsync(sc.halo_send, 0, sc.recb, ctx->stream) == hipSuccess ? PQH_OK : PQH_ERR_HIP);
         if (n > 0 && !err) {
-            local(hipMemsetAsync(halo_send, 1, 1, ctx->stream) == hipSuccess ? PQH_OK : PQH_ERR_HIP);
-            local(hipMemcpyAsync(halo_send + kHaloData,
+            local(hipMemsetAsync(sc.halo_send, 1, 1, ctx->stream) == hipSuccess ? PQH_OK : PQH_ERR_HIP);
+            local(hipMemcpyAsync(sc.halo_send + kHaloData,
                                  static_cast<const unsigned char*>(d_codes) + (n - 1) * m, m,
                                  hipMemcpyDeviceToDevice, ctx->stream) == hipSuccess
                       ? PQH_OK : PQH_ERR_HIP);
         }
-        if (comm->all_gather(comm->user, halo_send, halo_recv, recb, st))
-            return pqh_set_error(ctx, PQH_ERR_ARG, "shard halo all-gather failed");
-        hipLaunchKernelGGL(shard_halo_pick, dim3(1), dim3(64), 0, ctx->stream, halo_recv, recb,
-                           world, rank, m, halo_row, d_rawf);
+        if (comm->all_gather(comm->user, sc.halo_send, sc.halo_recv, sc.recb, st))
+            return pqh_set_error(ctx, PQH_ERR_COMM, "shard halo all-gather failed");
+        hipLaunchKernelGGL(shard_halo_pick, dim3(1), dim3(64), 0, ctx->stream, sc.halo_recv,
+                           sc.recb, world, rank, m, sc.halo_row, sc.rawf);
         local(hipGetLastError() == hipSuccess ? PQH_OK : PQH_ERR_HIP);
     }
-    // 2. the shard's histogram (+ the halo pair), summed over ranks -> identical tables
+    // the shard's histogram (+ the halo pair), summed over ranks -> identical tables
     const long long items = context ? (long long)k * k : k;
-    if (err) {
+    if (err)
         local(hipMemsetAsync(d_counts, 0, (size_t)m * items * 4, ctx->stream) == hipSuccess
                   ? PQH_OK : PQH_ERR_HIP);
-    } else if (context) {
-        local(pqh_histogram_set_dev(ctx, d_codes, n, m, k, halo_row, d_rawf, d_counts));
-    } else {
+    else if (context)
+        local(pqh_histogram_set_dev(ctx, d_codes, n, m, k, sc.halo_row, sc.rawf, d_counts));
+    else
         local(pqh_histogram_set(ctx, d_codes, n, m, k, 0, nullptr, d_counts));
-    }
     if (comm->all_reduce_sum_u32(comm->user, d_counts, (long long)m * items, st))
-        return pqh_set_error(ctx, PQH_ERR_ARG, "shard histogram all-reduce failed");
+        return pqh_set_error(ctx, PQH_ERR_COMM, "shard histogram all-reduce failed");
     if (!err) local(pqh_tables_build(ctx, tables, d_counts));
-    // 3. place the shard: its exact length, everyone's, the exclusive scan on the device
-    if (!err)
-        local(context ? pqh_encode_size_dev(ctx, tables, d_codes, n, halo_row, d_rawf, len_send)
-                      : pqh_encode_size(ctx, tables, d_codes, n, 0, nullptr, len_send));
-    if (err) (void)hipMemsetAsync(len_send, 0xFF, 8, ctx->stream);   // the sentinel length
-    if (comm->all_gather(comm->user, len_send, len_recv, 8, st))
-        return pqh_set_error(ctx, PQH_ERR_ARG, "shard length all-gather failed");
-    hipLaunchKernelGGL(shard_prefix, dim3(1), dim3(64), 0, ctx->stream, len_recv, world, rank,
+    return err;
+}
+
+// Phase 2: the shard's exact length, everyone's (all-gather; the sentinel ~0 when status,
+// the rank's phase-1 result, or this phase fails locally), the exclusive scan on the device,
+// and the write.
+int pqh_shard_encode_write(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm, const block_t* shard,
+                           const void* d_codes, int m, int k, int context, pqh_tables_t* tables,
+                           unsigned char* d_out, unsigned long long out_bytes, int chunk_vectors,
+                           unsigned long long* d_chunk_offsets, void* d_chunk_prev,
+                           unsigned long long* d_offsets, void* d_scratch, int status,
+                           int* raw_first_out) {
+    if (shard_fatal(ctx, comm, m, k, context, d_scratch) || !d_offsets) return PQH_ERR_ARG;
+    int rc = pqh_use_device(ctx);
+    if (rc) return rc;
+    int err = status;
+    if (!err && (shard_local_bad(shard, d_codes, tables, m, k, context) || !d_out || out_bytes < 4))
+        err = PQH_ERR_ARG;
+    const long long n = err ? 0 : shard->size;
+    const int world = comm->world, rank = comm->rank;
+    ShardScratch sc(d_scratch, world, m);
+    if (!err) {
+        const int r = context ? pqh_encode_size_dev(ctx, tables, d_codes, n, sc.halo_row, sc.rawf,
+                                                    sc.len_send)
+                              : pqh_encode_size(ctx, tables, d_codes, n, 0, nullptr, sc.len_send);
+        if (r) err = r;
+    }
+    if (err) (void)hipMemsetAsync(sc.len_send, 0xFF, 8, ctx->stream);   // the sentinel length
+    if (comm->all_gather(comm->user, sc.len_send, sc.len_recv, 8, ctx->stream))
+        return pqh_set_error(ctx, PQH_ERR_COMM, "shard length all-gather failed");
+    hipLaunchKernelGGL(shard_prefix, dim3(1), dim3(64), 0, ctx->stream, sc.len_recv, world, rank,
                        d_offsets);
     PQH_LAUNCH_CHECK(ctx);
     if (err) return err;
-    // 4. write it (word 0 of d_out = the global word offset / 32; the bits before the shard's
-    // offset in that word belong to the previous shard and stay zero here)
+    // word 0 of d_out = the global word offset / 32; the bits before the shard's offset in
+    // that word belong to the previous shard and stay zero here
     PQH_HIP(ctx, hipMemsetAsync(d_out, 0, 4, ctx->stream));
-    rc = context ? pqh_encode_write_at_dev(ctx, tables, d_codes, n, halo_row, d_rawf, d_offsets,
+    rc = context ? pqh_encode_write_at_dev(ctx, tables, d_codes, n, sc.halo_row, sc.rawf, d_offsets,
                                            d_out, out_bytes, chunk_vectors, d_chunk_offsets,
                                            d_chunk_prev)
                  : pqh_encode_write_at(ctx, tables, d_codes, n, 0, nullptr, d_offsets, d_out,
                                        out_bytes, chunk_vectors, d_chunk_offsets, d_chunk_prev,
                                        nullptr);
     if (rc) return rc;
-    if (raw_first_out) {   // (optional: the one host read of the call, at its end)
+    if (raw_first_out) {   // (optional: the one host read, at the end)
         int rf = rank == 0 ? 1 : 0;
         if (context) {
-            PQH_HIP(ctx, hipMemcpyAsync(&rf, d_rawf, 4, hipMemcpyDeviceToHost, ctx->stream));
+            PQH_HIP(ctx, hipMemcpyAsync(&rf, sc.rawf, 4, hipMemcpyDeviceToHost, ctx->stream));
             PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
         }
         *raw_first_out = rf;
     }
     return PQH_OK;
+}
+
+int pqh_shard_encode(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm, const block_t* shard,
+                     const void* d_codes, int m, int k, int context, pqh_tables_t* tables,
+                     uint32_t* d_counts, unsigned char* d_out, unsigned long long out_bytes,
+                     int chunk_vectors, unsigned long long* d_chunk_offsets, void* d_chunk_prev,
+                     unsigned long long* d_offsets, void* d_scratch, int* raw_first_out) {
+    if (shard_fatal(ctx, comm, m, k, context, d_scratch) || !d_counts || !d_offsets)
+        return PQH_ERR_ARG;
+    const int rc1 = pqh_shard_encode_tables(ctx, comm, shard, d_codes, m, k, context, tables,
+                                            d_counts, d_scratch);
+    // (a failed collective hook leaves the sequence unfinishable: phase 2 is not attempted)
+    if (rc1 == PQH_ERR_COMM) return rc1;
+    const int rc2 = pqh_shard_encode_write(ctx, comm, shard, d_codes, m, k, context, tables, d_out,
+                                           out_bytes, chunk_vectors, d_chunk_offsets, d_chunk_prev,
+                                           d_offsets, d_scratch, rc1, raw_first_out);
+    return rc1 ? rc1 : rc2;
 }
 
 int pqh_shard_status(pqh_ctx_t* ctx, const unsigned long long* d_offsets) {

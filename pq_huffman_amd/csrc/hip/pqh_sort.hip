@@ -330,8 +330,13 @@ static int sort_rows_radix(pqh_ctx_t* ctx, uint8_t* codes, long long n, int m) {
         PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));   // no launch may still use it
         if (ctx->sort_state) (void)hipFree(ctx->sort_state);
         ctx->sort_state = nullptr;
+        ctx->sort_cap = 0;
         const long long cap = tiles + tiles / 4 + 16;
-        PQH_HIP(ctx, hipMalloc(&ctx->sort_state, (size_t)(cap * 256 + 1) * 8));
+        if (hipMalloc(&ctx->sort_state, (size_t)(cap * 256 + 1) * 8) != hipSuccess) {
+            ctx->sort_state = nullptr;
+            (void)hipGetLastError();
+            return pqh_set_error(ctx, PQH_ERR_NOMEM, "sort: cannot allocate the tile state");
+        }
         PQH_HIP(ctx, hipMemsetAsync(ctx->sort_state, 0, (size_t)(cap * 256 + 1) * 8, ctx->stream));
         ctx->sort_cap = cap;
         ctx->sort_epoch = 0;
@@ -401,8 +406,12 @@ int pqh_sort_rows(pqh_ctx_t* ctx, void* d_codes, long long n, int m, void* d_tmp
         return e && !std::strcmp(e, "rocprim");
     }();
     if (m >= 2 && m <= 8 && n < (1ll << 31) && !force_lib &&
-        (m != 8 || (reinterpret_cast<uintptr_t>(d_codes) & 7) == 0))
-        return sort_rows_radix(ctx, static_cast<uint8_t*>(d_codes), n, m);
+        (m != 8 || (reinterpret_cast<uintptr_t>(d_codes) & 7) == 0)) {
+        rc = sort_rows_radix(ctx, static_cast<uint8_t*>(d_codes), n, m);
+        if (rc != PQH_ERR_NOMEM) return rc;
+        // out of device memory for the in-tree sort's 32 B/row: the rocPRIM path below
+        // needs 24 B/row + its temp when the caller passes d_tmp
+    }
     // workspace: keys in/out (u64), index in/out (u32), rocPRIM temp, row buffer if no d_tmp
     size_t temp = 0;
     if (rocprim::radix_sort_pairs(nullptr, temp, (unsigned long long*)nullptr,

@@ -598,7 +598,16 @@ huff_trees_small(const uint32_t* __restrict__ counts, int k, long long trees,
     if (stamp) g_tree_stamps[1] = __builtin_amdgcn_s_memtime();
     int next;
     // u32 heap: key payloads are the leaf's symbol (< 256) or 256 + the internal node's
-    // creation index, so the code pass reads no symbol table; the 64-bit heap's are node ids
+    // creation index, so the code pass reads no symbol table; the 64-bit heap's are node ids.
+    // The packing weight << 10 | tie << 9 | payload holds because (1) k <= 256 (the host
+    // launches this kernel, like huff_trees_grp, only for k <= 256 -- checked again here), so
+    // symbols fit 8 bits and the <= 255 internal nodes give payloads <= 256 + 254 < 512, and
+    // (2) the tree's total weight is < 2^22, so every node weight (<= total) shifted by 10
+    // stays below 2^32; heavier trees take the 64-bit path.
+    if (k > 256) {
+        atomicOr(err, 2u);
+        return;
+    }
     const bool symp = total < (1ull << 22);
     if (symp) {
         SentinelHeap<TPW> hp{heap_all + t, 0};
@@ -2270,6 +2279,7 @@ int pqh_tables_status(pqh_ctx_t* ctx, const pqh_tables_t* t) {
     uint32_t e = 0;
     PQH_HIP(ctx, hipMemcpyAsync(&e, t->d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
     PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (e & 2u) return pqh_set_error(ctx, PQH_ERR_UNSUPPORTED, "a k <= 256 tree builder ran with k > 256");
     return e ? pqh_set_error(ctx, PQH_ERR_CODE_TOO_LONG, "a Huffman code exceeds 56 bits") : PQH_OK;
 }
 

@@ -419,3 +419,73 @@ def status(ctx, offsets):
     from .capi import check
     check(_lib().pqh_shard_status(ctx.ptr, ctypes.c_void_p(offsets.data_ptr())),
           "pqh_shard_status")
+
+
+# ---- the same protocol in two phases (pqh_shard_encode_tables / _write), for a caller that
+# pipelines batches: phase 1 on the table lane, phase 2 on the encode stream, other batches'
+# collectives between them (bench.py's world > 1 schedule) ----
+
+def scratch_for(comm: TorchComm, m: int, device):
+    """the d_scratch of one in-flight batch (halo records, halo row, lengths)"""
+    import torch
+    return torch.empty(int(_lib().pqh_shard_scratch_bytes(comm.world, m)), dtype=torch.uint8,
+                       device=device)
+
+
+def _block(first_row, n):
+    from .capi import Block
+    b = Block()
+    b.id, b.size, b.capacity = first_row, n, n
+    return b
+
+
+def shard_encode_tables(ctx, comm: TorchComm, codes, tables, counts, scratch, first_row=0) -> int:
+    """Phase 1 on ctx's stream: halo, histogram, all-reduce, code tables.  Returns the
+    rank's status (0 or a negative pqh status), to be handed to shard_encode_write."""
+    n, m = codes.shape
+    ptr = (lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None)
+    comm.error = None
+    comm.register(counts, scratch)
+    try:
+        rc = _lib().pqh_shard_encode_tables(ctx.ptr, ctypes.byref(comm.struct),
+                                            ctypes.byref(_block(first_row, n)),
+                                            ptr(codes) if n else None, m, tables.k,
+                                            int(tables.context), tables.ptr, ptr(counts),
+                                            ptr(scratch))
+    finally:
+        comm.clear()
+    if comm.error is not None:
+        raise comm.error
+    return rc
+
+
+def shard_encode_write(ctx, comm: TorchComm, codes, tables, out, chunk_vectors, chunk_offsets,
+                       chunk_prev, offsets, scratch, status=0, first_row=0):
+    """Phase 2 on ctx's stream: length, all-gather, device offsets (into `offsets`, a (2,)
+    int64 tensor), the write.  Raises on this rank's failure; another rank's shows in
+    offsets[1] == -1 (status())."""
+    from .capi import check
+    n, m = codes.shape
+    ptr = (lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None)
+    comm.error = None
+    comm.register(scratch)
+    try:
+        rc = _lib().pqh_shard_encode_write(ctx.ptr, ctypes.byref(comm.struct),
+                                           ctypes.byref(_block(first_row, n)),
+                                           ptr(codes) if n else None, m, tables.k,
+                                           int(tables.context), tables.ptr, ptr(out), out.numel(),
+                                           chunk_vectors, ptr(chunk_offsets), ptr(chunk_prev),
+                                           ptr(offsets), ptr(scratch), int(status), None)
+    finally:
+        comm.clear()
+    if comm.error is not None:
+        raise comm.error
+    check(rc, "pqh_shard_encode_write")
+
+
+def scratch_shard_bits(scratch, world: int, m: int):
+    """this shard's exact length in bits, as phase 2 left it in the scratch (a (1,) int64
+    device view)"""
+    rec = (16 + m + 15) // 16 * 16
+    off = rec * (world + 2)
+    return scratch[off:off + 8].view(__import__("torch").int64)

@@ -1,16 +1,21 @@
 #!/bin/bash
-# Collect the rocprofv3 evidence for one round (run on the GPU box from the repo root):
-#   kernel trace + per-kernel stats of the default bench command, then the HBM byte
-#   counters in their own passes (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass).
-# usage: bash profiles/collect.sh <round-tag> [bench args...]
+# Collect one configuration's evidence for profiles/ (run on the GPU box from the repo root):
+#   1. the bench line itself (no profiler attached)        -> $OUT/bench.log
+#   2. kernel trace + per-kernel stats of the same command -> $OUT/kt/
+#   3. the HBM byte counters, each in a pass of its own (FETCH_SIZE and WRITE_SIZE do not fit
+#      one TCC pass; MI355X_MICROARCH.md "HBM")           -> $OUT/fetch/, $OUT/write/
+# then `python profiles/summarize.py <tag>` writes profiles/<tag>_{bench.json,kernel_stats.csv,
+# pmc_summary.json}.
+# usage: bash profiles/collect.sh <tag, e.g. r3_sift> [bench args...]
 set -euo pipefail
-TAG=${1:?round tag}
+TAG=${1:?tag}
 shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
+timeout -k 10 300 python3 "$R/bench.py" --no-cpu-baseline "$@" > "$OUT/bench.log" 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv \
     -- python3 "$R/bench.py" --no-cpu-baseline "$@" > "$OUT/kt.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o fetch --output-format csv \

@@ -1,4 +1,6 @@
-"""Summarise one round's rocprofv3 output (gpurun_out/prof_<tag>) into profiles/:
+"""Summarise one configuration's collection (gpurun_out/prof_<tag>, profiles/collect.sh) into
+profiles/:
+  <tag>_bench.json         the unprofiled bench JSON line
   <tag>_kernel_stats.csv   the --kernel-trace --stats summary (copied)
   <tag>_pmc_summary.json   per-kernel average duration and HBM bytes per launch:
                            FETCH_SIZE x 2 (gfx950 reports half of wide streaming reads,
@@ -32,8 +34,20 @@ def per_kernel(path, counter):
     return {k: sum(v) / len(v) for k, v in acc.items()}
 
 
+def bench_line(src, tag):
+    """the unprofiled bench JSON line of the collection -> profiles/<tag>_bench.json"""
+    path = os.path.join(src, "bench.log")
+    if not os.path.exists(path):
+        return
+    lines = [x for x in open(path) if x.startswith("{")]
+    if lines:
+        with open(os.path.join(HERE, f"{tag}_bench.json"), "w") as f:
+            json.dump(json.loads(lines[-1]), f, indent=1)
+
+
 def main(tag):
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    bench_line(src, tag)
     shutil.copy(os.path.join(src, "kt", "kt_kernel_stats.csv"),
                 os.path.join(HERE, f"{tag}_kernel_stats.csv"))
     dur = {}

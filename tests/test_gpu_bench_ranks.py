@@ -1,6 +1,7 @@
 """The multi-rank bench schedule on one GPU (gloo process group, every rank on cuda:0):
-two ranks run bench.py's real lane schedule (halo all-gather, histogram all-reduce, device
-bit offsets, encode_write_at) as fresh child processes; the shards' streams stitched on
+two ranks run bench.py's real lane schedule -- the library's two-phase pqh_shard_encode, or
+the Python composition (halo all-gather, histogram all-reduce, device bit offsets,
+encode_write_at) -- as fresh child processes; the shards' streams stitched on
 rank 0 must equal the oracle's one-shot stream over all ranks' rows (huffman_encoder.c
 :207-238 over the concatenated input), and both ranks must exit cleanly (status 0, no
 signal at teardown)."""
@@ -23,15 +24,19 @@ def _free_port():
         return s.getsockname()[1]
 
 
+@pytest.mark.parametrize("path", ["library", "python"])
 @pytest.mark.parametrize("mode", ["ctx", "noctx"])
-def test_two_rank_rehearsal_stitched_stream(oracle, tmp_path, mode):
+def test_two_rank_rehearsal_stitched_stream(oracle, tmp_path, mode, path):
+    """path library: the bench's default world > 1 schedule through the C ABI
+    (pqh_shard_encode_tables on the table lane, pqh_shard_encode_write on the encode stream,
+    torch.distributed hooks); python: the same steps composed in shard.py."""
     dump = tmp_path / "dump.npz"
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
            "--one-device", "--vectors", "30001", "--steps", "3", "--warmup", "1",
-           "--mode", mode, "--no-cpu-baseline", "--dump", str(dump)]
+           "--mode", mode, "--no-cpu-baseline", "--dump", str(dump), "--shard-path", path]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     d = np.load(dump, allow_pickle=False)

@@ -1,4 +1,6 @@
-import os, sys, time
+"""Context-histogram timing (diagnostic): the 1024-thread and 256-thread (PQH_HIST_BLOCK)
+variants of hist_ctx on the bench's 1M-row SIFT-shaped codes, then pq_assign_mfma alone."""
+import os, sys
 sys.path.insert(0, os.getcwd())
 import torch
 from pq_huffman_amd import codec
