@@ -105,13 +105,15 @@ def parse():
     ap.add_argument("--elanes", type=int, default=None,
                     help="> 0: encode + decode on this many streams of their own; the --lanes "
                          "streams then build code tables only (default 1; 0 for k4096)")
-    ap.add_argument("--drain-trees", choices=["wave", "lane"], default="wave",
+    ap.add_argument("--drain-trees", choices=["default", "grp", "wave", "lane"],
+                    default="default",
                     help="tree builder of the run's last batch, built after the assignment "
-                         "stream is done: one wavefront per tree (lower latency) or the "
-                         "default one lane per tree")
-    ap.add_argument("--fill-trees", choices=["wave", "lane"], default="lane",
+                         "stream is done (default: the library's, 16 lanes per tree for "
+                         "k <= 256)")
+    ap.add_argument("--fill-trees", choices=["default", "grp", "wave", "lane"],
+                    default="default",
                     help="tree builder of the first batch on each table lane (the pipeline's "
-                         "fill: the lanes start their back-to-back builds earlier)")
+                         "fill)")
     ap.add_argument("--hist-on", choices=["assign", "lanes"], default="assign",
                     help="stream of the context histogram: the assignment's, or the batch's "
                          "lane (before its code tables)")
@@ -525,9 +527,9 @@ def main():
                 sL.wait_event(ev_dec[t0i])
                 sL.wait_event(ev_dec[ti])
                 e = rec("codebook", sL)
-                if i == state["nsteps"] - 1 and args.drain_trees == "wave":
-                    tabs[t0i].build(counts[s0], c, trees="wave")   # the drain: lower latency
-                    tabs[ti].build(counts[s], c, trees="wave")
+                if i == state["nsteps"] - 1 and args.drain_trees != "default":
+                    tabs[t0i].build(counts[s0], c, trees=args.drain_trees)   # the drain
+                    tabs[ti].build(counts[s], c, trees=args.drain_trees)
                 else:
                     tabs[t0i].build_pair(counts[s0], tabs[ti], counts[s], c)
                 done(e, sL)
@@ -539,17 +541,20 @@ def main():
             if elanes is not lanes:              # tabs[ti] free: its last decode is done
                 sL.wait_event(ev_dec[ti])
             e = rec("codebook", sL)
-            # GPU trees + lookup tables, no host trip.  The run's last batch builds while
-            # the assignment stream has nothing left to do: there the one-wavefront-per-tree
-            # build (lower latency, more waves) shortens the drain (--drain-trees).
-            last = (i == state["nsteps"] - 1 and args.drain_trees == "wave") or \
-                (i < nl and args.fill_trees == "wave")
+            # GPU trees + lookup tables, no host trip.  --drain-trees / --fill-trees pick
+            # another builder for the run's last batch (built after the assignment stream is
+            # done) and the lanes' first batches.
+            tr = None
+            if i == state["nsteps"] - 1 and args.drain_trees != "default":
+                tr = args.drain_trees
+            elif i < nl and args.fill_trees != "default":
+                tr = args.fill_trees
             if lut_a:   # trees here, the decode tables on A dl batches later (lut())
-                tabs[ti].build_trees(counts[s], c, trees="wave" if last else None)
+                tabs[ti].build_trees(counts[s], c, trees=tr)
                 done(e, sL)
                 ev_trees[s].record(sL)
             else:
-                tabs[ti].build(counts[s], c, trees="wave" if last else None)
+                tabs[ti].build(counts[s], c, trees=tr)
                 done(e, sL)
                 ev_tab[s].record(sL)
         if lut_a and i >= dl:
