@@ -71,9 +71,30 @@ hist_ctx(const CodeT* __restrict__ codes, long long n, int m_total, int k,
     };
     unsigned prevc = v0 > 0 ? (v0 - 1 < n ? ld_code(codes, (v0 - 1) * m_total + m) : ~0u)
                             : (prev_row ? (unsigned)prev_row[m] : ~0u);
-    const bool wide = sizeof(CodeT) == 1 && m_total == 8 && v0 + kRun <= n;
+    const bool full = sizeof(CodeT) == 1 && v0 + kRun <= n;
+    const bool wide = full && m_total == 8;
+    // other part counts that are a multiple of 4 (configs[3]: M = 16): the dword of the row
+    // that holds part m, kSub rows' dwords issued before their counter updates
+    const bool dw = full && m_total != 8 && (m_total & 3) == 0 &&
+                    (reinterpret_cast<uintptr_t>(codes) & 3) == 0;
     __syncthreads();   // the counters are zeroed (one barrier on every path: `wide` varies)
-    if (wide) {
+    if (dw) {
+        const int rw = m_total >> 2;   // dwords per row
+        const uint32_t* rows = reinterpret_cast<const uint32_t*>(codes) + v0 * rw + (m >> 2);
+        const int sh = 8 * (m & 3);
+#pragma unroll 1
+        for (int g = 0; g < kRun / kSub; ++g) {
+            uint32_t q[kSub];
+#pragma unroll
+            for (int u = 0; u < kSub; ++u) q[u] = rows[(long long)(g * kSub + u) * rw];
+#pragma unroll
+            for (int u = 0; u < kSub; ++u) {
+                const unsigned c = (q[u] >> sh) & 0xFFu;
+                count(prevc, c);
+                prevc = c;
+            }
+        }
+    } else if (wide) {
         // this thread's part-m codes of kSub consecutive rows per group, all of a group's
         // loads issued before its counter updates (8-byte rows of u8 codes: 16 B per load)
         const uint4* rows = reinterpret_cast<const uint4*>(codes + v0 * 8);
@@ -98,6 +119,107 @@ hist_ctx(const CodeT* __restrict__ codes, long long n, int m_total, int k,
             const unsigned cur = v < n ? ld_code(codes, v * m_total + m) : ~0u;
             count(prevc, cur);
             prevc = cur;
+        }
+    }
+    __syncthreads();
+    uint32_t* out = partial + ((long long)m * chunks + chunk) * all_words + (long long)zs * words;
+    if ((words & 3) == 0) {
+        const uint4* src = reinterpret_cast<const uint4*>(pairs);
+        uint4* dst = reinterpret_cast<uint4*>(out);
+#pragma clang loop unroll_count(2) vectorize(disable) interleave(disable)
+        for (int w = threadIdx.x; w < words / 4; w += blockDim.x) dst[w] = src[w];
+    } else {
+#pragma clang loop unroll(disable) vectorize(disable) interleave(disable)
+        for (int w = threadIdx.x; w < words; w += blockDim.x) out[w] = pairs[w];
+    }
+}
+
+// the value of lane l - 1 (lane 0: `first`), a DPP wave shift -- no LDS round trip
+__device__ __forceinline__ unsigned wave_shr1(unsigned v, unsigned first) {
+    return (unsigned)__builtin_amdgcn_update_dpp((int)first, (int)v, 0x138, 0xF, 0xF, false);
+}
+
+// Context histogram, pass 1, wave-contiguous form (u8 codes, m % 4 == 0, 4-byte aligned):
+// same workgroups, LDS counters and partials as hist_ctx, but wave w of the workgroup counts
+// the rows [w R, (w + 1) R) of the chunk in tiles of 64 (or, at m = 8, 128) consecutive rows,
+// lane l holding row(s) l of the tile, so each load instruction covers 1 KB of consecutive
+// rows (16 cache lines) instead of one line per lane; a row's predecessor is the previous
+// lane's row (a DPP wave shift), the tile's first row's the previous tile's last (readlane).
+// G tiles' loads are issued before their counter updates.
+template <int BLK, int G>
+__global__ void __launch_bounds__(BLK)
+hist_ctx_w(const uint8_t* __restrict__ codes, long long n, int m_total, int k,
+           const uint8_t* __restrict__ prev_row, const int* __restrict__ d_rawf,
+           uint32_t* __restrict__ partial, int split, int chunks, int prio) {
+    extern __shared__ uint32_t pairs[];   // (k / split) * k u16 counters packed two per word
+    pqh_set_prio(prio);
+    if (d_rawf && *d_rawf) prev_row = nullptr;   // decided on the device (pqh_shard_encode)
+    const int per_chunk = m_total * split;
+    const int q = (int)(blockIdx.x >> 3);
+    const int chunk = (q / per_chunk) * 8 + (int)(blockIdx.x & 7);
+    if (chunk >= chunks) return;   // (uniform: the XCD's list is shorter)
+    const int m = (q % per_chunk) / split;
+    const int zs = q % split;
+    const int prows = k / split;
+    const unsigned plo = (unsigned)(zs * prows);
+    const int all_words = (k * k + 1) / 2;
+    const int words = split == 1 ? all_words : prows * k / 2;
+#pragma clang loop unroll_count(4) vectorize(disable) interleave(disable)
+    for (int w = threadIdx.x; w < words; w += blockDim.x) pairs[w] = 0;
+    auto count = [&](unsigned prev, unsigned cur) {
+        if (prev >= (unsigned)k || cur >= (unsigned)k) return;   // absent / out of alphabet
+        const unsigned pr = prev - plo;
+        if (pr >= (unsigned)prows) return;                       // another split's range
+        const unsigned bin = pr * (unsigned)k + cur;
+        atomicAdd(&pairs[bin >> 1], 1u << ((bin & 1u) * 16));
+    };
+    const int lane = threadIdx.x & 63;
+    constexpr int kR = kHistChunk / (BLK / 64);   // rows per wave
+    static_assert(kR % (128 * G) == 0, "whole tile groups per wave");
+    const long long w0 = (long long)chunk * kHistChunk + (long long)(threadIdx.x >> 6) * kR;
+    const long long w1 = min(n, w0 + kR);
+    unsigned carry = w0 > 0 ? (w0 - 1 < n ? (unsigned)codes[(w0 - 1) * m_total + m] : ~0u)
+                            : (prev_row ? (unsigned)prev_row[m] : ~0u);
+    carry = (unsigned)__builtin_amdgcn_readfirstlane((int)carry);
+    const int sh = 8 * (m & 3);
+    __syncthreads();   // the counters are zeroed
+    if (m_total == 8 && w1 - w0 == kR) {
+        // two 8-byte rows per lane: one 16-byte load covers rows 2l, 2l + 1 of a 128-row tile
+        const uint4* pr = reinterpret_cast<const uint4*>(codes) + w0 / 2 + lane;
+#pragma unroll 1
+        for (int t0 = 0; t0 < kR / 128; t0 += G) {
+            uint4 v[G];
+#pragma unroll
+            for (int u = 0; u < G; ++u) v[u] = pr[(t0 + u) * 64];
+#pragma unroll
+            for (int u = 0; u < G; ++u) {
+                const unsigned a = m < 4 ? v[u].x : v[u].y, b = m < 4 ? v[u].z : v[u].w;
+                const unsigned ca = (a >> sh) & 0xFFu, cb = (b >> sh) & 0xFFu;
+                count(wave_shr1(cb, carry), ca);
+                count(ca, cb);
+                carry = (unsigned)__builtin_amdgcn_readlane((int)cb, 63);
+            }
+        }
+    } else if (w1 > w0) {
+        // one row per lane: the dword of row r that holds part m (rows past the wave's range
+        // clamp their load and count nothing)
+        const int rw = m_total >> 2;
+        const uint32_t* c32 = reinterpret_cast<const uint32_t*>(codes) + (m >> 2);
+#pragma unroll 1
+        for (long long r0 = w0; r0 < w1; r0 += 64 * 2 * G) {
+            uint32_t v[2 * G];
+#pragma unroll
+            for (int u = 0; u < 2 * G; ++u) {
+                const long long r = min(r0 + u * 64 + lane, n - 1);
+                v[u] = c32[r * rw];
+            }
+#pragma unroll
+            for (int u = 0; u < 2 * G; ++u) {
+                const bool valid = r0 + u * 64 + lane < w1;
+                const unsigned c = valid ? (v[u] >> sh) & 0xFFu : ~0u;
+                count(wave_shr1(c, carry), c);
+                carry = (unsigned)__builtin_amdgcn_readlane((int)c, 63);
+            }
         }
     }
     __syncthreads();
@@ -632,7 +754,25 @@ static int histogram_impl(pqh_ctx_t* ctx, const void* d_codes, long long n, int 
         // beside the assignment grid (measured: histogram 0.19 vs 0.075 ms in the bench -- a
         // quarter of the loads in flight -- and the bench 2,119 vs 2,534 Mvec/s)
         const char* hb = std::getenv("PQH_HIST_BLOCK");
-        if (!(hb && std::atoi(hb) == 256)) {
+        // the wave-contiguous form for u8 codes with m % 4 == 0 (aligned rows; PQH_HIST_IMPL=
+        // thread keeps the per-thread runs of hist_ctx)
+        static const bool thread_form = [] {
+            const char* e = std::getenv("PQH_HIST_IMPL");
+            return e && !std::strcmp(e, "thread");
+        }();
+        const uintptr_t al = reinterpret_cast<uintptr_t>(d_codes);
+        // (m = 8 only: measured 0.027 vs 0.035 ms per 1M rows; at m = 16 the per-thread
+        // runs won, 0.108 vs 0.51 ms -- tools/bench_hist.py)
+        const bool wave_form = !thread_form && !(hb && std::atoi(hb) == 256) && m == 8 &&
+                               (al & 15u) == 0;
+        if (wave_form) {
+            PQH_HIP(ctx, hipFuncSetAttribute((const void*)hist_ctx_w<1024, 5>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            hipLaunchKernelGGL((hist_ctx_w<1024, 5>), dim3(grid), dim3(1024), lds, ctx->stream,
+                               static_cast<const uint8_t*>(d_codes), n, m, k,
+                               static_cast<const uint8_t*>(d_prev_row), d_rawf, partial, split,
+                               (int)chunks, pqh_prio("HIST", 0));
+        } else if (!(hb && std::atoi(hb) == 256)) {
             PQH_HIP(ctx, hipFuncSetAttribute((const void*)hist_ctx<uint8_t>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
             hipLaunchKernelGGL(hist_ctx<uint8_t>, dim3(grid), dim3(1024), lds, ctx->stream,

@@ -1928,58 +1928,74 @@ __device__ __forceinline__ int dec_sym8(BitRd<LDS>& br, const Row8Tabs& T, unsig
     return sym < (unsigned)T.k ? (int)sym : -1;
 }
 
-template <bool CTX, bool LDS>
-__device__ __forceinline__ bool dec_row8_lane(const uint32_t* src, uint32_t lim,
-                                              unsigned long long start, long long j, long long n,
-                                              int chunk_vectors, int raw_first,
-                                              const unsigned long long* __restrict__ chunk_prev,
-                                              const Row8Tabs& T, unsigned long long* st) {
+// One lane's chunk: rows of NW u64 words, SB-bit symbols packed little-end first (SB = 8:
+// u8 codes, 8 NW parts; SB = 16: u16 codes, 4 NW parts), so a row is decoded into NW
+// registers, staged in LDS and stored whole; the context row is those registers.
+template <bool CTX, bool LDS, int NW, int SB>
+__device__ __forceinline__ bool dec_row_lane(const uint32_t* src, uint32_t lim,
+                                             unsigned long long start, long long j, long long n,
+                                             int chunk_vectors, int raw_first,
+                                             const unsigned long long* __restrict__ chunk_prev,
+                                             const Row8Tabs& T, unsigned long long* st) {
+    constexpr int PW = 64 / SB;   // parts per word
+    constexpr unsigned SMASK = (1u << SB) - 1u;
     BitRd<LDS> br{src, lim, 0, 0, 0};
     br.init(start);
     const long long v0 = j * chunk_vectors;
     const int cnt = (int)min((long long)chunk_vectors, n - v0);
-    unsigned long long prev = 0;
+    unsigned long long prev[NW];
+#pragma unroll
+    for (int w = 0; w < NW; ++w) prev[w] = 0;
     int s = 0;
     if (CTX) {
         if (j == 0 && raw_first) {   // global row 0: ceil(log2 K) raw bits per part
             int wb = 1;              // (huffman_decode.c:73-76; the encoder writes 8)
             while ((1 << wb) < T.k) ++wb;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) {
 #pragma unroll 1
-            for (int i = 0; i < 8; ++i) {
-                prev |= (unsigned long long)br.peek(wb) << (8 * i);
-                br.skip(wb);
+                for (int i = 0; i < PW; ++i) {
+                    prev[w] |= (unsigned long long)br.peek(wb) << (SB * i);
+                    br.skip(wb);
+                }
+                st[w] = prev[w];
             }
-            st[0] = prev;
             s = 1;
         } else {
-            prev = chunk_prev[j];
+#pragma unroll
+            for (int w = 0; w < NW; ++w) prev[w] = chunk_prev[j * NW + w];
         }
     }
     const unsigned roots = CTX ? (unsigned)T.k : 1u;
     for (; s < cnt; ++s) {
-        unsigned long long row = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            unsigned long long row = 0;
 #pragma unroll 1
-        for (int i = 0; i < 8; ++i) {   // (rolled: one copy of the lookup code, fewer registers)
-            const unsigned tab = (unsigned)i * roots + (CTX ? (unsigned)(prev >> (8 * i)) & 0xFFu : 0u);
-            const int sym = dec_sym8(br, T, tab);
-            if (sym < 0) return false;
-            row |= (unsigned long long)sym << (8 * i);
+            for (int i = 0; i < PW; ++i) {   // (rolled: one copy of the lookup code, fewer registers)
+                const unsigned part = (unsigned)(w * PW + i);
+                const unsigned tab =
+                    part * roots + (CTX ? (unsigned)(prev[w] >> (SB * i)) & SMASK : 0u);
+                const int sym = dec_sym8(br, T, tab);
+                if (sym < 0) return false;
+                row |= (unsigned long long)sym << (SB * i);
+            }
+            prev[w] = row;
+            st[s * NW + w] = row;
         }
-        prev = row;
-        st[s] = row;
     }
     return true;
 }
 
-template <bool CTX>
+template <bool CTX, int NW, int SB>
 __global__ void __launch_bounds__(64)
-dec_row8(const uint32_t* __restrict__ words, long long nwords, long long n, int raw_first,
+dec_rows(const uint32_t* __restrict__ words, long long nwords, long long n, int raw_first,
          int chunk_vectors, const unsigned long long* __restrict__ chunk_off,
          const unsigned long long* __restrict__ chunk_prev, Row8Tabs T,
          unsigned long long* __restrict__ out, unsigned long long* __restrict__ err, int win_words) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
-    unsigned long long* stage = reinterpret_cast<unsigned long long*>(lds);   // [64][C] rows
-    uint32_t* win = reinterpret_cast<uint32_t*>(lds + 64 * 8 * chunk_vectors);
+    unsigned long long* stage = reinterpret_cast<unsigned long long*>(lds);   // [64][C][NW]
+    uint32_t* win = reinterpret_cast<uint32_t*>(lds + 64 * 8 * NW * chunk_vectors);
     const int lane = threadIdx.x;
     pqh_set_prio(T.prio);   // latency-bound: issue ahead of the assignment's waves
     const long long chunks = (n + chunk_vectors - 1) / chunk_vectors;
@@ -2013,18 +2029,19 @@ dec_row8(const uint32_t* __restrict__ words, long long nwords, long long n, int 
     bool ok = true;
     if (lane < jn) {
         const unsigned long long start = chunk_off[j] - (unsigned long long)w_lo * 32;
-        unsigned long long* st = stage + (long long)lane * chunk_vectors;
-        ok = in_lds ? dec_row8_lane<CTX, true>(win, (uint32_t)(nw + 3), start, j, n, chunk_vectors,
-                                               raw_first, chunk_prev, T, st)
-                    : dec_row8_lane<CTX, false>(words + w_lo, (uint32_t)(nwords - 1 - w_lo), start,
-                                                j, n, chunk_vectors, raw_first, chunk_prev, T, st);
+        unsigned long long* st = stage + (long long)lane * chunk_vectors * NW;
+        ok = in_lds ? dec_row_lane<CTX, true, NW, SB>(win, (uint32_t)(nw + 3), start, j, n,
+                                                      chunk_vectors, raw_first, chunk_prev, T, st)
+                    : dec_row_lane<CTX, false, NW, SB>(words + w_lo, (uint32_t)(nwords - 1 - w_lo),
+                                                       start, j, n, chunk_vectors, raw_first,
+                                                       chunk_prev, T, st);
     }
     __syncthreads();
     // the workgroup's rows are contiguous: whole-row stores
-    const long long r0 = j0 * chunk_vectors;
-    const long long rows = min(n, (j0 + 64) * chunk_vectors) - r0;
+    const long long r0 = j0 * chunk_vectors * NW;
+    const long long words_out = (min(n, (j0 + 64) * chunk_vectors) - j0 * chunk_vectors) * NW;
 #pragma unroll 1
-    for (long long q = lane; q < rows; q += 64) __builtin_nontemporal_store(stage[q], out + r0 + q);
+    for (long long q = lane; q < words_out; q += 64) __builtin_nontemporal_store(stage[q], out + r0 + q);
     if (!ok) atomicOr(err, 1ull);
 }
 
@@ -2347,25 +2364,43 @@ int pqh_decode(pqh_ctx_t* ctx, const pqh_tables_t* t, const unsigned char* d_str
     const size_t lds = meta_bytes + (lds_l1 ? ((l1_bytes + 15) & ~(size_t)15) : 0) +
                        ((size_t)win_words + 4) * 4 + (size_t)64 * S * t->m * esz + 16;
     if (lds > 160 * 1024) return PQH_ERR_UNSUPPORTED;
-    // 8-part u8 rows (aligned, C <= 32): the slim decoder
-    if (t->k <= 256 && t->m == 8 && chunk_vectors <= 32 && nwords < (1ll << 31) &&
-        !(reinterpret_cast<uintptr_t>(d_codes) & 7) && !(reinterpret_cast<uintptr_t>(d_chunk_prev) & 7)) {
-        const int ww = (int)std::min<long long>(3072, std::max<long long>(
-            256, (64ll * chunk_vectors * 8 * 12 + 31) / 32 + 8));
-        const size_t lds8 = (size_t)64 * 8 * chunk_vectors + ((size_t)ww + 4) * 4;
+    // whole-row decoders (<= 32 VGPRs: they run beside the assignment grid): rows of 8 or 16
+    // u8 codes, or of 8 u16 codes, chunks of C <= 32 vectors, 8-byte aligned rows
+    const int esz_b = (int)esz;
+    const int row_bytes = t->m * esz_b;
+    if ((row_bytes == 8 || row_bytes == 16) && (esz_b == 1 || t->m == 8) && chunk_vectors <= 32 &&
+        nwords < (1ll << 31) && !(reinterpret_cast<uintptr_t>(d_codes) & 7) &&
+        !(reinterpret_cast<uintptr_t>(d_chunk_prev) & 7)) {
+        const int nw_row = row_bytes / 8;
+        const int ww = (int)std::min<long long>(4096 - 1024 * (nw_row - 1), std::max<long long>(
+            256, (64ll * chunk_vectors * t->m * sym_bits + 31) / 32 + 8));
+        const size_t lds_r = (size_t)64 * row_bytes * chunk_vectors + ((size_t)ww + 4) * 4;
         const Row8Tabs T{t->d_lut1, t->d_lut2, t->d_meta, t->d_long, t->d_long_cnt, t->lut2_cap,
                          t->l1_bits, t->k, pqh_prio("DECODE", 3)};
-        if (t->context)
-            hipLaunchKernelGGL(dec_row8<true>, dim3(blocks), dim3(64), lds8, ctx->stream,
-                               reinterpret_cast<const uint32_t*>(d_stream), nwords, n, raw_first,
-                               chunk_vectors, d_chunk_offsets,
-                               static_cast<const unsigned long long*>(d_chunk_prev), T,
-                               static_cast<unsigned long long*>(d_codes), ctx->d_diag + 1, ww);
+        const uint32_t* wp = reinterpret_cast<const uint32_t*>(d_stream);
+        const unsigned long long* cp = static_cast<const unsigned long long*>(d_chunk_prev);
+        unsigned long long* op = static_cast<unsigned long long*>(d_codes);
+#define PQH_DEC_ROWS(CTX, NW, SB)                                                               \
+    do {                                                                                         \
+        if (lds_r > 64 * 1024)                                                                   \
+            PQH_HIP(ctx, hipFuncSetAttribute((const void*)(dec_rows<CTX, NW, SB>),               \
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,         \
+                                             (int)lds_r));                                       \
+        hipLaunchKernelGGL((dec_rows<CTX, NW, SB>), dim3(blocks), dim3(64), lds_r, ctx->stream,   \
+                           wp, nwords, n, raw_first, chunk_vectors, d_chunk_offsets, cp, T, op,  \
+                           ctx->d_diag + 1, ww);                                                 \
+    } while (0)
+        if (esz_b == 2)
+            PQH_DEC_ROWS(false, 2, 16);
+        else if (nw_row == 1 && t->context)
+            PQH_DEC_ROWS(true, 1, 8);
+        else if (nw_row == 1)
+            PQH_DEC_ROWS(false, 1, 8);
+        else if (t->context)
+            PQH_DEC_ROWS(true, 2, 8);
         else
-            hipLaunchKernelGGL(dec_row8<false>, dim3(blocks), dim3(64), lds8, ctx->stream,
-                               reinterpret_cast<const uint32_t*>(d_stream), nwords, n, raw_first,
-                               chunk_vectors, d_chunk_offsets, nullptr, T,
-                               static_cast<unsigned long long*>(d_codes), ctx->d_diag + 1, ww);
+            PQH_DEC_ROWS(false, 2, 8);
+#undef PQH_DEC_ROWS
         PQH_LAUNCH_CHECK(ctx);
         return PQH_OK;
     }

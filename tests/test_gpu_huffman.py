@@ -75,6 +75,24 @@ def test_histogram_set_overwrites(gpu, oracle, ctxm):
         assert np.array_equal(codec.counts_to_host(junk), want)
 
 
+@pytest.mark.parametrize("m", [4, 8, 12, 16])
+def test_context_histogram_part_counts_and_offsets(gpu, oracle, m):
+    """The context histogram's kernel forms: wave-contiguous rows for m % 4 == 0 (aligned),
+    per-thread runs otherwise; full and partial waves and chunks (n spans three 61,440-row
+    chunks), a sliced start row (unaligned for the wave form at m = 8), and the halo row."""
+    torch, codec, ctx = gpu
+    n = 130001
+    codes = datagen.skewed_codes(n, m, seed=11 + m)
+    cd = torch.from_numpy(np.ascontiguousarray(codes)).cuda().reshape(n, m)
+    got = codec.counts_to_host(codec.histogram(ctx, cd, 256, True))
+    assert np.array_equal(got, oracle.histogram(codes, 256, True))
+    for s in (1, 3, 64):   # rows [s, n) with row s - 1 as the halo
+        part = codec.histogram(ctx, cd[s:], 256, True, prev_row=cd[s - 1])
+        want = oracle.histogram(codes[s - 1:], 256, True)
+        want -= oracle.histogram(codes[s - 1:s], 256, True)   # (the raw row's own count: none)
+        assert np.array_equal(codec.counts_to_host(part), want), s
+
+
 @pytest.mark.parametrize("ctxm", [True, False])
 def test_histogram_vs_oracle_with_halo(gpu, oracle, ctxm):
     torch, codec, ctx = gpu
