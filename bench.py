@@ -72,6 +72,12 @@ def pmc_traffic(kernel, tag):
     return None, None, None
 
 
+def lib_shard_req(args, world):
+    """world > 1 through the C ABI's two-phase shard encode (bench's default there)"""
+    return world > 1 and args.shard_path == "library" and not args.sort and \
+        not (args.sched == "serial" or args.no_overlap)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -114,6 +120,13 @@ def parse():
                     default="default",
                     help="tree builder of the first batch on each table lane (the pipeline's "
                          "fill)")
+    ap.add_argument("--encode-after", choices=["tables", "trees"], default="tables",
+                    help="the encode waits for the batch's whole tables, or (trees) only for its "
+                         "Huffman trees when they completed the encode tables (group builder), "
+                         "running beside the decode-table build")
+    ap.add_argument("--astreams", type=int, default=1,
+                    help="assignment + histogram streams, batch i on stream i %% N (N > 1: the "
+                         "next batch's assignment grid fills the previous one's tail)")
     ap.add_argument("--hist-on", choices=["assign", "lanes"], default="assign",
                     help="stream of the context histogram: the assignment's, or the batch's "
                          "lane (before its code tables)")
@@ -361,6 +374,11 @@ def main():
                                                        for _ in range(args.elanes)]
     ne = len(elanes)
     pq = codec.PQ(ctx, cent)
+    # more assignment streams: each with its own context (histogram workspace) and PQ object
+    # (the assignment's work-queue state is per object, so launches may overlap)
+    na = 1 if serial or lib_shard_req(args, world) else max(1, args.astreams)
+    actx = [ctx] + [codec.Context(local, cus=1 << 20) for _ in range(na - 1)]
+    apq = [pq] + [codec.PQ(c, cent) for c in actx[1:]]
     items = k * k if ctxm else k
     # codes / counts buffers: the assignment runs up to `slots` batches ahead of the oldest
     # batch not yet encoded
@@ -376,6 +394,7 @@ def main():
     dl = max(1, min(args.lut_lag, nl * (1 if elanes is lanes else max(1, args.tbufs)) - 1)) \
         if lut_a else 0
     used = [False] * slots    # slot s has held a batch (its events were recorded)
+    early = [False] * slots   # batch in slot s: encode may start after its trees
     chunks = (n + args.chunk - 1) // args.chunk
     # code tables: one set per lane; two per table lane when encode/decode have streams of
     # their own, so a lane builds batch i + lanes's tables while batch i's are still read
@@ -488,12 +507,13 @@ def main():
         s, j = i % slots, lane_of(i)
         c = lanes[j]
         sL = c.stream
-        cF, sF = ctx, sA             # the stream of assignment + histogram
+        cF = actx[i % na]            # the stream of assignment + histogram
+        sF = cF.stream
         with torch.cuda.stream(sF):
             if used[s]:              # the slot's previous batch: encoded (codes[s] free) ...
                 sF.wait_event(ev_enc[s])
             e = rec("assign", sF)
-            pq.assign(x, codes[s], ctx=cF)
+            apq[i % na].assign(x, codes[s], ctx=cF)
             done(e, sF)
             if args.sort:            # stable strncmp-key sort of the batch's rows (in place)
                 e = rec("sort", sF)
@@ -554,7 +574,13 @@ def main():
                 done(e, sL)
                 ev_trees[s].record(sL)
             else:
-                tabs[ti].build(counts[s], c, trees=tr)
+                # trees, then the decode tables: with the group builder the encode tables
+                # are complete after the trees (encode_ready), so the encode stream waits
+                # for ev_trees only and runs beside the decode-table build
+                tabs[ti].build_trees(counts[s], c, trees=tr)
+                early[s] = args.encode_after == "trees" and tabs[ti].encode_ready()
+                ev_trees[s].record(sL)
+                tabs[ti].build_luts(c)
                 done(e, sL)
                 ev_tab[s].record(sL)
         if lut_a and i >= dl:
@@ -581,7 +607,7 @@ def main():
         tj = tabs[jt]
         with torch.cuda.stream(sL):
             if elanes is not lanes:
-                sL.wait_event(ev_tab[s])
+                sL.wait_event(ev_trees[s] if early[s] and not lib_shard else ev_tab[s])
             if halo[s] is not None:   # made on the table lane: keep it until this stream's use
                 halo[s].record_stream(sL)
             e = rec("encode", sL)
@@ -609,6 +635,8 @@ def main():
             done(e, sL)
             ev_enc[s].record(sL)
             enc = codec.Encoded(out[j], -1, args.chunk, coff[j], cprev[j], n, raw_first)
+            if elanes is not lanes and early[s] and not lib_shard:
+                sL.wait_event(ev_tab[s])   # the decode tables
             e = rec("decode", sL)
             codec.decode(c, tj, enc, out=dec[j])
             done(e, sL)
@@ -808,8 +836,9 @@ def main():
     torch.cuda.empty_cache()
     for t in tabs:
         t.close()
-    pq.close()
-    for c in {id(c): c for c in list(lanes) + list(elanes) + [ctx]}.values():
+    for q in apq:
+        q.close()
+    for c in {id(c): c for c in list(lanes) + list(elanes) + list(actx)}.values():
         c.close()
     if world > 1:
         dist.barrier()

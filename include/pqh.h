@@ -137,9 +137,16 @@ enum { PQH_TREES_DEFAULT = 0, PQH_TREES_LANE = 1, PQH_TREES_WAVE = 2, PQH_TREES_
 int pqh_tables_build_impl(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts, int which);
 /* The two halves of pqh_tables_build_impl, for callers that run them on different streams:
  * the Huffman trees (code table) on ctx's stream, then -- after the caller orders it behind
- * the trees (an event) -- the decode tables and the encoder's gather copy on ctx's stream. */
+ * the trees (an event) -- the decode tables and the encoder's gather copy on ctx's stream.
+ * With the K <= 256 group builder (PQH_TREES_GROUP, the default) the tree build writes the
+ * encoder's gather copy itself, so pqh_encode* may run as soon as pqh_tables_build_trees is
+ * done, concurrently with pqh_tables_build_luts (pqh_tables_encode_ready says which case
+ * holds); pqh_decode always needs pqh_tables_build_luts. */
 int pqh_tables_build_trees(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts, int which);
 int pqh_tables_build_luts(pqh_ctx_t* ctx, pqh_tables_t* t);
+/* 1 if the last pqh_tables_build_trees completed the encoder's tables (no LUT build needed
+ * before pqh_encode*), else 0. */
+int pqh_tables_encode_ready(const pqh_tables_t* t);
 /* Two table sets (same m, K <= 256, mode) built by one launch of the default K <= 256
  * build: twice the trees in one latency-bound pass, for a caller whose table builds are the
  * bound; then both sets' decode tables.  Same tables as two pqh_tables_build calls. */

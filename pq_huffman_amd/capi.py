@@ -130,6 +130,7 @@ SIGNATURES = [
     ("pqh_tables_alloc", I, [P, I, I, I, P]), ("pqh_tables_build", I, [P, P, P]),
     ("pqh_tables_build_impl", I, [P, P, P, I]),
     ("pqh_tables_build_trees", I, [P, P, P, I]), ("pqh_tables_build_luts", I, [P, P]),
+    ("pqh_tables_encode_ready", I, [P]),
     ("pqh_tables_build_pair", I, [P, P, P, P, P]),
     ("pqh_tables_upload", I, [P, P, P]), ("pqh_tables_status", I, [P, P]),
     ("pqh_tables_codebooks", I, [P, P, P]),

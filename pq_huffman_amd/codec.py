@@ -302,6 +302,11 @@ class Tables:
         check(lib().pqh_tables_build_luts(c.ptr, self.ptr), "pqh_tables_build_luts")
         return self
 
+    def encode_ready(self) -> bool:
+        """whether the last build_trees completed the encoder's tables (the group builder
+        writes the gather copy itself), so an encode need not wait for build_luts"""
+        return bool(lib().pqh_tables_encode_ready(self.ptr))
+
     def status(self) -> None:
         st = lib().pqh_tables_status(self.ctx.ptr, self.ptr)
         if st:

@@ -43,6 +43,9 @@ namespace {
 #ifndef PQH_ASSIGN_WPG
 #define PQH_ASSIGN_WPG 4
 #endif
+#ifndef PQH_ASSIGN_RING   // K = 4096: A-fragment tiles in flight from L2 (ring depth)
+#define PQH_ASSIGN_RING 4
+#endif
 #ifndef PQH_ASSIGN_NB
 #define PQH_ASSIGN_NB 2
 #endif
@@ -612,7 +615,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
             }
         } else {
             // A fragments from L2 into a ring of kRing tile sets, kRing - 1 tiles ahead of use
-            constexpr int kRing = 4;
+            constexpr int kRing = PQH_ASSIGN_RING;
             static_assert(KT % kRing == 0, "the ring unrolls the tile loop");
 #pragma unroll
             for (int b = 0; b < kNB; ++b) {

@@ -176,21 +176,23 @@ hist_ctx_w(const uint8_t* __restrict__ codes, long long n, int m_total, int k,
     const int lane = threadIdx.x & 63;
     constexpr int kR = kHistChunk / (BLK / 64);   // rows per wave
     static_assert(kR % (128 * G) == 0, "whole tile groups per wave");
-    const long long w0 = (long long)chunk * kHistChunk + (long long)(threadIdx.x >> 6) * kR;
-    const long long w1 = min(n, w0 + kR);
+    // (uniform values through readfirstlane: SGPR bases, 32-bit per-lane offsets)
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const long long w0 = (long long)chunk * kHistChunk + (long long)wv * kR;
+    const int cnt = (int)max(0ll, min(n - w0, (long long)kR));   // rows this wave counts
     unsigned carry = w0 > 0 ? (w0 - 1 < n ? (unsigned)codes[(w0 - 1) * m_total + m] : ~0u)
                             : (prev_row ? (unsigned)prev_row[m] : ~0u);
     carry = (unsigned)__builtin_amdgcn_readfirstlane((int)carry);
     const int sh = 8 * (m & 3);
     __syncthreads();   // the counters are zeroed
-    if (m_total == 8 && w1 - w0 == kR) {
+    if (m_total == 8 && cnt == kR) {
         // two 8-byte rows per lane: one 16-byte load covers rows 2l, 2l + 1 of a 128-row tile
-        const uint4* pr = reinterpret_cast<const uint4*>(codes) + w0 / 2 + lane;
+        const uint4* pr = reinterpret_cast<const uint4*>(codes + w0 * 8);
 #pragma unroll 1
         for (int t0 = 0; t0 < kR / 128; t0 += G) {
             uint4 v[G];
 #pragma unroll
-            for (int u = 0; u < G; ++u) v[u] = pr[(t0 + u) * 64];
+            for (int u = 0; u < G; ++u) v[u] = pr[(t0 + u) * 64 + lane];
 #pragma unroll
             for (int u = 0; u < G; ++u) {
                 const unsigned a = m < 4 ? v[u].x : v[u].y, b = m < 4 ? v[u].z : v[u].w;
@@ -200,23 +202,19 @@ hist_ctx_w(const uint8_t* __restrict__ codes, long long n, int m_total, int k,
                 carry = (unsigned)__builtin_amdgcn_readlane((int)cb, 63);
             }
         }
-    } else if (w1 > w0) {
+    } else if (cnt > 0) {
         // one row per lane: the dword of row r that holds part m (rows past the wave's range
         // clamp their load and count nothing)
         const int rw = m_total >> 2;
-        const uint32_t* c32 = reinterpret_cast<const uint32_t*>(codes) + (m >> 2);
+        const uint32_t* c32 = reinterpret_cast<const uint32_t*>(codes + w0 * m_total) + (m >> 2);
 #pragma unroll 1
-        for (long long r0 = w0; r0 < w1; r0 += 64 * 2 * G) {
+        for (int r0 = 0; r0 < cnt; r0 += 64 * 2 * G) {
             uint32_t v[2 * G];
 #pragma unroll
-            for (int u = 0; u < 2 * G; ++u) {
-                const long long r = min(r0 + u * 64 + lane, n - 1);
-                v[u] = c32[r * rw];
-            }
+            for (int u = 0; u < 2 * G; ++u) v[u] = c32[min(r0 + u * 64 + lane, cnt - 1) * rw];
 #pragma unroll
             for (int u = 0; u < 2 * G; ++u) {
-                const bool valid = r0 + u * 64 + lane < w1;
-                const unsigned c = valid ? (v[u] >> sh) & 0xFFu : ~0u;
+                const unsigned c = r0 + u * 64 + lane < cnt ? (v[u] >> sh) & 0xFFu : ~0u;
                 count(wave_shr1(c, carry), c);
                 carry = (unsigned)__builtin_amdgcn_readlane((int)c, 63);
             }
@@ -756,23 +754,33 @@ static int histogram_impl(pqh_ctx_t* ctx, const void* d_codes, long long n, int 
         const char* hb = std::getenv("PQH_HIST_BLOCK");
         // the wave-contiguous form for u8 codes with m % 4 == 0 (aligned rows; PQH_HIST_IMPL=
         // thread keeps the per-thread runs of hist_ctx)
-        static const bool thread_form = [] {
+        static const int form_env = [] {   // 1: thread, 2: wave (any m % 4 == 0), 0: default
             const char* e = std::getenv("PQH_HIST_IMPL");
-            return e && !std::strcmp(e, "thread");
+            return !e ? 0 : !std::strcmp(e, "thread") ? 1 : !std::strcmp(e, "wave") ? 2 : 0;
         }();
+        const bool thread_form = form_env == 1;
         const uintptr_t al = reinterpret_cast<uintptr_t>(d_codes);
-        // (m = 8 only: measured 0.027 vs 0.035 ms per 1M rows; at m = 16 the per-thread
-        // runs won, 0.108 vs 0.51 ms -- tools/bench_hist.py)
-        const bool wave_form = !thread_form && !(hb && std::atoi(hb) == 256) && m == 8 &&
-                               (al & 15u) == 0;
-        if (wave_form) {
+        // (measured alone, tools/bench_hist.py: 0.027 vs 0.035 ms per 1M rows at m = 8, 0.052
+        // vs 0.108 at m = 16; the Deep bench 1,300 vs 1,218 Mvec/s)
+        const bool slim = hb && std::atoi(hb) == 256;
+        const bool wave_form = !thread_form && m % 4 == 0 && (al & (m == 8 ? 15u : 3u)) == 0;
+        if (wave_form && slim) {
+            // 256 threads, <= 32 VGPRs: fits on a CU beside the assignment grid (one wave
+            // per SIMD, 64 KB of LDS beside its ~75 KB), for a histogram off stream A
+            PQH_HIP(ctx, hipFuncSetAttribute((const void*)hist_ctx_w<256, 3>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            hipLaunchKernelGGL((hist_ctx_w<256, 3>), dim3(grid), dim3(256), lds, ctx->stream,
+                               static_cast<const uint8_t*>(d_codes), n, m, k,
+                               static_cast<const uint8_t*>(d_prev_row), d_rawf, partial, split,
+                               (int)chunks, pqh_prio("HIST", 0));
+        } else if (wave_form) {
             PQH_HIP(ctx, hipFuncSetAttribute((const void*)hist_ctx_w<1024, 5>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
             hipLaunchKernelGGL((hist_ctx_w<1024, 5>), dim3(grid), dim3(1024), lds, ctx->stream,
                                static_cast<const uint8_t*>(d_codes), n, m, k,
                                static_cast<const uint8_t*>(d_prev_row), d_rawf, partial, split,
                                (int)chunks, pqh_prio("HIST", 0));
-        } else if (!(hb && std::atoi(hb) == 256)) {
+        } else if (!slim) {
             PQH_HIP(ctx, hipFuncSetAttribute((const void*)hist_ctx<uint8_t>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
             hipLaunchKernelGGL(hist_ctx<uint8_t>, dim3(grid), dim3(1024), lds, ctx->stream,

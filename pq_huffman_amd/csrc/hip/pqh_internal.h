@@ -119,6 +119,7 @@ struct pqh_tables {
     long long lut2_cap = 0;
     unsigned long long* d_enc = nullptr;
     uint32_t* d_enc32 = nullptr;     // [m][items] len << 26 | code (len <= 26), else ~0u
+    bool enc32_by_trees = false;     // the last tree build wrote d_enc32 (the LUT build skips it)
                                      // (escape: read d_enc) -- the encoder's gather table
     uint16_t* d_lut1 = nullptr;
     uint16_t* d_lut2 = nullptr;

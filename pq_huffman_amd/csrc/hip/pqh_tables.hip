@@ -866,19 +866,23 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(32)))
 huff_trees_grp(const uint32_t* __restrict__ counts, int k, long long trees,
                unsigned long long* __restrict__ enc, uint32_t* __restrict__ err,
                long long trees2, const uint32_t* __restrict__ counts2,
-               unsigned long long* __restrict__ enc2, uint32_t* __restrict__ err2, int prio) {
-    // trees [0, trees) from counts -> enc; a paired build adds [trees, trees + trees2)
+               unsigned long long* __restrict__ enc2, uint32_t* __restrict__ err2, int prio,
+               uint32_t* __restrict__ e32, uint32_t* __restrict__ e32_2) {
+    // trees [0, trees) from counts -> enc (and the encoder's u32 gather copy e32); a paired
+    // build adds [trees, trees + trees2)
     const long long blocks1 = (trees + kGrpTrees - 1) / kGrpTrees;
     if ((long long)blockIdx.x >= blocks1) {
         const long long b = (long long)blockIdx.x - blocks1;
         counts = counts2 + b * kGrpTrees * k;
         enc = enc2 + b * kGrpTrees * k;
+        e32 = e32_2 + b * kGrpTrees * k;
         err = err2;
         trees = trees2 - b * kGrpTrees;
     } else {
         trees -= (long long)blockIdx.x * kGrpTrees;
         counts += (long long)blockIdx.x * kGrpTrees * k;
         enc += (long long)blockIdx.x * kGrpTrees * k;
+        e32 += (long long)blockIdx.x * kGrpTrees * k;
     }
     __shared__ __attribute__((aligned(16))) char lds[kGrpTrees * kGrpTreeBytes];
     const int lane = threadIdx.x, grp = lane >> 4, gl = lane & 15, gsh = grp * 16;
@@ -971,6 +975,7 @@ huff_trees_grp(const uint32_t* __restrict__ counts, int k, long long trees,
     int grp2 = grp;
     asm volatile("" : "+v"(grp2));
     unsigned long long* out = enc + (long long)grp2 * k;
+    uint32_t* out32 = e32 + (long long)grp2 * k;
     bool too_long = false;
     for (int s = gl; s < k; s += 16) {
         unsigned long long e = 0;
@@ -982,6 +987,10 @@ huff_trees_grp(const uint32_t* __restrict__ counts, int k, long long trees,
             }
         }
         out[s] = e;
+        // the encoder's gather copy here too, so an encode may start before the decode
+        // tables (lut_grp / lut_build then skip it)
+        const unsigned len = (unsigned)(e >> 56);
+        out32[s] = len <= 26 ? (uint32_t)((len << 26) | (uint32_t)(e & ((1ull << 26) - 1))) : ~0u;
     }
     if (too_long) atomicOr(err, 1u);
     if (stamp) {
@@ -1084,7 +1093,8 @@ __device__ __forceinline__ void grp_luts(const GrpLut& L, long long t, int k, in
     for (int s = gl; s < k; s += 16) {
         const unsigned long long v = code[s];
         const int len = (int)(v >> 56);
-        L.enc32[t * k + s] = len <= 26 ? (uint32_t)(((unsigned long long)len << 26) | (v & kCodeMask)) : ~0u;
+        if (L.enc32)   // (null: the tree build wrote it)
+            L.enc32[t * k + s] = len <= 26 ? (uint32_t)(((unsigned long long)len << 26) | (v & kCodeMask)) : ~0u;
         if (!len) continue;
         const unsigned long long cbits = v & kCodeMask;
         if (len <= w1) {   // replicated over the 2^(W1 - len) patterns that start with it
@@ -1508,8 +1518,9 @@ lut_build(const unsigned long long* __restrict__ enc, uint32_t* __restrict__ enc
     for (int s = threadIdx.x; s < k; s += blockDim.x) {
         const unsigned long long v = e[s];
         const int len = (int)(v >> 56);
-        enc32[t * k + s] = len <= 26 ? (uint32_t)(((unsigned long long)len << 26) | (v & kCodeMask))
-                                     : ~0u;
+        if (enc32)   // (null: the tree build wrote it)
+            enc32[t * k + s] = len <= 26 ? (uint32_t)(((unsigned long long)len << 26) | (v & kCodeMask))
+                                         : ~0u;
         if (!len) continue;
         const unsigned long long code = v & kCodeMask;
         if (len <= w1) {
@@ -2102,7 +2113,7 @@ int pqh_tables_destroy(pqh_tables_t* t) {
 }
 
 static void launch_lut_grp(pqh_ctx* ctx, pqh_tables* t) {
-    const GrpLut lut{t->d_enc32, t->d_lut1, t->d_lut2, t->d_meta, t->d_long, t->d_long_cnt,
+    const GrpLut lut{t->enc32_by_trees ? nullptr : t->d_enc32, t->d_lut1, t->d_lut2, t->d_meta, t->d_long, t->d_long_cnt,
                      reinterpret_cast<unsigned long long*>(t->d_err + 2), t->lut2_cap,
                      t->l1_bits, t->l2_bits, pqh_prio("LUTS", 3)};
     hipLaunchKernelGGL(lut_grp, dim3((unsigned)((t->tables + kGrpTrees - 1) / kGrpTrees)), dim3(64),
@@ -2120,7 +2131,7 @@ static int launch_luts(pqh_ctx* ctx, pqh_tables* t) {
     }
     // (the pool head, d_err[2..3], was zeroed with the error word before the trees)
     hipLaunchKernelGGL(lut_build, dim3((unsigned)t->tables), dim3(256), 0, ctx->stream, t->d_enc,
-                       t->d_enc32, t->k, t->l1_bits, t->l2_bits, t->d_meta, t->d_lut1, t->d_lut2,
+                       t->enc32_by_trees ? nullptr : t->d_enc32, t->k, t->l1_bits, t->l2_bits, t->d_meta, t->d_lut1, t->d_lut2,
                        t->lut2_cap, t->d_long, t->d_long_cnt,
                        reinterpret_cast<unsigned long long*>(t->d_err + 2));
     PQH_LAUNCH_CHECK(ctx);
@@ -2172,6 +2183,8 @@ static int build_trees(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts
     PQH_HIP(ctx, hipMemsetAsync(t->d_err, 0, 16, ctx->stream));   // error word + LUT pool head
     if (t2) PQH_HIP(ctx, hipMemsetAsync(t2->d_err, 0, 16, ctx->stream));
     if (reinterpret_cast<uintptr_t>(d_counts) & 15u) return PQH_ERR_ARG;
+    t->enc32_by_trees = false;   // (set below by the builds that write the gather copy)
+    if (t2) t2->enc32_by_trees = false;
     const long long trees = t->tables;
     // Three builds of the same trees (K <= 256):
     //  * 16 lanes per tree, four trees per wavefront (huff_trees_grp, the default): two LDS
@@ -2197,8 +2210,11 @@ static int build_trees(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts
         hipLaunchKernelGGL(huff_trees_grp, dim3((unsigned)blocks), dim3(64), 0, ctx->stream, d_counts,
                            t->k, trees, t->d_enc, t->d_err, t2 ? t2->tables : 0ll,
                            t2 ? d_counts2 : d_counts, t2 ? t2->d_enc : t->d_enc,
-                           t2 ? t2->d_err : t->d_err, pqh_prio("TREES", 3));
+                           t2 ? t2->d_err : t->d_err, pqh_prio("TREES", 3), t->d_enc32,
+                           t2 ? t2->d_enc32 : t->d_enc32);
         PQH_LAUNCH_CHECK(ctx);
+        t->enc32_by_trees = true;
+        if (t2) t2->enc32_by_trees = true;
         return PQH_OK;
     }
     // (every build writes every entry, 0 for symbols that never occur: no memset)
@@ -2254,6 +2270,8 @@ int pqh_debug_tree_stamps(pqh_ctx_t* ctx, unsigned long long* out16) {
     return PQH_OK;
 }
 
+int pqh_tables_encode_ready(const pqh_tables_t* t) { return t && t->enc32_by_trees ? 1 : 0; }
+
 int pqh_tables_upload(pqh_ctx_t* ctx, pqh_tables_t* t, const huffman_codebook_t* cbs) {
     if (!ctx || !t || !cbs) return PQH_ERR_ARG;
     for (int i = 0; i < t->m; ++i)
@@ -2273,6 +2291,7 @@ int pqh_tables_upload(pqh_ctx_t* ctx, pqh_tables_t* t, const huffman_codebook_t*
         }
     PQH_HIP(ctx, hipMemsetAsync(t->d_err, 0, 16, ctx->stream));   // error word + LUT pool head
     PQH_HIP(ctx, hipMemcpyAsync(t->d_enc, h.data(), h.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+    t->enc32_by_trees = false;   // the LUT build writes the gather copy
     rc = launch_luts(ctx, t);
     if (rc) return rc;
     PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));  // h goes out of scope

@@ -285,6 +285,27 @@ def test_gpu_tree_builder_random_shapes(gpu, impl, monkeypatch):
     assert dev.codebooks().file_bytes() == host.file_bytes()
 
 
+@pytest.mark.parametrize("impl", ["grp", "lane"])
+def test_encode_after_trees_only(gpu, oracle, impl):
+    """The group tree build writes the encoder's gather copy itself (encode_ready): an encode
+    issued right after build_trees, before the decode tables, gives the one-shot stream; the
+    lane build does not claim it.  Then the decode tables decode that stream."""
+    torch, codec, ctx = gpu
+    codes = datagen.skewed_codes(20001, 8, seed=21)
+    cd = torch.from_numpy(codes).cuda()
+    counts = codec.histogram(ctx, cd, 256, True)
+    ref = codec.encode(ctx, codec.Tables(ctx, 8, 256, True).build(counts), cd, chunk_vectors=8)
+    t = codec.Tables(ctx, 8, 256, True).build_trees(counts, trees=impl)
+    assert t.encode_ready() == (impl == "grp")
+    if impl == "grp":
+        enc = codec.encode(ctx, t, cd, chunk_vectors=8)
+        assert codec.indices_file_bytes(enc) == codec.indices_file_bytes(ref)
+    t.build_luts()
+    assert not t.encode_ready() or impl == "grp"
+    dec = codec.decode(ctx, t, ref)
+    assert np.array_equal(dec.cpu().numpy(), codes)
+
+
 @pytest.mark.parametrize("luts", ["grp", "block"])
 def test_gpu_decode_tables_long_codes(gpu, luts, monkeypatch):
     """Context decode tables (lut_grp, the default, and lut_build, PQH_LUT_IMPL=block) for
