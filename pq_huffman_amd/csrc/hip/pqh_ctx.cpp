@@ -185,6 +185,8 @@ const char* pqh_status_string(int s) {
         case PQH_ERR_CORRUPT: return "corrupt stream";
         case PQH_ERR_NOMEM: return "out of memory";
         case PQH_ERR_CAPACITY: return "output buffer too small";
+        case PQH_ERR_REMOTE: return "another rank's part of the sharded call failed";
+        case PQH_ERR_COMM: return "a collective hook failed";
         default: return "unknown status";
     }
 }

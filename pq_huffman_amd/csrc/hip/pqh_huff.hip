@@ -469,7 +469,7 @@ __device__ __forceinline__ void gather_entries(const CodeT* __restrict__ codes, 
 // stamps of the mid-grid workgroup, read by pqh_debug_enc_stamps.)
 __device__ unsigned long long g_enc_stamps[8];
 
-template <typename CodeT, int MAXM, int BLK, bool ROW8 = false>
+template <typename CodeT, int MAXM, int BLK, bool ROW8 = false, int CS = 1>
 __global__ void __launch_bounds__(BLK)
 enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, int context,
             int raw_first, const CodeT* __restrict__ prev_row, const int* __restrict__ d_rawf,
@@ -484,6 +484,9 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
             unsigned long long* __restrict__ ticket, unsigned long long ticket_base,
             unsigned epoch, long long nb, unsigned long long* __restrict__ total_out,
             const uint16_t* __restrict__ tree_prev, int prio) {
+    // ROW8: n counts 8-byte rows of 8 u8 codes, CS of them per vector (m_total = 8 CS: a
+    // 16-part vector is two consecutive 8-part rows, which are also consecutive in the
+    // stream); a row's context row is CS rows back and its parts are (row % CS) * 8 + i
     extern __shared__ uint32_t img[];   // LDS image of this block's bit range
     pqh_set_prio(prio);
     __shared__ uint32_t wsum[BLK / 64];
@@ -513,30 +516,34 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
             static_assert(MAXM == 8 && sizeof(CodeT) == 1, "8-byte rows");
             const unsigned long long* r8 = reinterpret_cast<const unsigned long long*>(codes);
             const unsigned long long row = r8[v];
+            const unsigned half = (unsigned)(v % CS);   // (CS = 1: 0)
             unsigned long long prow = 0;
             bool raw = false;
             if (context) {
-                if (v > 0) {
-                    prow = r8[v - 1];
+                if (v >= CS) {
+                    prow = r8[v - CS];
                 } else if (!raw_first && prev_row) {
 #pragma unroll
-                    for (int i = 0; i < 8; ++i) prow |= (unsigned long long)prev_row[i] << (8 * i);
+                    for (int i = 0; i < 8; ++i)
+                        prow |= (unsigned long long)prev_row[half * 8 + i] << (8 * i);
                 } else {
                     raw = true;   // row 0 raw, 8 bits per part (huffman_encoder.c:234)
                 }
             }
+            const unsigned ibase = half * 8u * (unsigned)items;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 const unsigned cur = (unsigned)(row >> (8 * i)) & 0xFFu;
                 const unsigned prv = (unsigned)(prow >> (8 * i)) & 0xFFu;
                 const bool ok = cur < (unsigned)k && (!context || prv < (unsigned)k);
-                const unsigned idx = (unsigned)i * (unsigned)items + (context ? prv * (unsigned)k + cur : cur);
+                const unsigned idx = ibase + (unsigned)i * (unsigned)items + (context ? prv * (unsigned)k + cur : cur);
                 ent[i] = raw ? ((8u << 26) | cur) : ok ? enc32[idx] : 0u;
             }
 #pragma unroll
             for (int i = 0; i < 8; ++i)
                 bits += ent[i] != ~0u ? ent[i] >> 26
-                                      : (uint32_t)(sym_entry(codes, v, i, 8, k, context, raw_first,
+                                      : (uint32_t)(sym_entry(codes, v / CS, (int)half * 8 + i,
+                                                             8 * CS, k, context, raw_first,
                                                              prev_row, enc, items, nullptr) >> 56);
         } else if constexpr (MAXM > 0) {
             gather_entries<CodeT, MAXM>(codes, v, m_total, k, context, raw_first, prev_row,
@@ -614,17 +621,20 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
 
     unsigned long long pos = bs + before + incl - bits;
     if (v < n) {
-        if (chunk_vectors > 0 && v % chunk_vectors == 0) {
-            const long long j = v / chunk_vectors;
+        const long long vv = ROW8 ? v / CS : v;   // the vector
+        if (chunk_vectors > 0 && (!ROW8 || v % CS == 0) && vv % chunk_vectors == 0) {
+            const long long j = vv / chunk_vectors;
             chunk_off[j] = pos;
             if (context && chunk_prev) {
-                if (ROW8 && v > 0)   // (chunk_prev rows are 8 bytes: aligned)
-                    reinterpret_cast<unsigned long long*>(chunk_prev)[j] =
-                        reinterpret_cast<const unsigned long long*>(codes)[v - 1];
-                else
+                if (ROW8 && vv > 0) {   // (chunk_prev rows are 8 CS bytes: aligned)
+                    for (int q = 0; q < CS; ++q)
+                        reinterpret_cast<unsigned long long*>(chunk_prev)[j * CS + q] =
+                            reinterpret_cast<const unsigned long long*>(codes)[v - CS + q];
+                } else {
                     for (int i = 0; i < m_total; ++i)
                         chunk_prev[j * m_total + i] =
-                            v > 0 ? codes[(v - 1) * m_total + i] : (prev_row ? prev_row[i] : (CodeT)0);
+                            vv > 0 ? codes[(vv - 1) * m_total + i] : (prev_row ? prev_row[i] : (CodeT)0);
+                }
             }
         }
         // assemble this vector's bits in registers: words wholly inside its range are
@@ -664,7 +674,10 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
             for (int i = 0; i < MAXM; ++i) {   // length 0 past m_total
                 if (ent[i] != ~0u) {
                     if (ent[i] >> 26) append(ent[i] & ((1u << 26) - 1), (int)(ent[i] >> 26));
-                } else {   // a code longer than 26 bits: its u64 entry
+                } else if (ROW8) {   // a code longer than 26 bits: its u64 entry
+                    put(sym_entry(codes, v / CS, (int)(v % CS) * 8 + i, 8 * CS, k, context,
+                                  raw_first, prev_row, enc, items, nullptr));
+                } else {
                     put(sym_entry(codes, v, i, m_total, k, context, raw_first, prev_row, enc,
                                   items, tree_prev));
                 }
@@ -887,11 +900,18 @@ static int encode_write_impl(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* 
         if (d_total_bits) PQH_HIP(ctx, hipMemsetAsync(d_total_bits, 0, 8, ctx->stream));
         return PQH_OK;
     }
-    // m <= 8: 256-vector workgroups (one wave per SIMD, <= 32 VGPRs), which fit on a CU beside
-    // the assignment grid's waves; wider rows: 512
-    const int blk = t->m <= 8 ? 256 : kEncBlock;
-    const long long nb = (n + blk - 1) / blk;
-    const size_t lds = ((size_t)blk * t->m * kMaxCodeLen / 32 + 4) * 4;
+    // 8-byte rows: m = 8 (one row per vector) or m = 16 (two rows per vector), u8 codes,
+    // aligned, no tree order: the <= 32-VGPR row encoder on 256 rows per workgroup, which fits
+    // on a CU beside the assignment grid's waves; other shapes the generic encoder (m <= 8:
+    // 256 vectors per workgroup, wider rows 512)
+    const bool row8 = t->k <= 256 && (t->m == 8 || t->m == 16) && !tree_prev &&
+                      !(reinterpret_cast<uintptr_t>(d_codes) & 7) &&
+                      !(reinterpret_cast<uintptr_t>(d_chunk_prev) & 7);
+    const int cs = row8 ? t->m / 8 : 1;
+    const long long rows = n * cs;
+    const int blk = row8 || t->m <= 8 ? 256 : kEncBlock;
+    const long long nb = (rows + blk - 1) / blk;
+    const size_t lds = ((size_t)blk * (row8 ? 8 : t->m) * kMaxCodeLen / 32 + 4) * 4;
     if (lds > 160 * 1024) return PQH_ERR_UNSUPPORTED;
     // look-back state: grow-only, epoch-tagged so it never needs clearing between calls
     if (nb > ctx->lb_cap) {
@@ -915,15 +935,15 @@ static int encode_write_impl(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* 
     unsigned long long* total = d_total_bits ? d_total_bits : ctx->d_diag + 3;
     uint32_t* words = reinterpret_cast<uint32_t*>(d_out);
     const int enc_prio = pqh_prio("ENCODE", 0);
-#define PQH_ENC(T, MAXM, R8)                                                                      \
+#define PQH_ENC(T, MAXM, R8, CS)                                                                  \
     do {                                                                                          \
         constexpr int B = MAXM > 0 && MAXM <= 8 ? 256 : kEncBlock;                                \
         if (lds > 64 * 1024)                                                                      \
-            PQH_HIP(ctx, hipFuncSetAttribute((const void*)(enc_onepass<T, MAXM, B, R8>),          \
+            PQH_HIP(ctx, hipFuncSetAttribute((const void*)(enc_onepass<T, MAXM, B, R8, CS>),      \
                                              hipFuncAttributeMaxDynamicSharedMemorySize,          \
                                              (int)lds));                                          \
-        hipLaunchKernelGGL((enc_onepass<T, MAXM, B, R8>), dim3((unsigned)nb), dim3(B), lds,       \
-                           ctx->stream, static_cast<const T*>(d_codes), n, t->m, t->k,            \
+        hipLaunchKernelGGL((enc_onepass<T, MAXM, B, R8, CS>), dim3((unsigned)nb), dim3(B), lds,   \
+                           ctx->stream, static_cast<const T*>(d_codes), R8 ? rows : n, t->m, t->k, \
                            t->context, raw_first, static_cast<const T*>(d_prev_row), d_rawf,     \
                            t->d_enc,                                                              \
                            t->d_enc32, t->items, bit_offset, d_bit_offset, words,                 \
@@ -933,17 +953,15 @@ static int encode_write_impl(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* 
                            (unsigned)ctx->lb_epoch, nb, total, tree_prev, enc_prio);              \
     } while (0)
     if (t->k <= 256) {
-        // 8-byte rows (m = 8, aligned codes, no tree order): one load per row
-        if (t->m == 8 && !tree_prev && !(reinterpret_cast<uintptr_t>(d_codes) & 7) &&
-            !(reinterpret_cast<uintptr_t>(d_chunk_prev) & 7))
-            PQH_ENC(uint8_t, 8, true);
-        else if (t->m <= 8) PQH_ENC(uint8_t, 8, false);
-        else if (t->m <= 16) PQH_ENC(uint8_t, 16, false);
-        else PQH_ENC(uint8_t, 0, false);
+        if (row8 && cs == 2) PQH_ENC(uint8_t, 8, true, 2);
+        else if (row8) PQH_ENC(uint8_t, 8, true, 1);
+        else if (t->m <= 8) PQH_ENC(uint8_t, 8, false, 1);
+        else if (t->m <= 16) PQH_ENC(uint8_t, 16, false, 1);
+        else PQH_ENC(uint8_t, 0, false, 1);
     } else {
-        if (t->m <= 8) PQH_ENC(uint16_t, 8, false);
-        else if (t->m <= 16) PQH_ENC(uint16_t, 16, false);
-        else PQH_ENC(uint16_t, 0, false);
+        if (t->m <= 8) PQH_ENC(uint16_t, 8, false, 1);
+        else if (t->m <= 16) PQH_ENC(uint16_t, 16, false, 1);
+        else PQH_ENC(uint16_t, 0, false, 1);
     }
 #undef PQH_ENC
     PQH_LAUNCH_CHECK(ctx);
