@@ -120,6 +120,12 @@ def parse():
                     default="default",
                     help="tree builder of the first batch on each table lane (the pipeline's "
                          "fill)")
+    ap.add_argument("--stage-events", choices=["after", "timed"], default="after",
+                    help="per-stage HIP events other than the assignment's: recorded in extra "
+                         "untimed steps after the timed region (default: an event record is a "
+                         "packet on its stream, +2-3 %% when all ride in the timed steps), or "
+                         "inside the timed steps; the assignment's (the roofline kernel) are "
+                         "always recorded in the timed steps")
     ap.add_argument("--encode-after", choices=["tables", "trees"], default="tables",
                     help="the encode waits for the batch's whole tables, or (trees) only for its "
                          "Huffman trees when they completed the encode tables (group builder), "
@@ -440,7 +446,10 @@ def main():
     ev_pool = []         # timing events made before the timed region (not while issuing)
 
     def rec(name, stream):
-        if not state["timed"]:
+        # the assignment's events over the timed steps (the roofline's kernel time), the other
+        # stages' over the timed steps too (--stage-events timed) or the untimed ones after
+        timed_ev = state["timed"] and (name == "assign" or args.stage_events == "timed")
+        if not (timed_ev or (state.get("after") and name != "assign")):
             return None
         e0, e1 = ev_pool.pop() if ev_pool else (torch.cuda.Event(enable_timing=True),
                                                 torch.cuda.Event(enable_timing=True))
@@ -683,8 +692,22 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     state["timed"] = False
+    if args.stage_events == "after":
+        # the other stages' events, in untimed steps of the same schedule (an event record is
+        # a packet on its stream: inside the timed steps they would cost stream time)
+        ev_pool.extend((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                       for _ in range(max(args.steps, 20) * len(stages)))
+        state["after"] = True
+        run(max(args.steps, 20))
+        barrier()
+        state["after"] = False   # (the checks below use the last batch of these steps)
+    nev = {s: 0 for s in acc}
     for name, e0, e1 in events:
         acc[name] += e0.elapsed_time(e1) / 1e3
+        nev[name] += 1
+    for name in acc:   # per-batch averages over the recorded launches
+        if name != "collectives" and nev[name]:
+            acc[name] *= args.steps / nev[name]
     if args.timeline and rank == 0 and events:
         f0 = events[0][1]
         for i, (name, e0, e1) in enumerate(events):
@@ -797,7 +820,9 @@ def main():
                                             if prof_avg_us is not None else None)},
             "stages_ms": {s: round(v / args.steps * 1e3, 4) for s, v in acc.items()
                           if (s != "sort" or args.sort) and (s != "lut" or lut_a)},
-            "stages_note": ("per-stage HIP-event times on their own streams" +
+            "stages_note": ("per-stage HIP-event times on their own streams (the assignment's "
+                            "over the timed steps, the others over untimed steps of the same "
+                            "schedule after them, --stage-events)" +
                             ("" if serial else "; the stages of consecutive batches run "
                              "concurrently, so they sum to more than ms_per_step")),
             # encode-side HBM-read roofline = 512 B/vec x N / t_encode / 8 TB/s, with
