@@ -120,6 +120,9 @@ def parse():
                     default="default",
                     help="tree builder of the first batch on each table lane (the pipeline's "
                          "fill)")
+    ap.add_argument("--hist-split", choices=["on", "off"], default="on",
+                    help="context histogram in two halves: the per-chunk partial counts on the "
+                         "assignment stream, their reduce on the batch's table lane")
     ap.add_argument("--stage-events", choices=["after", "timed"], default="after",
                     help="per-stage HIP events other than the assignment's: recorded in extra "
                          "untimed steps after the timed region (default: an event record is a "
@@ -462,17 +465,32 @@ def main():
             e1.record(stream)
 
     hist_on_lane = args.hist_on == "lanes" and not serial
+    # the split histogram: partial counts per slot (the assignment stream writes slot s's while
+    # a lane may still reduce another's)
+    hist_split = args.hist_split == "on" and ctxm and not serial and not hist_on_lane and \
+        not lib_shard and code_t == torch.uint8
+    hparts = [torch.empty(codec.histogram_partial_bytes(n, m, k), dtype=torch.uint8, device=dev)
+              for _ in range(slots)] if hist_split else None
     parts = torch.arange(m, device=dev)
     ones_m = torch.ones(m, dtype=torch.int32, device=dev)
 
     def hist(s, c, st):
-        """batch s's symbol histogram on stream st (context c)"""
+        """batch s's symbol histogram on stream st (context c); with hist_split only its
+        partial counts (the lane reduces them, hist_reduce)"""
         if used[s]:                  # the slot's previous batch: tables built (counts free)
             st.wait_event(ev_tab[s])
         e = rec("hist", st)
-        codec.histogram(c, codes[s], k, ctxm, prev_row=halo[s], counts=counts[s],
-                        accumulate=False)            # overwrites: no zeroing pass
+        if hist_split:
+            codec.histogram_partial(c, codes[s], k, hparts[s], prev_row=halo[s])
+        else:
+            codec.histogram(c, codes[s], k, ctxm, prev_row=halo[s], counts=counts[s],
+                            accumulate=False)        # overwrites: no zeroing pass
         done(e, st)
+
+    def hist_reduce(s, c):
+        """the second half of batch s's split histogram, on the current (lane) stream"""
+        if hist_split:
+            codec.histogram_reduce(c, hparts[s], n, m, k, counts[s])
 
     def reduce(s):
         """batch s's histogram all-reduce, issued on the current stream (a table lane): RCCL
@@ -534,6 +552,7 @@ def main():
             ev_hist[s].record(sF)
         with torch.cuda.stream(sL):
             sL.wait_event(ev_hist[s])
+            hist_reduce(s, c)
             # the one-row halo all-gather on the lane too, so the assignment stream never
             # waits for RCCL; the pair (previous shard's last row, first row) is one more
             # count per part, exactly what pqh_histogram's prev_row adds

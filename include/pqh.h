@@ -113,6 +113,16 @@ int pqh_histogram(pqh_ctx_t* ctx, const void* d_codes, long long n, int m, int k
 /* counts = histogram of codes (overwrites; no zeroing by the caller).  Same arguments. */
 int pqh_histogram_set(pqh_ctx_t* ctx, const void* d_codes, long long n, int m, int k,
                       int context, const void* d_prev_row, uint32_t* d_counts);
+/* The context histogram in two halves, for a pipelined caller that keeps the short first
+ * half on its critical stream and moves the reduce to another (ordered by an event): the
+ * per-chunk partial counts of the (prev, cur) pairs into d_partials (device,
+ * pqh_histogram_partial_bytes(n, m, k) bytes, K <= 256), then counts (+)= their sum
+ * (set != 0: overwrite).  Same pairs as pqh_histogram with context = 1. */
+long long pqh_histogram_partial_bytes(long long n, int m, int k);
+int pqh_histogram_partial(pqh_ctx_t* ctx, const void* d_codes, long long n, int m, int k,
+                          const void* d_prev_row, void* d_partials);
+int pqh_histogram_reduce(pqh_ctx_t* ctx, const void* d_partials, long long n, int m, int k,
+                         uint32_t* d_counts, int set);
 
 /* ---- code tables ------------------------------------------------------------------ */
 /* Device-resident Huffman code tables of m parts: encode entries + decode lookup tables. */

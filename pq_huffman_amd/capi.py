@@ -126,6 +126,9 @@ SIGNATURES = [
     ("pqh_kmeans_train", I, [P, P, LL, LL, I, I, I, I, P]),
     ("pqh_histogram", I, [P, P, LL, I, I, I, P, P]),
     ("pqh_histogram_set", I, [P, P, LL, I, I, I, P, P]),
+    ("pqh_histogram_partial_bytes", LL, [LL, I, I]),
+    ("pqh_histogram_partial", I, [P, P, LL, I, I, P, P]),
+    ("pqh_histogram_reduce", I, [P, P, LL, I, I, P, I]),
     ("pqh_tables_create", I, [P, P, I, P]), ("pqh_tables_destroy", I, [P]),
     ("pqh_tables_alloc", I, [P, I, I, I, P]), ("pqh_tables_build", I, [P, P, P]),
     ("pqh_tables_build_impl", I, [P, P, P, I]),

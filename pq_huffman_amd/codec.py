@@ -348,6 +348,27 @@ def histogram(ctx: Context, codes, k: int, context: bool, prev_row=None, counts=
     return counts
 
 
+def histogram_partial_bytes(n: int, m: int, k: int) -> int:
+    return int(lib().pqh_histogram_partial_bytes(n, m, k))
+
+
+def histogram_partial(ctx: Context, codes, k: int, partials, prev_row=None):
+    """First half of the context histogram: per-chunk partial pair counts into `partials`
+    (a device byte buffer of histogram_partial_bytes(n, m, k)); pqh_histogram_partial."""
+    n, m = codes.shape
+    check(lib().pqh_histogram_partial(ctx.ptr, _ptr(codes), n, m, k, _ptr(prev_row),
+                                      _ptr(partials)), "pqh_histogram_partial")
+    return partials
+
+
+def histogram_reduce(ctx: Context, partials, n: int, m: int, k: int, counts,
+                     accumulate: bool = False):
+    """Second half: counts (+)= the sum of the partials (pqh_histogram_reduce)."""
+    check(lib().pqh_histogram_reduce(ctx.ptr, _ptr(partials), n, m, k, _ptr(counts),
+                                     0 if accumulate else 1), "pqh_histogram_reduce")
+    return counts
+
+
 def sort_rows(ctx: Context, codes, tmp=None):
     """In-place stable sort of uint8 code rows in strncmp order -- the reference encoder's
     default mode (huffman_encoder.c:301-317).  `tmp`: optional n*m byte device scratch."""

@@ -735,15 +735,21 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
 
 extern "C" {
 
+// phase: 0 = partials + reduce (pqh_histogram*), 1 = the context partials only, into
+// d_partials (pqh_histogram_partial), 2 = the reduce of d_partials only (pqh_histogram_reduce)
 static int histogram_impl(pqh_ctx_t* ctx, const void* d_codes, long long n, int m, int k,
                           int context, const void* d_prev_row, uint32_t* d_counts, int set,
-                          const int* d_rawf = nullptr) {
-    if (!ctx || m <= 0 || k <= 0 || n < 0 || !d_counts || (n > 0 && !d_codes)) return PQH_ERR_ARG;
+                          const int* d_rawf = nullptr, int phase = 0,
+                          uint32_t* d_partials = nullptr) {
+    if (!ctx || m <= 0 || k <= 0 || n < 0) return PQH_ERR_ARG;
+    if (phase != 1 && !d_counts) return PQH_ERR_ARG;
+    if (phase != 2 && n > 0 && !d_codes) return PQH_ERR_ARG;
+    if (phase && (!context || !d_partials)) return PQH_ERR_ARG;
     if (context && k > 256) return PQH_ERR_UNSUPPORTED;
     int rc = pqh_use_device(ctx);
     if (rc) return rc;
     const long long items = context ? (long long)k * k : k;
-    if (set && (n == 0 || !context))   // the plain kernel and an empty input only add
+    if (set && (n == 0 || !context) && phase != 1)   // the plain kernel and an empty input only add
         PQH_HIP(ctx, hipMemsetAsync(d_counts, 0, (size_t)m * items * 4, ctx->stream));
     if (n == 0) return PQH_OK;
     if (context) {
@@ -757,9 +763,19 @@ static int histogram_impl(pqh_ctx_t* ctx, const void* d_codes, long long n, int 
         }();
         const int split = k % (2 * split_env) == 0 ? split_env : (k % 4 == 0 ? 2 : 1);
         const size_t lds = (size_t)(split == 1 ? words : (k / split) * k / 2) * 4;
-        rc = pqh_ensure_ws(ctx, (size_t)m * chunks * words * 4);
-        if (rc) return rc;
-        uint32_t* partial = static_cast<uint32_t*>(ctx->ws);
+        uint32_t* partial = d_partials;
+        if (!partial) {
+            rc = pqh_ensure_ws(ctx, (size_t)m * chunks * words * 4);
+            if (rc) return rc;
+            partial = static_cast<uint32_t*>(ctx->ws);
+        }
+        if (phase == 2) {
+            hipLaunchKernelGGL(hist_ctx_reduce, dim3((unsigned)((words + 255) / 256), m), dim3(256),
+                               0, ctx->stream, partial, (int)chunks, words, (long long)k * k,
+                               d_counts, set);
+            PQH_LAUNCH_CHECK(ctx);
+            return PQH_OK;
+        }
         const unsigned grid = 8u * ((chunks + 7u) / 8u) * (unsigned)(m * split);
         // 1024-thread workgroups; PQH_HIST_BLOCK=256: 256 threads with <= 32 VGPRs, which fit
         // beside the assignment grid (measured: histogram 0.19 vs 0.075 ms in the bench -- a
@@ -809,9 +825,10 @@ static int histogram_impl(pqh_ctx_t* ctx, const void* d_codes, long long n, int 
                                (int)chunks, pqh_prio("HIST", 0));
         }
         PQH_LAUNCH_CHECK(ctx);
-        hipLaunchKernelGGL(hist_ctx_reduce, dim3((unsigned)((words + 255) / 256), m), dim3(256), 0,
-                           ctx->stream, partial, (int)chunks, words, (long long)k * k, d_counts,
-                           set);
+        if (phase == 0)
+            hipLaunchKernelGGL(hist_ctx_reduce, dim3((unsigned)((words + 255) / 256), m), dim3(256),
+                               0, ctx->stream, partial, (int)chunks, words, (long long)k * k,
+                               d_counts, set);
     } else {
         const unsigned blocks = (unsigned)std::min<long long>((n + 4095) / 4096, 512);
         if (k <= 256)
@@ -823,6 +840,24 @@ static int histogram_impl(pqh_ctx_t* ctx, const void* d_codes, long long n, int 
     }
     PQH_LAUNCH_CHECK(ctx);
     return PQH_OK;
+}
+
+long long pqh_histogram_partial_bytes(long long n, int m, int k) {
+    if (n < 0 || m <= 0 || k <= 0 || k > 256) return -1;
+    const long long chunks = (n + kHistChunk - 1) / kHistChunk;
+    return (long long)m * chunks * ((k * k + 1) / 2) * 4;
+}
+
+int pqh_histogram_partial(pqh_ctx_t* ctx, const void* d_codes, long long n, int m, int k,
+                          const void* d_prev_row, void* d_partials) {
+    return histogram_impl(ctx, d_codes, n, m, k, 1, d_prev_row, nullptr, 0, nullptr, 1,
+                          static_cast<uint32_t*>(d_partials));
+}
+
+int pqh_histogram_reduce(pqh_ctx_t* ctx, const void* d_partials, long long n, int m, int k,
+                         uint32_t* d_counts, int set) {
+    return histogram_impl(ctx, nullptr, n, m, k, 1, nullptr, d_counts, set ? 1 : 0, nullptr, 2,
+                          static_cast<uint32_t*>(const_cast<void*>(d_partials)));
 }
 
 int pqh_histogram(pqh_ctx_t* ctx, const void* d_codes, long long n, int m, int k, int context,

@@ -93,6 +93,27 @@ def test_context_histogram_part_counts_and_offsets(gpu, oracle, m):
         assert np.array_equal(codec.counts_to_host(part), want), s
 
 
+@pytest.mark.parametrize("m", [8, 16])
+def test_histogram_partial_then_reduce(gpu, oracle, m):
+    """pqh_histogram_partial + pqh_histogram_reduce (the bench's split histogram) == the
+    one-call context histogram: set and accumulate, with and without the halo row, n = 0."""
+    torch, codec, ctx = gpu
+    n = 130001
+    codes = datagen.skewed_codes(n, m, seed=71 + m)
+    cd = torch.from_numpy(np.ascontiguousarray(codes)).cuda()
+    parts = torch.empty(codec.histogram_partial_bytes(n, m, 256), dtype=torch.uint8, device="cuda")
+    junk = torch.full((m, 65536), 777, dtype=torch.int32, device="cuda")
+    codec.histogram_partial(ctx, cd, 256, parts)
+    codec.histogram_reduce(ctx, parts, n, m, 256, junk)
+    whole = codec.counts_to_host(junk)
+    assert np.array_equal(whole, oracle.histogram(codes, 256, True))
+    codec.histogram_partial(ctx, cd[1:], 256, parts, prev_row=cd[0])
+    codec.histogram_reduce(ctx, parts, n - 1, m, 256, junk, accumulate=True)
+    assert np.array_equal(codec.counts_to_host(junk), 2 * whole)
+    codec.histogram_reduce(ctx, parts, 0, m, 256, junk)   # n = 0 with set: zeros
+    assert not codec.counts_to_host(junk).any()
+
+
 @pytest.mark.parametrize("ctxm", [True, False])
 def test_histogram_vs_oracle_with_halo(gpu, oracle, ctxm):
     torch, codec, ctx = gpu
