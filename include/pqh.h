@@ -157,9 +157,10 @@ int pqh_tables_build_luts(pqh_ctx_t* ctx, pqh_tables_t* t);
 /* 1 if the last pqh_tables_build_trees completed the encoder's tables (no LUT build needed
  * before pqh_encode*), else 0. */
 int pqh_tables_encode_ready(const pqh_tables_t* t);
-/* Two table sets (same m, K <= 256, mode) built by one launch of the default K <= 256
- * build: twice the trees in one latency-bound pass, for a caller whose table builds are the
- * bound; then both sets' decode tables.  Same tables as two pqh_tables_build calls. */
+/* Two table sets (same m, K, mode) built by one launch of the default tree build (K <= 256:
+ * the group builder, K > 256: one wavefront per tree): twice the trees in one latency-bound
+ * pass, for a caller whose table builds are the bound; then both sets' decode tables.  Same
+ * tables as two pqh_tables_build calls. */
 int pqh_tables_build_pair(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts,
                           pqh_tables_t* t2, const uint32_t* d_counts2);
 /* Load codes from m host codebooks (e.g. huffman_codebooks.bin read by huffman_codebook_load). */

@@ -1312,7 +1312,16 @@ struct ParHeap {
 template <int KMAX>
 __global__ void __launch_bounds__(64)
 huff_trees_par(const uint32_t* __restrict__ counts, int k, long long trees,
-               unsigned long long* __restrict__ enc, uint32_t* __restrict__ err) {
+               unsigned long long* __restrict__ enc, uint32_t* __restrict__ err,
+               const uint32_t* __restrict__ counts2, unsigned long long* __restrict__ enc2,
+               uint32_t* __restrict__ err2) {
+    // trees [0, trees) from counts -> enc; a paired build (pqh_tables_build_pair) continues
+    // with the second table set's trees at workgroups trees, trees + 1, ...
+    if ((long long)blockIdx.x >= trees) {
+        counts = counts2 - trees * k;
+        enc = enc2 - trees * k;
+        err = err2;
+    }
     using Key = ParHeap::Key;
     extern __shared__ __attribute__((aligned(16))) char lds[];
     Key* heap = reinterpret_cast<Key*>(lds);                              // [KMAX + 1]
@@ -1321,8 +1330,7 @@ huff_trees_par(const uint32_t* __restrict__ counts, int k, long long trees,
     uint16_t* lsym = reinterpret_cast<uint16_t*>(kid + KMAX);            // [KMAX]
     uint16_t* par = lsym + KMAX;                                         // [2 KMAX]
     const int lane = threadIdx.x;
-    const long long tree = blockIdx.x;
-    if (tree >= trees) return;
+    const long long tree = blockIdx.x;   // (a paired build's grid covers both sets exactly)
     const uint32_t* cnt = counts + tree * k;
     unsigned long long* out = enc + tree * k;
     const bool stamp = tree == 0 && lane == 0;
@@ -2158,7 +2166,7 @@ int pqh_tables_build_pair(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_cou
                           pqh_tables_t* t2, const uint32_t* d_counts2) {
     if (!t || !t2 || t == t2 || !d_counts2 || t2->k != t->k || t2->m != t->m ||
         t2->context != t->context || !t2->ctx || t2->ctx->device != t->ctx->device ||
-        t->k > 256 || (reinterpret_cast<uintptr_t>(d_counts2) & 15u))
+        (reinterpret_cast<uintptr_t>(d_counts2) & 15u))
         return PQH_ERR_ARG;
     int rc = build_trees(ctx, t, d_counts, PQH_TREES_DEFAULT, t2, d_counts2);
     if (!rc) rc = launch_luts(ctx, t);
@@ -2248,9 +2256,12 @@ static int build_trees(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts
         const size_t lds = (size_t)(4096 + 1) * 8 + (size_t)4096 * (16 + 4 + 2 + 4);
         PQH_HIP(ctx, hipFuncSetAttribute((const void*)huff_trees_par<4096>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL((huff_trees_par<4096>), dim3((unsigned)trees), dim3(64), lds, ctx->stream,
-                           d_counts, t->k, trees, t->d_enc, t->d_err);
+        const long long all = trees + (t2 ? t2->tables : 0);
+        hipLaunchKernelGGL((huff_trees_par<4096>), dim3((unsigned)all), dim3(64), lds, ctx->stream,
+                           d_counts, t->k, trees, t->d_enc, t->d_err, t2 ? d_counts2 : d_counts,
+                           t2 ? t2->d_enc : t->d_enc, t2 ? t2->d_err : t->d_err);
     } else {   // (PQH_TREE_IMPL=lane: one lane per tree through LDS)
+        if (t2) return pqh_set_error(ctx, PQH_ERR_UNSUPPORTED, "paired K > 256 build: lane builder");
         constexpr int TPW = 1;
         const size_t lds = (size_t)4096 * TPW * (16 + 4 + 4 + 2);
         PQH_HIP(ctx, hipFuncSetAttribute((const void*)huff_trees<4096, TPW>,

@@ -392,6 +392,25 @@ def test_gpu_tree_builder_pair(gpu, ctxm):
     codec.decode_status(ctx)
 
 
+def test_gpu_tree_builder_pair_k4096(gpu):
+    """pqh_tables_build_pair at K = 4096 (one huff_trees_par launch over both sets' 16 trees):
+    each set == its host codebooks, and each set's decode tables decode its stream."""
+    torch, codec, ctx = gpu
+    k = 4096
+    codes = datagen.skewed_codes(30000, 8, k=k, seed=83)
+    cd = torch.from_numpy(codes.view(np.int16)).cuda()
+    c1 = codec.histogram(ctx, cd, k, False)
+    c2 = c1 * 3 + (c1 > 0).to(c1.dtype)
+    t1, t2 = codec.Tables(ctx, 8, k, False), codec.Tables(ctx, 8, k, False)
+    t1.build_pair(c1, t2, c2)
+    for t, c in ((t1, c1), (t2, c2)):
+        t.status()
+        host = codec.Codebooks(c.cpu().numpy().astype(np.float64), k, False)
+        assert t.codebooks().file_bytes() == host.file_bytes()
+        enc = codec.encode(ctx, t, cd, chunk_vectors=8)
+        assert torch.equal(codec.decode(ctx, t, enc), cd)
+
+
 @pytest.mark.parametrize("ctxm", [True, False])
 @pytest.mark.parametrize("impl", ["grp", "lane", "wave"])
 def test_gpu_tree_builder_heavy_and_rebuilt(gpu, ctxm, impl, monkeypatch):
