@@ -811,11 +811,16 @@ def main():
                        "mode": "ctx" if ctxm else "noctx",
                        "chunk_vectors": args.chunk, "parallelism": f"dp{world} row shards",
                        "schedule": ("serial" if serial else
-                                    f"lanes: assignment + histogram of every batch on one stream; "
-                                    f"batch i's code tables, encode and decode on lane stream "
-                                    f"i % {nl}, beside the assignment of the next batches; "
-                                    "every timed step runs all five stages and the pipeline "
-                                    "fills and drains inside the timed region")},
+                                    "lanes: assignment + histogram " +
+                                    ("partial counts " if hist_split else "") +
+                                    "of every batch on one stream; batch i's " +
+                                    ("histogram reduce and " if hist_split else "") +
+                                    f"code tables on table lane i % {nl}" +
+                                    ("" if elanes is lanes else
+                                     f", its encode and decode on {ne} stream(s) of their own") +
+                                    ", beside the assignment of the next batches; every timed "
+                                    "step runs all five stages and the pipeline fills and "
+                                    "drains inside the timed region")},
             "roofline": {"kernel": akern,
                          # `bound`: the roofline the fraction is taken against (the contract's
                          # HBM read roofline); `measured_limiter`: what the PMC counters show
