@@ -606,7 +606,9 @@ def main():
                 # are complete after the trees (encode_ready), so the encode stream waits
                 # for ev_trees only and runs beside the decode-table build
                 tabs[ti].build_trees(counts[s], c, trees=tr)
-                early[s] = args.encode_after == "trees" and tabs[ti].encode_ready()
+                # (the run's last batch always: its encode is on the drain's critical path)
+                early[s] = (args.encode_after == "trees" or i == state["nsteps"] - 1) and \
+                    tabs[ti].encode_ready()
                 ev_trees[s].record(sL)
                 tabs[ti].build_luts(c)
                 done(e, sL)
