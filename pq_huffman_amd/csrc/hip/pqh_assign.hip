@@ -43,6 +43,9 @@ namespace {
 #ifndef PQH_ASSIGN_WPG
 #define PQH_ASSIGN_WPG 4
 #endif
+#ifndef PQH_ASSIGN_OCC_LARGE   // K = 4096: waves per SIMD
+#define PQH_ASSIGN_OCC_LARGE 2
+#endif
 #ifndef PQH_ASSIGN_RING   // K = 4096: A-fragment tiles in flight from L2 (ring depth)
 #define PQH_ASSIGN_RING 4
 #endif
@@ -397,7 +400,7 @@ __device__ __forceinline__ int tile_row(int t, int i, int h) {
 // streamed from L2 a few tiles ahead, no fused histogram)
 // (dsub 32 and K = 4096 hold more live state per wave: two waves per SIMD, no spills)
 template <int D, int KT, typename CodeT>
-__global__ void __launch_bounds__(64 * kWavesPerWG, (D == 32 || KT > 8) ? 2 : PQH_ASSIGN_OCC)
+__global__ void __launch_bounds__(64 * kWavesPerWG, D == 32 ? 2 : KT > 8 ? PQH_ASSIGN_OCC_LARGE : PQH_ASSIGN_OCC)
 pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_total,
                const bf16x8* __restrict__ afrag, const float* __restrict__ cnorm,
                const float* __restrict__ cent,
