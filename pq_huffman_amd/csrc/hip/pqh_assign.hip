@@ -121,6 +121,22 @@ __device__ __forceinline__ unsigned anchor_min(unsigned a, unsigned b, float nin
     return __float_as_uint(__builtin_amdgcn_fmed3f(__uint_as_float(a), __uint_as_float(b), ninf));
 }
 
+// a 32-bit constant in a VGPR the compiler cannot see into (so (x & mask) | s stays one
+// v_and_or_b32 with the mask in a register instead of a literal and + an add)
+__device__ __forceinline__ unsigned opaque_u32(unsigned v) {
+    unsigned r;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "i"(v));
+    return r;
+}
+
+// a wave-uniform value in an SGPR the compiler cannot split into SGPR + constant (so a
+// key's index goes into one v_and_or_b32, not an and + an or3 with an inline constant)
+__device__ __forceinline__ unsigned opaque_s32(int v) {
+    unsigned r;
+    asm("s_mov_b32 %0, %1" : "=s"(r) : "s"(v));
+    return r;
+}
+
 __device__ __forceinline__ float opaque_ninf() {
     float r;
     asm volatile("v_mov_b32 %0, 0xff800000" : "=v"(r));
@@ -177,6 +193,16 @@ __device__ __forceinline__ float exact_dist(const float* x, const float* c) {
 // {s_memrealtime at start, at end, blocks done | s_memtime lifetime << 16, XCC id}
 constexpr int kStampWaves = 8192;
 __device__ unsigned long long g_assign_stamps[kStampWaves][4];
+// re-rank phases per wave (PQH_ASSIGN_STAMPS): ticks {x rows arrived, screening, candidate
+// rounds} summed over the wave's batches, and the rounds
+__device__ unsigned long long g_assign_rr[kStampWaves][4];
+#ifdef PQH_ASSIGN_STAMPS
+#define PQH_RR_STAMP(var)                                                \
+    do {                                                                 \
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");      \
+        var = __builtin_amdgcn_s_memrealtime();                          \
+    } while (0)
+#endif
 
 // ---- screening steps shared by pq_assign_mfma and pq_rerank_window: a deferred vector is
 // re-screened by the same instruction sequence, so its scores are bitwise the same.
@@ -441,7 +467,11 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     const int bx = inter ? (L / (8 * m_total)) * 8 + (L & 7) : L % gx;
     const int r = lane & 31;
     const int h = lane >> 5;
-    pqh_set_prio(prio);   // (pqh_prio "ASSIGN": against the kernels running beside it)
+    // prio: bits 0-1 the wave priority against the kernels running beside it (pqh_prio
+    // "ASSIGN"), bits 2-3 the priority of a re-rank batch ("ASSIGN_RR"; 0 = the same)
+    const int rr_prio = (prio >> 2) & 3;
+    prio &= 3;
+    pqh_set_prio(prio);
     if (L == 0 && wave == 0) {   // the next launch's queue heads and re-rank counter
         // (agent-scope stores: written through to where the next launch's atomics act)
         if (sched_next)
@@ -464,15 +494,22 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     // where the A fragments come from: the LDS copy, or this subspace's slice in global
     const uint4* const asrc =
         kLdsA ? As : reinterpret_cast<const uint4*>(afrag) + (long long)m * P::PA * KT * 64;
+    // (K = 4096: the subspace's fragments as a buffer; built from wave-uniform values)
+    const auto arsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint4*>(reinterpret_cast<const uint4*>(afrag) + (long long)m * P::PA * KT * 64),
+        0, P::PA * KT * 64 * 16, 0x00020000);
 #ifdef PQH_ASSIGN_STAMPS
     const unsigned long long st0 = __builtin_amdgcn_s_memtime();
     const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
     unsigned long long nbdone = 0, rr_ticks = 0, rr_batches = 0;
+    unsigned long long rr_x = 0, rr_scr = 0, rr_cand = 0, rr_rounds = 0;
 #endif
     const float cm = cmax[m];
     const float sc = sqrt_cmax[m];
     const TauCoef tq = tau_coef(cm, sc);
     const float ninf = opaque_ninf();
+    // the P-key mask: an inline constant for 4 index bits, a register for 8
+    const unsigned keymask = PB == 4 ? ~PMASK : opaque_u32(~PMASK);
     const float* cl = cent + (long long)m * K * D;   // fp32 centroids (L2-resident, 16 KB)
     const long long nblk = (n + 31) / 32;
     unsigned long long slow_count = 0;
@@ -559,8 +596,20 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
 #ifdef PQH_ASSIGN_KTNOMEM   // diagnostic: every tile re-reads tile t % 4 (cache hits)
             if constexpr (!kLdsA) t &= 3;
 #endif
+            if constexpr (kLdsA) {
 #pragma unroll
-            for (int p = 0; p < P::PA; ++p) a[p] = frag_at<KT>(asrc, p, t, lane);
+                for (int p = 0; p < P::PA; ++p) a[p] = frag_at<KT>(asrc, p, t, lane);
+            } else {
+                // buffer loads: the tile's offset in a scalar register, the lane's constant
+                // (no per-tile 64-bit address arithmetic on the VALU)
+#pragma unroll
+                for (int p = 0; p < P::PA; ++p) {
+                    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+                    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(
+                        arsrc, (int)((p * KT * 64 + lane) * 16), t * 1024, 0);
+                    a[p] = __builtin_bit_cast(bf16x8, v);
+                }
+            }
         };
         // first: the tile that starts the running minima (compile-time in the unrolled
         // K = 256 loop; the streamed K = 4096 loop starts them at +inf instead)
@@ -573,11 +622,11 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
             // (e0, e1: the compiler-generated first reads of the tile's results, see min3d)
             const unsigned e0 = anchor_min(a[6], a[7], ninf), e1 = anchor_min(a[14], a[15], ninf);
             const unsigned k0 =
-                (min3u(min3d(a[0], a[1], a[2], e0), min3d(a[3], a[4], a[5], e0), e0) & ~PMASK) |
+                (min3u(min3d(a[0], a[1], a[2], e0), min3d(a[3], a[4], a[5], e0), e0) & keymask) |
                 (unsigned)(2 * t);
             const unsigned k1 =
-                (min3u(min3d(a[8], a[9], a[10], e1), min3d(a[11], a[12], a[13], e1), e1) & ~PMASK) |
-                (unsigned)(2 * t + 1);
+                (min3u(min3d(a[8], a[9], a[10], e1), min3d(a[11], a[12], a[13], e1), e1) & keymask) |
+                (PB == 4 ? (unsigned)(2 * t + 1) : opaque_s32(2 * t + 1));
             if (first) {
                 pm1[b] = minu(k0, k1);
                 pm2[b] = maxu(k0, k1);
@@ -637,13 +686,15 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
 #pragma unroll
                 for (int u = 0; u < kRing; ++u) {
                     const int t = t0 + u;
-                    if (t + kRing - 1 < KT) load_a(t + kRing - 1, ar[(u + kRing - 1) % kRing]);
-                    if (t + 1 < KT) cn = tile_norms(Cn, t + 1, h);
+                    // unconditional: past the last tile the ring wraps to tiles 0, 1, ...
+                    // whose scores are never reduced (a conditional load or MFMA made the
+                    // compiler copy the accumulators at every ring turn)
+                    load_a((t + kRing - 1) & (KT - 1), ar[(u + kRing - 1) % kRing]);
+                    cn = tile_norms(Cn, (t + 1) & (KT - 1), h);
 #pragma unroll
                     for (int b = 0; b < kNB; ++b) {
                         reduce(acc[b], t, b, false);
-                        if (t + 1 < KT)
-                            acc[b] = tile_scores_a<D>(ar[(u + 1) % kRing], Bm[b], Bl[b], LO, cn);
+                        acc[b] = tile_scores_a<D>(ar[(u + 1) % kRing], Bm[b], Bl[b], LO, cn);
                         __builtin_amdgcn_sched_barrier(0);
                     }
                 }
@@ -848,6 +899,10 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     // One batch of queued vectors (lane r: entry r; invalid lanes idle): re-screen, collect
     // the candidates at or below the entry's threshold, evaluate them exactly (see the tail).
     auto rerank32 = [&](const uint2 ent, const bool valid) {
+        // A batch is latency: with the issue going to the oldest wave first, a batch run
+        // beside two waves' main loops took 3-8x its time alone -- and a batch begun near
+        // the end of the grid is what the last waves wait for.
+        if (rr_prio) pqh_set_prio(rr_prio);
 #ifdef PQH_ASSIGN_STAMPS
         const unsigned long long rr0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -873,6 +928,12 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         bool lo;
         float xh[XD], xl[XD];
         split_x<D>(xs, X, lo, xh, xl);
+#ifdef PQH_ASSIGN_STAMPS
+        unsigned long long rr1, rr2, rr3;
+        asm volatile("" ::"v"(X), "v"(xh[0]));
+        PQH_RR_STAMP(rr1);
+        rr_x += rr1 - rr0;
+#endif
         bf16x8 Bm[P::PM];
         bf16x8 Bl[P::PL];
         build_b<D>(xh, xl, h, Bm, Bl);
@@ -900,6 +961,11 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
 #pragma unroll
                 for (int w = 0; w < (kGT + 1) / 2; ++w) cw[w] |= w == (u >> 1) ? bits : 0u;
             }
+#ifdef PQH_ASSIGN_STAMPS
+            asm volatile("" ::"v"(cw[0]));
+            PQH_RR_STAMP(rr2);
+            rr_scr += rr2 - rr1;
+#endif
             for (;;) {
                 int kc[kCand];
                 bool hc[kCand];
@@ -918,6 +984,9 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
                     }
                 }
                 if (!__any(hc[0])) break;
+#ifdef PQH_ASSIGN_STAMPS
+                ++rr_rounds;
+#endif
                 float cr[kCand][D];   // (lanes without a candidate read row 0)
 #pragma unroll
                 for (int c = 0; c < kCand; ++c) {
@@ -940,6 +1009,12 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
                     if (hc[c] && (dd < best || (dd == best && k < bidx))) { best = dd; bidx = k; }
                 }
             }
+#ifdef PQH_ASSIGN_STAMPS
+            asm volatile("" ::"v"(best));
+            PQH_RR_STAMP(rr3);
+            rr_cand += rr3 - rr2;
+            rr1 = rr3;
+#endif
         }
         const float ob = __uint_as_float(partner32(__float_as_uint(best)));
         const int oi = (int)partner32((unsigned)bidx);
@@ -953,6 +1028,10 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         rr_ticks += __builtin_amdgcn_s_memrealtime() - rr0;
         ++rr_batches;
 #endif
+        if (rr_prio) {
+            __builtin_amdgcn_s_setprio(0);
+            pqh_set_prio(prio);
+        }
     };
     long long ch = wave_id;
     float xn[kNB][XD];
@@ -1007,6 +1086,10 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     {
         const unsigned gw = (unsigned)((m * gx + bx) * kWavesPerWG + wave);
         if (lane == 0 && gw < (unsigned)kStampWaves) {
+            g_assign_rr[gw][0] = rr_x;
+            g_assign_rr[gw][1] = rr_scr;
+            g_assign_rr[gw][2] = rr_cand;
+            g_assign_rr[gw][3] = rr_rounds;
             g_assign_stamps[gw][0] = rt0;   // 100 MHz, chip-wide
             g_assign_stamps[gw][1] = __builtin_amdgcn_s_memrealtime();
             g_assign_stamps[gw][2] = nbdone | ((__builtin_amdgcn_s_memtime() - st0) << 16);
@@ -1201,7 +1284,7 @@ int launch_mfma(pqh_ctx* ctx, pqh_pq* pq, const float* x, long long n, long long
 #else
     uint32_t* sched = pq->m <= kSchedMax ? ctx->d_sched + ring * kSchedSet : nullptr;
 #endif
-    const int prio = pqh_prio("ASSIGN", 0);
+    const int prio = pqh_prio("ASSIGN", 0) | (pqh_prio("ASSIGN_RR", 0) << 2);
     // grid = the workgroups that are resident at once (persistent, grid-stride over the
     // 32-vector blocks): more would only queue behind the first wave of workgroups
 #define PQH_CASE(DD) PQH_CASE_KT(DD, 8)
@@ -1354,16 +1437,25 @@ int pqh_pq_assign(pqh_ctx_t* ctx, const pqh_pq_t* cpq, const float* d_x, long lo
         PQH_HIP(ctx, hipMemsetAsync(ctx->d_diag + 6, 0, sizeof(unsigned long long), ctx->stream));
     }
     if (n == 0) return PQH_OK;
+    // the MFMA kernel queues re-rank rows as 32-bit indices: at most 2^30 rows a launch
+    constexpr long long kLaunchRows = 1ll << 30;
+    auto pieces = [&](auto* c, uint32_t* counts) {
+        for (long long off = 0; off < n; off += kLaunchRows) {
+            const int r = launch_mfma(ctx, pq, d_x + off * ld_x, std::min(kLaunchRows, n - off),
+                                      ld_x, c + off * pq->m, counts);
+            if (r) return r;
+        }
+        return (int)PQH_OK;
+    };
     if (pq->k <= 256) {
         uint8_t* c = static_cast<uint8_t*>(d_codes);
-        return mfma ? launch_mfma(ctx, pq, d_x, n, ld_x, c, d_counts)
-                    : launch_exact(ctx, pq, d_x, n, ld_x, c, d_counts);
+        return mfma ? pieces(c, d_counts) : launch_exact(ctx, pq, d_x, n, ld_x, c, d_counts);
     }
     uint16_t* c16 = static_cast<uint16_t*>(d_codes);
     if (!mfma) return launch_exact(ctx, pq, d_x, n, ld_x, c16, d_counts);
     // K = 4096: the screening kernel keeps no per-workgroup histogram (16 KB of counters per
     // wave); the requested counts come from the histogram kernel over the codes just written
-    rc = launch_mfma(ctx, pq, d_x, n, ld_x, c16, nullptr);
+    rc = pieces(c16, nullptr);
     if (rc || !d_counts) return rc;
     return pqh_histogram(ctx, d_codes, n, pq->m, pq->k, 0, nullptr, d_counts);
 }
@@ -1375,6 +1467,15 @@ int pqh_debug_assign_stamps(pqh_ctx_t* ctx, unsigned long long* out, int max_wav
     PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
     const int w = std::min(max_waves, kStampWaves);
     PQH_HIP(ctx, hipMemcpyFromSymbol(out, HIP_SYMBOL(g_assign_stamps), (size_t)w * 4 * 8));
+    return PQH_OK;
+}
+
+// diagnostics: the per-wave re-rank phase sums of the last launch (PQH_ASSIGN_STAMPS builds)
+int pqh_debug_assign_rr(pqh_ctx_t* ctx, unsigned long long* out, int max_waves) {
+    if (!ctx || !out || max_waves <= 0) return PQH_ERR_ARG;
+    PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    const int w = std::min(max_waves, kStampWaves);
+    PQH_HIP(ctx, hipMemcpyFromSymbol(out, HIP_SYMBOL(g_assign_rr), (size_t)w * 4 * 8));
     return PQH_OK;
 }
 

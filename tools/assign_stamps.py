@@ -27,7 +27,14 @@ def main():
     buf = (ctypes.c_ulonglong * (W * 4))()
     lib().pqh_debug_assign_stamps(ctx.ptr, buf, W)
     a = np.frombuffer(buf, dtype=np.uint64).reshape(W, 4).astype(np.int64)
+    rbuf = (ctypes.c_ulonglong * (W * 4))()
+    lib().pqh_debug_assign_rr(ctx.ptr, rbuf, W)
+    rr = np.frombuffer(rbuf, dtype=np.uint64).reshape(W, 4).astype(np.int64)
+    idx = np.nonzero(a[:, 1] > 0)[0]
+    rr = rr[a[:, 1] > 0]
     a = a[a[:, 1] > 0]
+    wps = int(os.environ.get("STAMPS_WAVES_PER_SUBSPACE", 384))   # gx * 4 (gx = 96 on 256 CUs)
+    sub = idx // wps
     t0 = a[:, 0].min()
     st, en, nb, xcc = a[:, 0] - t0, a[:, 1] - t0, a[:, 2] & 0xFFFF, a[:, 3] & 15
     loop_end = st + ((a[:, 3] >> 8) & 0xFFFFFF)   # the chunk loop's end (the tail after it)
@@ -47,6 +54,18 @@ def main():
             print(f"xcc {c}: waves {sel.sum()} blocks {nb[sel].sum()} start p50/max {int(np.median(st[sel]))}/"
                   f"{st[sel].max()} end p5/p50/max {int(np.percentile(en[sel], 5))}/{int(np.median(en[sel]))}/"
                   f"{en[sel].max()}")
+    nbat = np.maximum((a[:, 3] >> 56) & 0xFF, 1)
+    for name, v in (("rr_x/batch", rr[:, 0] // nbat), ("rr_screen/batch", rr[:, 1] // nbat),
+                    ("rr_cand/batch", rr[:, 2] // nbat), ("rr_rounds/batch", rr[:, 3] / nbat)):
+        q = np.percentile(v, [0, 5, 25, 50, 75, 95, 100]).round(1)
+        print(f"{name:16s} p0/5/25/50/75/95/100: {list(q)}")
+    for c in range(m):
+        sel = sub == c
+        if sel.any():
+            print(f"subspace {c}: waves {sel.sum()} blocks {nb[sel].sum()} loopend p50/max "
+                  f"{int(np.median(loop_end[sel]))}/{loop_end[sel].max()} end p50/p95/max "
+                  f"{int(np.median(en[sel]))}/{int(np.percentile(en[sel], 95))}/{en[sel].max()} "
+                  f"rr_batches {rr_n[sel].sum()}")
     print("clock GHz (cycles / life):", round(float(np.median(cyc / np.maximum(life, 1))) / 10, 3))
     print("ticks per block (median life/blocks):", int(np.median(life / np.maximum(nb, 1))))
 
