@@ -1244,6 +1244,18 @@ struct ParHeap {
     Key* h;     // slots [0, cap]; slot cap and every slot >= size hold kMaxKey
     int cap;
     int size;
+    // pop's lane constants for subtree position q = lane: its ancestors in the stretch (bit p
+    // for position p) and, among them, those whose path to q takes the right child
+    unsigned long long anc = 0, dir = 0;
+    __device__ __forceinline__ void init_masks(int lane) {
+        const int q = lane;
+        const int d = q ? 31 - __clz(q) : 0;
+        for (int j = 0; j < d; ++j) {
+            const int p = q >> (j + 1);
+            anc |= 1ull << p;
+            if ((q >> j) & 1) dir |= 1ull << p;
+        }
+    }
     __device__ __forceinline__ void push(Key e, int lane) {
         const int i = size++;
         const int anc = ((i + 1) >> (lane + 1)) - 1;   // lane l: ancestor l + 1 (-1: none)
@@ -1282,27 +1294,23 @@ struct ParHeap {
             if (c0 + 1 == size) kr = kMaxKey;
             const Key kc = kl < (kr | kTie) ? kl : (kr | kTie);
             const bool mv = q >= 1 && kc < lw;
-            const int ch = 2 * q + ((kc & kTie) ? 1 : 0);
-            const int packed = mv ? (256 | ch) : 0;
-            // reached: every ancestor of q in the stretch moved toward q (independent
-            // shuffles instead of a serial chase)
-            int pa[6];
-#pragma unroll
-            for (int j = 0; j < 6; ++j) pa[j] = __shfl(packed, q >> (j + 1));
-            asm volatile("" : "+v"(pa[0]), "+v"(pa[1]), "+v"(pa[2]), "+v"(pa[3]), "+v"(pa[4]),
-                         "+v"(pa[5]));   // all six shuffles in flight together
-            bool reached = q >= 1;
-#pragma unroll
-            for (int j = 0; j < 6; ++j) reached &= (j >= d) | (pa[j] == (256 | (q >> j)));
+            // reached: every ancestor of q in the stretch moved toward q -- from two wave
+            // ballots (who moves, who took the right child) and the lane's constant masks of
+            // its ancestors (anc) and of the directions towards it (dir): no LDS round trip
+            const unsigned long long M = __ballot(mv);
+            const unsigned long long Rt = __ballot((kc & kTie) != 0);
+            const bool reached = q >= 1 && (anc & (~M | (Rt ^ dir))) == 0ull;
             if (reached && mv) h[g] = kc & ~kTie;   // the candidates move up one level
             const unsigned long long stop = __ballot(reached && !mv);
             if (stop) {                              // `last` settles where the path ends
                 if (reached && !mv) h[g] = last;
                 break;
             }
-            // the path left the stretch below its depth-5 position: continue there
+            // the path left the stretch below its depth-5 position: continue there (at the
+            // chosen child of the one reached depth-5 lane that moved)
             const unsigned long long deep = __ballot(reached && mv && q >= 32);
-            const int pq = __builtin_amdgcn_readlane(packed, __ffsll((long long)deep) - 1) & 255;
+            const int qd = __ffsll((long long)deep) - 1;
+            const int pq = 2 * qd + (int)((Rt >> qd) & 1ull);
             i = ((i + 1) << 6) + (pq - 64) - 1;
         }
         return top;
@@ -1354,6 +1362,7 @@ huff_trees_par(const uint32_t* __restrict__ counts, int k, long long trees,
     }
     if (nz == 0) return;
     ParHeap hp{heap, KMAX, 0};
+    hp.init_masks(lane);
     constexpr Key kNode = ParHeap::kTie - 1;
     if (stamp) g_tree_stamps[1] = __builtin_amdgcn_s_memtime();
     for (int j = 0; j < nz; ++j) hp.push((ncode[j] << 16) | (Key)j, lane);
