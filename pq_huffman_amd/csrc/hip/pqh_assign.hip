@@ -467,11 +467,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     const int bx = inter ? (L / (8 * m_total)) * 8 + (L & 7) : L % gx;
     const int r = lane & 31;
     const int h = lane >> 5;
-    // prio: bits 0-1 the wave priority against the kernels running beside it (pqh_prio
-    // "ASSIGN"), bits 2-3 the priority of a re-rank batch ("ASSIGN_RR"; 0 = the same)
-    const int rr_prio = (prio >> 2) & 3;
-    prio &= 3;
-    pqh_set_prio(prio);
+    pqh_set_prio(prio);   // (pqh_prio "ASSIGN": against the kernels running beside it)
     if (L == 0 && wave == 0) {   // the next launch's queue heads and re-rank counter
         // (agent-scope stores: written through to where the next launch's atomics act)
         if (sched_next)
@@ -592,6 +588,9 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         // and only the 24 group minima get index bits (the winner's P-group in the low 4
         // bits, its Q-group as row bits in the low 4).
         unsigned pm1[kNB], pm2[kNB], qg[kNB][8];
+        // streamed K = 4096: the P-groups span tile pairs and the Q-groups split by tile
+        // parity (reduce_pair): qh = the odd tiles' Q minima, pp = the even tile's P minima
+        unsigned qh[kNB][8], pp[kNB][2];
         auto load_a = [&](int t, bf16x8* a) {
 #ifdef PQH_ASSIGN_KTNOMEM   // diagnostic: every tile re-reads tile t % 4 (cache hits)
             if constexpr (!kLdsA) t &= 3;
@@ -642,6 +641,38 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
                 qg[b][j] = first ? min3d(a[j], a[j + 8], a[j + 8], e1)
                                  : min3d(qg[b][j], a[j], a[j + 8], e1);
         };
+        // Streamed K = 4096, tiles 2s and 2s + 1 (par = t & 1): P-group (s, g) = registers
+        // [8g, 8g + 8) of BOTH tiles (16 cells, one key and one top-two fold per pair of
+        // tiles), Q-group (j, par) = registers j and j + 8 of the tiles of parity par; a P-
+        // and a Q-group still share exactly one cell (tile 2s + par, register j + 8g).  The
+        // even tile's two half minima wait in pp for the odd tile: 40 VALU per tile pair
+        // instead of 44.
+        auto reduce_pair = [&](const f32x16& acc, int t, int b, int par) {
+            unsigned a[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) a[i] = __float_as_uint(acc[i]);
+            const unsigned e0 = anchor_min(a[6], a[7], ninf), e1 = anchor_min(a[14], a[15], ninf);
+            if (par == 0) {
+                pp[b][0] = min3u(min3d(a[0], a[1], a[2], e0), min3d(a[3], a[4], a[5], e0), e0);
+                pp[b][1] = min3u(min3d(a[8], a[9], a[10], e1), min3d(a[11], a[12], a[13], e1), e1);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) qg[b][j] = min3d(qg[b][j], a[j], a[j + 8], e1);
+            } else {
+                const unsigned w0 =
+                    minu(min3u(pp[b][0], min3d(a[0], a[1], a[2], e0), min3d(a[3], a[4], a[5], e0)), e0);
+                const unsigned w1 =
+                    minu(min3u(pp[b][1], min3d(a[8], a[9], a[10], e1), min3d(a[11], a[12], a[13], e1)), e1);
+                // P index 2s + g = t - 1 + g (7 bits)
+                const unsigned k0 = (w0 & keymask) | opaque_s32(t - 1);
+                const unsigned k1 = (w1 & keymask) | opaque_s32(t);
+                pm2[b] = med3u(pm1[b], pm2[b], k0);
+                pm1[b] = minu(pm1[b], k0);
+                pm2[b] = med3u(pm1[b], pm2[b], k1);
+                pm1[b] = minu(pm1[b], k1);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) qh[b][j] = min3d(qh[b][j], a[j], a[j + 8], e1);
+            }
+        };
         // Software pipeline over the tiles: block b's MFMA chain for tile t + 1 is issued
         // right after its tile-t keys are reduced, so it runs while the other block's keys
         // are (the scheduling barriers keep the compiler from sinking the chain behind them).
@@ -673,8 +704,9 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
             for (int b = 0; b < kNB; ++b) {
                 pm1[b] = pm2[b] = 0x7F800000u;   // +inf: any key is smaller
 #pragma unroll
-                for (int j = 0; j < 8; ++j) qg[b][j] = 0x7F800000u;
+                for (int j = 0; j < 8; ++j) qg[b][j] = qh[b][j] = 0x7F800000u;
             }
+            static_assert(kRing % 2 == 0, "tile pairs within a ring turn");
             bf16x8 ar[kRing][P::PA];
 #pragma unroll
             for (int u = 0; u < kRing - 1; ++u) load_a(u, ar[u]);
@@ -693,7 +725,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
                     cn = tile_norms(Cn, (t + 1) & (KT - 1), h);
 #pragma unroll
                     for (int b = 0; b < kNB; ++b) {
-                        reduce(acc[b], t, b, false);
+                        reduce_pair(acc[b], t, b, u & 1);
                         acc[b] = tile_scores_a<D>(ar[(u + 1) % kRing], Bm[b], Bl[b], LO, cn);
                         __builtin_amdgcn_sched_barrier(0);
                     }
@@ -705,15 +737,35 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         unsigned own1[kNB], own2[kNB], cbits[kNB];
 #pragma unroll
         for (int b = 0; b < kNB; ++b) {
-            unsigned qk[8];
+            if constexpr (kLdsA) {
+                unsigned qk[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) qk[j] = (qg[b][j] & ~15u) | q_code_bits(j);
-            unsigned q1, q2;
-            top2_8(qk, q1, q2);
-            own1[b] = pm1[b];
-            own2[b] = minu(pm2[b], q2);
-            // the winner's row (tile_row): 16 (2t + g) from its P key, the rest from its Q key
-            cbits[b] = ((pm1[b] & PMASK) << 4) | (q1 & 15u) | ((unsigned)h << 2);
+                for (int j = 0; j < 8; ++j) qk[j] = (qg[b][j] & ~15u) | q_code_bits(j);
+                unsigned q1, q2;
+                top2_8(qk, q1, q2);
+                own1[b] = pm1[b];
+                own2[b] = minu(pm2[b], q2);
+                // the winner's row (tile_row): 16 (2t + g) from its P key, the rest from its Q key
+                cbits[b] = ((pm1[b] & PMASK) << 4) | (q1 & 15u) | ((unsigned)h << 2);
+            } else {
+                // 16 Q keys: (j, par) with the row bits 32 par + q_code_bits(j) (6 bits)
+                unsigned qe[8], qo[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    qe[j] = (qg[b][j] & ~63u) | q_code_bits(j);
+                    qo[j] = (qh[b][j] & ~63u) | 32u | q_code_bits(j);
+                }
+                unsigned e1_, e2_, o1_, o2_;
+                top2_8(qe, e1_, e2_);
+                top2_8(qo, o1_, o2_);
+                const unsigned q1 = minu(e1_, o1_);
+                const unsigned q2 = min3u(maxu(e1_, o1_), e2_, o2_);
+                own1[b] = pm1[b];
+                own2[b] = minu(pm2[b], q2);
+                // row 64 s + 16 g (P index 2s + g) + 32 par + (j & 3) + 8 (j >> 2) + 4 h
+                const unsigned pi = pm1[b] & PMASK;
+                cbits[b] = ((pi >> 1) << 6) | ((pi & 1u) << 4) | (q1 & 63u) | ((unsigned)h << 2);
+            }
         }
         // The two half-waves hold the two halves of a vector's centroids.  Blocks are merged
         // in pairs by one v_permlane32_swap per value: swap(block b0's, block b0 + 1's) leaves
@@ -899,10 +951,6 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     // One batch of queued vectors (lane r: entry r; invalid lanes idle): re-screen, collect
     // the candidates at or below the entry's threshold, evaluate them exactly (see the tail).
     auto rerank32 = [&](const uint2 ent, const bool valid) {
-        // A batch is latency: with the issue going to the oldest wave first, a batch run
-        // beside two waves' main loops took 3-8x its time alone -- and a batch begun near
-        // the end of the grid is what the last waves wait for.
-        if (rr_prio) pqh_set_prio(rr_prio);
 #ifdef PQH_ASSIGN_STAMPS
         const unsigned long long rr0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1028,10 +1076,6 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         rr_ticks += __builtin_amdgcn_s_memrealtime() - rr0;
         ++rr_batches;
 #endif
-        if (rr_prio) {
-            __builtin_amdgcn_s_setprio(0);
-            pqh_set_prio(prio);
-        }
     };
     long long ch = wave_id;
     float xn[kNB][XD];
@@ -1284,7 +1328,7 @@ int launch_mfma(pqh_ctx* ctx, pqh_pq* pq, const float* x, long long n, long long
 #else
     uint32_t* sched = pq->m <= kSchedMax ? ctx->d_sched + ring * kSchedSet : nullptr;
 #endif
-    const int prio = pqh_prio("ASSIGN", 0) | (pqh_prio("ASSIGN_RR", 0) << 2);
+    const int prio = pqh_prio("ASSIGN", 0);
     // grid = the workgroups that are resident at once (persistent, grid-stride over the
     // 32-vector blocks): more would only queue behind the first wave of workgroups
 #define PQH_CASE(DD) PQH_CASE_KT(DD, 8)
