@@ -139,9 +139,10 @@ def parse():
     ap.add_argument("--astreams", type=int, default=1,
                     help="assignment + histogram streams, batch i on stream i %% N (N > 1: the "
                          "next batch's assignment grid fills the previous one's tail)")
-    ap.add_argument("--hist-on", choices=["assign", "lanes"], default="assign",
-                    help="stream of the context histogram: the assignment's, or the batch's "
-                         "lane (before its code tables)")
+    ap.add_argument("--hist-on", choices=["assign", "lanes", "own"], default="assign",
+                    help="stream of the context histogram: the assignment's, the batch's "
+                         "lane (before its code tables), or a stream of its own (a fifth "
+                         "stream: the process then asks HIP for 8 hardware queues)"),
     ap.add_argument("--tbufs", type=int, default=2,
                     help="code-table sets per table lane when --elanes > 0")
     ap.add_argument("--a-priority", action="store_true",
@@ -320,7 +321,7 @@ def pcie_ms(torch, x, codes, stream_bytes):
 
 def main():
     args = parse()
-    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.hist_on == "own":
         # 4 library/torch streams + RCCL's own: give each a hardware queue (HIP reads this at
         # initialisation; measured neutral at one rank, 2,150 vs 2,153 Mvec/s)
         os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
@@ -468,6 +469,10 @@ def main():
             e1.record(stream)
 
     hist_on_lane = args.hist_on == "lanes" and not serial
+    # --hist-on own: the histogram of batch i on a stream of its own, after batch i's
+    # assignment, so stream A carries the assignments only
+    hctx = codec.Context(local, cus=1 << 20) if args.hist_on == "own" and not serial else None
+    ev_asg = [torch.cuda.Event() for _ in range(slots)]
     # the split histogram: partial counts per slot (the assignment stream writes slot s's while
     # a lane may still reduce another's)
     hist_split = args.hist_split == "on" and ctxm and not serial and not hist_on_lane and \
@@ -550,9 +555,19 @@ def main():
                 codec.sort_rows(cF, codes[s], sort_tmp)
                 done(e, sF)
             halo[s] = None
-            if not hist_on_lane:     # (the shard-boundary pair is added on the lane)
+            if hctx is not None:
+                ev_asg[s].record(sF)
+            elif not hist_on_lane:   # (the shard-boundary pair is added on the lane)
                 hist(s, cF, sF)
-            ev_hist[s].record(sF)
+                ev_hist[s].record(sF)
+            else:
+                ev_hist[s].record(sF)
+        if hctx is not None:
+            sH = hctx.stream
+            with torch.cuda.stream(sH):
+                sH.wait_event(ev_asg[s])
+                hist(s, hctx, sH)
+                ev_hist[s].record(sH)
         with torch.cuda.stream(sL):
             sL.wait_event(ev_hist[s])
             hist_reduce(s, c)
@@ -908,7 +923,8 @@ def main():
         t.close()
     for q in apq:
         q.close()
-    for c in {id(c): c for c in list(lanes) + list(elanes) + list(actx)}.values():
+    for c in {id(c): c for c in list(lanes) + list(elanes) + list(actx) +
+              ([hctx] if hctx is not None else [])}.values():
         c.close()
     if world > 1:
         dist.barrier()

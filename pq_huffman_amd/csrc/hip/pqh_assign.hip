@@ -470,8 +470,9 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     pqh_set_prio(prio);   // (pqh_prio "ASSIGN": against the kernels running beside it)
     if (L == 0 && wave == 0) {   // the next launch's queue heads and re-rank counter
         // (agent-scope stores: written through to where the next launch's atomics act)
-        if (sched_next)
-            for (int q = lane; q < m_total * kXcds; q += 64)
+        if (sched_next)   // every subspace's heads, not only this launch's m_total: the next
+                          // launch on this context may have more subspaces
+            for (int q = lane; q < kSchedMax * kXcds; q += 64)
                 __hip_atomic_store(sched_next + q * kSchedStride, 0u, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
         if (lane == 0)
@@ -507,7 +508,12 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     // the P-key mask: an inline constant for 4 index bits, a register for 8
     const unsigned keymask = PB == 4 ? ~PMASK : opaque_u32(~PMASK);
     const float* cl = cent + (long long)m * K * D;   // fp32 centroids (L2-resident, 16 KB)
-    const long long nblk = (n + 31) / 32;
+    // block and chunk indices are 32-bit, so their tests are scalar compares (a 64-bit signed
+    // compare of wave-uniform values is a VALU instruction pair): 0.2436 -> 0.2413 ms per 1M
+    // (the host splits launches at 2^30 rows)
+    const int n32 = (int)n;
+    const int nblk = (n32 + 31) / 32;
+    const int nfull = n32 / 32;   // blocks with 32 valid rows
     unsigned long long slow_count = 0;
 
     // x slice of a block.  D == 16 (SIFT): lane (r, h) holds dims [8h, 8h + 8) of vector r
@@ -528,13 +534,13 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     const char* const xm = reinterpret_cast<const char*>(x + (long long)m * D);
     const unsigned code_lane_off = (unsigned)r * (unsigned)m_total * (unsigned)sizeof(CodeT);
     const unsigned code_pair_off = (unsigned)lane * (unsigned)m_total * (unsigned)sizeof(CodeT);
-    auto load_x = [&](long long b, float* dst) {
+    auto load_x = [&](int b, float* dst) {
 #ifdef PQH_ASSIGN_NOMEM   // diagnostic: every chunk re-reads the first 64 blocks (cache hits)
         b &= 63;
 #endif
-        long long row0 = b * 32;
+        long long row0 = (long long)b * 32;
         unsigned off = xlane_off;
-        if (row0 + 32 > n) {   // (uniform) the last, partial block: rows past n read row n - 1
+        if (b >= nfull) {   // (uniform) the last, partial block: rows past n read row n - 1
             row0 = row0 < n - 1 ? row0 : n - 1;
             const long long left = n - 1 - row0;
             const unsigned last = (unsigned)(left < 31 ? left : 31);
@@ -913,10 +919,10 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     // shared head per subspace saturated at a few dequeues per microsecond.  The ticket for
     // the next chunk is requested a whole step ahead, and the next chunk's x is loaded
     // during the current one.
-    const long long wave_id = (long long)bx * kWavesPerWG + wave;   // within subspace
-    const long long waves_m = (long long)gx * kWavesPerWG;
-    const long long nchunk = (nblk + kNB - 1) / kNB;
-    const long long R = nchunk > waves_m ? (nchunk - waves_m + kXcds - 1) / kXcds : 0;
+    const int wave_id = bx * kWavesPerWG + wave;
+    const int waves_m = gx * kWavesPerWG;
+    const int nchunk = (nblk + kNB - 1) / kNB;
+    const int R = nchunk > waves_m ? (nchunk - waves_m + kXcds - 1) / kXcds : 0;
     uint32_t* head = sched ? sched + (long long)m * kXcds * kSchedStride : nullptr;
     int xr = head ? (int)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & (kXcds - 1)) : 0;
     int tries = head && R > 0 ? 0 : kXcds;
@@ -930,10 +936,10 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     };
     unsigned traw = 0;
     if (tries < kXcds) traw = ticket();
-    auto next_dyn = [&]() -> long long {   // the next dynamic chunk, -1 once all are taken
+    auto next_dyn = [&]() -> int {
         while (tries < kXcds) {
-            const long long t = (unsigned)__builtin_amdgcn_readfirstlane(traw);
-            const long long lo = waves_m + xr * R;
+            const int t = (int)__builtin_amdgcn_readfirstlane(traw);
+            const int lo = waves_m + xr * R;
             if (t < std::min(R, nchunk - lo)) {
                 traw = ticket();           // prefetch the one after
                 return lo + t;
@@ -1077,7 +1083,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         ++rr_batches;
 #endif
     };
-    long long ch = wave_id;
+    int ch = wave_id;
     float xn[kNB][XD];
 #pragma unroll
     for (int b = 0; b < kNB; ++b) load_x(ch * kNB + b, xn[b]);
@@ -1087,17 +1093,17 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         for (int b = 0; b < kNB; ++b)
 #pragma unroll
             for (int j = 0; j < XD; ++j) xa[b][j] = xn[b][j];
-        long long nc;
+        int nc;
         if (!head) {
             nc = ch + waves_m;
         } else {
-            const long long c = next_dyn();
+            const int c = next_dyn();
             nc = c < 0 ? nchunk : c;
         }
-        const long long pre = nc < nchunk ? nc : ch;   // branch-free: re-load at the end
+        const int pre = nc < nchunk ? nc : ch;   // branch-free: re-load at the end
 #pragma unroll
         for (int b = 0; b < kNB; ++b) load_x(pre * kNB + b, xn[b]);
-        step(ch * kNB, xa);
+        step((long long)ch * kNB, xa);
         while (qn >= 32u) {   // full batches of deferred vectors: done while the SIMD is busy
             rerank32(rqs[wave][qn - 32u + (unsigned)r], true);
             qn -= 32u;

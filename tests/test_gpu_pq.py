@@ -85,6 +85,20 @@ def test_assign_rerank_queue_overflow(gpu, oracle):
     assert np.array_equal(codec.counts_to_host(counts), oracle.histogram(got, 256, False))
 
 
+def test_assign_alternating_subspace_counts_one_context(gpu, oracle):
+    """m = 16, then 8, then 16 on one context, each with enough rows for the dynamic work
+    queues: a launch resets the next launch's queue heads (and spill counters) for every
+    subspace, not only its own, so the third launch finds subspaces 8-15 fresh."""
+    x = datagen.sift_like(150_000, 128, seed=21)
+    c16 = datagen.lloyd_centroids(x, 16, 256, iters=1, sample=4000, seed=5)
+    c8 = datagen.lloyd_centroids(x, 8, 256, iters=1, sample=4000, seed=6)
+    want16, _ = oracle.pq_assign(x, c16, threads=0)
+    want8, _ = oracle.pq_assign(x, c8, threads=0)
+    for cent, want in ((c16, want16), (c8, want8), (c16, want16), (c8, want8), (c16, want16)):
+        got, _ = _assign(gpu, x, cent)
+        assert np.array_equal(got, want), (got != want).sum()
+
+
 def test_assign_nonfinite_rows(gpu, oracle):
     x = datagen.sift_like(300, 128, seed=2)
     cent = datagen.lloyd_centroids(x, 8, 256, iters=1, sample=300)
