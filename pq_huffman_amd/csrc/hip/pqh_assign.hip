@@ -61,6 +61,10 @@ namespace {
 constexpr int kRqLds = 128;      // deferred re-rank queue entries per wave (LDS)
 constexpr int kWavesPerWG = PQH_ASSIGN_WPG;   // subspace waves per workgroup
 constexpr int kNB = PQH_ASSIGN_NB;            // 32-vector blocks screened together per step
+#ifndef PQH_ASSIGN_CLDS
+#define PQH_ASSIGN_CLDS 0
+#endif
+constexpr bool kCentLds = PQH_ASSIGN_CLDS != 0;
 
 template <int D>
 struct Plan {
@@ -451,6 +455,8 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     // each wave's re-rank queue (the LDS budget stays at 32 KB, so a workgroup still fits on
     // a CU beside a code-table build's 112 KB)
     __shared__ uint2 rqs[kWavesPerWG][kRqLds];
+    // (PQH_ASSIGN_CLDS, K = 256) the fp32 centroids for the exact re-rank's candidate rows
+    __shared__ __attribute__((aligned(16))) float Cf[kLdsA && kCentLds ? K * D : 1];
 
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // (uniform: SGPR math)
@@ -486,6 +492,8 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
             Cn[i] = cnorm[(long long)m * KT * 2 * 16 + i];
         if (kLdsA && counts)
             for (int i = lane; i < K; i += 64) hist[wave][i] = 0;
+        if constexpr (kLdsA && kCentLds)
+            for (int i = threadIdx.x; i < K * D; i += blockDim.x) Cf[i] = cent[(long long)m * K * D + i];
         __syncthreads();   // the only workgroup barrier
     }
     // where the A fragments come from: the LDS copy, or this subspace's slice in global
@@ -507,7 +515,8 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     const float ninf = opaque_ninf();
     // the P-key mask: an inline constant for 4 index bits, a register for 8
     const unsigned keymask = PB == 4 ? ~PMASK : opaque_u32(~PMASK);
-    const float* cl = cent + (long long)m * K * D;   // fp32 centroids (L2-resident, 16 KB)
+    // fp32 centroids (L2-resident, 16 KB at dsub 16; or the workgroup's LDS copy)
+    const float* cl = kLdsA && kCentLds ? Cf : cent + (long long)m * K * D;
     // block and chunk indices are 32-bit, so their tests are scalar compares (a 64-bit signed
     // compare of wave-uniform values is a VALU instruction pair): 0.2436 -> 0.2413 ms per 1M
     // (the host splits launches at 2^30 rows)
