@@ -1,6 +1,6 @@
 """Context-histogram timing (diagnostic): codec.histogram (hist_ctx + hist_ctx_reduce) on the
 bench's 1M-row codes, HIP events around 50 back-to-back calls.
-  python tools/bench_hist.py [sift|deep]
+  python tools/bench_hist.py [sift|deep]     (BENCH_HIST_REP=r: the codes tiled r times)
 The kernel form is picked per process: PQH_HIST_IMPL=thread (per-thread row runs) or the
 default wave-contiguous form; PQH_HIST_BLOCK=256 the 256-thread per-thread form."""
 import os
@@ -22,6 +22,9 @@ ctx = codec.Context(0)
 pq = codec.PQ(ctx, cent)
 codes = torch.empty((n, m), dtype=torch.uint8, device=dev)
 pq.assign(x, codes)
+rep = int(os.environ.get("BENCH_HIST_REP", "1"))   # the batch's codes tiled rep times
+if rep > 1:
+    codes = codes.repeat(rep, 1)
 counts = torch.empty((m, 65536), dtype=torch.int32, device=dev)
 for _ in range(3):
     codec.histogram(ctx, codes, 256, True, counts=counts, accumulate=False)
@@ -33,5 +36,6 @@ for _ in range(50):
 e1.record()
 torch.cuda.synchronize()
 form = os.environ.get("PQH_HIST_IMPL", "wave") + "/" + os.environ.get("PQH_HIST_BLOCK", "1024")
-print(f"hist {name} {form} {e0.elapsed_time(e1) / 50:.4f} ms "
+print(f"hist {name} {form} rows {codes.shape[0]} big_min {os.environ.get('PQH_HIST_BIG_MIN', '4000000')} "
+      f"{e0.elapsed_time(e1) / 50:.4f} ms "
       f"checksum {int(counts.to(torch.int64).sum())}", flush=True)
