@@ -45,9 +45,14 @@ ASSIGN_KERNEL = {"sift": "pq_assign_mfma<16, 8, unsigned char>",
                  "k4096": "pq_assign_mfma<16, 128, unsigned short>"}
 
 
-def profile_tag(config, sort):
-    """the profiles/ tag of a bench configuration (profiles/collect.sh r<N>_<tag>)"""
-    return config + ("_sort" if sort else "")
+def profile_tag(config, sort, vectors=1_000_000):
+    """the profiles/ tag of a bench configuration (profiles/collect.sh r<N>_<tag>): sift,
+    deep, k4096, sift_sort; another batch size adds its millions (sift at 125M rows: 125m,
+    collected by profiles/collect.sh r<N>_125m --vectors 125000000 ...)"""
+    tag = config + ("_sort" if sort else "")
+    if vectors != 1_000_000:
+        tag = f"{vectors // 1_000_000}m" if tag == "sift" else f"{tag}_{vectors // 1_000_000}m"
+    return tag
 
 
 def pmc_traffic(kernel, tag):
@@ -806,7 +811,7 @@ def main():
         vec_read, vec_write = 4 * d, m * code_bytes
         achieved = (vec_read + vec_write) * n / t_assign / 1e9
         akern = ASSIGN_KERNEL[args.config]
-        traffic, traffic_src, prof_avg_us = pmc_traffic(akern, profile_tag(args.config, args.sort))
+        traffic, traffic_src, prof_avg_us = pmc_traffic(akern, profile_tag(args.config, args.sort, args.vectors))
         t_enc = (acc["assign"] + acc["hist"] + acc["codebook"] + acc["lut"] + acc["encode"]) / args.steps
         tf = 2.0 * k * d * n / t_assign / 1e12   # algorithmic: 2 K D flop per vector
         workload = {
