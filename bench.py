@@ -447,6 +447,9 @@ def main():
         scratch = [shard.scratch_for(comm, m, dev) for _ in range(slots)]
         status = [0] * slots
         offs = [torch.zeros(2, dtype=torch.int64, device=dev) for _ in elanes]
+        # every batch's global length, folded by min on the encode streams: -1 (the sentinel
+        # ~0) if any rank's phase 2 failed for any batch (checked after the timed region)
+        shard_min = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in elanes]
     stages = ("assign", "sort", "hist", "codebook", "lut", "encode", "decode")
     if args.sort and (k > 256 or world > 1):
         raise SystemExit("--sort: one rank, K <= 256 (the distributed sort is shard.py's)")
@@ -670,6 +673,7 @@ def main():
                                          cprev[j], offs[j], scratch[s], status[s],
                                          first_row=rank * n)
                 tot_dev[j].copy_(shard.scratch_shard_bits(scratch[s], world, m))
+                torch.minimum(shard_min[j], offs[j][1:], out=shard_min[j])
                 state["goff"] = offs[j][:1]
                 acc["collectives"] += time.perf_counter() - tc if state["timed"] else 0.0
             elif world > 1:   # place the shard in the global stream before writing it: sizes,
@@ -787,6 +791,8 @@ def main():
     assert torch.equal(dec[j_last], codes[s_last]), "round trip mismatch"
     if lib_shard:   # every rank's pqh_shard_encode_write succeeded (no sentinel length)
         shard.status(elanes[j_last], offs[j_last])
+        for j, sm in enumerate(shard_min):   # ... for every batch, not only the last
+            assert int(sm.item()) >= 0, f"a rank's shard encode failed (encode stream {j})"
     rerank = pq.rerank_count(ctx)
     bits_per_vec = int(tot_dev[j_last].item()) / n
 

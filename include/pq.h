@@ -42,8 +42,9 @@ int fvecs_load_meta(const char* filename, long long* num_vectors, int* num_dimen
 float* fvecs_load(const char* filename, long long* num_vectors, int* num_dimensions);
 
 /* codes: n x M, uint8 when K <= 256 else uint16 (row-major, pq_indices.bvecsl order).
- * Streams: the rows go to the GPU a chunk at a time (PQH_ENCODE_CHUNK rows, default 2^18)
- * through two pinned buffers, so device memory is bounded for any n. */
+ * Streams: the rows go to the GPU a chunk at a time (PQH_ENCODE_CHUNK rows, default 2^18
+ * capped at 128 MB of rows per buffer, halved on an allocation failure) through two pinned
+ * buffers, so device memory is bounded for any n. */
 int pq_encode(const centroids_codebook_t* codebook, const float* x, long long n, int d,
               void* codes);
 /* pq_encode over rows produced by the caller: read(user, row0, rows, dst) fills rows
@@ -56,11 +57,24 @@ int pq_encode_rows(const centroids_codebook_t* codebook, int d, long long n, pq_
                    void* user, void* codes, long long chunk_rows);
 /* Train the codebook in place on the GPU: `iters` deterministic Lloyd iterations
  * (pqh_kmeans_train) from the centroids it holds -- the build's replacement for the
- * training done by yael kmeans at pq_encoder.c:265-274. */
+ * training done by yael kmeans at pq_encoder.c:265-274.  Streams like pq_encode. */
 int pq_train(centroids_codebook_t* codebook, const float* x, long long n, int d, int iters);
-/* mean over vectors of the summed squared reconstruction error (double). */
+/* pq_train over rows produced by the caller (read as for pq_encode_rows): one pass for the
+ * fixed-point scale, then one pass per iteration; device memory stays at two chunks for any
+ * n, and the centroids equal pq_train's on the same rows bit for bit (exact fixed-point
+ * sums).  The reference holds one N x dsub slice at a time (pq_encoder.c:265-269). */
+int pq_train_rows(centroids_codebook_t* codebook, int d, long long n, pq_rows_fn read,
+                  void* user, int iters, long long chunk_rows);
+/* mean over vectors of the summed squared reconstruction error (double), as
+ * compute_error (pq_encoder.c:82-119). */
 int pq_compute_error(const centroids_codebook_t* codebook, const float* x, long long n, int d,
                      const void* codes, double* error_out);
+/* pq_compute_error over rows produced by the caller, a chunk at a time (the reference reads
+ * 128K-row batches, pq_encoder.c:89-113); codes are the n x M host codes.  The result equals
+ * pq_compute_error's bit for bit (256-row partial sums added in row order). */
+int pq_compute_error_rows(const centroids_codebook_t* codebook, int d, long long n,
+                          pq_rows_fn read, void* user, const void* codes, long long chunk_rows,
+                          double* error_out);
 
 #ifdef __cplusplus
 }

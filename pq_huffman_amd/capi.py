@@ -113,6 +113,8 @@ SIGNATURES = [
     ("fvecs_load_meta", I, [S, P, P]), ("fvecs_load", P, [S, P, P]),
     ("pq_encode", I, [P, P, LL, I, P]), ("pq_compute_error", I, [P, P, LL, I, P, P]),
     ("pq_train", I, [P, P, LL, I, I]), ("pq_encode_rows", I, [P, I, LL, P, P, P, LL]),
+    ("pq_train_rows", I, [P, I, LL, P, P, I, LL]),
+    ("pq_compute_error_rows", I, [P, I, LL, P, P, P, LL, P]),
     # pqh.h
     ("pqh_ctx_create", I, [P, I]), ("pqh_ctx_destroy", I, [P]), ("pqh_ctx_set_stream", I, [P, P]),
     ("pqh_ctx_create_cu_limited", I, [P, I, I]), ("pqh_ctx_create_cu_split", I, [P, I, I, I]), ("pqh_ctx_stream", P, [P]),

@@ -1549,6 +1549,18 @@ int pqh_pq_last_rerank_count(pqh_ctx_t* ctx, unsigned long long* count) {
 int pqh_pq_error(pqh_ctx_t* ctx, const pqh_pq_t* pq, const float* d_x, long long n,
                  long long ld_x, const void* d_codes, double* error_out) {
     if (!ctx || !pq || !error_out || n <= 0) return PQH_ERR_ARG;
+    double s = 0.0;
+    const int rc = pqh_pq_error_accum(ctx, pq, d_x, n, ld_x, d_codes, &s);
+    if (rc) return rc;
+    *error_out = s / (double)n;
+    return PQH_OK;
+}
+
+}  // extern "C"
+
+int pqh_pq_error_accum(pqh_ctx* ctx, const pqh_pq_t* pq, const float* d_x, long long n,
+                       long long ld_x, const void* d_codes, double* sum) {
+    if (!ctx || !pq || !sum || n <= 0) return PQH_ERR_ARG;
     int rc = pqh_use_device(ctx);
     if (rc) return rc;
     const long long blocks = (n + 255) / 256;
@@ -1568,11 +1580,13 @@ int pqh_pq_error(pqh_ctx_t* ctx, const pqh_pq_t* pq, const float* d_x, long long
     PQH_HIP(ctx, hipMemcpyAsync(h.data(), part, blocks * sizeof(double), hipMemcpyDeviceToHost,
                                 ctx->stream));
     PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    double s = 0.0;
+    double s = *sum;
     for (double v : h) s += v;
-    *error_out = s / (double)n;
+    *sum = s;
     return PQH_OK;
 }
+
+extern "C" {
 
 int pqh_pq_reconstruct(pqh_ctx_t* ctx, const pqh_pq_t* pq, const void* d_codes, long long n,
                        float* d_out, long long ld_out) {

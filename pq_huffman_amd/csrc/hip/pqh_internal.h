@@ -9,6 +9,14 @@
 
 #include "pqh.h"
 
+// The kernels are written for gfx950 (CDNA4) only: wave64 DPP controls that exist only on
+// GFX9/CDNA (row_bcast:15/31, wave_shr:1 in the scans, the encoder's look-back and the wave
+// histogram), v_permlane32_swap, the 32x32x16 bf16 MFMA.  A device pass for any other target
+// stops here instead of miscompiling.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "pq_huffman_amd device code targets gfx950 only (--offload-arch=gfx950)"
+#endif
+
 struct pqh_tables;
 
 struct pqh_ctx {
@@ -50,6 +58,18 @@ int pqh_set_error(pqh_ctx* ctx, int code, const char* fmt, ...);
 int pqh_ensure_ws(pqh_ctx* ctx, size_t bytes);
 int pqh_use_device(pqh_ctx* ctx);
 int pqh_kmeans_fixed_shift(float max_abs, long long n);
+// k-means iteration pieces (pqh_kmeans.hip), shared by the one-shot and the streamed trainers
+int pqh_kmeans_absmax_launch(pqh_ctx* ctx, const float* d_x, long long n, long long ld_x, int d,
+                             unsigned* d_max);
+int pqh_kmeans_accum_launch(pqh_ctx* ctx, const float* d_x, long long n, long long ld_x, int m,
+                            int k, int dsub, const void* d_codes, int s, long long* d_sums,
+                            unsigned long long* d_cnt);
+int pqh_kmeans_update_launch(pqh_ctx* ctx, const long long* d_sums, const unsigned long long* d_cnt,
+                             long long cells, int dsub, int s, float* d_cent);
+// the error pass over n rows, its 256-row block partials added to *sum in row order (so a
+// caller streaming chunks of a multiple of 256 rows gets pqh_pq_error's sum bit for bit)
+int pqh_pq_error_accum(pqh_ctx* ctx, const pqh_pq_t* pq, const float* d_x, long long n,
+                       long long ld_x, const void* d_codes, double* sum);
 // pqh_shard_encode's histogram / size / write with this shard's raw-first flag in device
 // memory (1: row 0 raw, no halo pair; 0: row 0 in the context of d_prev_row) -- pqh_huff.hip
 extern "C" {

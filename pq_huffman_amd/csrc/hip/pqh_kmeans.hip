@@ -85,6 +85,52 @@ kmeans_update(const long long* __restrict__ sums, const unsigned long long* __re
 
 }  // namespace
 
+// The three launches of an iteration, shared by pqh_kmeans_train (device-resident rows) and
+// the streamed trainer pq_train_rows (pqh_pq_host.cpp, rows a chunk at a time): the
+// fixed-point sums are exact integers, so accumulating chunk by chunk gives the same bits.
+int pqh_kmeans_absmax_launch(pqh_ctx* ctx, const float* d_x, long long n, long long ld_x, int d,
+                             unsigned* d_max) {
+    if (n <= 0) return PQH_OK;
+    hipLaunchKernelGGL(absmax_kernel, dim3(1024), dim3(256), 0, ctx->stream, d_x, n, ld_x, d, d_max);
+    return hipGetLastError() == hipSuccess ? PQH_OK : PQH_ERR_HIP;
+}
+
+int pqh_kmeans_accum_launch(pqh_ctx* ctx, const float* d_x, long long n, long long ld_x, int m,
+                            int k, int dsub, const void* d_codes, int s, long long* d_sums,
+                            unsigned long long* d_cnt) {
+    if (n <= 0) return PQH_OK;
+    const bool lds = (size_t)k * dsub * 8 + (size_t)k * 4 <= 48 * 1024;
+    const size_t lds_bytes = lds ? (size_t)k * dsub * 8 + (size_t)k * 4 : 0;
+    const unsigned bx = (unsigned)std::min<long long>(std::max<long long>(1, n / 4096), 256);
+    if (k <= 256) {
+        if (lds)
+            hipLaunchKernelGGL((kmeans_accum<uint8_t, true>), dim3(bx, m), dim3(256), lds_bytes,
+                               ctx->stream, d_x, n, ld_x, m, k, dsub,
+                               static_cast<const uint8_t*>(d_codes), s, d_sums, d_cnt);
+        else
+            hipLaunchKernelGGL((kmeans_accum<uint8_t, false>), dim3(bx, m), dim3(256), 0,
+                               ctx->stream, d_x, n, ld_x, m, k, dsub,
+                               static_cast<const uint8_t*>(d_codes), s, d_sums, d_cnt);
+    } else {
+        if (lds)
+            hipLaunchKernelGGL((kmeans_accum<uint16_t, true>), dim3(bx, m), dim3(256), lds_bytes,
+                               ctx->stream, d_x, n, ld_x, m, k, dsub,
+                               static_cast<const uint16_t*>(d_codes), s, d_sums, d_cnt);
+        else
+            hipLaunchKernelGGL((kmeans_accum<uint16_t, false>), dim3(bx, m), dim3(256), 0,
+                               ctx->stream, d_x, n, ld_x, m, k, dsub,
+                               static_cast<const uint16_t*>(d_codes), s, d_sums, d_cnt);
+    }
+    return hipGetLastError() == hipSuccess ? PQH_OK : PQH_ERR_HIP;
+}
+
+int pqh_kmeans_update_launch(pqh_ctx* ctx, const long long* d_sums, const unsigned long long* d_cnt,
+                             long long cells, int dsub, int s, float* d_cent) {
+    hipLaunchKernelGGL(kmeans_update, dim3((unsigned)((cells * dsub + 255) / 256)), dim3(256), 0,
+                       ctx->stream, d_sums, d_cnt, cells, dsub, s, d_cent);
+    return hipGetLastError() == hipSuccess ? PQH_OK : PQH_ERR_HIP;
+}
+
 extern "C" {
 
 int pqh_kmeans_train(pqh_ctx_t* ctx, const float* d_x, long long n, long long ld_x, int m,
@@ -123,9 +169,8 @@ int pqh_kmeans_train(pqh_ctx_t* ctx, const float* d_x, long long n, long long ld
     int s;
     {
         hipError_t e = hipMemsetAsync(d_max, 0, 4, ctx->stream);
-        hipLaunchKernelGGL(absmax_kernel, dim3(1024), dim3(256), 0, ctx->stream, d_x, n, ld_x,
-                           m * dsub, d_max);
-        if (e == hipSuccess) e = hipGetLastError();
+        if (e == hipSuccess && pqh_kmeans_absmax_launch(ctx, d_x, n, ld_x, m * dsub, d_max))
+            e = hipErrorLaunchFailure;
         if (e == hipSuccess) e = hipMemcpyAsync(&hmax, d_max, 4, hipMemcpyDeviceToHost, ctx->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
         if (e != hipSuccess) {
@@ -136,9 +181,6 @@ int pqh_kmeans_train(pqh_ctx_t* ctx, const float* d_x, long long n, long long ld
         std::memcpy(&fmax, &hmax, 4);
         s = pqh_kmeans_fixed_shift(fmax, n);
     }
-    const bool lds = (size_t)k * dsub * 8 + (size_t)k * 4 <= 48 * 1024;
-    const size_t lds_bytes = lds ? (size_t)k * dsub * 8 + (size_t)k * 4 : 0;
-    const unsigned bx = (unsigned)std::min<long long>(std::max<long long>(1, n / 4096), 256);
     for (int it = 0; it < iters; ++it) {
         pqh_pq_t* pq = nullptr;
         rc = pqh_pq_create(ctx, centroids, m, k, dsub, &pq);
@@ -153,33 +195,11 @@ int pqh_kmeans_train(pqh_ctx_t* ctx, const float* d_x, long long n, long long ld
         if (e == hipSuccess)
             e = hipMemcpyAsync(d_cent, centroids, (size_t)cells * dsub * 4, hipMemcpyHostToDevice,
                                ctx->stream);
-        if (e == hipSuccess) {
-            if (esz == 1) {
-                if (lds)
-                    hipLaunchKernelGGL((kmeans_accum<uint8_t, true>), dim3(bx, m), dim3(256), lds_bytes,
-                                       ctx->stream, d_x, n, ld_x, m, k, dsub,
-                                       static_cast<const uint8_t*>(d_codes), s, d_sums, d_cnt);
-                else
-                    hipLaunchKernelGGL((kmeans_accum<uint8_t, false>), dim3(bx, m), dim3(256), 0,
-                                       ctx->stream, d_x, n, ld_x, m, k, dsub,
-                                       static_cast<const uint8_t*>(d_codes), s, d_sums, d_cnt);
-            } else {
-                if (lds)
-                    hipLaunchKernelGGL((kmeans_accum<uint16_t, true>), dim3(bx, m), dim3(256), lds_bytes,
-                                       ctx->stream, d_x, n, ld_x, m, k, dsub,
-                                       static_cast<const uint16_t*>(d_codes), s, d_sums, d_cnt);
-                else
-                    hipLaunchKernelGGL((kmeans_accum<uint16_t, false>), dim3(bx, m), dim3(256), 0,
-                                       ctx->stream, d_x, n, ld_x, m, k, dsub,
-                                       static_cast<const uint16_t*>(d_codes), s, d_sums, d_cnt);
-            }
-            e = hipGetLastError();
-        }
-        if (e == hipSuccess) {
-            hipLaunchKernelGGL(kmeans_update, dim3((unsigned)((cells * dsub + 255) / 256)), dim3(256), 0,
-                               ctx->stream, d_sums, d_cnt, cells, dsub, s, d_cent);
-            e = hipGetLastError();
-        }
+        if (e == hipSuccess && pqh_kmeans_accum_launch(ctx, d_x, n, ld_x, m, k, dsub, d_codes, s,
+                                                       d_sums, d_cnt))
+            e = hipErrorLaunchFailure;
+        if (e == hipSuccess && pqh_kmeans_update_launch(ctx, d_sums, d_cnt, cells, dsub, s, d_cent))
+            e = hipErrorLaunchFailure;
         if (e == hipSuccess)
             e = hipMemcpyAsync(centroids, d_cent, (size_t)cells * dsub * 4, hipMemcpyDeviceToHost,
                                ctx->stream);

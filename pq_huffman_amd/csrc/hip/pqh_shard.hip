@@ -53,6 +53,28 @@ __global__ void shard_halo_pick(const unsigned char* __restrict__ recs, long lon
         row[i] = prev >= 0 ? recs[prev * recb + kHaloData + i] : (unsigned char)0;
 }
 
+// The shard's exact bit length from its LOCAL histogram (kept in the scratch before the
+// all-reduce) and the code lengths of the shared tables: sum over (part, item) of count x
+// len -- huffman_estimate_size's sum (huffman_encode.c:271-277) over this shard -- plus 8 bits
+// per part when the shard writes the raw first row (huffman_encoder.c:234).  The histogram
+// counts exactly the symbols the encoder codes (the halo pair when it is not raw-first, no
+// out-of-alphabet symbol), so this equals the size pass over the codes without reading them.
+// *out must be zero on entry.
+__global__ void __launch_bounds__(256)
+shard_length(const uint32_t* __restrict__ local, const unsigned long long* __restrict__ enc,
+             long long total, int m, const int* __restrict__ rawf, int nonempty,
+             unsigned long long* __restrict__ out) {
+    unsigned long long s = 0;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const uint32_t c = local[i];
+        if (c) s += (unsigned long long)c * (enc[i] >> 56);
+    }
+    for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && nonempty && rawf && *rawf) s += 8ull * m;
+    if ((threadIdx.x & 63) == 0 && s) atomicAdd(out, s);
+}
+
 }  // namespace
 
 extern "C" {
@@ -70,10 +92,15 @@ int pqh_shard_block(long long n_total, int world, int rank, block_t* block) {
 }
 
 // scratch: [send record][world records][halo row (a record's size)][send length]
-//          [world lengths][raw-first flag, 64 B]
+//          [world lengths][raw-first flag, 64 B][pad to 256 B][local histogram, m x K^2 u32
+//          at K = 256: the largest histogram a shard encode takes]
+static long long shard_local_offset(int world, int m) {
+    return ((halo_record_bytes(m) * (world + 2) + 8ll * (world + 1) + 64 + 255) / 256) * 256;
+}
+
 long long pqh_shard_scratch_bytes(int world, int m) {
     if (world <= 0 || m <= 0) return PQH_ERR_ARG;
-    return halo_record_bytes(m) * (world + 2) + 8ll * (world + 1) + 64;
+    return shard_local_offset(world, m) + (long long)m * 65536 * 4;
 }
 
 int pqh_shard_offsets(const unsigned long long* lengths, int world, int rank,
@@ -132,6 +159,7 @@ struct ShardScratch {
     unsigned long long* len_send;
     unsigned long long* len_recv;
     int* rawf;
+    uint32_t* local;   // the shard's own histogram, kept for its length (phase 2)
     long long recb;
     ShardScratch(void* d, int world, int m) {
         unsigned char* p = static_cast<unsigned char*>(d);
@@ -142,6 +170,7 @@ struct ShardScratch {
         len_send = reinterpret_cast<unsigned long long*>(p + recb * (world + 2));
         len_recv = len_send + 1;
         rawf = reinterpret_cast<int*>(len_recv + world);
+        local = reinterpret_cast<uint32_t*>(p + shard_local_offset(world, m));
     }
 };
 
@@ -205,6 +234,10 @@ int pqh_shard_encode_tables(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm, const 
         local(pqh_histogram_set_dev(ctx, d_codes, n, m, k, sc.halo_row, sc.rawf, d_counts));
     else
         local(pqh_histogram_set(ctx, d_codes, n, m, k, 0, nullptr, d_counts));
+    // (the local counts give phase 2 the shard's length without a pass over its codes)
+    if (!err)
+        local(hipMemcpyAsync(sc.local, d_counts, (size_t)m * items * 4, hipMemcpyDeviceToDevice,
+                             ctx->stream) == hipSuccess ? PQH_OK : PQH_ERR_HIP);
     if (comm->all_reduce_sum_u32(comm->user, d_counts, (long long)m * items, st))
         return pqh_set_error(ctx, PQH_ERR_COMM, "shard histogram all-reduce failed");
     if (!err) local(pqh_tables_build(ctx, tables, d_counts));
@@ -229,11 +262,18 @@ int pqh_shard_encode_write(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm, const b
     const long long n = err ? 0 : shard->size;
     const int world = comm->world, rank = comm->rank;
     ShardScratch sc(d_scratch, world, m);
-    if (!err) {
-        const int r = context ? pqh_encode_size_dev(ctx, tables, d_codes, n, sc.halo_row, sc.rawf,
-                                                    sc.len_send)
-                              : pqh_encode_size(ctx, tables, d_codes, n, 0, nullptr, sc.len_send);
-        if (r) err = r;
+    if (!err) {   // the exact length: local histogram x code lengths (no size pass)
+        const long long total = (long long)m * tables->items;
+        if (hipMemsetAsync(sc.len_send, 0, 8, ctx->stream) != hipSuccess) {
+            err = PQH_ERR_HIP;
+        } else {
+            const long long want = (total + 255) / 256;
+            const unsigned grid = (unsigned)(want < 1024 ? (want > 0 ? want : 1) : 1024);
+            hipLaunchKernelGGL(shard_length, dim3(grid), dim3(256), 0, ctx->stream, sc.local,
+                               tables->d_enc, total, m, context ? sc.rawf : nullptr,
+                               n > 0 ? 1 : 0, sc.len_send);
+            if (hipGetLastError() != hipSuccess) err = PQH_ERR_HIP;
+        }
     }
     if (err) (void)hipMemsetAsync(sc.len_send, 0xFF, 8, ctx->stream);   // the sentinel length
     if (comm->all_gather(comm->user, sc.len_send, sc.len_recv, 8, ctx->stream))

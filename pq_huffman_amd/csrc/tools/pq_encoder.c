@@ -3,9 +3,11 @@
  *   pq_encoder <input.fvecs> <output template> <m> [--num-threads t] [--compute-error]
  *              [--kmeans-iterations n] [--centroids <pq_centroids.fvecsl>] [--seed s]
  * Assignment and training run on the GPU (libpqh).  Training: deterministic Lloyd
- * iterations on the GPU (pq_train: exact assignment, fixed-point centroid means) from a
+ * iterations on the GPU (pq_train_rows: exact assignment, fixed-point centroid means) from a
  * seeded sample init (yael's time-seeded Berkeley init is not reproducible); --centroids
- * skips training.  --num-threads is accepted for compatibility. */
+ * skips training.  Training, encoding and --compute-error all stream the file in chunks
+ * (PQH_ENCODE_CHUNK rows), so neither host nor device memory holds the input whole.
+ * --num-threads is accepted for compatibility. */
 #define _FILE_OFFSET_BITS 64
 #define _POSIX_C_SOURCE 200809L
 #include <stdint.h>
@@ -85,7 +87,14 @@ int main(int argc, const char* argv[]) {
     }
     const int ds = d / m;
     unsigned char* codes = (unsigned char*)malloc((size_t)n * m + 1);
-    float* x = NULL;   /* the whole input: only for training and the error pass */
+    /* every pass streams the file (the reference reads 128K-row batches, pq_encoder.c:58-80,
+     * 89-113): the input is never held whole, on the host or on the device */
+    fvecs_reader_t rd = {fopen(input, "rb"), d, NULL, 1 << 16, 0};
+    rd.raw = (int32_t*)malloc((size_t)rd.cap * (d + 1) * 4);
+    if (!rd.f || !rd.raw || !codes) {
+        fprintf(stderr, "cannot read %s\n", input);
+        return 1;
+    }
     centroids_codebook_t cb;
     if (cfile) {
         if (centroids_codebook_load(&cb, cfile, m, k) || cb.num_dimensions != ds) {
@@ -93,33 +102,27 @@ int main(int argc, const char* argv[]) {
             return 1;
         }
     } else {
-        x = fvecs_load(input, &n, &d);
-        if (!x) {
-            fprintf(stderr, "cannot read %s\n", input);
-            return 1;
-        }
+        /* seeded init: k rows drawn from the file, then GPU Lloyd with fixed-point means */
         centroids_codebook_init(&cb, m, k, ds);
+        float* row = (float*)malloc((size_t)d * sizeof(float));
         for (int c = 0; c < k; ++c) {
             long long v = n ? (long long)(rng_next() % (unsigned long long)n) : 0;
+            if (n && fvecs_rows(&rd, v, 1, row)) {
+                fprintf(stderr, "cannot read %s\n", input);
+                return 1;
+            }
             for (int i = 0; i < m; ++i)
-                memcpy(cb.centroids[i] + (size_t)c * ds, x + v * d + (long long)i * ds, ds * sizeof(float));
+                memcpy(cb.centroids[i] + (size_t)c * ds, n ? row + (long long)i * ds : row,
+                       n ? ds * sizeof(float) : 0);
         }
-        int trc = pq_train(&cb, x, n, d, iters);   /* GPU Lloyd, fixed-point means */
+        free(row);
+        int trc = pq_train_rows(&cb, d, n, fvecs_rows, &rd, iters, 0);
         if (trc) {
             fprintf(stderr, "pq_train failed: %d\n", trc);
             return 1;
         }
     }
-    int rc;
-    if (x) {
-        rc = pq_encode(&cb, x, n, d, codes);   /* streamed to the GPU in chunks */
-    } else {   /* fixed centroids: stream the file itself, never holding it whole */
-        fvecs_reader_t rd = {fopen(input, "rb"), d, NULL, 1 << 16, 0};
-        rd.raw = (int32_t*)malloc((size_t)rd.cap * (d + 1) * 4);
-        rc = rd.f && rd.raw ? pq_encode_rows(&cb, d, n, fvecs_rows, &rd, codes, 0) : -1;
-        if (rd.f) fclose(rd.f);
-        free(rd.raw);
-    }
+    int rc = pq_encode_rows(&cb, d, n, fvecs_rows, &rd, codes, 0);
     if (rc) {
         fprintf(stderr, "pq_encode failed: %d\n", rc);
         return 1;
@@ -142,9 +145,8 @@ int main(int argc, const char* argv[]) {
         return 1;
     }
     if (compute_error) {
-        if (!x) x = fvecs_load(input, &n, &d);
         double err = 0;
-        if (!x || pq_compute_error(&cb, x, n, d, codes, &err)) {
+        if (pq_compute_error_rows(&cb, d, n, fvecs_rows, &rd, codes, 0, &err)) {
             fprintf(stderr, "compute_error failed\n");
             return 1;
         }
@@ -160,6 +162,7 @@ int main(int argc, const char* argv[]) {
     free(pi);
     centroids_codebook_destroy(&cb);
     free(codes);
-    free(x);
+    fclose(rd.f);
+    free(rd.raw);
     return 0;
 }

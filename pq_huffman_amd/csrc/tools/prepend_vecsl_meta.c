@@ -4,9 +4,11 @@
  * The file must hold exactly num_vectors x num_dimensions elements (1, 4, 4 or 8 bytes by
  * the letter before "vecsl"); it is rewritten as u32 N, u32 D, then the same payload.  A
  * file already 8 bytes longer is reported as processed and left alone.  The payload is
- * streamed through a temporary file next to it (the reference holds it in memory), then
- * renamed over the original; messages and exit codes follow the reference (an extension it
- * asserts on is reported with exit status 1). */
+ * streamed to a temporary file next to it (the reference holds it in memory), then written
+ * back into the SAME file after the header, as the reference rewrites it in place
+ * (prepend_vecsl_meta.c:65-68): the inode, its mode, owner and hard links are kept, and a
+ * symlink still points at the rewritten file.  Messages and exit codes follow the reference
+ * (an extension it asserts on is reported with exit status 1). */
 #define _FILE_OFFSET_BITS 64
 #define _POSIX_C_SOURCE 200809L
 #include <stdio.h>
@@ -75,12 +77,11 @@ int main(int argc, const char* argv[]) {
         fclose(in);
         return 1;
     }
-    save_vecs_light_meta_file(out, num_vectors, num_dimensions);
     enum { kBuf = 1 << 22 };
     char* buf = (char*)malloc(kBuf);
     long long left = elements * esz;
     int bad = 0;
-    while (left > 0 && !bad) {
+    while (left > 0 && !bad) {   /* 1. the payload -> the temporary copy */
         const size_t want = left < kBuf ? (size_t)left : (size_t)kBuf;
         const size_t got = fread(buf, 1, want, in);
         if (got != want) {
@@ -93,14 +94,42 @@ int main(int argc, const char* argv[]) {
         }
         left -= (long long)got;
     }
-    free(buf);
     fclose(in);
-    if (fclose(out) || bad || rename(tmp, filename)) {
-        if (!bad) fprintf(stderr, "Cannot replace %s\n", filename);
+    if (fclose(out) || bad) {
+        if (!bad) fprintf(stderr, "Cannot write %s\n", tmp);
         remove(tmp);
+        free(buf);
         free(tmp);
         return 1;
     }
+    /* 2. header + payload back into the original file, in place */
+    FILE* src = fopen(tmp, "rb");
+    FILE* dst = src ? fopen(filename, "r+b") : NULL;
+    if (!dst) {
+        fprintf(stderr, "Cannot replace %s\n", filename);
+        if (src) fclose(src);
+        remove(tmp);
+        free(buf);
+        free(tmp);
+        return 1;
+    }
+    save_vecs_light_meta_file(dst, num_vectors, num_dimensions);
+    left = elements * esz;
+    while (left > 0 && !bad) {
+        const size_t want = left < kBuf ? (size_t)left : (size_t)kBuf;
+        if (fread(buf, 1, want, src) != want || fwrite(buf, 1, want, dst) != want) bad = 1;
+        left -= (long long)want;
+    }
+    fclose(src);
+    if (fclose(dst) || bad) {
+        /* the original is partly rewritten: keep the copy of its payload */
+        fprintf(stderr, "Cannot replace %s (its payload is kept in %s)\n", filename, tmp);
+        free(buf);
+        free(tmp);
+        return 1;
+    }
+    remove(tmp);
+    free(buf);
     free(tmp);
     return 0;
 }

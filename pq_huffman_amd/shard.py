@@ -376,14 +376,15 @@ class _null:
 
 
 def shard_encode(ctx, comm: TorchComm, codes, tables, counts, out, chunk_vectors=0,
-                 chunk_offsets=None, chunk_prev=None, first_row=0, raw_first=True):
+                 chunk_offsets=None, chunk_prev=None, first_row=0, raw_first=True, check=False):
     """This rank's encode through pqh_shard_encode (halo, histogram all-reduce, GPU code
     tables, lengths all-gather, device offsets, write) -- asynchronous on ctx's stream.
     codes: (n, m) uint8 cuda tensor (n may be 0); counts: (m, items) int32; out: uint8
     buffer.  Returns (offsets, raw): offsets a (2,) int64 device tensor {global bit offset,
     global length}; raw = whether this shard wrote the raw first row (read back from the
     device when raw_first is True -- the call's one host round trip -- else None).  A failure
-    on another rank shows in offsets[1] == -1 (status())."""
+    on another rank shows in offsets[1] == -1: check=True synchronises and raises on it here
+    (status()); otherwise the caller checks with status()."""
     import torch
     from .capi import Block, check
     n, m = codes.shape
@@ -410,6 +411,8 @@ def shard_encode(ctx, comm: TorchComm, codes, tables, counts, out, chunk_vectors
     check(rc, "pqh_shard_encode")
     if ctx.stream != torch.cuda.current_stream(dev):
         scratch.record_stream(ctx.stream)   # (asynchronous: keep it until the stream is done)
+    if check:
+        status(ctx, offsets)
     return offsets, (raw.value if raw_first else None)
 
 

@@ -77,7 +77,7 @@ def main():
         ctx.close()
         dist.destroy_process_group()
         return
-    offsets, raw = shard.shard_encode(ctx, comm, mine, tabs, counts, out, first_row=b)
+    offsets, raw = shard.shard_encode(ctx, comm, mine, tabs, counts, out, first_row=b, check=True)
     torch.cuda.synchronize()
     goff, total = (int(v) for v in offsets.cpu().tolist())
     # every rank's length, for the stitch on rank 0

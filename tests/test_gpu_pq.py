@@ -264,3 +264,98 @@ def test_pq_encode_streams_in_chunks(gpu, oracle, monkeypatch):
     assert np.array_equal(codes, one_shot)
     want, _ = oracle.pq_assign(x, cent, threads=0)
     assert np.array_equal(codes, want)
+
+
+def _cb_struct():
+    import ctypes
+
+    class CB(ctypes.Structure):   # pq.h centroids_codebook_t
+        _fields_ = [("num_clusters", ctypes.c_int), ("num_dimensions", ctypes.c_int),
+                    ("num_parts", ctypes.c_int), ("centroids_pool", ctypes.c_void_p),
+                    ("centroids", ctypes.c_void_p)]
+    return CB
+
+
+def _row_reader(x):
+    """a pq_rows_fn over a numpy array, counting the rows it hands out"""
+    import ctypes
+    seen = {"rows": 0, "max_chunk": 0}
+    fn_t = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_longlong,
+                            ctypes.c_void_p)
+
+    def read(_user, row0, rows, dst):
+        ctypes.memmove(dst, x[row0:row0 + rows].ctypes.data, rows * x.shape[1] * 4)
+        seen["rows"] += rows
+        seen["max_chunk"] = max(seen["max_chunk"], rows)
+        return 0
+    return fn_t(read), seen
+
+
+def test_streamed_error_and_training_equal_one_shot(gpu, oracle):
+    """pq_compute_error_rows / pq_train_rows (pq.h) over 1,024-row chunks -- device memory two
+    chunks -- equal the one-shot device passes bit for bit: the error's 256-row partials are
+    summed in row order, the k-means sums are exact fixed-point integers
+    (src/pq_encoder.c:82-119 reads 128K-row batches; :265-269 one slice at a time)."""
+    import ctypes
+    from pq_huffman_amd.capi import lib
+    torch, codec, ctx = gpu
+    n = 7777
+    x = datagen.sift_like(n, 128, seed=11)
+    init = _init_from_rows(x, 8, 256, 3)
+    CB = _cb_struct()
+    # training: 3 iterations streamed vs the one-shot device trainer vs the oracle
+    cent = np.ascontiguousarray(init.copy(), np.float32)
+    cb = CB(256, 16, 8, cent.ctypes.data, None)
+    rd, seen = _row_reader(x)
+    assert lib().pq_train_rows(ctypes.byref(cb), 128, n, rd, None, 3, 1024) == 0
+    assert seen["max_chunk"] == 1024 and seen["rows"] == 4 * n   # absmax + 3 iterations
+    one = codec.kmeans_train(ctx, torch.from_numpy(x).cuda(), init, 3)
+    assert np.array_equal(cent.view(np.uint32), one.view(np.uint32))
+    assert np.array_equal(cent.view(np.uint32), oracle.kmeans(x, init, 3, threads=0).view(np.uint32))
+    # error of the trained codebook's codes: streamed vs one-shot vs the oracle
+    codes, _ = oracle.pq_assign(x, cent, threads=0)
+    rd2, seen2 = _row_reader(x)
+    err = ctypes.c_double()
+    assert lib().pq_compute_error_rows(ctypes.byref(cb), 128, n, rd2, None, codes.ctypes.data,
+                                       1024, ctypes.byref(err)) == 0
+    assert seen2["max_chunk"] == 1024 and seen2["rows"] == n
+    pq = codec.PQ(ctx, cent)
+    one_err = pq.error(torch.from_numpy(x).cuda(), torch.from_numpy(codes).cuda())
+    assert err.value == one_err
+    want = oracle.compute_error(x, cent, codes)
+    assert abs(err.value - want) <= 1e-12 * abs(want)
+
+
+def test_cli_pq_encoder_compute_error_streams(gpu, oracle, tmp_path):
+    """pq_encoder --compute-error on an input of several chunks (PQH_ENCODE_CHUNK=1024): the
+    training, the codes and the appended pq_error equal the one-shot passes on the same rows."""
+    import os
+    import subprocess
+    from conftest import ROOT
+    torch, codec, ctx = gpu
+    n = 6000
+    x = datagen.sift_like(n, 128, seed=12)
+    datagen.write_fvecs(str(tmp_path / "x.fvecs"), x)
+    bind = os.path.join(ROOT, "pq_huffman_amd", "bin")
+    env = dict(os.environ, PQH_ENCODE_CHUNK="1024")
+    subprocess.run([os.path.join(bind, "pq_encoder"), str(tmp_path / "x.fvecs"),
+                    str(tmp_path) + "/", "8", "--kmeans-iterations", "2", "--compute-error"],
+                   check=True, capture_output=True, timeout=300, env=env)
+    state = 0x9E3779B97F4A7C15
+    mask = (1 << 64) - 1
+    rows = []
+    for _ in range(256):                       # tools/pq_encoder.c rng_next
+        state ^= (state << 13) & mask
+        state ^= state >> 7
+        state ^= (state << 17) & mask
+        rows.append(state % n)
+    init = np.ascontiguousarray(x[rows].reshape(256, 8, 16).transpose(1, 0, 2))
+    cent = codec.kmeans_train(ctx, torch.from_numpy(x).cuda(), init, 2)
+    got = np.frombuffer((tmp_path / "pq_centroids.fvecsl").read_bytes()[8:], np.float32)
+    assert np.array_equal(got.view(np.uint32), cent.reshape(-1).view(np.uint32))
+    codes = np.frombuffer((tmp_path / "pq_indices.bvecsl").read_bytes()[8:], np.uint8).reshape(n, 8)
+    want_codes, _ = oracle.pq_assign(x, cent, threads=0)
+    assert np.array_equal(codes, want_codes)
+    one_err = codec.PQ(ctx, cent).error(torch.from_numpy(x).cuda(),
+                                        torch.from_numpy(np.ascontiguousarray(codes)).cuda())
+    assert (tmp_path / "pq_error").read_text() == "%f\n" % one_err

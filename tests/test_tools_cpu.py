@@ -43,3 +43,23 @@ def test_prepend_vecsl_meta(tmp_path, kind, dtype):
     other = tmp_path / "x.qvecsl"
     other.write_bytes(b"")
     assert _run(OURS, other, 0, 0)[0] == 1     # unknown letter
+
+
+def test_prepend_vecsl_meta_rewrites_in_place(tmp_path):
+    """The file is rewritten in place like the reference's (src/prepend_vecsl_meta.c:65-68):
+    same inode and mode, a hard link sees the new bytes, a symlink still points at it."""
+    data = np.arange(60, dtype=np.float32).tobytes()
+    want = np.array([6, 10], np.uint32).tobytes() + data
+    p = tmp_path / "x.fvecsl"
+    p.write_bytes(data)
+    os.chmod(p, 0o640)
+    link = tmp_path / "hard.fvecsl"
+    os.link(p, link)
+    sym = tmp_path / "sym.fvecsl"
+    os.symlink(p, sym)
+    ino = os.stat(p).st_ino
+    assert _run(OURS, sym, 6, 10) == (0, "")
+    assert os.path.islink(sym) and sym.read_bytes() == want
+    assert os.stat(p).st_ino == ino and (os.stat(p).st_mode & 0o777) == 0o640
+    assert link.read_bytes() == want
+    assert not any(q.name.endswith(".pqh_tmp") for q in tmp_path.iterdir())
