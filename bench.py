@@ -144,6 +144,9 @@ def parse():
     ap.add_argument("--astreams", type=int, default=1,
                     help="assignment + histogram streams, batch i on stream i %% N (N > 1: the "
                          "next batch's assignment grid fills the previous one's tail)")
+    ap.add_argument("--sort-on", choices=["assign", "lanes"], default="lanes",
+                    help="--sort: the sort (and then the histogram) of batch i on its table lane "
+                         "after its assignment (default), or on the assignment stream")
     ap.add_argument("--hist-on", choices=["assign", "lanes", "own"], default="assign",
                     help="stream of the context histogram: the assignment's, the batch's "
                          "lane (before its code tables), or a stream of its own (a fifth "
@@ -454,6 +457,12 @@ def main():
     if args.sort and (k > 256 or world > 1):
         raise SystemExit("--sort: one rank, K <= 256 (the distributed sort is shard.py's)")
     sort_tmp = torch.empty((n, m), dtype=torch.uint8, device=dev) if args.sort else None
+    # sort mode: the sort of batch i runs on its table lane (after the assignment), so the
+    # assignment stream carries the assignments only; the histogram follows it there
+    sort_on_lane = args.sort and args.sort_on == "lanes" and not serial
+    # (one rocPRIM-path scratch per lane when the lanes sort concurrently)
+    sort_tmps = [torch.empty((n, m), dtype=torch.uint8, device=dev) for _ in lanes] \
+        if sort_on_lane else None
     events = []          # (stage, start, end) of timed steps, read after the timed region
     acc = {s: 0.0 for s in list(stages) + ["collectives"]}
     state = {"timed": False}
@@ -476,7 +485,7 @@ def main():
         if e1 is not None:
             e1.record(stream)
 
-    hist_on_lane = args.hist_on == "lanes" and not serial
+    hist_on_lane = (args.hist_on == "lanes" or sort_on_lane) and not serial
     # --hist-on own: the histogram of batch i on a stream of its own, after batch i's
     # assignment, so stream A carries the assignments only
     hctx = codec.Context(local, cus=1 << 20) if args.hist_on == "own" and not serial else None
@@ -558,7 +567,7 @@ def main():
             e = rec("assign", sF)
             apq[i % na].assign(x, codes[s], ctx=cF)
             done(e, sF)
-            if args.sort:            # stable strncmp-key sort of the batch's rows (in place)
+            if args.sort and not sort_on_lane:   # stable strncmp-key sort (in place)
                 e = rec("sort", sF)
                 codec.sort_rows(cF, codes[s], sort_tmp)
                 done(e, sF)
@@ -585,6 +594,10 @@ def main():
             tc = time.perf_counter()
             halo[s] = shard.exchange_halo(codes[s][-1], world, rank) if ctxm else None
             acc["collectives"] += time.perf_counter() - tc if state["timed"] else 0.0
+            if sort_on_lane:         # the batch's sort, on its lane, before its histogram
+                e = rec("sort", sL)
+                codec.sort_rows(c, codes[s], sort_tmps[j])
+                done(e, sL)
             if hist_on_lane:
                 hist(s, c, sL)
             elif halo[s] is not None:

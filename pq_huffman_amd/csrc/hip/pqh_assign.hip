@@ -286,25 +286,33 @@ __device__ __forceinline__ void split_x(const float* xs, float& X, bool& lo, flo
 
 // Error bound E0 of the screening score S_k = D_k - X against the fp32 direct-form
 // distance D_k (DESIGN.md "pq_assign error bound"), P = sqrt(X) sqrt(Cmax):
-//   E0 = c_lo P + 2^-22 Cmax + 2^-17 (2.02 P + 1.01 Cmax + 1.05 X),
-// c_lo = 2^-13 when some x of the block has a bf16 remainder, else 2^-15.  The acceptance
-// gap tau = 2.2 E0 is evaluated as a1 sqrt(X) + (c X + b) with per-subspace coefficients
-// (TauCoef); every term is positive, so inflating each coefficient by 2^-20 covers the
-// rounding of the coefficients and of the two fmas, and the 1e-5 on sqrt(Cmax) covers
-// v_sqrt_f32 (1 ulp) against the correctly rounded root.
+//   E0 = split + 2^-22 Cmax + 2^-17 (2.02 P + 1.01 Cmax + 1.05 X).
+// split is what the bf16 halves leave out of 2 x.c: with a bf16 remainder in some x of the
+// block 2^-13 P; without one (x = xh) exactly 2 |x . r'_k| with r'_k = c_k - ch_k - cl_k,
+// <= 2 sqrt(X) R, R = max_k ||r'_k|| measured on the host (R <= 2^-16 sqrt(Cmax), so this is
+// never looser than the 2^-15 P it replaces; typically ~3x tighter, fewer re-ranks).  The
+// acceptance gap tau = 2.2 E0 is evaluated as a1 sqrt(X) + (c X + b) with per-subspace
+// coefficients (TauCoef); every term is positive, so inflating each coefficient by 2^-20
+// covers the rounding of the coefficients and of the two fmas, and the 1e-5 on sqrt(Cmax)
+// covers v_sqrt_f32 (1 ulp) against the correctly rounded root.
 struct TauCoef {
     float a_nolo, a_lo, b, c;
 };
 
-__device__ __forceinline__ TauCoef tau_coef(float cm, float sc) {
+// cm = Cmax, sc = sqrt(Cmax), r2 = 2 R (all rounded up on the host)
+__device__ __forceinline__ TauCoef tau_coef(float cm, float sc, float r2) {
     constexpr float up = 1.0f + 0x1p-20f;
-    const float s = 2.2f * 1.00001f * sc;
-    return {s * (0x1p-15f + 2.02f * 0x1p-17f) * up, s * (0x1p-13f + 2.02f * 0x1p-17f) * up,
+    const float s = 2.2f * 1.00001f;
+    return {s * (r2 + 2.02f * 0x1p-17f * sc) * up, s * sc * (0x1p-13f + 2.02f * 0x1p-17f) * up,
             2.2f * cm * (0x1p-22f + 1.01f * 0x1p-17f) * up + 1e-30f,
             2.2f * 1.05f * 0x1p-17f * up};
 }
 
 __device__ __forceinline__ float screen_tau(float X, bool any_lo, const TauCoef& q) {
+#ifdef PQH_ASSIGN_TAU_SCALE   // diagnostic builds only (breaks exactness): re-rank rate sweeps
+    return PQH_ASSIGN_TAU_SCALE *
+           fmaf(any_lo ? q.a_lo : q.a_nolo, __builtin_amdgcn_sqrtf(X), fmaf(q.c, X, q.b));
+#endif
     return fmaf(any_lo ? q.a_lo : q.a_nolo, __builtin_amdgcn_sqrtf(X), fmaf(q.c, X, q.b));
 }
 
@@ -511,7 +519,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
 #endif
     const float cm = cmax[m];
     const float sc = sqrt_cmax[m];
-    const TauCoef tq = tau_coef(cm, sc);
+    const TauCoef tq = tau_coef(cm, sc, sqrt_cmax[m_total + m]);   // ([m, 2m): 2 R)
     const float ninf = opaque_ninf();
     // the P-key mask: an inline constant for 4 index bits, a register for 8
     const unsigned keymask = PB == 4 ? ~PMASK : opaque_u32(~PMASK);
@@ -1271,26 +1279,32 @@ namespace {
 // bf16) and the rows' ||c||^2 in accumulator order (the C operand of each tile's chain)
 template <int D>
 void build_afrag(const float* c, int k, std::vector<uint16_t>& out, std::vector<float>& cn,
-                 int m, float& cmax_out) {
+                 int m, float& cmax_out, float& r2_out) {
     using P = Plan<D>;
     const int slots = 16 * P::PM;
     std::vector<uint16_t> main((size_t)k * slots, 0);
     std::vector<double> norm(k);
-    double cmax = 0.0;
+    double cmax = 0.0, rmax = 0.0;
     for (int row = 0; row < k; ++row) {
         const float* cr = c + (size_t)row * D;
-        double q = 0.0;
+        double q = 0.0, rq = 0.0;
         for (int j = 0; j < D; ++j) {
             q += (double)cr[j] * (double)cr[j];
             uint16_t hi = bf16_rne(cr[j]);
             uint16_t lw = bf16_rne(cr[j] - bf16_to_f(hi));
             main[(size_t)row * slots + j] = bf16_rne(-2.0f * bf16_to_f(hi));       // exact
             main[(size_t)row * slots + D + j] = bf16_rne(-2.0f * bf16_to_f(lw));   // exact
+            // the split's remainder r' (exact in double: three floats' sum)
+            const double r = (double)cr[j] - (double)bf16_to_f(hi) - (double)bf16_to_f(lw);
+            rq += r * r;
         }
         norm[row] = q;
         cmax = q > cmax ? q : cmax;
+        rmax = rq > rmax ? rq : rmax;
     }
     cmax_out = (float)(cmax * (1.0 + 1e-6)) + 1e-30f;
+    // 2 max_k ||r'_k||, rounded up (the 1e-6 covers the double sum and root)
+    r2_out = (float)(2.0 * std::sqrt(rmax) * (1.0 + 1e-6)) + 1e-30f;
     // fragment order [m][PA][tile][lane][8]
     const int kt = k / 32;
     const size_t base = (size_t)m * P::PA * kt * 64 * 8;
@@ -1433,30 +1447,32 @@ int pqh_pq_create(pqh_ctx_t* ctx, const float* centroids, int m, int k, int dsub
     if (pq->mfma_ok) {
         std::vector<uint16_t> frag((size_t)m * pa * (k / 32) * 64 * 8);
         std::vector<float> cn((size_t)m * (k / 32) * 32);
-        std::vector<float> cmax(m), sqc(m);
+        // sqc: [0, m) sqrt(Cmax), [m, 2m) 2 R (the split remainder's bound, see TauCoef)
+        std::vector<float> cmax(m), sqc(2 * (size_t)m);
         for (int i = 0; i < m; ++i) {
             const float* c = centroids + (size_t)i * k * dsub;
+            float& r2 = sqc[(size_t)m + i];
             switch (dsub) {
-                case 4: build_afrag<4>(c, k, frag, cn, i, cmax[i]); break;
-                case 6: build_afrag<6>(c, k, frag, cn, i, cmax[i]); break;
-                case 8: build_afrag<8>(c, k, frag, cn, i, cmax[i]); break;
-                case 12: build_afrag<12>(c, k, frag, cn, i, cmax[i]); break;
-                case 16: build_afrag<16>(c, k, frag, cn, i, cmax[i]); break;
-                case 32: build_afrag<32>(c, k, frag, cn, i, cmax[i]); break;
+                case 4: build_afrag<4>(c, k, frag, cn, i, cmax[i], r2); break;
+                case 6: build_afrag<6>(c, k, frag, cn, i, cmax[i], r2); break;
+                case 8: build_afrag<8>(c, k, frag, cn, i, cmax[i], r2); break;
+                case 12: build_afrag<12>(c, k, frag, cn, i, cmax[i], r2); break;
+                case 16: build_afrag<16>(c, k, frag, cn, i, cmax[i], r2); break;
+                case 32: build_afrag<32>(c, k, frag, cn, i, cmax[i], r2); break;
             }
             sqc[i] = (float)(std::sqrt((double)cmax[i]) * (1.0 + 1e-6)) + 1e-30f;
         }
         if (hipMalloc(&pq->d_afrag, frag.size() * 2) != hipSuccess ||
             hipMalloc(&pq->d_cn, cn.size() * sizeof(float)) != hipSuccess ||
             hipMalloc(&pq->d_cmax, m * sizeof(float)) != hipSuccess ||
-            hipMalloc(&pq->d_sqc, m * sizeof(float)) != hipSuccess) {
+            hipMalloc(&pq->d_sqc, 2 * (size_t)m * sizeof(float)) != hipSuccess) {
             pqh_pq_destroy(pq);
             return pqh_set_error(ctx, PQH_ERR_NOMEM, "hipMalloc fragments");
         }
         (void)hipMemcpy(pq->d_afrag, frag.data(), frag.size() * 2, hipMemcpyHostToDevice);
         (void)hipMemcpy(pq->d_cn, cn.data(), cn.size() * sizeof(float), hipMemcpyHostToDevice);
         (void)hipMemcpy(pq->d_cmax, cmax.data(), m * sizeof(float), hipMemcpyHostToDevice);
-        (void)hipMemcpy(pq->d_sqc, sqc.data(), m * sizeof(float), hipMemcpyHostToDevice);
+        (void)hipMemcpy(pq->d_sqc, sqc.data(), 2 * (size_t)m * sizeof(float), hipMemcpyHostToDevice);
     }
     *out = pq;
     return PQH_OK;

@@ -28,6 +28,36 @@ template <typename CodeT>
 __device__ __forceinline__ unsigned ld_code(const CodeT* c, long long i) { return (unsigned)c[i]; }
 
 // ---------------------------------------------------------------- histograms
+// Multi-round workgroups (large inputs): a workgroup counts `rounds` consecutive chunks into
+// the same u16-pair LDS image, so the partials are bounded by the grid, not by n.  A chunk
+// adds at most kHistChunk counts, so the image cannot overflow while every counter starts a
+// chunk at <= kHistCarry = 65535 - kHistChunk = 4095: between chunks each counter above that
+// is added to the u32 accumulator `acc` (a memory-side global atomic) and cleared.  Each
+// flush moves >= 4096 counts, so a chunk causes at most 15 of them per workgroup.
+constexpr unsigned kHistCarry = 65535u - (unsigned)kHistChunk;
+static_assert(kHistCarry == 4095u, "the flush test reads the top nibble of each u16");
+
+__device__ __forceinline__ void hist_flush_carry(uint32_t* pairs, int words, unsigned base_bin,
+                                                 int k, uint32_t* __restrict__ acc) {
+    __syncthreads();   // the chunk's counts are in
+    for (int w = threadIdx.x; w < words; w += blockDim.x) {
+        const uint32_t x = pairs[w];
+        if (!(x & 0xF000F000u)) continue;   // both halves <= 4095
+        uint32_t keep = x;
+        const unsigned bin = base_bin + 2u * (unsigned)w;
+        if (x & 0xF000u) {
+            atomicAdd(&acc[bin], x & 0xFFFFu);
+            keep &= 0xFFFF0000u;
+        }
+        if (x & 0xF0000000u) {
+            atomicAdd(&acc[bin + 1], x >> 16);
+            keep &= 0xFFFFu;
+        }
+        pairs[w] = keep;   // (this thread owns the word between the barriers)
+    }
+    __syncthreads();
+}
+
 // Context histogram, pass 1: workgroup (chunk of kHistChunk vectors, part, prev-range z)
 // counts its (prev, cur) pairs with prev in [z k / split, (z + 1) k / split) in LDS as u16
 // pairs (a chunk cannot overflow 16 bits) and stores the packed counters as its slice of
@@ -43,14 +73,17 @@ template <typename CodeT, int BLK = 1024, int kSub = 20>
 __global__ void __launch_bounds__(BLK)
 hist_ctx(const CodeT* __restrict__ codes, long long n, int m_total, int k,
          const CodeT* __restrict__ prev_row, const int* __restrict__ d_rawf,
-         uint32_t* __restrict__ partial, int split, int chunks, int prio) {
+         uint32_t* __restrict__ partial, int split, int chunks, int rounds,
+         uint32_t* __restrict__ acc, int prio) {
     extern __shared__ uint32_t pairs[];   // (k / split) * k u16 counters packed two per word
     pqh_set_prio(prio);
     if (d_rawf && *d_rawf) prev_row = nullptr;   // decided on the device (pqh_shard_encode)
     const int per_chunk = m_total * split;
     const int q = (int)(blockIdx.x >> 3);
-    const int chunk = (q / per_chunk) * 8 + (int)(blockIdx.x & 7);
-    if (chunk >= chunks) return;   // (uniform: the XCD's list is shorter)
+    // group g = chunks [g rounds, (g + 1) rounds), its partial image g
+    const int groups = (chunks + rounds - 1) / rounds;
+    const int grp = (q / per_chunk) * 8 + (int)(blockIdx.x & 7);
+    if (grp >= groups) return;   // (uniform: the XCD's list is shorter)
     const int m = (q % per_chunk) / split;
     const int zs = q % split;
     const int prows = k / split;
@@ -61,6 +94,11 @@ hist_ctx(const CodeT* __restrict__ codes, long long n, int m_total, int k,
     for (int w = threadIdx.x; w < words; w += blockDim.x) pairs[w] = 0;
     constexpr int kRun = kHistChunk / BLK;    // consecutive vectors per thread, taken kSub
     static_assert(kRun % kSub == 0 && kSub % 2 == 0, "whole 16-byte row pairs per group");
+    const int c_end = min(chunks, (grp + 1) * rounds);
+#pragma unroll 1
+    for (int chunk = grp * rounds; chunk < c_end; ++chunk) {
+    if (chunk > grp * rounds)   // the previous chunk's counters above the carry go to acc
+        hist_flush_carry(pairs, words, (unsigned)m * (unsigned)(k * k) + plo * (unsigned)k, k, acc);
     const long long v0 = (long long)chunk * kHistChunk + (long long)threadIdx.x * kRun;
     auto count = [&](unsigned prev, unsigned cur) {
         if (prev >= (unsigned)k || cur >= (unsigned)k) return;   // absent / out of alphabet
@@ -121,8 +159,9 @@ hist_ctx(const CodeT* __restrict__ codes, long long n, int m_total, int k,
             prevc = cur;
         }
     }
+    }   // chunk
     __syncthreads();
-    uint32_t* out = partial + ((long long)m * chunks + chunk) * all_words + (long long)zs * words;
+    uint32_t* out = partial + ((long long)m * groups + grp) * all_words + (long long)zs * words;
     if ((words & 3) == 0) {
         const uint4* src = reinterpret_cast<const uint4*>(pairs);
         uint4* dst = reinterpret_cast<uint4*>(out);
@@ -150,14 +189,17 @@ template <int BLK, int G>
 __global__ void __launch_bounds__(BLK)
 hist_ctx_w(const uint8_t* __restrict__ codes, long long n, int m_total, int k,
            const uint8_t* __restrict__ prev_row, const int* __restrict__ d_rawf,
-           uint32_t* __restrict__ partial, int split, int chunks, int prio) {
+           uint32_t* __restrict__ partial, int split, int chunks, int rounds,
+           uint32_t* __restrict__ acc, int prio) {
     extern __shared__ uint32_t pairs[];   // (k / split) * k u16 counters packed two per word
     pqh_set_prio(prio);
     if (d_rawf && *d_rawf) prev_row = nullptr;   // decided on the device (pqh_shard_encode)
     const int per_chunk = m_total * split;
     const int q = (int)(blockIdx.x >> 3);
-    const int chunk = (q / per_chunk) * 8 + (int)(blockIdx.x & 7);
-    if (chunk >= chunks) return;   // (uniform: the XCD's list is shorter)
+    // group g = chunks [g rounds, (g + 1) rounds), its partial image g
+    const int groups = (chunks + rounds - 1) / rounds;
+    const int grp = (q / per_chunk) * 8 + (int)(blockIdx.x & 7);
+    if (grp >= groups) return;   // (uniform: the XCD's list is shorter)
     const int m = (q % per_chunk) / split;
     const int zs = q % split;
     const int prows = k / split;
@@ -178,13 +220,20 @@ hist_ctx_w(const uint8_t* __restrict__ codes, long long n, int m_total, int k,
     static_assert(kR % (128 * G) == 0, "whole tile groups per wave");
     // (uniform values through readfirstlane: SGPR bases, 32-bit per-lane offsets)
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int sh = 8 * (m & 3);
+    const int c_end = min(chunks, (grp + 1) * rounds);
+    bool first = true;
+#pragma unroll 1
+    for (int chunk = grp * rounds; chunk < c_end; ++chunk) {
+    if (!first)   // the previous chunk's counters above the carry go to acc
+        hist_flush_carry(pairs, words, (unsigned)m * (unsigned)(k * k) + plo * (unsigned)k, k, acc);
     const long long w0 = (long long)chunk * kHistChunk + (long long)wv * kR;
     const int cnt = (int)max(0ll, min(n - w0, (long long)kR));   // rows this wave counts
     unsigned carry = w0 > 0 ? (w0 - 1 < n ? (unsigned)codes[(w0 - 1) * m_total + m] : ~0u)
                             : (prev_row ? (unsigned)prev_row[m] : ~0u);
     carry = (unsigned)__builtin_amdgcn_readfirstlane((int)carry);
-    const int sh = 8 * (m & 3);
-    __syncthreads();   // the counters are zeroed
+    if (first) __syncthreads();   // the counters are zeroed
+    first = false;
     if (m_total == 8 && cnt == kR) {
         // two 8-byte rows per lane: one 16-byte load covers rows 2l, 2l + 1 of a 128-row tile
         const uint4* pr = reinterpret_cast<const uint4*>(codes + w0 * 8);
@@ -220,8 +269,9 @@ hist_ctx_w(const uint8_t* __restrict__ codes, long long n, int m_total, int k,
             }
         }
     }
+    }   // chunk
     __syncthreads();
-    uint32_t* out = partial + ((long long)m * chunks + chunk) * all_words + (long long)zs * words;
+    uint32_t* out = partial + ((long long)m * groups + grp) * all_words + (long long)zs * words;
     if ((words & 3) == 0) {
         const uint4* src = reinterpret_cast<const uint4*>(pairs);
         uint4* dst = reinterpret_cast<uint4*>(out);
@@ -237,16 +287,26 @@ hist_ctx_w(const uint8_t* __restrict__ codes, long long n, int m_total, int k,
 // packed word, so every counter has a single writer)
 __global__ void __launch_bounds__(256)
 hist_ctx_reduce(const uint32_t* __restrict__ partial, int chunks, int words, long long items,
-                uint32_t* __restrict__ counts, int set) {
+                uint32_t* __restrict__ counts, int set, uint32_t* __restrict__ acc) {
     const int m = blockIdx.y;
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= words) return;
     const uint32_t* p = partial + (long long)m * chunks * words + w;
     uint32_t lo = 0, hi = 0;
+#pragma unroll 8
     for (int c = 0; c < chunks; ++c) {
         const uint32_t x = p[(long long)c * words];
         lo += x & 0xFFFFu;
         hi += x >> 16;
+    }
+    if (acc) {   // the multi-round form's carries; cleared for the next launch
+        uint32_t* a = acc + (long long)m * items + 2 * w;
+        lo += a[0];
+        a[0] = 0;
+        if (2 * w + 1 < items) {
+            hi += a[1];
+            a[1] = 0;
+        }
     }
     uint32_t* out = counts + (long long)m * items;
     if (set) {   // every counter has exactly one writer: a plain store overwrites
@@ -733,6 +793,50 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
 
 }  // namespace
 
+// The context histogram's shape for n rows: its prev-range split, and the workgroup groups.
+// Up to 4 groups' worth of chunks (3.9M rows at m = 8) every chunk is a workgroup of its own
+// (one round); past that the chunks are spread over a fixed number of groups per (part,
+// split) -- ~256 workgroups in all, one per CU -- each counting its chunks in rounds, so the partial images
+// (and the reduce's reads) no longer grow with n; the u32 carry accumulator follows them.
+struct HistPlan {
+    int split, rounds, groups;
+    long long chunks;
+    size_t partial_bytes, acc_offset, total_bytes;
+};
+
+static int hist_split(int k) {
+    static const int split_env = [] {   // PQH_HIST_SPLIT = 1, 2 or 4; default 2 for even k
+        const char* e = std::getenv("PQH_HIST_SPLIT");
+        const int v = e ? std::atoi(e) : 2;
+        return v == 1 || v == 4 ? v : 2;
+    }();
+    return k % (2 * split_env) == 0 ? split_env : (k % 4 == 0 ? 2 : 1);
+}
+
+static HistPlan hist_plan(long long n, int m, int k) {
+    HistPlan p{};
+    p.split = hist_split(k);
+    p.chunks = (n + kHistChunk - 1) / kHistChunk;
+    static const int target = [] {   // PQH_HIST_WGS: the multi-round grid's workgroups
+        const char* e = std::getenv("PQH_HIST_WGS");
+        const int v = e ? std::atoi(e) : 256;
+        return v >= 8 ? v : 256;
+    }();
+    const int gt = std::max(8, (target / (m * p.split)) / 8 * 8);   // groups per (part, split)
+    if (p.chunks <= 4ll * gt) {
+        p.rounds = 1;
+        p.groups = (int)p.chunks;
+    } else {
+        p.rounds = (int)((p.chunks + gt - 1) / gt);
+        p.groups = (int)((p.chunks + p.rounds - 1) / p.rounds);
+    }
+    const size_t words = (size_t)((k * k + 1) / 2);
+    p.partial_bytes = (size_t)m * p.groups * words * 4;
+    p.acc_offset = (p.partial_bytes + 255) & ~(size_t)255;
+    p.total_bytes = p.rounds > 1 ? p.acc_offset + (size_t)m * k * k * 4 : p.partial_bytes;
+    return p;
+}
+
 extern "C" {
 
 // phase: 0 = partials + reduce (pqh_histogram*), 1 = the context partials only, into
@@ -753,30 +857,30 @@ static int histogram_impl(pqh_ctx_t* ctx, const void* d_codes, long long n, int 
         PQH_HIP(ctx, hipMemsetAsync(d_counts, 0, (size_t)m * items * 4, ctx->stream));
     if (n == 0) return PQH_OK;
     if (context) {
-        const unsigned chunks = (unsigned)((n + kHistChunk - 1) / kHistChunk);
+        const HistPlan hp = hist_plan(n, m, k);
         const int words = (k * k + 1) / 2;
-        // prev-range splits per chunk (PQH_HIST_SPLIT = 1, 2 or 4; default 2 for even k)
-        static const int split_env = [] {
-            const char* e = std::getenv("PQH_HIST_SPLIT");
-            const int v = e ? std::atoi(e) : 2;
-            return v == 1 || v == 4 ? v : 2;
-        }();
-        const int split = k % (2 * split_env) == 0 ? split_env : (k % 4 == 0 ? 2 : 1);
+        const int split = hp.split;
         const size_t lds = (size_t)(split == 1 ? words : (k / split) * k / 2) * 4;
         uint32_t* partial = d_partials;
         if (!partial) {
-            rc = pqh_ensure_ws(ctx, (size_t)m * chunks * words * 4);
+            rc = pqh_ensure_ws(ctx, hp.total_bytes);
             if (rc) return rc;
             partial = static_cast<uint32_t*>(ctx->ws);
         }
+        uint32_t* acc = hp.rounds > 1
+                            ? reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(partial) + hp.acc_offset)
+                            : nullptr;
         if (phase == 2) {
             hipLaunchKernelGGL(hist_ctx_reduce, dim3((unsigned)((words + 255) / 256), m), dim3(256),
-                               0, ctx->stream, partial, (int)chunks, words, (long long)k * k,
-                               d_counts, set);
+                               0, ctx->stream, partial, hp.groups, words, (long long)k * k,
+                               d_counts, set, acc);
             PQH_LAUNCH_CHECK(ctx);
             return PQH_OK;
         }
-        const unsigned grid = 8u * ((chunks + 7u) / 8u) * (unsigned)(m * split);
+        // the carry accumulator starts at zero (the reduce clears it again after reading)
+        if (acc) PQH_HIP(ctx, hipMemsetAsync(acc, 0, (size_t)m * k * k * 4, ctx->stream));
+        const int chunks = (int)hp.chunks, rounds = hp.rounds;
+        const unsigned grid = 8u * (((unsigned)hp.groups + 7u) / 8u) * (unsigned)(m * split);
         // 1024-thread workgroups; PQH_HIST_BLOCK=256: 256 threads with <= 32 VGPRs, which fit
         // beside the assignment grid (measured: histogram 0.19 vs 0.075 ms in the bench -- a
         // quarter of the loads in flight -- and the bench 2,119 vs 2,534 Mvec/s)
@@ -801,34 +905,34 @@ static int histogram_impl(pqh_ctx_t* ctx, const void* d_codes, long long n, int 
             hipLaunchKernelGGL((hist_ctx_w<256, 3>), dim3(grid), dim3(256), lds, ctx->stream,
                                static_cast<const uint8_t*>(d_codes), n, m, k,
                                static_cast<const uint8_t*>(d_prev_row), d_rawf, partial, split,
-                               (int)chunks, pqh_prio("HIST", 0));
+                               chunks, rounds, acc, pqh_prio("HIST", 0));
         } else if (wave_form) {
             PQH_HIP(ctx, hipFuncSetAttribute((const void*)hist_ctx_w<1024, 5>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
             hipLaunchKernelGGL((hist_ctx_w<1024, 5>), dim3(grid), dim3(1024), lds, ctx->stream,
                                static_cast<const uint8_t*>(d_codes), n, m, k,
                                static_cast<const uint8_t*>(d_prev_row), d_rawf, partial, split,
-                               (int)chunks, pqh_prio("HIST", 0));
+                               chunks, rounds, acc, pqh_prio("HIST", 0));
         } else if (!slim) {
             PQH_HIP(ctx, hipFuncSetAttribute((const void*)hist_ctx<uint8_t>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
             hipLaunchKernelGGL(hist_ctx<uint8_t>, dim3(grid), dim3(1024), lds, ctx->stream,
                                static_cast<const uint8_t*>(d_codes), n, m, k,
                                static_cast<const uint8_t*>(d_prev_row), d_rawf, partial, split,
-                               (int)chunks, pqh_prio("HIST", 0));
+                               chunks, rounds, acc, pqh_prio("HIST", 0));
         } else {
             PQH_HIP(ctx, hipFuncSetAttribute((const void*)hist_ctx<uint8_t, 256, 8>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
             hipLaunchKernelGGL((hist_ctx<uint8_t, 256, 8>), dim3(grid), dim3(256), lds, ctx->stream,
                                static_cast<const uint8_t*>(d_codes), n, m, k,
                                static_cast<const uint8_t*>(d_prev_row), d_rawf, partial, split,
-                               (int)chunks, pqh_prio("HIST", 0));
+                               chunks, rounds, acc, pqh_prio("HIST", 0));
         }
         PQH_LAUNCH_CHECK(ctx);
         if (phase == 0)
             hipLaunchKernelGGL(hist_ctx_reduce, dim3((unsigned)((words + 255) / 256), m), dim3(256),
-                               0, ctx->stream, partial, (int)chunks, words, (long long)k * k,
-                               d_counts, set);
+                               0, ctx->stream, partial, hp.groups, words, (long long)k * k,
+                               d_counts, set, acc);
     } else {
         const unsigned blocks = (unsigned)std::min<long long>((n + 4095) / 4096, 512);
         if (k <= 256)
@@ -844,8 +948,7 @@ static int histogram_impl(pqh_ctx_t* ctx, const void* d_codes, long long n, int 
 
 long long pqh_histogram_partial_bytes(long long n, int m, int k) {
     if (n < 0 || m <= 0 || k <= 0 || k > 256) return -1;
-    const long long chunks = (n + kHistChunk - 1) / kHistChunk;
-    return (long long)m * chunks * ((k * k + 1) / 2) * 4;
+    return (long long)hist_plan(n, m, k).total_bytes;
 }
 
 int pqh_histogram_partial(pqh_ctx_t* ctx, const void* d_codes, long long n, int m, int k,

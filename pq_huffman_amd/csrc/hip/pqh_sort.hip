@@ -7,11 +7,12 @@
 // compared as an unsigned big-endian byte string (verified by the oracle's
 // orc_sort_rows against reference-built fixtures).
 //
-// GPU, 2 <= M <= 8 (the CLI's M = 8 among them): a hand-written LSD radix sort, one pass
-// per key byte, least significant first (stable passes compose into a stable sort by the
-// whole key).  Each element carries its big-endian key and the row itself (both u64), so
-// the first pass reads the codes and the last writes the sorted rows in place -- no index
-// permutation and no gather.  One kernel counts the digits
+// GPU, 2 <= M <= 16 (the CLI's M = 8 and configs[3]'s M = 16 among them): a hand-written LSD
+// radix sort, one pass per key byte, least significant first (stable passes compose into a
+// stable sort by the whole key).  Each element is the row itself (one u64 word for M <= 8,
+// two for M <= 16); a pass derives its key byte from the row (cleared past the row's first 0
+// byte), so the first pass reads the codes and the last writes the sorted rows in place -- no
+// index permutation and no gather.  One kernel counts the digits
 // of the first pass's byte (`sort_digits`); each pass (`sort_pass`) is one kernel over
 // 8,192-row tiles taken in ticket order: a wave ranks its rows among equal digits with 8
 // ballots per 64 rows (stable: rows are ranked in index order), counts the next pass's
@@ -20,8 +21,8 @@
 // + earlier waves + its rank.  Measured (1M x 8, alone): 0.25 ms, as the rocPRIM path
 // (PQH_SORT_IMPL=rocprim); a pass is ~29 us, of which the look-back ~11 and the scatter ~8
 // (PQH_SORT_DIAG timing runs).
-// Other M: LSD over 8-byte key chunks, each a stable rocPRIM radix sort of (key, row index)
-// pairs, then a gather of the rows.
+// Other M (> 16): LSD over 8-byte key chunks, each a stable rocPRIM radix sort of (key, row
+// index) pairs, then a gather of the rows.
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
@@ -95,26 +96,43 @@ constexpr int kLookWin = PQH_SORT_WIN;                     // tiles read per loo
 constexpr unsigned long long kStAgg = 1ull << 46, kStPre = 1ull << 47;
 constexpr unsigned long long kStVal = (1ull << 46) - 1;
 
-// row v's bytes (byte j at bits 8j) and its strncmp key: bytes after the first 0 cleared,
-// big-endian (byte 0 most significant); bytes >= m are absent (0)
-__device__ __forceinline__ void sort_row_key(const uint8_t* __restrict__ codes, long long v, int m,
-                                             unsigned long long& key, unsigned long long& row) {
-    unsigned long long r = 0;
-    if (m == 8) {
-        r = reinterpret_cast<const unsigned long long*>(codes)[v];
+// row v of the codes as W little-endian u64 words (byte j at bits 8 (j % 8) of word j / 8);
+// bytes >= m are 0
+template <int W>
+__device__ __forceinline__ void sort_load_row(const uint8_t* __restrict__ codes, long long v, int m,
+                                              unsigned long long* r) {
+    if (W == 1 && m == 8) {
+        r[0] = reinterpret_cast<const unsigned long long*>(codes)[v];
+    } else if (W == 2 && m == 16) {
+        const uint4 q = reinterpret_cast<const uint4*>(codes)[v];
+        r[0] = (unsigned long long)q.x | ((unsigned long long)q.y << 32);
+        r[1] = (unsigned long long)q.z | ((unsigned long long)q.w << 32);
     } else {
-        for (int j = 0; j < m; ++j) r |= (unsigned long long)codes[v * m + j] << (8 * j);
+#pragma unroll
+        for (int w = 0; w < W; ++w) r[w] = 0;
+        for (int j = 0; j < m; ++j) r[j >> 3] |= (unsigned long long)codes[v * m + j] << (8 * (j & 7));
     }
-    // the lowest zero byte is flagged exactly (only bytes above a zero can be false hits)
-    const unsigned long long zb = (r - 0x0101010101010101ull) & ~r & 0x8080808080808080ull;
-    const int z = zb ? (__ffsll((long long)zb) - 1) >> 3 : 8;
-    const unsigned long long keep = z >= 7 ? ~0ull : ((1ull << (8 * (z + 1))) - 1);
-    key = __builtin_bswap64(r & keep);
-    row = r;
 }
 
-__device__ __forceinline__ unsigned key_digit(unsigned long long key, int j) {
-    return (unsigned)(key >> (56 - 8 * j)) & 0xFFu;
+// the index of the row's first 0 byte (W * 8 if none): the lowest flag of the zero-byte test
+// is exact (only flags above a zero byte can be false)
+template <int W>
+__device__ __forceinline__ int sort_first_zero(const unsigned long long* r) {
+    int z = 8 * W;
+#pragma unroll
+    for (int w = W - 1; w >= 0; --w) {
+        const unsigned long long zb = (r[w] - 0x0101010101010101ull) & ~r[w] & 0x8080808080808080ull;
+        if (zb) z = 8 * w + ((__ffsll((long long)zb) - 1) >> 3);
+    }
+    return z;
+}
+
+// key byte j of the row: its byte j while no 0 byte comes before it (strncmp stops there),
+// else 0
+template <int W>
+__device__ __forceinline__ unsigned row_digit(const unsigned long long* r, int z, int j) {
+    const unsigned b = (unsigned)(r[j >> 3] >> (8 * (j & 7))) & 0xFFu;
+    return j <= z ? b : 0u;
 }
 
 // lanes (among `valid`) holding the same 8-bit value as this lane
@@ -135,6 +153,7 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long match) {
 
 // digit counts of the first pass's byte position j (counts[256], zeroed by the caller); the
 // passes count the next pass's byte as they go
+template <int W>
 __global__ void __launch_bounds__(256)
 sort_digits(const uint8_t* __restrict__ codes, long long n, int m, int j, uint32_t* __restrict__ counts) {
     __shared__ uint32_t h[4][256];   // one histogram per wave
@@ -144,30 +163,31 @@ sort_digits(const uint8_t* __restrict__ codes, long long n, int m, int j, uint32
     constexpr int kPer = 8;   // rows per thread, loaded together
     for (long long v0 = (long long)blockIdx.x * blockDim.x * kPer + threadIdx.x; v0 < n;
          v0 += (long long)gridDim.x * blockDim.x * kPer) {
-        unsigned long long key[kPer];
+        unsigned long long row[kPer][W];
 #pragma unroll
         for (int i = 0; i < kPer; ++i) {
             const long long v = v0 + (long long)i * blockDim.x;
-            unsigned long long row;
-            key[i] = 0;
-            if (v < n) sort_row_key(codes, v, m, key[i], row);
+#pragma unroll
+            for (int w = 0; w < W; ++w) row[i][w] = 0;
+            if (v < n) sort_load_row<W>(codes, v, m, row[i]);
         }
 #pragma unroll
         for (int i = 0; i < kPer; ++i)
-            if (v0 + (long long)i * blockDim.x < n) atomicAdd(&h[wave][key_digit(key[i], j)], 1u);
+            if (v0 + (long long)i * blockDim.x < n)
+                atomicAdd(&h[wave][row_digit<W>(row[i], sort_first_zero<W>(row[i]), j)], 1u);
     }
     __syncthreads();
     const uint32_t c = h[0][threadIdx.x] + h[1][threadIdx.x] + h[2][threadIdx.x] + h[3][threadIdx.x];
     if (c) atomicAdd(counts + threadIdx.x, c);
 }
 
-// the last pass's u64 rows -> m bytes per row (m < 8)
+// the last pass's rows (W u64 words each) -> m bytes per row (m other than 8 and 16)
+template <int W>
 __global__ void __launch_bounds__(256)
 sort_unpack(const unsigned long long* __restrict__ rows, long long n, int m, uint8_t* __restrict__ codes) {
     const long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (v >= n) return;
-    const unsigned long long r = rows[v];
-    for (int q = 0; q < m; ++q) codes[v * m + q] = (uint8_t)(r >> (8 * q));
+    for (int q = 0; q < m; ++q) codes[v * m + q] = (uint8_t)(rows[v * W + (q >> 3)] >> (8 * (q & 7)));
 }
 
 __device__ __forceinline__ void st_store(unsigned long long* p, unsigned long long v) {
@@ -178,13 +198,12 @@ __device__ __forceinline__ unsigned long long st_load(const unsigned long long* 
 }
 
 // one stable counting pass by byte position j (digit counts of j in `counts`, the next
-// pass's byte jn counted into `counts_next`).  FIRST: rows come from the codes; LAST: the
-// rows go to the codes (never both in one launch: m >= 2)
-template <bool FIRST, bool LAST>
+// pass's byte j - 1 counted into `counts_next`).  Elements are rows of W u64 words.  FIRST:
+// rows come from the codes; LAST: the rows go to the codes (never both in one launch: m >= 2)
+template <bool FIRST, bool LAST, int W>
 __global__ void __launch_bounds__(kSortThreads)
 sort_pass(const uint8_t* __restrict__ codes_in, uint8_t* __restrict__ codes_out, long long n, int m,
-          int j, const unsigned long long* __restrict__ kin, const unsigned long long* __restrict__ rin,
-          unsigned long long* __restrict__ kout, unsigned long long* __restrict__ rout,
+          int j, const unsigned long long* __restrict__ rin, unsigned long long* __restrict__ rout,
           const uint32_t* __restrict__ counts, uint32_t* __restrict__ counts_next,
           unsigned long long* __restrict__ state, unsigned long long* __restrict__ ticket,
           unsigned long long ticket_base, unsigned epoch, int diag) {
@@ -200,30 +219,36 @@ sort_pass(const uint8_t* __restrict__ codes_in, uint8_t* __restrict__ codes_out,
     __syncthreads();
     const long long tile = s_tile;
     const long long base = tile * kSortTile + (long long)wave * 64 * kSortItems;
-    unsigned long long key[kSortItems], row[kSortItems];
+    unsigned long long row[kSortItems][W];
     uint32_t rank[kSortItems];
+    uint8_t dig[kSortItems];   // this pass's key byte of each row
     // every load first (the ranking below needs each key; issuing them all up front keeps
     // the tile's reads in flight together)
 #pragma unroll
     for (int it = 0; it < kSortItems; ++it) {
         const long long v = base + it * 64 + lane;
-        key[it] = 0;
-        row[it] = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) row[it][w] = 0;
         if (v < n) {
             if (FIRST) {
-                sort_row_key(codes_in, v, m, key[it], row[it]);
+                sort_load_row<W>(codes_in, v, m, row[it]);
+            } else if (W == 2) {
+                const uint4 q = reinterpret_cast<const uint4*>(rin)[v];
+                row[it][0] = (unsigned long long)q.x | ((unsigned long long)q.y << 32);
+                row[it][W - 1] = (unsigned long long)q.z | ((unsigned long long)q.w << 32);
             } else {
-                key[it] = kin[v];
-                row[it] = rin[v];
+                row[it][0] = rin[v];
             }
         }
     }
 #pragma unroll
     for (int it = 0; it < kSortItems; ++it) {
         const bool valid = base + it * 64 + lane < n;
-        if (!LAST && valid) atomicAdd(&hnext[wave & 1][key_digit(key[it], j - 1)], 1u);
+        const int z = sort_first_zero<W>(row[it]);
+        if (!LAST && valid) atomicAdd(&hnext[wave & 1][row_digit<W>(row[it], z, j - 1)], 1u);
         // lanes with this lane's digit, among the valid ones, in lane order
-        const unsigned d = key_digit(key[it], j);
+        const unsigned d = row_digit<W>(row[it], z, j);
+        dig[it] = (uint8_t)d;
         const unsigned long long match = match_digit(d, valid);
         const uint32_t below = lanes_below(match);
         // every lane reads the counter, then the group's lowest lane adds the group's size
@@ -300,31 +325,31 @@ sort_pass(const uint8_t* __restrict__ codes_in, uint8_t* __restrict__ codes_out,
     }
     __syncthreads();
     if (diag & 2) {   // (diagnostic: no scatter)
-        if (rank[0] == 0xFFFFFFFFu) kout[0] = key[0] + key[kSortItems - 1];
+        if (rank[0] == 0xFFFFFFFFu) rout[0] = row[0][0] + row[kSortItems - 1][W - 1];
         return;
     }
 #pragma unroll
     for (int it = 0; it < kSortItems; ++it) {
         const long long v = base + it * 64 + lane;
         if (v >= n) continue;
-        long long dst = (long long)wcnt[wave][key_digit(key[it], j)] + rank[it];
+        long long dst = (long long)wcnt[wave][dig[it]] + rank[it];
         if (diag) dst = dst < n ? dst : n - 1;   // (diagnostic runs: bases are wrong, stay in range)
-        if (LAST && m == 8) {
-            reinterpret_cast<unsigned long long*>(codes_out)[dst] = row[it];
-        } else if (LAST) {   // (m < 8: the rows are unpacked by sort_unpack)
-            rout[dst] = row[it];
+        // (the last pass writes 8- and 16-byte rows straight into the codes; other m go
+        // through sort_unpack)
+        unsigned long long* dstp = LAST && m == 8 * W ? reinterpret_cast<unsigned long long*>(codes_out)
+                                                      : rout;
+        if (W == 2) {
+            reinterpret_cast<uint4*>(dstp)[dst] =
+                make_uint4((uint32_t)row[it][0], (uint32_t)(row[it][0] >> 32),
+                           (uint32_t)row[it][W - 1], (uint32_t)(row[it][W - 1] >> 32));
         } else {
-            kout[dst] = key[it];
-            rout[dst] = row[it];
+            dstp[dst] = row[it][0];
         }
     }
 }
 
-}  // namespace
-
-extern "C" {
-
-static int sort_rows_radix(pqh_ctx_t* ctx, uint8_t* codes, long long n, int m) {
+template <int W>
+int sort_rows_radix(pqh_ctx_t* ctx, uint8_t* codes, long long n, int m) {
     const long long tiles = (n + kSortTile - 1) / kSortTile;
     if (tiles > ctx->sort_cap) {
         PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));   // no launch may still use it
@@ -343,18 +368,16 @@ static int sort_rows_radix(pqh_ctx_t* ctx, uint8_t* codes, long long n, int m) {
         ctx->sort_ticket_base = 0;
     }
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    const size_t eb = al((size_t)n * 8);
-    int rc = pqh_ensure_ws(ctx, 4 * eb + al(8 * 256 * 4));
+    const size_t eb = al((size_t)n * 8 * W);
+    int rc = pqh_ensure_ws(ctx, 2 * eb + al(16 * 256 * 4));
     if (rc) return rc;
     char* w = static_cast<char*>(ctx->ws);
-    unsigned long long* k0 = reinterpret_cast<unsigned long long*>(w);
-    unsigned long long* r0 = reinterpret_cast<unsigned long long*>(w + eb);
-    unsigned long long* k1 = reinterpret_cast<unsigned long long*>(w + 2 * eb);
-    unsigned long long* r1 = reinterpret_cast<unsigned long long*>(w + 3 * eb);
-    uint32_t* dcnt = reinterpret_cast<uint32_t*>(w + 4 * eb);
+    unsigned long long* r0 = reinterpret_cast<unsigned long long*>(w);
+    unsigned long long* r1 = reinterpret_cast<unsigned long long*>(w + eb);
+    uint32_t* dcnt = reinterpret_cast<uint32_t*>(w + 2 * eb);
     PQH_HIP(ctx, hipMemsetAsync(dcnt, 0, (size_t)m * 256 * 4, ctx->stream));
     const unsigned dgrid = (unsigned)std::min<long long>((n + 2047) / 2048, 1024);
-    hipLaunchKernelGGL(sort_digits, dim3(dgrid), dim3(256), 0, ctx->stream, codes, n, m, m - 1,
+    hipLaunchKernelGGL(sort_digits<W>, dim3(dgrid), dim3(256), 0, ctx->stream, codes, n, m, m - 1,
                        dcnt + (m - 1) * 256);
     PQH_LAUNCH_CHECK(ctx);
     unsigned long long* ticket = ctx->sort_state + ctx->sort_cap * 256;
@@ -369,14 +392,12 @@ static int sort_rows_radix(pqh_ctx_t* ctx, uint8_t* codes, long long n, int m) {
             ctx->sort_epoch = 1;
         }
         const bool first = p == 0, last = p == m - 1;
-        // (first: codes -> k0/r0; middle: ping-pong; last: -> codes)
-        const unsigned long long* kin = (p & 1) ? k0 : k1;
+        // (first: codes -> r0; middle: ping-pong; last: -> codes, or r0/r1 + unpack)
         const unsigned long long* rin = (p & 1) ? r0 : r1;
-        unsigned long long* kout = (p & 1) ? k1 : k0;
         unsigned long long* rout = (p & 1) ? r1 : r0;
 #define PQH_SORT_PASS(F, L)                                                                       \
-    hipLaunchKernelGGL((sort_pass<F, L>), dim3((unsigned)tiles), dim3(kSortThreads), 0, ctx->stream, \
-                       codes, codes, n, m, j, kin, rin, kout, rout, dcnt + j * 256,                \
+    hipLaunchKernelGGL((sort_pass<F, L, W>), dim3((unsigned)tiles), dim3(kSortThreads), 0,          \
+                       ctx->stream, codes, codes, n, m, j, rin, rout, dcnt + j * 256,              \
                        dcnt + (j > 0 ? j - 1 : 0) * 256, ctx->sort_state, ticket,                  \
                        ctx->sort_ticket_base, ctx->sort_epoch, diag)
         if (first) PQH_SORT_PASS(true, false);
@@ -385,15 +406,17 @@ static int sort_rows_radix(pqh_ctx_t* ctx, uint8_t* codes, long long n, int m) {
 #undef PQH_SORT_PASS
         PQH_LAUNCH_CHECK(ctx);
         ctx->sort_ticket_base += (unsigned long long)tiles;
-        if (last && m < 8) {
-            hipLaunchKernelGGL(sort_unpack, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+        if (last && m != 8 * W) {
+            hipLaunchKernelGGL(sort_unpack<W>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                                ctx->stream, rout, n, m, codes);
             PQH_LAUNCH_CHECK(ctx);
         }
     }
     return PQH_OK;
 }
+}  // namespace
 
+extern "C" {
 
 int pqh_sort_rows(pqh_ctx_t* ctx, void* d_codes, long long n, int m, void* d_tmp) {
     if (!ctx || n < 0 || m <= 0 || (n > 0 && !d_codes)) return PQH_ERR_ARG;
@@ -405,12 +428,14 @@ int pqh_sort_rows(pqh_ctx_t* ctx, void* d_codes, long long n, int m, void* d_tmp
         const char* e = std::getenv("PQH_SORT_IMPL");
         return e && !std::strcmp(e, "rocprim");
     }();
-    if (m >= 2 && m <= 8 && n < (1ll << 31) && !force_lib &&
-        (m != 8 || (reinterpret_cast<uintptr_t>(d_codes) & 7) == 0)) {
-        rc = sort_rows_radix(ctx, static_cast<uint8_t*>(d_codes), n, m);
+    const uintptr_t addr = reinterpret_cast<uintptr_t>(d_codes);
+    if (m >= 2 && m <= 16 && n < (1ll << 31) && !force_lib &&
+        (m != 8 || (addr & 7) == 0) && (m != 16 || (addr & 15) == 0)) {
+        rc = m <= 8 ? sort_rows_radix<1>(ctx, static_cast<uint8_t*>(d_codes), n, m)
+                    : sort_rows_radix<2>(ctx, static_cast<uint8_t*>(d_codes), n, m);
         if (rc != PQH_ERR_NOMEM) return rc;
-        // out of device memory for the in-tree sort's 32 B/row: the rocPRIM path below
-        // needs 24 B/row + its temp when the caller passes d_tmp
+        // out of device memory for the in-tree sort's 16 (m <= 8) or 32 B/row: the rocPRIM
+        // path below needs 24 B/row + its temp when the caller passes d_tmp
     }
     // workspace: keys in/out (u64), index in/out (u32), rocPRIM temp, row buffer if no d_tmp
     size_t temp = 0;

@@ -296,3 +296,15 @@ def test_shard_host_protocol():
     assert L.pqh_shard_stitch(3, ptrs, offs, nbs, out.ctypes.data, 12) == 0
     assert np.array_equal(out, np.packbits(bits))
     assert L.pqh_shard_stitch(3, ptrs, offs, nbs, out.ctypes.data, 11) != 0   # too small
+
+
+def test_histogram_partials_bounded_by_the_grid():
+    """pqh_histogram_partial_bytes: one partial image per 61,440-row chunk up to 64 chunks,
+    then a fixed number of images (the multi-round form) + the u32 carry accumulator, so the
+    125M-row shard of configs[2] needs ~18 MB instead of 2.1 GB (no GPU call)."""
+    from pq_huffman_amd.capi import lib
+    img = 32768 * 4
+    assert lib().pqh_histogram_partial_bytes(1_000_000, 8, 256) == 17 * 8 * img
+    big = lib().pqh_histogram_partial_bytes(125_000_000, 8, 256)
+    assert big <= 16 * 8 * img + 8 * 65536 * 4 + 256
+    assert lib().pqh_histogram_partial_bytes(10**10, 16, 256) <= 8 * 16 * img + 16 * 65536 * 4 + 256

@@ -133,6 +133,18 @@ def test_bench_path_sort_1m_all_rows(gpu, oracle):
     _check_against_oracle(gpu, oracle, x.cpu().numpy(), cent, codes, tabs, enc, dec, sort=True)
 
 
+def test_bench_path_deep_sort_1m_all_rows(gpu, oracle):
+    """configs[3] in the reference's default sort + context mode (`bench.py --config deep
+    --sort`): 16-byte rows through the hand-written radix sort (two words per row, 16
+    passes), then the context path, against the oracle on all 1,000,000 rows."""
+    torch, codec, ctx = gpu
+    xh = datagen.deep_like(1_000_000, 96, seed=33)
+    cent = datagen.lloyd_centroids(xh, 16, 256, iters=2, sample=30000, seed=6)
+    x = torch.from_numpy(xh).cuda()
+    pq, codes, counts, tabs, enc, dec = _bench_path(gpu, x, cent, sort=True)
+    _check_against_oracle(gpu, oracle, xh, cent, codes, tabs, enc, dec, sort=True)
+
+
 def test_configs2_shard_125m_rows(gpu, oracle):
     """BASELINE.json configs[2]: the per-rank shard (1e9 / 8 = 125M rows x 128-d, 64 GB)."""
     import bench

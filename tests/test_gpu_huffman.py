@@ -529,10 +529,12 @@ def _zero_heavy_rows(n, m, seed):
 
 @pytest.mark.parametrize("n,m", [(1, 8), (2, 8), (1000, 8), (1000, 16), (777, 3), (513, 12),
                                  (300, 1), (2000, 24), (2048, 8), (2049, 8), (4097, 2),
-                                 (50_000, 8), (30_001, 7), (100_000, 4), (300_000, 8)])
+                                 (50_000, 8), (30_001, 7), (100_000, 4), (300_000, 8),
+                                 (8193, 16), (40_000, 9), (20_001, 15), (300_000, 16)])
 def test_gpu_sort_rows_vs_oracle(gpu, oracle, n, m):
-    """2 <= m <= 8 runs the hand-written radix passes (tiles of 2,048 rows chained by the
-    look-back: the sizes straddle tile edges), other m the rocPRIM chunk sort."""
+    """2 <= m <= 16 runs the hand-written radix passes (one or two words per row; tiles of
+    8,192 rows chained by the look-back: the sizes straddle tile edges), m = 1 and m > 16
+    the rocPRIM chunk sort."""
     torch, codec, ctx = gpu
     for seed in (1, 2):
         a = _zero_heavy_rows(n, m, seed)
@@ -564,9 +566,11 @@ def test_gpu_sort_rows_radix_vs_rocprim(gpu):
         np.testing.assert_array_equal(d.cpu().numpy(), np.load(f))
 
 
-def test_gpu_sort_full_size_vs_oracle(gpu, oracle):
+@pytest.mark.parametrize("m", [8, 16])
+def test_gpu_sort_full_size_vs_oracle(gpu, oracle, m):
     torch, codec, ctx = gpu
-    a = datagen.skewed_codes(1_000_000, 8, 256, seed=5)
+    a = datagen.skewed_codes(1_000_000, m, 256, seed=5, stay=0)
+    a[::5] = a[7]                                   # one key repeated across every tile
     d = torch.from_numpy(a).cuda()
     tmp = torch.empty_like(d)
     codec.sort_rows(ctx, d, tmp)
@@ -606,3 +610,41 @@ def test_gpu_sort_key_words_and_local_sort(gpu, oracle):
                                           shard.library_sort(ctx))
         torch.cuda.synchronize()
         assert np.array_equal(out.cpu().numpy(), oracle.sort_rows(a))
+
+
+def _long_codes(n, m, seed):
+    """skewed codes with long constant runs: (0, 0) and (255, 255) pairs far above the
+    multi-round form's 4,095 carry threshold in every chunk they cover"""
+    codes = datagen.skewed_codes(n, m, seed=seed, stay=0)
+    codes[300_000:500_000] = 0
+    codes[900_000:1_030_000] = 255
+    codes[1_500_000:1_500_000 + 61_440] = 7   # one whole chunk of one pair (61,440 counts)
+    return codes
+
+
+@pytest.mark.parametrize("m", [6, 8, 16])
+def test_context_histogram_multi_round(gpu, oracle, m):
+    """Past 4 groups' worth of chunks the context histogram counts several chunks per
+    workgroup in one u16 image, moving counters above 4,095 into a u32 accumulator between
+    chunks: its partials stay bounded by the grid (not by n).  4.2M rows (69 chunks: 5 to 9
+    rounds) with long constant runs, wave form (m = 8, 16) and thread form (m = 6), one call
+    and partial + reduce, set and accumulate, with a halo row."""
+    torch, codec, ctx = gpu
+    n = 4_200_001
+    codes = _long_codes(n, m, 90 + m)
+    cd = torch.from_numpy(np.ascontiguousarray(codes)).cuda()
+    want = oracle.histogram(codes, 256, True)
+    assert want.max() > 100_000
+    got = codec.counts_to_host(codec.histogram(ctx, cd, 256, True))
+    assert np.array_equal(got, want)
+    # the bounded partial buffer: far below one image per chunk
+    assert codec.histogram_partial_bytes(n, m, 256) < 69 * m * 32768 * 4 // 2
+    parts = torch.empty(codec.histogram_partial_bytes(n, m, 256), dtype=torch.uint8, device="cuda")
+    junk = torch.full((m, 65536), 777, dtype=torch.int32, device="cuda")
+    for rep in range(2):   # the reduce clears the accumulator for the next launch
+        codec.histogram_partial(ctx, cd, 256, parts)
+        codec.histogram_reduce(ctx, parts, n, m, 256, junk)
+        assert np.array_equal(codec.counts_to_host(junk), want), rep
+    codec.histogram_partial(ctx, cd[1:], 256, parts, prev_row=cd[0])
+    codec.histogram_reduce(ctx, parts, n - 1, m, 256, junk, accumulate=True)
+    assert np.array_equal(codec.counts_to_host(junk), 2 * want)
