@@ -144,6 +144,10 @@ def parse():
     ap.add_argument("--astreams", type=int, default=1,
                     help="assignment + histogram streams, batch i on stream i %% N (N > 1: the "
                          "next batch's assignment grid fills the previous one's tail)")
+    ap.add_argument("--code-layout", choices=["rows", "parts"], default="rows",
+                    help="parts: the assignment writes part-major codes (whole lines) that the "
+                         "histogram and the row encoder read directly (one rank, no sort, "
+                         "u8 codes, m = 8 or 16); rows: pq_indices.bvecsl order")
     ap.add_argument("--sort-on", choices=["assign", "lanes"], default="lanes",
                     help="--sort: the sort (and then the histogram) of batch i on its table lane "
                          "after its assignment (default), or on the assignment stream")
@@ -404,7 +408,11 @@ def main():
     # codes / counts buffers: the assignment runs up to `slots` batches ahead of the oldest
     # batch not yet encoded
     slots = nl + max(1, args.extra_slots)
-    codes = [torch.empty((n, m), dtype=code_t, device=dev) for _ in range(slots)]
+    # part-major codes (--code-layout parts): codes[s] is (m, n), part i's codes in row i
+    pm = args.code_layout == "parts" and not args.sort and world == 1 and \
+        code_t == torch.uint8 and m in (8, 16) and not serial
+    codes = [torch.empty((m, n) if pm else (n, m), dtype=code_t, device=dev)
+             for _ in range(slots)]
     counts = [torch.zeros((m, items), dtype=torch.int32, device=dev) for _ in range(slots)]
     halo = [None] * slots
     ev_hist = [torch.cuda.Event() for _ in range(slots)]
@@ -505,8 +513,13 @@ def main():
         if used[s]:                  # the slot's previous batch: tables built (counts free)
             st.wait_event(ev_tab[s])
         e = rec("hist", st)
-        if hist_split:
+        if hist_split and pm:
+            codec.histogram_partial_parts(c, codes[s], n, k, hparts[s], prev_row=halo[s])
+        elif hist_split:
             codec.histogram_partial(c, codes[s], k, hparts[s], prev_row=halo[s])
+        elif pm:
+            codec.histogram_parts(c, codes[s], n, k, ctxm, prev_row=halo[s], counts=counts[s],
+                                  accumulate=False)
         else:
             codec.histogram(c, codes[s], k, ctxm, prev_row=halo[s], counts=counts[s],
                             accumulate=False)        # overwrites: no zeroing pass
@@ -565,7 +578,10 @@ def main():
             if used[s]:              # the slot's previous batch: encoded (codes[s] free) ...
                 sF.wait_event(ev_enc[s])
             e = rec("assign", sF)
-            apq[i % na].assign(x, codes[s], ctx=cF)
+            if pm:
+                apq[i % na].assign_parts(x, codes[s], ctx=cF)
+            else:
+                apq[i % na].assign(x, codes[s], ctx=cF)
             done(e, sF)
             if args.sort and not sort_on_lane:   # stable strncmp-key sort (in place)
                 e = rec("sort", sF)
@@ -592,7 +608,7 @@ def main():
             # waits for RCCL; the pair (previous shard's last row, first row) is one more
             # count per part, exactly what pqh_histogram's prev_row adds
             tc = time.perf_counter()
-            halo[s] = shard.exchange_halo(codes[s][-1], world, rank) if ctxm else None
+            halo[s] = shard.exchange_halo(codes[s][-1], world, rank) if ctxm and not pm else None
             acc["collectives"] += time.perf_counter() - tc if state["timed"] else 0.0
             if sort_on_lane:         # the batch's sort, on its lane, before its histogram
                 e = rec("sort", sL)
@@ -698,6 +714,9 @@ def main():
                 acc["collectives"] += time.perf_counter() - tc if state["timed"] else 0.0
                 codec.encode_write_at(c, tj, codes[s], out[j], goff, raw_first, halo[s],
                                       args.chunk, coff[j], cprev[j], total=tot_dev[j])
+            elif pm:   # the row encoder gathering each row from the part runs
+                codec.encode_write_parts(c, tj, codes[s], n, out[j], 0, raw_first, halo[s],
+                                         args.chunk, coff[j], cprev[j], total=tot_dev[j])
             else:
                 # one pass: look-back offsets, every word stored once (no zeroing of `out`)
                 codec.encode_write(c, tj, codes[s], out[j], 0, raw_first, halo[s],
@@ -754,7 +773,10 @@ def main():
         tw = time.perf_counter()
         while (time.perf_counter() - tw) * 1e3 < args.device_warmup_ms:
             for _ in range(8):
-                pq.assign(x, codes[0], ctx=ctx)
+                if pm:
+                    pq.assign_parts(x, codes[0], ctx=ctx)
+                else:
+                    pq.assign(x, codes[0], ctx=ctx)
             torch.cuda.synchronize()
         dw_ms = (time.perf_counter() - tw) * 1e3
     run(args.warmup)
@@ -801,7 +823,8 @@ def main():
     for c in elanes:
         codec.decode_status(c)
         codec.encode_status(c)
-    assert torch.equal(dec[j_last], codes[s_last]), "round trip mismatch"
+    rows_last = codec.transpose_codes(ctx, codes[s_last], n) if pm else codes[s_last]
+    assert torch.equal(dec[j_last], rows_last), "round trip mismatch"
     if lib_shard:   # every rank's pqh_shard_encode_write succeeded (no sentinel length)
         shard.status(elanes[j_last], offs[j_last])
         for j, sm in enumerate(shard_min):   # ... for every batch, not only the last
@@ -812,7 +835,7 @@ def main():
     if args.dump:   # the last batch's shard stream + codes, gathered to rank 0 (tests)
         nb = (int(tot_dev[j_last].item()) + 7) // 8 + 8
         goff = int(state["goff"].item()) if world > 1 else 0
-        mine = {"codes": codes[s_last].cpu().numpy(), "bits": int(tot_dev[j_last].item()),
+        mine = {"codes": rows_last.cpu().numpy(), "bits": int(tot_dev[j_last].item()),
                 "goff": goff, "buf": out[j_last][:nb].cpu().numpy()}
         allp = [None] * world
         if world > 1:
@@ -867,6 +890,7 @@ def main():
                                    + ("rows sorted by the strncmp key (the reference's default "
                                       "mode)" if args.sort else "no sort"),
                        "sort": bool(args.sort),
+                       "code_layout": "parts" if pm else "rows",
                        "vectors_per_gpu": n, "d": d, "m": m, "k": k,
                        "mode": "ctx" if ctxm else "noctx",
                        "chunk_vectors": args.chunk, "parallelism": f"dp{world} row shards",
@@ -926,7 +950,7 @@ def main():
         if world == 1:
             # (after the timed region, on a scratch copy of a 1M-row slice)
             r1 = min(n, 1_000_000)
-            res["pcie_ms"] = pcie_ms(torch, x[:r1].clone(), codes[s_last][:r1],
+            res["pcie_ms"] = pcie_ms(torch, x[:r1].clone(), rows_last[:r1],
                                      (bits_per_vec * r1 + 7) // 8)
             res["pcie_ms"]["rows"] = r1
         if not args.no_cpu_baseline and world == 1:

@@ -84,6 +84,14 @@ int pqh_pq_destroy(pqh_pq_t* pq);
  * contexts on different streams may assign concurrently. */
 int pqh_pq_assign(pqh_ctx_t* ctx, const pqh_pq_t* pq, const float* d_x, long long n,
                   long long ld_x, void* d_codes, uint32_t* d_counts, int mode);
+/* pqh_pq_assign writing the codes PART-MAJOR: codes of part i at d_codes[i * ld_codes + v]
+ * (ld_codes >= n elements): each subspace's codes are contiguous, so the kernel stores
+ * whole lines and a part's histogram reads one contiguous run (pqh_histogram_parts,
+ * pqh_encode_write_parts consume this layout; pqh_transpose_codes converts to rows).
+ * d_counts: as pqh_pq_assign (K <= 256 only). */
+int pqh_pq_assign_parts(pqh_ctx_t* ctx, const pqh_pq_t* pq, const float* d_x, long long n,
+                        long long ld_x, void* d_codes, long long ld_codes, uint32_t* d_counts,
+                        int mode);
 /* diagnostics of the last pqh_pq_assign (synchronises): vectors x parts re-ranked
  * exactly because the screening could not separate the best two centroids. */
 int pqh_pq_last_rerank_count(pqh_ctx_t* ctx, unsigned long long* count);
@@ -119,6 +127,15 @@ int pqh_histogram_set(pqh_ctx_t* ctx, const void* d_codes, long long n, int m, i
  * pqh_histogram_partial_bytes(n, m, k) bytes, K <= 256), then counts (+)= their sum
  * (set != 0: overwrite).  Same pairs as pqh_histogram with context = 1. */
 long long pqh_histogram_partial_bytes(long long n, int m, int k);
+/* The same histograms over PART-MAJOR codes (pqh_pq_assign_parts: part i's codes at
+ * d_codes[i * ld_codes + v]); set != 0 overwrites the counts.  d_prev_row stays a row of m
+ * codes. */
+int pqh_histogram_parts(pqh_ctx_t* ctx, const void* d_codes, long long ld_codes, long long n,
+                        int m, int k, int context, const void* d_prev_row, uint32_t* d_counts,
+                        int set);
+int pqh_histogram_partial_parts(pqh_ctx_t* ctx, const void* d_codes, long long ld_codes,
+                                long long n, int m, int k, const void* d_prev_row,
+                                void* d_partials);
 int pqh_histogram_partial(pqh_ctx_t* ctx, const void* d_codes, long long n, int m, int k,
                           const void* d_prev_row, void* d_partials);
 int pqh_histogram_reduce(pqh_ctx_t* ctx, const void* d_partials, long long n, int m, int k,
@@ -212,6 +229,19 @@ int pqh_encode_write_at(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_cod
                         unsigned long long out_bytes, int chunk_vectors,
                         unsigned long long* d_chunk_offsets, void* d_chunk_prev,
                         unsigned long long* d_total_bits);
+
+/* pqh_encode_write over PART-MAJOR codes (pqh_pq_assign_parts; part i of vector v at
+ * d_codes[i * ld_codes + v]): the same stream, chunk index and chunk_prev rows.  The row
+ * encoder only: K <= 256 and m = 8 or 16 (else PQH_ERR_UNSUPPORTED). */
+int pqh_encode_write_parts(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes,
+                           long long ld_codes, long long n, int raw_first, const void* d_prev_row,
+                           unsigned long long bit_offset, unsigned char* d_out,
+                           unsigned long long out_bytes, int chunk_vectors,
+                           unsigned long long* d_chunk_offsets, void* d_chunk_prev,
+                           unsigned long long* d_total_bits);
+/* part-major codes [m][ld_parts] -> rows [n][m] (pq_indices.bvecsl order); code_bytes 1 or 2. */
+int pqh_transpose_codes(pqh_ctx_t* ctx, const void* d_parts, long long ld_parts, long long n, int m,
+                        int code_bytes, void* d_rows);
 
 /* Synchronises; PQH_ERR_CAPACITY if a pqh_encode_write since the last call had to drop
  * words because out_bytes was too small (nothing is written out of bounds). */

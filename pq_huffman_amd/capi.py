@@ -122,12 +122,15 @@ SIGNATURES = [
     ("pqh_device_count", I, [P]),
     ("pqh_pq_create", I, [P, P, I, I, I, P]), ("pqh_pq_destroy", I, [P]),
     ("pqh_pq_assign", I, [P, P, P, LL, LL, P, P, I]),
+    ("pqh_pq_assign_parts", I, [P, P, P, LL, LL, P, LL, P, I]),
     ("pqh_pq_last_rerank_count", I, [P, P]),
     ("pqh_pq_error", I, [P, P, P, LL, LL, P, P]),
     ("pqh_pq_reconstruct", I, [P, P, P, LL, P, LL]),
     ("pqh_kmeans_train", I, [P, P, LL, LL, I, I, I, I, P]),
     ("pqh_histogram", I, [P, P, LL, I, I, I, P, P]),
     ("pqh_histogram_set", I, [P, P, LL, I, I, I, P, P]),
+    ("pqh_histogram_parts", I, [P, P, LL, LL, I, I, I, P, P, I]),
+    ("pqh_histogram_partial_parts", I, [P, P, LL, LL, I, I, P, P]),
     ("pqh_histogram_partial_bytes", LL, [LL, I, I]),
     ("pqh_histogram_partial", I, [P, P, LL, I, I, P, P]),
     ("pqh_histogram_reduce", I, [P, P, LL, I, I, P, I]),
@@ -143,6 +146,8 @@ SIGNATURES = [
     ("pqh_encode_size", I, [P, P, P, LL, I, P, P]),
     ("pqh_encode_write", I, [P, P, P, LL, I, P, ULL, P, ULL, I, P, P, P]),
     ("pqh_encode_write_at", I, [P, P, P, LL, I, P, P, P, ULL, I, P, P, P]),
+    ("pqh_encode_write_parts", I, [P, P, P, LL, LL, I, P, ULL, P, ULL, I, P, P, P]),
+    ("pqh_transpose_codes", I, [P, P, LL, LL, I, I, P]),
     ("pqh_decode", I, [P, P, P, ULL, LL, I, I, P, P, P]),
     ("pqh_decode_status", I, [P]), ("pqh_encode_status", I, [P]),
     ("pqh_chunk_index_host", I, [P, P, ULL, LL, I, I, P, P]),

@@ -129,6 +129,19 @@ class PQ:
                                   _ptr(counts), mode), "pqh_pq_assign")
         return codes
 
+    def assign_parts(self, x, parts=None, counts=None, mode: int = 0, ctx: Context = None):
+        """codes of x PART-MAJOR: parts (m, >= n), part i's codes contiguous in parts[i]
+        (pqh_pq_assign_parts: the kernel stores whole lines)."""
+        torch = _torch()
+        n = x.shape[0]
+        if parts is None:
+            parts = torch.empty((self.m, n), dtype=self.code_dtype, device=x.device)
+        c = ctx or self.ctx
+        check(lib().pqh_pq_assign_parts(c.ptr, self.ptr, _ptr(x), n, x.stride(0), _ptr(parts),
+                                        parts.stride(0), _ptr(counts), mode),
+              "pqh_pq_assign_parts")
+        return parts
+
     def rerank_count(self, ctx: Context = None) -> int:
         v = ctypes.c_ulonglong(0)
         check(lib().pqh_pq_last_rerank_count((ctx or self.ctx).ptr, ctypes.byref(v)))
@@ -361,6 +374,41 @@ def histogram_partial(ctx: Context, codes, k: int, partials, prev_row=None):
     return partials
 
 
+def histogram_parts(ctx: Context, parts, n: int, k: int, context: bool, prev_row=None,
+                    counts=None, accumulate: bool = True):
+    """histogram() of part-major codes parts (m, >= n) (pqh_histogram_parts)."""
+    torch = _torch()
+    m = parts.shape[0]
+    items = k * k if context else k
+    if counts is None:
+        counts = torch.empty((m, items), dtype=torch.int32, device=parts.device)
+        accumulate = False
+    check(lib().pqh_histogram_parts(ctx.ptr, _ptr(parts), parts.stride(0), n, m, k, int(context),
+                                    _ptr(prev_row), _ptr(counts), 0 if accumulate else 1),
+          "pqh_histogram_parts")
+    return counts
+
+
+def histogram_partial_parts(ctx: Context, parts, n: int, k: int, partials, prev_row=None):
+    """histogram_partial() of part-major codes (pqh_histogram_partial_parts)."""
+    m = parts.shape[0]
+    check(lib().pqh_histogram_partial_parts(ctx.ptr, _ptr(parts), parts.stride(0), n, m, k,
+                                            _ptr(prev_row), _ptr(partials)),
+          "pqh_histogram_partial_parts")
+    return partials
+
+
+def transpose_codes(ctx: Context, parts, n: int, rows=None):
+    """part-major codes (m, >= n) -> rows (n, m) (pqh_transpose_codes)."""
+    torch = _torch()
+    m = parts.shape[0]
+    if rows is None:
+        rows = torch.empty((n, m), dtype=parts.dtype, device=parts.device)
+    check(lib().pqh_transpose_codes(ctx.ptr, _ptr(parts), parts.stride(0), n, m,
+                                    parts.element_size(), _ptr(rows)), "pqh_transpose_codes")
+    return rows
+
+
 def histogram_reduce(ctx: Context, partials, n: int, m: int, k: int, counts,
                      accumulate: bool = False):
     """Second half: counts (+)= the sum of the partials (pqh_histogram_reduce)."""
@@ -416,6 +464,18 @@ def encode_write(ctx: Context, tables: Tables, codes, out, bit_offset: int = 0, 
                                  chunk_vectors, _ptr(chunk_offsets), _ptr(chunk_prev),
                                  _ptr(total)),
           "pqh_encode_write: " + ctx.last_error())
+    return total
+
+
+def encode_write_parts(ctx: Context, tables: Tables, parts, n: int, out, bit_offset: int = 0,
+                       raw_first: int = 1, prev_row=None, chunk_vectors: int = 64,
+                       chunk_offsets=None, chunk_prev=None, total=None):
+    """encode_write() of part-major codes parts (m, >= n) (pqh_encode_write_parts)."""
+    check(lib().pqh_encode_write_parts(ctx.ptr, tables.ptr, _ptr(parts), parts.stride(0), n,
+                                       raw_first, _ptr(prev_row), bit_offset, _ptr(out),
+                                       out.numel(), chunk_vectors, _ptr(chunk_offsets),
+                                       _ptr(chunk_prev), _ptr(total)),
+          "pqh_encode_write_parts: " + ctx.last_error())
     return total
 
 

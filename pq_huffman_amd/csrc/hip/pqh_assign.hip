@@ -446,7 +446,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
                CodeT* __restrict__ codes, uint32_t* __restrict__ counts,
                unsigned long long* __restrict__ rerank, uint32_t* __restrict__ sched, int gx,
                unsigned long long* __restrict__ rerank_next, uint32_t* __restrict__ sched_next,
-               int prio) {
+               int prio, long long ldc) {
     using P = Plan<D>;
     constexpr int K = KT * 32;
     constexpr bool kLdsA = KT <= 8;
@@ -549,8 +549,13 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     const unsigned xh_off = HALF ? 32u * (unsigned)h : 0u;
     const unsigned xlane_off = __umul24((unsigned)r, ldx4) + xh_off;
     const char* const xm = reinterpret_cast<const char*>(x + (long long)m * D);
-    const unsigned code_lane_off = (unsigned)r * (unsigned)m_total * (unsigned)sizeof(CodeT);
-    const unsigned code_pair_off = (unsigned)lane * (unsigned)m_total * (unsigned)sizeof(CodeT);
+    // codes: row-major [n][m_total] (ldc = 0: pq_indices.bvecsl order), or part-major
+    // [m_total][ldc] -- then a wave's 64 codes of a chunk are 64 contiguous bytes (whole
+    // lines from one wave instead of one byte in every 8 from 8 subspaces' workgroups)
+    const long long crs = ldc ? 1 : m_total;   // (uniform) row stride in codes
+    CodeT* const cbase = codes + (ldc ? (long long)m * ldc : (long long)m);
+    const unsigned code_lane_off = (unsigned)r * (unsigned)crs * (unsigned)sizeof(CodeT);
+    const unsigned code_pair_off = (unsigned)lane * (unsigned)crs * (unsigned)sizeof(CodeT);
     auto load_x = [&](int b, float* dst) {
 #ifdef PQH_ASSIGN_NOMEM   // diagnostic: every chunk re-reads the first 64 blocks (cache hits)
         b &= 63;
@@ -875,7 +880,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
             // every lane stores its vector's code (the lower half only for a self-merged
             // block), unless the vector waits in the queue
             if (valid && own_lane && !(slow && deferred)) {
-                *reinterpret_cast<CodeT*>(reinterpret_cast<char*>(codes + ((blk0 + ba) * 32 * m_total + m)) +
+                *reinterpret_cast<CodeT*>(reinterpret_cast<char*>(cbase + (blk0 + ba) * 32 * crs) +
                                           (pair ? code_pair_off : code_lane_off)) = (CodeT)code;
                 if (kLdsA && counts) atomicAdd(&hist[wave][code], 1u);
             }
@@ -891,7 +896,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
             float q = 0.0f;
 #pragma unroll
             for (int j = 0; j < XD; ++j) q += xs[b][j];
-            if (vv < n && h == 0) codes[vv * m_total + m] = (CodeT)(int)q;
+            if (vv < n && h == 0) cbase[vv * crs] = (CodeT)(int)q;
         }
         return;
 #endif
@@ -1092,7 +1097,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         if (ob < best || (ob == best && oi < bidx)) { best = ob; bidx = oi; }
         if (valid && h == 0) {
             const int code = bidx == 0x7FFFFFFF ? 0 : bidx;
-            codes[v * m_total + m] = (CodeT)code;
+            cbase[v * crs] = (CodeT)code;
             if (kLdsA && counts) atomicAdd(&hist[wave][code], 1u);
         }
 #ifdef PQH_ASSIGN_STAMPS
@@ -1182,7 +1187,8 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
 template <typename CodeT>
 __global__ void pq_assign_exact(const float* __restrict__ x, long long n, long long ldx, int m_total,
                                 int k, int dsub, const float* __restrict__ cent,
-                                CodeT* __restrict__ codes, uint32_t* __restrict__ counts) {
+                                CodeT* __restrict__ codes, uint32_t* __restrict__ counts,
+                                long long ldc) {
 #pragma clang fp contract(off)
     const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= n * m_total) return;
@@ -1200,7 +1206,7 @@ __global__ void pq_assign_exact(const float* __restrict__ x, long long n, long l
         }
         if (acc < best) { best = acc; code = c; }
     }
-    codes[gid] = (CodeT)code;
+    codes[ldc ? (long long)m * ldc + v : gid] = (CodeT)code;   // (ldc: part-major)
     if (counts) atomicAdd(&counts[(long long)m * k + code], 1u);
 }
 
@@ -1342,7 +1348,7 @@ int plan_pa(int dsub) {
 
 template <typename CodeT>
 int launch_mfma(pqh_ctx* ctx, pqh_pq* pq, const float* x, long long n, long long ldx,
-                CodeT* codes, uint32_t* counts) {
+                CodeT* codes, uint32_t* counts, long long ldc) {
     const long long nblk = (n + 31) / 32;
     const int groups = pq->m;   // grid y: one subspace per workgroup
     dim3 block(64 * kWavesPerWG);
@@ -1375,7 +1381,7 @@ int launch_mfma(pqh_ctx* ctx, pqh_pq* pq, const float* x, long long n, long long
                            0, ctx->stream, x, n, ldx, pq->m, pq->d_afrag, pq->d_cn, pq->d_cent, \
                            pq->d_cmax, pq->d_sqc, codes, counts, rr, sched, (int)gx,         \
                            rr_next, sched ? ctx->d_sched + (1 - ring) * kSchedSet : nullptr, \
-                           prio);                                                             \
+                           prio, ldc);                                                        \
         PQH_LAUNCH_CHECK(ctx);                                                              \
         break;                                                                              \
     }
@@ -1409,12 +1415,12 @@ int launch_mfma(pqh_ctx* ctx, pqh_pq* pq, const float* x, long long n, long long
 
 template <typename CodeT>
 int launch_exact(pqh_ctx* ctx, pqh_pq* pq, const float* x, long long n, long long ldx,
-                 CodeT* codes, uint32_t* counts) {
+                 CodeT* codes, uint32_t* counts, long long ldc) {
     const long long total = n * pq->m;
     if (total == 0) return PQH_OK;
     hipLaunchKernelGGL((pq_assign_exact<CodeT>), dim3((unsigned)((total + 255) / 256)), dim3(256),
                        0, ctx->stream, x, n, ldx, pq->m, pq->k, pq->dsub, pq->d_cent, codes,
-                       counts);
+                       counts, ldc);
     PQH_LAUNCH_CHECK(ctx);
     return PQH_OK;
 }
@@ -1491,13 +1497,16 @@ int pqh_pq_destroy(pqh_pq_t* pq) {
     return PQH_OK;
 }
 
-int pqh_pq_assign(pqh_ctx_t* ctx, const pqh_pq_t* cpq, const float* d_x, long long n,
-                  long long ld_x, void* d_codes, uint32_t* d_counts, int mode) {
+}  // extern "C"
+
+// ldc = 0: row-major codes [n][m] (pq_indices.bvecsl); ldc >= n: part-major [m][ldc]
+static int assign_impl(pqh_ctx_t* ctx, const pqh_pq_t* cpq, const float* d_x, long long n,
+                       long long ld_x, void* d_codes, long long ldc, uint32_t* d_counts, int mode) {
     pqh_pq* pq = const_cast<pqh_pq*>(cpq);
     // any context of the codebook's device may run the assignment (its stream, its
     // work-queue heads and counters), so several streams can assign concurrently
     if (!ctx || !pq || pq->ctx->device != ctx->device || (n > 0 && (!d_x || !d_codes)) || n < 0 ||
-        ld_x < (long long)pq->m * pq->dsub)
+        ld_x < (long long)pq->m * pq->dsub || (ldc != 0 && ldc < n))
         return PQH_ERR_ARG;
     int rc = pqh_use_device(ctx);
     if (rc) return rc;
@@ -1512,27 +1521,42 @@ int pqh_pq_assign(pqh_ctx_t* ctx, const pqh_pq_t* cpq, const float* d_x, long lo
         PQH_HIP(ctx, hipMemsetAsync(ctx->d_diag + 6, 0, sizeof(unsigned long long), ctx->stream));
     }
     if (n == 0) return PQH_OK;
+    if (ldc && pq->k > 256 && d_counts) return PQH_ERR_UNSUPPORTED;
     // the MFMA kernel queues re-rank rows as 32-bit indices: at most 2^30 rows a launch
     constexpr long long kLaunchRows = 1ll << 30;
     auto pieces = [&](auto* c, uint32_t* counts) {
         for (long long off = 0; off < n; off += kLaunchRows) {
             const int r = launch_mfma(ctx, pq, d_x + off * ld_x, std::min(kLaunchRows, n - off),
-                                      ld_x, c + off * pq->m, counts);
+                                      ld_x, c + (ldc ? off : off * pq->m), counts, ldc);
             if (r) return r;
         }
         return (int)PQH_OK;
     };
     if (pq->k <= 256) {
         uint8_t* c = static_cast<uint8_t*>(d_codes);
-        return mfma ? pieces(c, d_counts) : launch_exact(ctx, pq, d_x, n, ld_x, c, d_counts);
+        return mfma ? pieces(c, d_counts) : launch_exact(ctx, pq, d_x, n, ld_x, c, d_counts, ldc);
     }
     uint16_t* c16 = static_cast<uint16_t*>(d_codes);
-    if (!mfma) return launch_exact(ctx, pq, d_x, n, ld_x, c16, d_counts);
+    if (!mfma) return launch_exact(ctx, pq, d_x, n, ld_x, c16, d_counts, ldc);
     // K = 4096: the screening kernel keeps no per-workgroup histogram (16 KB of counters per
     // wave); the requested counts come from the histogram kernel over the codes just written
     rc = pieces(c16, nullptr);
     if (rc || !d_counts) return rc;
     return pqh_histogram(ctx, d_codes, n, pq->m, pq->k, 0, nullptr, d_counts);
+}
+
+extern "C" {
+
+int pqh_pq_assign(pqh_ctx_t* ctx, const pqh_pq_t* pq, const float* d_x, long long n,
+                  long long ld_x, void* d_codes, uint32_t* d_counts, int mode) {
+    return assign_impl(ctx, pq, d_x, n, ld_x, d_codes, 0, d_counts, mode);
+}
+
+int pqh_pq_assign_parts(pqh_ctx_t* ctx, const pqh_pq_t* pq, const float* d_x, long long n,
+                        long long ld_x, void* d_codes, long long ld_codes, uint32_t* d_counts,
+                        int mode) {
+    if (ld_codes < n || ld_codes <= 0) return PQH_ERR_ARG;
+    return assign_impl(ctx, pq, d_x, n, ld_x, d_codes, ld_codes, d_counts, mode);
 }
 
 // diagnostics: the per-wave stamps of the last assignment launch (PQH_ASSIGN_STAMPS builds;

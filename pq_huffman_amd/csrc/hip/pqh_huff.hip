@@ -185,12 +185,16 @@ __device__ __forceinline__ unsigned wave_shr1(unsigned v, unsigned first) {
 // rows (16 cache lines) instead of one line per lane; a row's predecessor is the previous
 // lane's row (a DPP wave shift), the tile's first row's the previous tile's last (readlane).
 // G tiles' loads are issued before their counter updates.
-template <int BLK, int G>
+// ldc > 0: the codes are part-major ([m_total][ldc], pqh_pq_assign_parts): part m's rows are
+// contiguous, so a lane's 4-byte load holds 4 consecutive rows (256 rows per wave load, no
+// byte of another part read).
+template <int BLK, int G, bool PM = false>
 __global__ void __launch_bounds__(BLK)
 hist_ctx_w(const uint8_t* __restrict__ codes, long long n, int m_total, int k,
            const uint8_t* __restrict__ prev_row, const int* __restrict__ d_rawf,
            uint32_t* __restrict__ partial, int split, int chunks, int rounds,
-           uint32_t* __restrict__ acc, int prio) {
+           uint32_t* __restrict__ acc, int prio, long long ldc_arg) {
+    const long long ldc = PM ? ldc_arg : 0;   // (row-major instances: the old register budget)
     extern __shared__ uint32_t pairs[];   // (k / split) * k u16 counters packed two per word
     pqh_set_prio(prio);
     if (d_rawf && *d_rawf) prev_row = nullptr;   // decided on the device (pqh_shard_encode)
@@ -229,12 +233,41 @@ hist_ctx_w(const uint8_t* __restrict__ codes, long long n, int m_total, int k,
         hist_flush_carry(pairs, words, (unsigned)m * (unsigned)(k * k) + plo * (unsigned)k, k, acc);
     const long long w0 = (long long)chunk * kHistChunk + (long long)wv * kR;
     const int cnt = (int)max(0ll, min(n - w0, (long long)kR));   // rows this wave counts
-    unsigned carry = w0 > 0 ? (w0 - 1 < n ? (unsigned)codes[(w0 - 1) * m_total + m] : ~0u)
+    const uint8_t* const pm = codes + (long long)m * ldc;        // (ldc > 0) part m's codes
+    unsigned carry = w0 > 0 ? (w0 - 1 < n ? (unsigned)(PM ? pm[w0 - 1] : codes[(w0 - 1) * m_total + m]) : ~0u)
                             : (prev_row ? (unsigned)prev_row[m] : ~0u);
     carry = (unsigned)__builtin_amdgcn_readfirstlane((int)carry);
     if (first) __syncthreads();   // the counters are zeroed
     first = false;
-    if (m_total == 8 && cnt == kR) {
+    if (PM && cnt == kR && !(reinterpret_cast<uintptr_t>(pm + w0) & 3)) {
+        // part-major: lane l holds rows 4l .. 4l + 3 of a 256-row tile (one 4-byte load)
+        static_assert(kR % (256 * G) == 0, "whole 256-row tile groups per wave");
+        const uint32_t* p4 = reinterpret_cast<const uint32_t*>(pm + w0);
+#pragma unroll 1
+        for (int t0 = 0; t0 < kR / 256; t0 += G) {
+            uint32_t v[G];
+#pragma unroll
+            for (int u = 0; u < G; ++u) v[u] = p4[(t0 + u) * 64 + lane];
+#pragma unroll
+            for (int u = 0; u < G; ++u) {
+                const unsigned c0 = v[u] & 0xFFu, c1 = (v[u] >> 8) & 0xFFu,
+                               c2 = (v[u] >> 16) & 0xFFu, c3 = v[u] >> 24;
+                count(wave_shr1(c3, carry), c0);
+                count(c0, c1);
+                count(c1, c2);
+                count(c2, c3);
+                carry = (unsigned)__builtin_amdgcn_readlane((int)c3, 63);
+            }
+        }
+    } else if (PM && cnt > 0) {
+        // part-major, a partial or unaligned range: one row per lane
+#pragma unroll 1
+        for (int r0 = 0; r0 < cnt; r0 += 64) {
+            const unsigned c = r0 + lane < cnt ? (unsigned)pm[w0 + r0 + lane] : ~0u;
+            count(wave_shr1(c, carry), c);
+            carry = (unsigned)__builtin_amdgcn_readlane((int)c, 63);
+        }
+    } else if (!PM && m_total == 8 && cnt == kR) {
         // two 8-byte rows per lane: one 16-byte load covers rows 2l, 2l + 1 of a 128-row tile
         const uint4* pr = reinterpret_cast<const uint4*>(codes + w0 * 8);
 #pragma unroll 1
@@ -251,7 +284,7 @@ hist_ctx_w(const uint8_t* __restrict__ codes, long long n, int m_total, int k,
                 carry = (unsigned)__builtin_amdgcn_readlane((int)cb, 63);
             }
         }
-    } else if (cnt > 0) {
+    } else if (!PM && cnt > 0) {
         // one row per lane: the dword of row r that holds part m (rows past the wave's range
         // clamp their load and count nothing)
         const int rw = m_total >> 2;
@@ -321,7 +354,7 @@ hist_ctx_reduce(const uint32_t* __restrict__ partial, int chunks, int words, lon
 template <typename CodeT>
 __global__ void __launch_bounds__(256)
 hist_plain(const CodeT* __restrict__ codes, long long n, int m_total, int k,
-           uint32_t* __restrict__ counts) {
+           uint32_t* __restrict__ counts, long long ldc) {
     extern __shared__ uint32_t bins[];
     const int m = blockIdx.y;
     for (int i = threadIdx.x; i < k; i += blockDim.x) bins[i] = 0;
@@ -329,12 +362,32 @@ hist_plain(const CodeT* __restrict__ codes, long long n, int m_total, int k,
     const long long per = (n + gridDim.x - 1) / gridDim.x;
     const long long v0 = (long long)blockIdx.x * per, v1 = min(n, v0 + per);
     for (long long v = v0 + threadIdx.x; v < v1; v += blockDim.x) {
-        const unsigned c = ld_code(codes, v * m_total + m);
+        const unsigned c = ld_code(codes, ldc ? (long long)m * ldc + v : v * m_total + m);
         if (c < (unsigned)k) atomicAdd(&bins[c], 1u);
     }
     __syncthreads();
     for (int i = threadIdx.x; i < k; i += blockDim.x)
         if (bins[i]) atomicAdd(&counts[(long long)m * k + i], bins[i]);
+}
+
+// part-major codes [m][ldc] -> rows [n][m] (one thread per row: coalesced loads of each part,
+// one 8- or 16-byte store per row where the row allows)
+template <typename CodeT>
+__global__ void __launch_bounds__(256)
+transpose_codes(const CodeT* __restrict__ parts, long long ldc, long long n, int m,
+                CodeT* __restrict__ rows) {
+    const long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= n) return;
+    if (sizeof(CodeT) == 1 && (m == 8 || m == 16)) {
+        unsigned long long w[2] = {0, 0};
+        for (int i = 0; i < m; ++i)
+            w[i >> 3] |= (unsigned long long)(uint8_t)parts[(long long)i * ldc + v] << (8 * (i & 7));
+        unsigned long long* d = reinterpret_cast<unsigned long long*>(rows) + v * (m / 8);
+        d[0] = w[0];
+        if (m == 16) d[1] = w[1];
+    } else {
+        for (int i = 0; i < m; ++i) rows[v * m + i] = parts[(long long)i * ldc + v];
+    }
 }
 
 // ---------------------------------------------------------------- encode
@@ -345,8 +398,11 @@ __device__ __forceinline__ unsigned long long sym_entry(const CodeT* codes, long
                                                         int raw_first, const CodeT* prev_row,
                                                         const unsigned long long* enc,
                                                         long long items,
-                                                        const uint16_t* tree_prev) {
-    const unsigned s = ld_code(codes, v * m_total + i);
+                                                        const uint16_t* tree_prev,
+                                                        long long ldc = 0) {
+    // (ldc > 0: part-major codes, part i of row v at i * ldc + v)
+    auto at = [&](long long row) { return ld_code(codes, ldc ? (long long)i * ldc + row : row * m_total + i); };
+    const unsigned s = at(v);
     if (s >= (unsigned)k) return 0;  // out-of-alphabet symbol: no code (length 0)
     if (!context) return enc[(long long)i * items + s];
     unsigned prev;
@@ -354,7 +410,7 @@ __device__ __forceinline__ unsigned long long sym_entry(const CodeT* codes, long
         prev = tree_prev[v * m_total + i];
         if (prev == 0xFFFFu) return (8ull << 56) | (s & 0xFFu);
     } else if (v > 0) {
-        prev = ld_code(codes, (v - 1) * m_total + i);
+        prev = at(v - 1);
     } else if (!raw_first && prev_row) {
         prev = ld_code(prev_row, i);
     } else {
@@ -529,7 +585,7 @@ __device__ __forceinline__ void gather_entries(const CodeT* __restrict__ codes, 
 // stamps of the mid-grid workgroup, read by pqh_debug_enc_stamps.)
 __device__ unsigned long long g_enc_stamps[8];
 
-template <typename CodeT, int MAXM, int BLK, bool ROW8 = false, int CS = 1>
+template <typename CodeT, int MAXM, int BLK, bool ROW8 = false, int CS = 1, bool PM = false>
 __global__ void __launch_bounds__(BLK)
 enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, int context,
             int raw_first, const CodeT* __restrict__ prev_row, const int* __restrict__ d_rawf,
@@ -543,10 +599,21 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
             unsigned long long* __restrict__ state, unsigned long long* __restrict__ tails,
             unsigned long long* __restrict__ ticket, unsigned long long ticket_base,
             unsigned epoch, long long nb, unsigned long long* __restrict__ total_out,
-            const uint16_t* __restrict__ tree_prev, int prio) {
+            const uint16_t* __restrict__ tree_prev, int prio, long long ldc_arg) {
+    const long long ldc = PM ? ldc_arg : 0;   // (row-major instances: the old register budget)
     // ROW8: n counts 8-byte rows of 8 u8 codes, CS of them per vector (m_total = 8 CS: a
     // 16-part vector is two consecutive 8-part rows, which are also consecutive in the
-    // stream); a row's context row is CS rows back and its parts are (row % CS) * 8 + i
+    // stream); a row's context row is CS rows back and its parts are (row % CS) * 8 + i.
+    // ldc > 0 (ROW8 only): the codes are part-major [m_total][ldc]; a row is gathered from
+    // its 8 parts' runs (coalesced byte loads across the wave's consecutive rows).
+    auto row8_at = [&](long long vec, unsigned hf) -> unsigned long long {
+        if (!PM) return reinterpret_cast<const unsigned long long*>(codes)[vec * CS + hf];
+        unsigned long long r = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            r |= (unsigned long long)(uint8_t)codes[(long long)(hf * 8 + i) * ldc + vec] << (8 * i);
+        return r;
+    };
     extern __shared__ uint32_t img[];   // LDS image of this block's bit range
     pqh_set_prio(prio);
     __shared__ uint32_t wsum[BLK / 64];
@@ -574,14 +641,13 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
             // m = 8 u8 codes: the row (and its context row) is one 8-byte load; entry loads
             // are a uniform base plus a 32-bit offset (m * items * 4 B < 4 GB)
             static_assert(MAXM == 8 && sizeof(CodeT) == 1, "8-byte rows");
-            const unsigned long long* r8 = reinterpret_cast<const unsigned long long*>(codes);
-            const unsigned long long row = r8[v];
             const unsigned half = (unsigned)(v % CS);   // (CS = 1: 0)
+            const unsigned long long row = row8_at(v / CS, half);
             unsigned long long prow = 0;
             bool raw = false;
             if (context) {
                 if (v >= CS) {
-                    prow = r8[v - CS];
+                    prow = row8_at(v / CS - 1, half);
                 } else if (!raw_first && prev_row) {
 #pragma unroll
                     for (int i = 0; i < 8; ++i)
@@ -604,7 +670,8 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
                 bits += ent[i] != ~0u ? ent[i] >> 26
                                       : (uint32_t)(sym_entry(codes, v / CS, (int)half * 8 + i,
                                                              8 * CS, k, context, raw_first,
-                                                             prev_row, enc, items, nullptr) >> 56);
+                                                             prev_row, enc, items, nullptr,
+                                                             ldc) >> 56);
         } else if constexpr (MAXM > 0) {
             gather_entries<CodeT, MAXM>(codes, v, m_total, k, context, raw_first, prev_row,
                                         enc32, items, ent, tree_prev);
@@ -689,7 +756,7 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
                 if (ROW8 && vv > 0) {   // (chunk_prev rows are 8 CS bytes: aligned)
                     for (int q = 0; q < CS; ++q)
                         reinterpret_cast<unsigned long long*>(chunk_prev)[j * CS + q] =
-                            reinterpret_cast<const unsigned long long*>(codes)[v - CS + q];
+                            row8_at(vv - 1, (unsigned)q);
                 } else {
                     for (int i = 0; i < m_total; ++i)
                         chunk_prev[j * m_total + i] =
@@ -736,7 +803,7 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
                     if (ent[i] >> 26) append(ent[i] & ((1u << 26) - 1), (int)(ent[i] >> 26));
                 } else if (ROW8) {   // a code longer than 26 bits: its u64 entry
                     put(sym_entry(codes, v / CS, (int)(v % CS) * 8 + i, 8 * CS, k, context,
-                                  raw_first, prev_row, enc, items, nullptr));
+                                  raw_first, prev_row, enc, items, nullptr, ldc));
                 } else {
                     put(sym_entry(codes, v, i, m_total, k, context, raw_first, prev_row, enc,
                                   items, tree_prev));
@@ -844,7 +911,8 @@ extern "C" {
 static int histogram_impl(pqh_ctx_t* ctx, const void* d_codes, long long n, int m, int k,
                           int context, const void* d_prev_row, uint32_t* d_counts, int set,
                           const int* d_rawf = nullptr, int phase = 0,
-                          uint32_t* d_partials = nullptr) {
+                          uint32_t* d_partials = nullptr, long long ldc = 0) {
+    if (ldc && ldc < n) return PQH_ERR_ARG;
     if (!ctx || m <= 0 || k <= 0 || n < 0) return PQH_ERR_ARG;
     if (phase != 1 && !d_counts) return PQH_ERR_ARG;
     if (phase != 2 && n > 0 && !d_codes) return PQH_ERR_ARG;
@@ -896,23 +964,26 @@ static int histogram_impl(pqh_ctx_t* ctx, const void* d_codes, long long n, int 
         // (measured alone, tools/bench_hist.py: 0.027 vs 0.035 ms per 1M rows at m = 8, 0.052
         // vs 0.108 at m = 16; the Deep bench 1,300 vs 1,218 Mvec/s)
         const bool slim = hb && std::atoi(hb) == 256;
-        const bool wave_form = !thread_form && m % 4 == 0 && (al & (m == 8 ? 15u : 3u)) == 0;
+        // (part-major codes: always the wave form, which reads each part's run directly)
+        const bool wave_form = ldc || (!thread_form && m % 4 == 0 && (al & (m == 8 ? 15u : 3u)) == 0);
         if (wave_form && slim) {
             // 256 threads, <= 32 VGPRs: fits on a CU beside the assignment grid (one wave
             // per SIMD, 64 KB of LDS beside its ~75 KB), for a histogram off stream A
-            PQH_HIP(ctx, hipFuncSetAttribute((const void*)hist_ctx_w<256, 3>,
+            auto kf = ldc ? hist_ctx_w<256, 3, true> : hist_ctx_w<256, 3, false>;
+            PQH_HIP(ctx, hipFuncSetAttribute((const void*)kf,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            hipLaunchKernelGGL((hist_ctx_w<256, 3>), dim3(grid), dim3(256), lds, ctx->stream,
+            hipLaunchKernelGGL(kf, dim3(grid), dim3(256), lds, ctx->stream,
                                static_cast<const uint8_t*>(d_codes), n, m, k,
                                static_cast<const uint8_t*>(d_prev_row), d_rawf, partial, split,
-                               chunks, rounds, acc, pqh_prio("HIST", 0));
+                               chunks, rounds, acc, pqh_prio("HIST", 0), ldc);
         } else if (wave_form) {
-            PQH_HIP(ctx, hipFuncSetAttribute((const void*)hist_ctx_w<1024, 5>,
+            auto kf = ldc ? hist_ctx_w<1024, 5, true> : hist_ctx_w<1024, 5, false>;
+            PQH_HIP(ctx, hipFuncSetAttribute((const void*)kf,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            hipLaunchKernelGGL((hist_ctx_w<1024, 5>), dim3(grid), dim3(1024), lds, ctx->stream,
+            hipLaunchKernelGGL(kf, dim3(grid), dim3(1024), lds, ctx->stream,
                                static_cast<const uint8_t*>(d_codes), n, m, k,
                                static_cast<const uint8_t*>(d_prev_row), d_rawf, partial, split,
-                               chunks, rounds, acc, pqh_prio("HIST", 0));
+                               chunks, rounds, acc, pqh_prio("HIST", 0), ldc);
         } else if (!slim) {
             PQH_HIP(ctx, hipFuncSetAttribute((const void*)hist_ctx<uint8_t>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -937,10 +1008,10 @@ static int histogram_impl(pqh_ctx_t* ctx, const void* d_codes, long long n, int 
         const unsigned blocks = (unsigned)std::min<long long>((n + 4095) / 4096, 512);
         if (k <= 256)
             hipLaunchKernelGGL(hist_plain<uint8_t>, dim3(blocks, m), dim3(256), k * 4, ctx->stream,
-                               static_cast<const uint8_t*>(d_codes), n, m, k, d_counts);
+                               static_cast<const uint8_t*>(d_codes), n, m, k, d_counts, ldc);
         else
             hipLaunchKernelGGL(hist_plain<uint16_t>, dim3(blocks, m), dim3(256), k * 4, ctx->stream,
-                               static_cast<const uint16_t*>(d_codes), n, m, k, d_counts);
+                               static_cast<const uint16_t*>(d_codes), n, m, k, d_counts, ldc);
     }
     PQH_LAUNCH_CHECK(ctx);
     return PQH_OK;
@@ -971,6 +1042,22 @@ int pqh_histogram(pqh_ctx_t* ctx, const void* d_codes, long long n, int m, int k
 int pqh_histogram_set(pqh_ctx_t* ctx, const void* d_codes, long long n, int m, int k,
                       int context, const void* d_prev_row, uint32_t* d_counts) {
     return histogram_impl(ctx, d_codes, n, m, k, context, d_prev_row, d_counts, 1);
+}
+
+int pqh_histogram_parts(pqh_ctx_t* ctx, const void* d_codes, long long ld_codes, long long n,
+                        int m, int k, int context, const void* d_prev_row, uint32_t* d_counts,
+                        int set) {
+    if (ld_codes <= 0) return PQH_ERR_ARG;
+    return histogram_impl(ctx, d_codes, n, m, k, context, d_prev_row, d_counts, set ? 1 : 0,
+                          nullptr, 0, nullptr, ld_codes);
+}
+
+int pqh_histogram_partial_parts(pqh_ctx_t* ctx, const void* d_codes, long long ld_codes,
+                                long long n, int m, int k, const void* d_prev_row,
+                                void* d_partials) {
+    if (ld_codes <= 0) return PQH_ERR_ARG;
+    return histogram_impl(ctx, d_codes, n, m, k, 1, d_prev_row, nullptr, 0, nullptr, 1,
+                          static_cast<uint32_t*>(d_partials), ld_codes);
 }
 
 // workspace layout for encode: [block_bits u32 nb][pad][block_off u64 nb]
@@ -1027,8 +1114,12 @@ static int encode_write_impl(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* 
                              unsigned long long out_bytes, int chunk_vectors,
                              unsigned long long* d_chunk_offsets, void* d_chunk_prev,
                              unsigned long long* d_total_bits,
-                             const uint16_t* tree_prev = nullptr, const int* d_rawf = nullptr) {
+                             const uint16_t* tree_prev = nullptr, const int* d_rawf = nullptr,
+                             long long ldc = 0) {
     if (!ctx || !t || n < 0 || (n > 0 && (!d_codes || !d_out))) return PQH_ERR_ARG;
+    if (ldc && (ldc < n || t->k > 256 || (t->m != 8 && t->m != 16) || tree_prev ||
+                (reinterpret_cast<uintptr_t>(d_chunk_prev) & 7)))
+        return ldc < n ? PQH_ERR_ARG : PQH_ERR_UNSUPPORTED;   // part-major: the row encoder only
     if ((reinterpret_cast<uintptr_t>(d_out) & 3u) || (out_bytes & 3u))
         return pqh_set_error(ctx, PQH_ERR_ARG, "stream buffer must be 4-byte aligned and sized");
     if (chunk_vectors > 0 && !d_chunk_offsets) return PQH_ERR_ARG;
@@ -1043,7 +1134,7 @@ static int encode_write_impl(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* 
     // on a CU beside the assignment grid's waves; other shapes the generic encoder (m <= 8:
     // 256 vectors per workgroup, wider rows 512)
     const bool row8 = t->k <= 256 && (t->m == 8 || t->m == 16) && !tree_prev &&
-                      !(reinterpret_cast<uintptr_t>(d_codes) & 7) &&
+                      (ldc || !(reinterpret_cast<uintptr_t>(d_codes) & 7)) &&
                       !(reinterpret_cast<uintptr_t>(d_chunk_prev) & 7);
     const int cs = row8 ? t->m / 8 : 1;
     const long long rows = n * cs;
@@ -1073,14 +1164,15 @@ static int encode_write_impl(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* 
     unsigned long long* total = d_total_bits ? d_total_bits : ctx->d_diag + 3;
     uint32_t* words = reinterpret_cast<uint32_t*>(d_out);
     const int enc_prio = pqh_prio("ENCODE", 0);
-#define PQH_ENC(T, MAXM, R8, CS)                                                                  \
+#define PQH_ENC(T, MAXM, R8, CS) PQH_ENC_PM(T, MAXM, R8, CS, false)
+#define PQH_ENC_PM(T, MAXM, R8, CS, PMV)                                                          \
     do {                                                                                          \
         constexpr int B = MAXM > 0 && MAXM <= 8 ? 256 : kEncBlock;                                \
         if (lds > 64 * 1024)                                                                      \
-            PQH_HIP(ctx, hipFuncSetAttribute((const void*)(enc_onepass<T, MAXM, B, R8, CS>),      \
+            PQH_HIP(ctx, hipFuncSetAttribute((const void*)(enc_onepass<T, MAXM, B, R8, CS, PMV>), \
                                              hipFuncAttributeMaxDynamicSharedMemorySize,          \
                                              (int)lds));                                          \
-        hipLaunchKernelGGL((enc_onepass<T, MAXM, B, R8, CS>), dim3((unsigned)nb), dim3(B), lds,   \
+        hipLaunchKernelGGL((enc_onepass<T, MAXM, B, R8, CS, PMV>), dim3((unsigned)nb), dim3(B), lds, \
                            ctx->stream, static_cast<const T*>(d_codes), R8 ? rows : n, t->m, t->k, \
                            t->context, raw_first, static_cast<const T*>(d_prev_row), d_rawf,     \
                            t->d_enc,                                                              \
@@ -1088,9 +1180,12 @@ static int encode_write_impl(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* 
                            (long long)(out_bytes / 4),                                            \
                            chunk_vectors, d_chunk_offsets, static_cast<T*>(d_chunk_prev),         \
                            ctx->d_diag + 2, st, tails, ticket, ctx->lb_ticket_base,               \
-                           (unsigned)ctx->lb_epoch, nb, total, tree_prev, enc_prio);              \
+                           (unsigned)ctx->lb_epoch, nb, total, tree_prev, enc_prio, ldc);         \
     } while (0)
-    if (t->k <= 256) {
+    if (ldc) {   // part-major codes: the row encoder (checked above)
+        if (cs == 2) PQH_ENC_PM(uint8_t, 8, true, 2, true);
+        else PQH_ENC_PM(uint8_t, 8, true, 1, true);
+    } else if (t->k <= 256) {
         if (row8 && cs == 2) PQH_ENC(uint8_t, 8, true, 2);
         else if (row8) PQH_ENC(uint8_t, 8, true, 1);
         else if (t->m <= 8) PQH_ENC(uint8_t, 8, false, 1);
@@ -1102,6 +1197,7 @@ static int encode_write_impl(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* 
         else PQH_ENC(uint16_t, 0, false, 1);
     }
 #undef PQH_ENC
+#undef PQH_ENC_PM
     PQH_LAUNCH_CHECK(ctx);
     ctx->lb_ticket_base += (unsigned long long)nb;
     return PQH_OK;
@@ -1115,6 +1211,41 @@ int pqh_encode_write(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes,
     return encode_write_impl(ctx, t, d_codes, n, raw_first, d_prev_row, bit_offset, nullptr,
                              d_out, out_bytes, chunk_vectors, d_chunk_offsets, d_chunk_prev,
                              d_total_bits);
+}
+
+int pqh_transpose_codes(pqh_ctx_t* ctx, const void* d_parts, long long ld_parts, long long n, int m,
+                        int code_bytes, void* d_rows) {
+    if (!ctx || n < 0 || m <= 0 || ld_parts < n || (code_bytes != 1 && code_bytes != 2) ||
+        (n > 0 && (!d_parts || !d_rows)))
+        return PQH_ERR_ARG;
+    if (code_bytes == 1 && (m == 8 || m == 16) && (reinterpret_cast<uintptr_t>(d_rows) & 7))
+        return pqh_set_error(ctx, PQH_ERR_ARG, "transpose: 8- and 16-byte rows must be 8-byte aligned");
+    int rc = pqh_use_device(ctx);
+    if (rc) return rc;
+    if (n == 0) return PQH_OK;
+    const unsigned blocks = (unsigned)((n + 255) / 256);
+    if (code_bytes == 1)
+        hipLaunchKernelGGL(transpose_codes<uint8_t>, dim3(blocks), dim3(256), 0, ctx->stream,
+                           static_cast<const uint8_t*>(d_parts), ld_parts, n, m,
+                           static_cast<uint8_t*>(d_rows));
+    else
+        hipLaunchKernelGGL(transpose_codes<uint16_t>, dim3(blocks), dim3(256), 0, ctx->stream,
+                           static_cast<const uint16_t*>(d_parts), ld_parts, n, m,
+                           static_cast<uint16_t*>(d_rows));
+    PQH_LAUNCH_CHECK(ctx);
+    return PQH_OK;
+}
+
+int pqh_encode_write_parts(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes,
+                           long long ld_codes, long long n, int raw_first, const void* d_prev_row,
+                           unsigned long long bit_offset, unsigned char* d_out,
+                           unsigned long long out_bytes, int chunk_vectors,
+                           unsigned long long* d_chunk_offsets, void* d_chunk_prev,
+                           unsigned long long* d_total_bits) {
+    if (ld_codes <= 0) return PQH_ERR_ARG;
+    return encode_write_impl(ctx, t, d_codes, n, raw_first, d_prev_row, bit_offset, nullptr,
+                             d_out, out_bytes, chunk_vectors, d_chunk_offsets, d_chunk_prev,
+                             d_total_bits, nullptr, nullptr, ld_codes);
 }
 
 int pqh_encode_write_at(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes, long long n,
