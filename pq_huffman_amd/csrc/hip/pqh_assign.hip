@@ -407,13 +407,8 @@ __device__ __forceinline__ f32x16 tile_scores_a(const bf16x8* a, const bf16x8* B
 
 // this lane's 16 rows of ||c||^2 for tile t (LDS image [tile][half][16]: every lane of a
 // half-wave reads the same 64 bytes, a broadcast)
-// (four 16-byte reads: with one 64-byte vector read the compiler loses track of which LDS
-// array it reads and waits for pq_assign_bkt's in-flight LDS DMA before every tile)
 __device__ __forceinline__ f32x16 tile_norms(const float* Cn, int t, int h) {
-    const f32x4* p = reinterpret_cast<const f32x4*>(Cn + (t * 2 + h) * 16);
-    const f32x4 a = p[0], b = p[1], c = p[2], d = p[3];
-    return f32x16{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3],
-                  c[0], c[1], c[2], c[3], d[0], d[1], d[2], d[3]};
+    return *reinterpret_cast<const f32x16*>(Cn + (t * 2 + h) * 16);
 }
 
 // A fragment p of tile t, [PA][KT][64 lanes] per subspace: from the workgroup's LDS copy
@@ -1186,614 +1181,6 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     if (lane == 0 && slow_count) atomicAdd(rerank, slow_count);
 }
 
-// ---- pq_assign_bkt (K = 256): the same codes by a two-pass reduction (DESIGN.md §4.1
-// "Two passes, bucketed by winning tile").
-//  Pass 1 reduces each tile's 16 scores of a lane to their minimum only -- min3 trees, half a
-//  VALU per score -- keyed with the tile and folded (two tiles at a time) into the lane's top
-//  two.  After the half-wave merge a vector has the minima of its 16 groups (tile t, half h:
-//  16 centroids each); if the second-best group is further than tau from the best, every
-//  centroid that could compete with the winner lies in the winning group, and the vector is
-//  appended to its wave's bucket of that tile (an LDS ring).  A bucket of 32 vectors is
-//  screened once more against its one tile -- the main loop's instruction sequence, so the
-//  same scores bit for bit -- and reduced by the P/Q partition of a single tile: the row of
-//  the minimum and the group's second score.  That certificate, the pass-1 gap and the queued
-//  exact re-rank of near ties are those of pq_assign_mfma, so the codes are the oracle's.
-//  Per 32-vector block: ~84 VALU of pass-1 reduction + ~45 in the bucket pass, against ~190
-//  for the P/Q reduction over all 8 tiles; the cost is one more tile of MFMAs per vector.
-constexpr int kBqCap = 64;   // bucket ring entries per (wave, tile): <= 31 waiting + 32 new
-// bucket entry: row (30 bits) | the row's block had a bf16 remainder << 30 | winning half << 31
-constexpr uint32_t kBqRow = 0x3FFFFFFFu;
-
-template <int D, typename CodeT>
-__global__ void __launch_bounds__(64 * kWavesPerWG, D == 32 ? 2 : PQH_ASSIGN_OCC)
-pq_assign_bkt(const float* __restrict__ x, long long n, long long ldx, int m_total,
-              const bf16x8* __restrict__ afrag, const float* __restrict__ cnorm,
-              const float* __restrict__ cent,
-              const float* __restrict__ cmax, const float* __restrict__ sqrt_cmax,
-              CodeT* __restrict__ codes, uint32_t* __restrict__ counts,
-              unsigned long long* __restrict__ rerank, uint32_t* __restrict__ sched, int gx,
-              unsigned long long* __restrict__ rerank_next, uint32_t* __restrict__ sched_next,
-              int prio, long long ldc) {
-    using P = Plan<D>;
-    constexpr int KT = 8;
-    constexpr int K = 256;
-    constexpr unsigned PMASK = 15u;            // key index bits (truncation < 2^4 ulp)
-    constexpr float kKeySlack = 0x1p-17f;      // see pq_assign_mfma's gap test
-    __shared__ uint32_t hist[kWavesPerWG][K];
-    __shared__ uint4 As[P::PA * KT * 64];
-    __shared__ __attribute__((aligned(64))) float Cn[KT * 2 * 16];
-    __shared__ uint2 rqs[kWavesPerWG][kRqLds];
-    // bucket rings (entries: kBqRow) per (wave, tile); bcnt = entries ever appended (each
-    // time the count reaches a multiple of 32 those 32 are flushed)
-    __shared__ uint32_t bq[kWavesPerWG][KT][kBqCap];
-    __shared__ uint32_t bcnt[kWavesPerWG][KT];
-    // staging slots: a full bucket's 32 rows (each lane's slice) copied from global memory by
-    // LDS DMA when the bucket fills, screened one step later -- the rows' latency (mostly
-    // Infinity-Cache hits) is spent on the next step's pass 1.  Pieces of 16 B (4 B when the
-    // slice is not a multiple of 4 floats) x 64 lanes.
-    constexpr int XD_ = Slice<D>::XD;
-    constexpr int PW = XD_ % 4 == 0 ? 4 : 1;           // floats per DMA piece
-    constexpr int NPC = XD_ / PW;                       // pieces per slice
-    constexpr int NS = D >= 32 ? 1 : 2;                 // staging slots per wave
-    __shared__ __attribute__((aligned(16))) float stg[kWavesPerWG][NS][NPC][64 * PW];
-
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int L = blockIdx.x;
-    const bool inter = (gx & 7) == 0;   // subspace placement: see pq_assign_mfma
-    const int m = inter ? (L >> 3) % m_total : L / gx;
-    const int bx = inter ? (L / (8 * m_total)) * 8 + (L & 7) : L % gx;
-    const int r = lane & 31;
-    const int h = lane >> 5;
-    pqh_set_prio(prio);
-    if (L == 0 && wave == 0) {   // the next launch's queue heads and re-rank counter
-        if (sched_next)
-            for (int q = lane; q < kSchedMax * kXcds; q += 64)
-                __hip_atomic_store(sched_next + q * kSchedStride, 0u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        if (lane == 0)
-            __hip_atomic_store(rerank_next, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    {
-        const uint4* src = reinterpret_cast<const uint4*>(afrag) + (long long)m * P::PA * KT * 64;
-        for (int i = threadIdx.x; i < P::PA * KT * 64; i += blockDim.x) As[i] = src[i];
-        for (int i = threadIdx.x; i < KT * 2 * 16; i += blockDim.x)
-            Cn[i] = cnorm[(long long)m * KT * 2 * 16 + i];
-        if (counts)
-            for (int i = lane; i < K; i += 64) hist[wave][i] = 0;
-        if (lane < KT) bcnt[wave][lane] = 0;
-        __syncthreads();   // the only workgroup barrier
-    }
-    const float cm = cmax[m];
-    const float sc = sqrt_cmax[m];
-    const TauCoef tq = tau_coef(cm, sc, sqrt_cmax[m_total + m]);
-    const float ninf = opaque_ninf();
-    const float* cl = cent + (long long)m * K * D;
-    const int n32 = (int)n;
-    const int nblk = (n32 + 31) / 32;
-    const int nfull = n32 / 32;
-    unsigned long long slow_count = 0;
-
-    constexpr bool HALF = Slice<D>::HALF;
-    constexpr int XD = Slice<D>::XD;
-    const unsigned ldx4 = (unsigned)ldx * 4u;
-    const unsigned xh_off = HALF ? 32u * (unsigned)h : 0u;
-    const unsigned xlane_off = __umul24((unsigned)r, ldx4) + xh_off;
-    const char* const xm = reinterpret_cast<const char*>(x + (long long)m * D);
-    const long long crs = ldc ? 1 : m_total;
-    CodeT* const cbase = codes + (ldc ? (long long)m * ldc : (long long)m);
-    auto slice_from = [&](const float* xp, float* dst) {
-        if constexpr (XD % 4 == 0) {
-#pragma unroll
-            for (int j = 0; j < XD; j += 4) {
-                const f32x4 q = *reinterpret_cast<const f32x4*>(xp + (HALF ? 16 * (j >> 3) + (j & 7) : j));
-                dst[j] = q.x; dst[j + 1] = q.y; dst[j + 2] = q.z; dst[j + 3] = q.w;
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < XD; ++j) dst[j] = xp[j];
-        }
-    };
-    auto load_x = [&](int b, float* dst) {   // block b's rows (clamped to n - 1)
-        long long row0 = (long long)b * 32;
-        unsigned off = xlane_off;
-        if (b >= nfull) {
-            row0 = row0 < n - 1 ? row0 : n - 1;
-            const long long left = n - 1 - row0;
-            const unsigned last = (unsigned)(left < 31 ? left : 31);
-            off = __umul24(min((unsigned)r, last), ldx4) + xh_off;
-        }
-        slice_from(reinterpret_cast<const float*>(xm + row0 * (long long)ldx4 + off), dst);
-    };
-    // a gathered row's slice (bucket entries)
-    auto load_row = [&](long long row, float* dst) {
-        slice_from(reinterpret_cast<const float*>(xm + row * (long long)ldx4 + xh_off), dst);
-    };
-    auto store_code = [&](long long row, int code) {
-        cbase[row * crs] = (CodeT)code;
-        if (counts) atomicAdd(&hist[wave][code], 1u);
-    };
-    // exact fp32 direct form over all K for one (wave-uniform) row; every lane takes part
-    auto exact_one = [&](long long vrow) -> int {
-        float xv[D];
-        const float* xr = x + vrow * ldx + (long long)m * D;
-#pragma unroll
-        for (int j = 0; j < D; ++j) xv[j] = xr[j];
-        float best = INFINITY;
-        int bidx = 0x7FFFFFFF;
-#pragma unroll 1
-        for (int q = 0; q < K / 64; ++q) {
-            const int c = lane + 64 * q;
-            const float dd = exact_dist<D>(xv, cl + c * D);
-            if (dd < best) { best = dd; bidx = c; }
-        }
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-            const float ob = __shfl_xor(best, off);
-            const int oi = __shfl_xor(bidx, off);
-            if (ob < best || (ob == best && oi < bidx)) { best = ob; bidx = oi; }
-        }
-        return bidx == 0x7FFFFFFF ? 0 : bidx;
-    };
-    unsigned qn = 0;   // entries in this wave's re-rank queue
-    // lanes with `want` (finite vectors: row, thr) go to the re-rank queue if all fit, else
-    // are finished inline here; returns nothing (the codes are stored either way later)
-    auto defer_or_exact = [&](bool want, long long row, float thr) __attribute__((always_inline)) {
-        const unsigned long long need = __ballot(want);
-        if (!need) return;
-        slow_count += __popcll(need);
-        const unsigned cnt = (unsigned)__popcll(need);
-        if (PQH_ASSIGN_DEFER && qn + cnt <= (unsigned)kRqLds) {
-            if (want)
-                rqs[wave][qn + __builtin_amdgcn_mbcnt_hi((unsigned)(need >> 32),
-                              __builtin_amdgcn_mbcnt_lo((unsigned)need, 0u))] =
-                    make_uint2((uint32_t)row, __float_as_uint(thr));
-            qn += cnt;
-            return;
-        }
-        unsigned long long todo = need;
-        while (todo) {
-            const int rs = __ffsll((long long)todo) - 1;
-            todo &= todo - 1;
-            const long long vrow = (long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)row, rs);
-            const int c = exact_one(vrow);
-            if (lane == rs) store_code(row, c);
-        }
-    };
-
-    // staging state (wave-uniform): the tile and first ring slot of each staged batch, -1 free
-    int st_t[NS];
-    unsigned st_s0[NS];
-#pragma unroll
-    for (int q = 0; q < NS; ++q) { st_t[q] = -1; st_s0[q] = 0; }
-    // copy the 32 rows of tile t's batch from ring slot s0 into staging slot q (LDS DMA: each
-    // lane's slice, piece by piece; the screen's LDS reads wait for them)
-    auto stage = [&](int t, unsigned s0, int q) __attribute__((always_inline)) {
-        const long long row = (long long)(bq[wave][t][(s0 + (unsigned)r) & (kBqCap - 1)] & kBqRow);
-        const float* xp = reinterpret_cast<const float*>(xm + row * (long long)ldx4 + xh_off);
-#pragma unroll
-        for (int c = 0; c < NPC; ++c) {
-            const int j = c * PW;   // the lane's value j sits at dim offset Slice::dim(j) - 8h
-            const float* src = xp + (HALF ? 16 * (j >> 3) + (j & 7) : j);
-#if defined(__HIP_DEVICE_COMPILE__)   // (the host pass rejects the 16-byte form)
-            __builtin_amdgcn_global_load_lds(
-                src, (__attribute__((address_space(3))) void*)(&stg[wave][q][c][0]),
-                Slice<D>::XD % 4 == 0 ? 16 : 4, 0, 0);
-#else
-            (void)src;
-#endif
-        }
-    };
-    // pass 2: `cnt` (<= 32) entries of tile t's bucket from ring slot s0; lane (r, h) screens
-    // entry r's vector against tile t (both halves), the entry's winning half decides
-    auto flush = [&](int t, unsigned s0, int cnt, const float* xs) __attribute__((always_inline)) {
-        const bool ok = r < cnt;
-        const uint32_t e = bq[wave][t][(s0 + (unsigned)r) & (kBqCap - 1)];
-        const long long row = ok ? (long long)(e & kBqRow) : 0;
-        const bool blo = ((e >> 30) & 1u) != 0;
-        const bool hs = (e >> 31) != 0;
-        // tau as pass 1 computed it: the same ||x||^2 sum (lower + upper half) and the same
-        // block-level remainder flag
-        const float tau = screen_tau(norm_x<D>(xs), blo, tq);
-        // the lo pass adds exact zeros to bf16-exact vectors, so their scores are the same
-        // with or without it: bitwise those of pass 1 (whose block had the pass when blo)
-        const bool lo_pass = __any(ok && blo);
-        bf16x8 Bm[P::PM], Bl[P::PL];
-        if (lo_pass)
-            make_b<D, true>(xs, h, Bm, Bl);
-        else
-            make_b<D, false>(xs, h, Bm, Bl);
-        bf16x8 a[P::PA];
-#pragma unroll
-        for (int p = 0; p < P::PA; ++p) a[p] = frag_at<KT>(As, p, t, lane);
-        const f32x16 acc = tile_scores_a<D>(a, Bm, Bl, lo_pass, tile_norms(Cn, t, h));
-        unsigned v[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) v[i] = __float_as_uint(acc[i]);
-        // P: registers [0, 8) and [8, 16); Q: the pairs (j, j + 8) -- see pq_assign_mfma
-        const unsigned e0 = anchor_min(v[6], v[7], ninf), e1 = anchor_min(v[14], v[15], ninf);
-        const unsigned k0 = min3u(min3d(v[0], v[1], v[2], e0), min3d(v[3], v[4], v[5], e0), e0) & ~PMASK;
-        const unsigned k1 =
-            (min3u(min3d(v[8], v[9], v[10], e1), min3d(v[11], v[12], v[13], e1), e1) & ~PMASK) | 1u;
-        unsigned qk[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-            qk[j] = (min3d(v[j], v[j + 8], v[j + 8], e1) & ~PMASK) | q_code_bits(j);
-        unsigned q1, q2;
-        top2_8(qk, q1, q2);
-        const unsigned own1 = minu(k0, k1), own2 = minu(maxu(k0, k1), q2);
-        const unsigned cb = ((own1 & 1u) << 4) | (q1 & 15u) | ((unsigned)h << 2);
-        // the winning half's values (s[0]: lower half's, s[1]: upper's)
-        const auto w1 = __builtin_amdgcn_permlane32_swap(own1, own1, false, false);
-        const auto w2 = __builtin_amdgcn_permlane32_swap(own2, own2, false, false);
-        const auto wc = __builtin_amdgcn_permlane32_swap(cb, cb, false, false);
-        const float K1 = __uint_as_float(hs ? (unsigned)w1[1] : (unsigned)w1[0]);
-        const float K2 = __uint_as_float(hs ? (unsigned)w2[1] : (unsigned)w2[0]);
-        const unsigned cw = hs ? (unsigned)wc[1] : (unsigned)wc[0];
-        const bool good = K2 - K1 > fmaf(kKeySlack, max_abs(K1, K2), tau);
-        const bool mine = ok && h == 0;
-        if (mine && good) store_code(row, t * 32 + (int)cw);
-        defer_or_exact(mine && !good, row, fmaf(2.0f * kKeySlack, fabsf(K1), K1 + tau));
-    };
-    // append the vectors of `go` lanes to the bucket of their winning tile tw; a bucket that
-    // reaches a multiple of 32 entries is flushed at once.  Two rounds (lower, upper lanes), so
-    // a ring holds at most 31 waiting + 32 new entries.
-    auto enqueue = [&](bool go, int tw, unsigned ent) __attribute__((always_inline)) {
-#pragma unroll
-        for (int half = 0; half < 2; ++half) {
-            const bool in = go && h == half;
-            unsigned s = 0;
-            if (in) {
-                s = atomicAdd(&bcnt[wave][tw], 1u);
-                bq[wave][tw][s & (kBqCap - 1)] = ent;
-            }
-            unsigned long long trig = __ballot(in && (s & 31u) == 31u);
-            while (trig) {
-                const int l = __ffsll((long long)trig) - 1;
-                trig &= trig - 1;
-                const int tt = __builtin_amdgcn_readlane(tw, l);
-                const unsigned se = (unsigned)__builtin_amdgcn_readlane((int)s, l) - 31u;
-                int slot = -1;
-#pragma unroll
-                for (int q = NS - 1; q >= 0; --q)
-                    if (st_t[q] < 0) slot = q;
-                if (slot >= 0) {   // stage it: screened at the next step (or the loop's end)
-#pragma unroll
-                    for (int q = 0; q < NS; ++q)
-                        if (q == slot) { st_t[q] = tt; st_s0[q] = se; stage(tt, se, q); }
-                } else {           // no free slot: screen it now (its rows from global)
-                    float xs[XD];
-                    load_row((long long)(bq[wave][tt][(se + (unsigned)r) & (kBqCap - 1)] & kBqRow), xs);
-                    flush(tt, se, 32, xs);
-                }
-            }
-        }
-    };
-    // the staged batches of the previous step
-    auto flush_staged = [&]() __attribute__((always_inline)) {
-#pragma unroll
-        for (int q = 0; q < NS; ++q) {
-            if (st_t[q] >= 0) {
-                float xs[XD];
-#pragma unroll
-                for (int c = 0; c < NPC; ++c)
-#pragma unroll
-                    for (int j = 0; j < PW; ++j) xs[c * PW + j] = stg[wave][q][c][lane * PW + j];
-                flush(st_t[q], st_s0[q], 32, xs);
-                st_t[q] = -1;
-            }
-        }
-    };
-
-    // one step: kNB consecutive blocks (see pq_assign_mfma's body)
-    auto body = [&](auto lo_c, long long blk0, float (*xs)[XD], const float* Xg,
-                    const bool* any_lo) {
-        constexpr bool LO = decltype(lo_c)::value;
-        bf16x8 Bm[kNB][P::PM], Bl[kNB][P::PL];
-#pragma unroll
-        for (int b = 0; b < kNB; ++b) make_b<D, LO>(xs[b], h, Bm[b], Bl[b]);
-        // pass 1: the tile's 16 scores -> their minimum (8 VALU), keyed with the tile, the
-        // keys of a tile pair folded into the running top two at once (3 VALU per pair)
-        unsigned pm1[kNB], pm2[kNB], pk[kNB];
-        auto reduce1 = [&](const f32x16& acc, int t, int b) {
-            unsigned a[16];
-#pragma unroll
-            for (int i = 0; i < 16; ++i) a[i] = __float_as_uint(acc[i]);
-            const unsigned e = anchor_min(a[14], a[15], ninf);
-            const unsigned u0 = min3d(a[0], a[1], a[2], e), u1 = min3d(a[3], a[4], a[5], e),
-                           u2 = min3d(a[6], a[7], a[8], e), u3 = min3d(a[9], a[10], a[11], e),
-                           u4 = min3d(a[12], a[13], e, e);
-            const unsigned k = (min3u(min3u(u0, u1, u2), u3, u4) & ~PMASK) | (unsigned)t;
-            if ((t & 1) == 0) {
-                pk[b] = k;
-            } else if (t == 1) {
-                pm1[b] = minu(pk[b], k);
-                pm2[b] = maxu(pk[b], k);
-            } else {   // second of {pm1 <= pm2, pk, k} = min(pm2, med3(pm1, pk, k))
-                pm2[b] = minu(pm2[b], med3u(pm1[b], pk[b], k));
-                pm1[b] = min3u(pm1[b], pk[b], k);
-            }
-        };
-        f32x16 acc[kNB];
-        {
-            bf16x8 a[P::PA];
-#pragma unroll
-            for (int p = 0; p < P::PA; ++p) a[p] = frag_at<KT>(As, p, 0, lane);
-            f32x16 cn = tile_norms(Cn, 0, h);
-#pragma unroll
-            for (int b = 0; b < kNB; ++b) acc[b] = tile_scores_a<D>(a, Bm[b], Bl[b], LO, cn);
-#pragma unroll
-            for (int t = 0; t < KT; ++t) {
-                if (t + 1 < KT) {
-#pragma unroll
-                    for (int p = 0; p < P::PA; ++p) a[p] = frag_at<KT>(As, p, t + 1, lane);
-                    cn = tile_norms(Cn, t + 1, h);
-                }
-#pragma unroll
-                for (int b = 0; b < kNB; ++b) {
-                    reduce1(acc[b], t, b);
-                    if (t + 1 < KT) acc[b] = tile_scores_a<D>(a, Bm[b], Bl[b], LO, cn);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }
-        }
-        // the batches staged at the previous step (their rows have arrived meanwhile)
-        flush_staged();
-        // merge the half-waves (block pairs, see pq_assign_mfma): the vector's 16 group
-        // minima -> K1 (its key names the tile; the half that holds it is the winning half)
-        // and K2 = the second-best group's minimum
-        constexpr int NG = (kNB + 1) / 2;
-#pragma unroll
-        for (int g = 0; g < NG; ++g) {
-            const int ba = 2 * g, bb = 2 * g + 1 < kNB ? 2 * g + 1 : 2 * g;
-            const bool pair = ba != bb;
-            const auto s1 = __builtin_amdgcn_permlane32_swap(pm1[ba], pm1[bb], false, false);
-            const auto s2 = __builtin_amdgcn_permlane32_swap(pm2[ba], pm2[bb], false, false);
-            const unsigned b1 = minu((unsigned)s1[0], (unsigned)s1[1]);
-            const unsigned b2 = minu(minu((unsigned)s2[0], (unsigned)s2[1]),
-                                     maxu((unsigned)s1[0], (unsigned)s1[1]));
-            // (equal keys in the two halves: K2 = K1, the gap test fails)
-            const unsigned hw = (unsigned)s1[0] == b1 ? 0u : 1u;
-            const int tw = (int)(b1 & 7u);
-            const long long rowl = (blk0 + ba) * 32 + (pair ? lane : r);
-            const bool valid = rowl < n;
-            const bool own_lane = pair || h == 0;
-            const float Xl = Xg[g];
-            const bool finite = isfinite(Xl);
-            const float tau = screen_tau(Xl, pair && h ? any_lo[bb] : any_lo[ba], tq);
-            const float K1 = __uint_as_float(b1), K2 = __uint_as_float(b2);
-            const float KA = max_abs(K1, K2);
-            const bool slow = !(K2 - K1 > fmaf(kKeySlack, KA, tau)) || !finite;
-            const bool vo = valid && own_lane;
-            // near ties (finite): the re-rank queue; non-finite x: the exact form inline
-            const unsigned long long nf = __ballot(vo && !finite);
-            if (nf) {
-                slow_count += __popcll(nf);
-                unsigned long long todo = nf;
-                while (todo) {
-                    const int rs = __ffsll((long long)todo) - 1;
-                    todo &= todo - 1;
-                    const long long vrow = (blk0 + ba) * 32 + (pair ? rs : (rs & 31));
-                    const int c = exact_one(vrow);
-                    if (lane == rs) store_code(rowl, c);
-                }
-            }
-            defer_or_exact(vo && slow && finite, rowl, fmaf(2.0f * kKeySlack, fabsf(K1), K1 + tau));
-            const bool blk_lo = pair && h ? any_lo[bb] : any_lo[ba];
-            enqueue(vo && !slow, tw, (unsigned)rowl | ((unsigned)blk_lo << 30) | (hw << 31));
-        }
-    };
-    auto step = [&](long long blk0, float (*xs)[XD]) {
-        constexpr int NG = (kNB + 1) / 2;
-        float Xg[NG];
-        bool any_lo[kNB];
-        bool chunk_lo = false;
-#pragma unroll
-        for (int g = 0; g < NG; ++g) {
-            const int ba = 2 * g, bb = 2 * g + 1 < kNB ? 2 * g + 1 : 2 * g;
-            if (ba == bb) {
-                Xg[g] = norm_x<D>(xs[ba]);
-            } else if constexpr (Slice<D>::HALF) {
-                const auto sw = __builtin_amdgcn_permlane32_swap(
-                    __float_as_uint(norm_part<D>(xs[ba])), __float_as_uint(norm_part<D>(xs[bb])),
-                    false, false);
-                Xg[g] = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
-            } else {
-                const float xa_ = norm_x<D>(xs[ba]), xb_ = norm_x<D>(xs[bb]);
-                Xg[g] = h ? xb_ : xa_;
-            }
-        }
-#pragma unroll
-        for (int b = 0; b < kNB; ++b) {
-            any_lo[b] = __any(has_lo<D>(xs[b]));
-            chunk_lo |= any_lo[b];
-        }
-        if (chunk_lo)
-            body(std::true_type{}, blk0, xs, Xg, any_lo);
-        else
-            body(std::false_type{}, blk0, xs, Xg, any_lo);
-    };
-    // one batch of queued near ties (see pq_assign_mfma's rerank32)
-    auto rerank32 = [&](const uint2 ent, const bool valid) {
-        const long long v = (long long)ent.x;
-        const float thr = __uint_as_float(ent.y);
-        float xv[D];
-        const float* xp = x + v * ldx + (long long)m * D;
-        if constexpr (D % 4 == 0) {
-#pragma unroll
-            for (int j = 0; j < D; j += 4) {
-                const float4 q = *reinterpret_cast<const float4*>(xp + j);
-                xv[j] = q.x; xv[j + 1] = q.y; xv[j + 2] = q.z; xv[j + 3] = q.w;
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < D; ++j) xv[j] = xp[j];
-        }
-        float xs[XD];
-#pragma unroll
-        for (int j = 0; j < XD; ++j)
-            xs[j] = valid ? (h ? xv[Slice<D>::dim(j, 1)] : xv[Slice<D>::dim(j, 0)]) : 0.0f;
-        float X;
-        bool lo;
-        float xh[XD], xl[XD];
-        split_x<D>(xs, X, lo, xh, xl);
-        bf16x8 Bm[P::PM];
-        bf16x8 Bl[P::PL];
-        build_b<D>(xh, xl, h, Bm, Bl);
-        const bool lo_pass = __any(lo);
-        float best = INFINITY;
-        int bidx = 0x7FFFFFFF;
-        constexpr int kCand = D <= 16 ? 4 : 2;
-        uint32_t cw[KT / 2];
-#pragma unroll
-        for (int w = 0; w < KT / 2; ++w) cw[w] = 0u;
-#pragma unroll 1
-        for (int u = 0; u < KT; ++u) {
-            const f32x16 acc = tile_scores<D, KT>(As, Cn, lane, u, Bm, Bl, lo_pass);
-            uint32_t bits = 0;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) bits |= (acc[i] <= thr ? 1u : 0u) << i;
-            bits = (valid ? bits : 0u) << (16 * (u & 1));
-#pragma unroll
-            for (int w = 0; w < KT / 2; ++w) cw[w] |= w == (u >> 1) ? bits : 0u;
-        }
-        for (;;) {
-            int kc[kCand];
-            bool hc[kCand];
-#pragma unroll
-            for (int c = 0; c < kCand; ++c) {
-                hc[c] = false;
-                kc[c] = 0;
-#pragma unroll
-                for (int w = 0; w < KT / 2; ++w) {
-                    if (!hc[c] && cw[w]) {
-                        const int i = __builtin_ctz(cw[w]);
-                        cw[w] &= cw[w] - 1;
-                        hc[c] = true;
-                        kc[c] = tile_row(2 * w + (i >> 4), i & 15, h);
-                    }
-                }
-            }
-            if (!__any(hc[0])) break;
-            float cr[kCand][D];
-#pragma unroll
-            for (int c = 0; c < kCand; ++c) {
-                const float* cp = cl + kc[c] * D;
-                if constexpr (D % 4 == 0) {
-#pragma unroll
-                    for (int j = 0; j < D; j += 4) {
-                        const float4 q = *reinterpret_cast<const float4*>(cp + j);
-                        cr[c][j] = q.x; cr[c][j + 1] = q.y; cr[c][j + 2] = q.z; cr[c][j + 3] = q.w;
-                    }
-                } else {
-#pragma unroll
-                    for (int j = 0; j < D; ++j) cr[c][j] = cp[j];
-                }
-            }
-#pragma unroll
-            for (int c = 0; c < kCand; ++c) {
-                const float dd = exact_dist<D>(xv, cr[c]);
-                const int k = kc[c];
-                if (hc[c] && (dd < best || (dd == best && k < bidx))) { best = dd; bidx = k; }
-            }
-        }
-        const float ob = __uint_as_float(partner32(__float_as_uint(best)));
-        const int oi = (int)partner32((unsigned)bidx);
-        if (ob < best || (ob == best && oi < bidx)) { best = ob; bidx = oi; }
-        if (valid && h == 0) store_code(v, bidx == 0x7FFFFFFF ? 0 : bidx);
-    };
-
-    // chunk schedule: as pq_assign_mfma (static stride, or per-XCD work queues)
-    const int wave_id = bx * kWavesPerWG + wave;
-    const int waves_m = gx * kWavesPerWG;
-    const int nchunk = (nblk + kNB - 1) / kNB;
-    const int R = nchunk > waves_m ? (nchunk - waves_m + kXcds - 1) / kXcds : 0;
-    uint32_t* head = sched ? sched + (long long)m * kXcds * kSchedStride : nullptr;
-    int xr = head ? (int)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & (kXcds - 1)) : 0;
-    int tries = head && R > 0 ? 0 : kXcds;
-    auto ticket = [&]() -> unsigned {
-        unsigned t = __builtin_nondeterministic_value(0u);
-        if (lane == 0)
-            t = __hip_atomic_fetch_add(head + xr * kSchedStride, 1u, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-        return t;
-    };
-    unsigned traw = 0;
-    if (tries < kXcds) traw = ticket();
-    auto next_dyn = [&]() -> int {
-        while (tries < kXcds) {
-            const int t = (int)__builtin_amdgcn_readfirstlane(traw);
-            const int lo = waves_m + xr * R;
-            if (t < std::min(R, nchunk - lo)) {
-                traw = ticket();
-                return lo + t;
-            }
-            if (++tries < kXcds) {
-                xr = (xr + 1) & (kXcds - 1);
-                traw = ticket();
-            }
-        }
-        return -1;
-    };
-    int ch = wave_id;
-    float xn[kNB][XD];
-#pragma unroll
-    for (int b = 0; b < kNB; ++b) load_x(ch * kNB + b, xn[b]);
-    while (ch < nchunk) {
-        float xa[kNB][XD];
-#pragma unroll
-        for (int b = 0; b < kNB; ++b)
-#pragma unroll
-            for (int j = 0; j < XD; ++j) xa[b][j] = xn[b][j];
-        int nc;
-        if (!head) {
-            nc = ch + waves_m;
-        } else {
-            const int c = next_dyn();
-            nc = c < 0 ? nchunk : c;
-        }
-        const int pre = nc < nchunk ? nc : ch;
-#pragma unroll
-        for (int b = 0; b < kNB; ++b) load_x(pre * kNB + b, xn[b]);
-        step((long long)ch * kNB, xa);
-        while (qn >= 32u) {
-            rerank32(rqs[wave][qn - 32u + (unsigned)r], true);
-            qn -= 32u;
-        }
-        ch = nc;
-    }
-    // the staged batches, the buckets' last partial batches (they may queue more near ties),
-    // then the queue
-    flush_staged();
-#pragma unroll 1
-    for (int t = 0; t < KT; ++t) {
-        const unsigned tail = (unsigned)__builtin_amdgcn_readfirstlane((int)bcnt[wave][t]);
-        const unsigned pend = tail & 31u;
-        if (pend) {
-            const uint32_t e = bq[wave][t][(tail - pend + (unsigned)r) & (kBqCap - 1)];
-            float xs[XD];
-            load_row((unsigned)r < pend ? (long long)(e & kBqRow) : 0, xs);
-            flush(t, tail - pend, (int)pend, xs);
-        }
-    }
-    while (qn >= 32u) {
-        rerank32(rqs[wave][qn - 32u + (unsigned)r], true);
-        qn -= 32u;
-    }
-    if (qn) {
-        const bool valid = (unsigned)r < qn;
-        rerank32(valid ? rqs[wave][r] : make_uint2(0u, 0u), valid);
-    }
-    if (counts) {
-        __builtin_amdgcn_wave_barrier();
-        for (int i = lane; i < K; i += 64) {
-            uint32_t c = hist[wave][i];
-            if (c) atomicAdd(&counts[(long long)m * K + i], c);
-        }
-    }
-    if (lane == 0 && slow_count) atomicAdd(rerank, slow_count);
-}
-
 // Exact VALU kernel: one thread per (vector, part); any K, any dsub.  Used for shapes the
 // MFMA kernel is not instantiated for, for inputs with non-finite centroids, and as the
 // independent cross-check of the MFMA kernel in the GPU tests.
@@ -1959,14 +1346,6 @@ int plan_pa(int dsub) {
     }
 }
 
-// K = 256: the two-pass bucketed kernel (default) or the one-pass P/Q kernel
-// (PQH_ASSIGN_IMPL=pq: an A/B knob; both give the oracle's codes)
-// (read per launch, so a test can switch it in-process)
-bool assign_impl_bkt() {
-    const char* s = getenv("PQH_ASSIGN_IMPL");
-    return !(s && strcmp(s, "pq") == 0);
-}
-
 template <typename CodeT>
 int launch_mfma(pqh_ctx* ctx, pqh_pq* pq, const float* x, long long n, long long ldx,
                 CodeT* codes, uint32_t* counts, long long ldc) {
@@ -1990,18 +1369,15 @@ int launch_mfma(pqh_ctx* ctx, pqh_pq* pq, const float* x, long long n, long long
 #define PQH_CASE(DD) PQH_CASE_KT(DD, 8)
 #define PQH_CASE_KT(DD, KTT)                                                                \
     case DD: {                                                                              \
-        auto kfn = pq_assign_mfma<DD, KTT, CodeT>;                                          \
-        if constexpr (KTT == 8) {                                                           \
-            if (assign_impl_bkt()) kfn = pq_assign_bkt<DD, CodeT>;                          \
-        }                                                                                   \
         int per_cu = 1;                                                                     \
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(                                   \
-                &per_cu, (const void*)kfn, (int)block.x, 0) != hipSuccess || per_cu < 1)    \
+                &per_cu, (const void*)(pq_assign_mfma<DD, KTT, CodeT>), (int)block.x, 0) != \
+                hipSuccess || per_cu < 1)                                                   \
             per_cu = 1;                                                                     \
         long long gx = (long long)ctx->num_cus * per_cu / groups;                           \
         gx = std::max(1ll, std::min(gx, ((nblk + kNB - 1) / kNB + kWavesPerWG - 1) / kWavesPerWG)); \
         if (gx >= 16) gx &= ~7ll;   /* CU-uniform subspace placement (see the kernel) */   \
-        hipLaunchKernelGGL(kfn, dim3((unsigned)(gx * groups)), block,                       \
+        hipLaunchKernelGGL((pq_assign_mfma<DD, KTT, CodeT>), dim3((unsigned)(gx * groups)), block, \
                            0, ctx->stream, x, n, ldx, pq->m, pq->d_afrag, pq->d_cn, pq->d_cent, \
                            pq->d_cmax, pq->d_sqc, codes, counts, rr, sched, (int)gx,         \
                            rr_next, sched ? ctx->d_sched + (1 - ring) * kSchedSet : nullptr, \

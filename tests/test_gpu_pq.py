@@ -85,6 +85,30 @@ def test_assign_rerank_queue_overflow(gpu, oracle):
     assert np.array_equal(codec.counts_to_host(counts), oracle.histogram(got, 256, False))
 
 
+@pytest.mark.parametrize("lo", [False, True])
+def test_assign_one_tile_winners(gpu, oracle, lo):
+    """Skewed data: every vector sits next to a centroid of tile 0 (rows 0-31), so every
+    winner comes from one MFMA tile and one P-group pair; with `lo` the x are not bf16-exact
+    (the lo MFMA pass).  Codes and fused counts == the oracle."""
+    torch, codec, ctx = gpu
+    rng = np.random.default_rng(23)
+    n, m, dsub = 200_003, 4, 16
+    cent = (rng.random((m, 256, dsub)) * 100).astype(np.float32)
+    pick = rng.integers(0, 32, (n, m))
+    x = np.empty((n, m * dsub), np.float32)
+    for i in range(m):
+        x[:, i * dsub:(i + 1) * dsub] = cent[i][pick[:, i]] + rng.normal(0, 0.5, (n, dsub))
+    if not lo:
+        x = np.round(x)
+    x = x.astype(np.float32)
+    want, _ = oracle.pq_assign(x, cent, threads=0)
+    assert (want < 32).all()
+    counts = torch.zeros((m, 256), dtype=torch.int32, device="cuda")
+    got, _ = _assign(gpu, x, cent, 0, counts)
+    assert np.array_equal(got, want), (got != want).sum()
+    assert np.array_equal(codec.counts_to_host(counts), oracle.histogram(got, 256, False))
+
+
 def test_assign_alternating_subspace_counts_one_context(gpu, oracle):
     """m = 16, then 8, then 16 on one context, each with enough rows for the dynamic work
     queues: a launch resets the next launch's queue heads (and spill counters) for every
