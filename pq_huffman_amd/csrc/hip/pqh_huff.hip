@@ -39,7 +39,12 @@ static_assert(kHistCarry == 4095u, "the flush test reads the top nibble of each 
 
 __device__ __forceinline__ void hist_flush_carry(uint32_t* pairs, int words, unsigned base_bin,
                                                  int k, uint32_t* __restrict__ acc) {
-    __syncthreads();   // the chunk's counts are in
+    // The chunk's counts are in.  The explicit wait matters: in the part-major instance of
+    // hist_ctx_w the compiler put no lgkmcnt wait before this barrier, so another wave's
+    // last LDS atomics could land after this flush read the counter and be overwritten by
+    // `keep` (64 or 128 counts of a hot pair lost, on some runs only; a GPU test caught it).
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
     for (int w = threadIdx.x; w < words; w += blockDim.x) {
         const uint32_t x = pairs[w];
         if (!(x & 0xF000F000u)) continue;   // both halves <= 4095
@@ -237,7 +242,10 @@ hist_ctx_w(const uint8_t* __restrict__ codes, long long n, int m_total, int k,
     unsigned carry = w0 > 0 ? (w0 - 1 < n ? (unsigned)(PM ? pm[w0 - 1] : codes[(w0 - 1) * m_total + m]) : ~0u)
                             : (prev_row ? (unsigned)prev_row[m] : ~0u);
     carry = (unsigned)__builtin_amdgcn_readfirstlane((int)carry);
-    if (first) __syncthreads();   // the counters are zeroed
+    if (first) {   // the counters are zeroed (explicit wait: see hist_flush_carry)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
     first = false;
     if (PM && cnt == kR && !(reinterpret_cast<uintptr_t>(pm + w0) & 3)) {
         // part-major: lane l holds rows 4l .. 4l + 3 of a 256-row tile (one 4-byte load)

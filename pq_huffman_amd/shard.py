@@ -386,7 +386,7 @@ def shard_encode(ctx, comm: TorchComm, codes, tables, counts, out, chunk_vectors
     on another rank shows in offsets[1] == -1: check=True synchronises and raises on it here
     (status()); otherwise the caller checks with status()."""
     import torch
-    from .capi import Block, check
+    from .capi import Block, check as _check
     n, m = codes.shape
     dev = codes.device
     scratch = torch.empty(int(_lib().pqh_shard_scratch_bytes(comm.world, m)), dtype=torch.uint8,
@@ -408,7 +408,7 @@ def shard_encode(ctx, comm: TorchComm, codes, tables, counts, out, chunk_vectors
         comm.clear()
     if comm.error is not None:
         raise comm.error
-    check(rc, "pqh_shard_encode")
+    _check(rc, "pqh_shard_encode")
     if ctx.stream != torch.cuda.current_stream(dev):
         scratch.record_stream(ctx.stream)   # (asynchronous: keep it until the stream is done)
     if check:
