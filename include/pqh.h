@@ -86,7 +86,8 @@ int pqh_pq_assign(pqh_ctx_t* ctx, const pqh_pq_t* pq, const float* d_x, long lon
                   long long ld_x, void* d_codes, uint32_t* d_counts, int mode);
 /* pqh_pq_assign writing the codes PART-MAJOR: codes of part i at d_codes[i * ld_codes + v]
  * (ld_codes >= n elements): each subspace's codes are contiguous, so the kernel stores
- * whole lines and a part's histogram reads one contiguous run (pqh_histogram_parts,
+ * whole 128-byte lines (when d_codes is 128-byte aligned and ld_codes a multiple of 128
+ * codes; any layout is correct) and a part's histogram reads one contiguous run (pqh_histogram_parts,
  * pqh_encode_write_parts consume this layout; pqh_transpose_codes converts to rows).
  * d_counts: as pqh_pq_assign (K <= 256 only). */
 int pqh_pq_assign_parts(pqh_ctx_t* ctx, const pqh_pq_t* pq, const float* d_x, long long n,

@@ -134,8 +134,9 @@ class PQ:
         (pqh_pq_assign_parts: the kernel stores whole lines)."""
         torch = _torch()
         n = x.shape[0]
-        if parts is None:
-            parts = torch.empty((self.m, n), dtype=self.code_dtype, device=x.device)
+        if parts is None:   # (rows padded to 128 codes: whole-line stores, see the kernel)
+            parts = torch.empty((self.m, (n + 127) // 128 * 128), dtype=self.code_dtype,
+                                device=x.device)[:, :n]
         c = ctx or self.ctx
         check(lib().pqh_pq_assign_parts(c.ptr, self.ptr, _ptr(x), n, x.stride(0), _ptr(parts),
                                         parts.stride(0), _ptr(counts), mode),

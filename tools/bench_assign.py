@@ -41,16 +41,21 @@ def run(reps, name):
     cent = bench.train_centroids(torch, x, m, k) if k == 256 else centroids_from_rows(x, m, k, 5)
     ctx = codec.Context(0)
     pq = codec.PQ(ctx, np.ascontiguousarray(cent, np.float32))
-    codes = torch.empty((n, m), dtype=torch.uint8 if k <= 256 else torch.int16, device=dev)
+    parts = os.environ.get("BENCH_ASSIGN_PARTS", "0") == "1"   # part-major codes
+    ct = torch.uint8 if k <= 256 else torch.int16
+    codes = torch.empty((m, (n + 127) // 128 * 128), dtype=ct, device=dev)[:, :n] if parts else \
+        torch.empty((n, m), dtype=ct, device=dev)
+    run_assign = (lambda mode: pq.assign_parts(x, codes, mode=mode)) if parts else \
+        (lambda mode: pq.assign(x, codes, mode=mode))
     modes = (0, 1) if k > 256 and os.environ.get("BENCH_ASSIGN_EXACT", "1") == "1" else (0,)
     for mode in modes:
         r = reps if mode == 0 else max(2, reps // 10)
         for _ in range(2):
-            pq.assign(x, codes, mode=mode)
+            run_assign(mode)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(r):
-            pq.assign(x, codes, mode=mode)
+            run_assign(mode)
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) / r * 1e3
         tf = 2.0 * k * d * n / (ms * 1e-3) / 1e12
