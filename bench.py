@@ -157,6 +157,12 @@ def parse():
                     help="stream of the context histogram: the assignment's, the batch's "
                          "lane (before its code tables), or a stream of its own (a fifth "
                          "stream: the process then asks HIP for 8 hardware queues)"),
+    ap.add_argument("--assign-event-every", type=int, default=4,
+                    help="record the assignment's start/end HIP events (the roofline's kernel "
+                         "time) on every N-th timed step (0: none -- the roofline then uses the "
+                         "untimed steps after the timed region).  An event record is a packet "
+                         "on stream A: every step 2,531-2,550 Mvec/s, every 4th 2,575-2,604, "
+                         "none 2,599-2,613 (200 steps)")
     ap.add_argument("--tbufs", type=int, default=2,
                     help="code-table sets per table lane when --elanes > 0")
     ap.add_argument("--a-priority", action="store_true",
@@ -486,8 +492,11 @@ def main():
     def rec(name, stream):
         # the assignment's events over the timed steps (the roofline's kernel time), the other
         # stages' over the timed steps too (--stage-events timed) or the untimed ones after
-        timed_ev = state["timed"] and (name == "assign" or args.stage_events == "timed")
-        if not (timed_ev or (state.get("after") and name != "assign")):
+        every = args.assign_event_every
+        asg_ev = name == "assign" and every > 0 and state.get("step", 0) % every == 0
+        timed_ev = state["timed"] and (asg_ev or (name != "assign" and args.stage_events == "timed"))
+        after_ev = state.get("after") and (name != "assign" or every <= 0)
+        if not (timed_ev or after_ev):
             return None
         e0, e1 = ev_pool.pop() if ev_pool else (torch.cuda.Event(enable_timing=True),
                                                 torch.cuda.Event(enable_timing=True))
@@ -513,11 +522,18 @@ def main():
     parts = torch.arange(m, device=dev)
     ones_m = torch.ones(m, dtype=torch.int32, device=dev)
 
+    def wait(stream, ev):
+        """stream waits for ev -- unless the host sees ev already complete (a slot's previous
+        batch, several steps back): a cross-stream wait is a barrier packet on the waiting
+        queue, ~7-15 us of stream time per wait in the profiled schedule"""
+        if not ev.query():
+            stream.wait_event(ev)
+
     def hist(s, c, st):
         """batch s's symbol histogram on stream st (context c); with hist_split only its
         partial counts (the lane reduces them, hist_reduce)"""
         if used[s]:                  # the slot's previous batch: tables built (counts free)
-            st.wait_event(ev_tab[s])
+            wait(st, ev_tab[s])
         e = rec("hist", st)
         if hist_split and pm:
             codec.histogram_partial_parts(c, codes[s], n, k, hparts[s], prev_row=halo[s])
@@ -552,7 +568,7 @@ def main():
         sL = c.stream
         with torch.cuda.stream(sA):
             if used[s]:              # the slot's previous batch: encoded (codes[s] free)
-                sA.wait_event(ev_enc[s])
+                wait(sA, ev_enc[s])
             e = rec("assign", sA)
             pq.assign(x, codes[s], ctx=ctx)
             done(e, sA)
@@ -561,7 +577,7 @@ def main():
             sL.wait_event(ev_hist[s])
             ti = tab_index(i)
             if elanes is not lanes:              # tabs[ti] free: its last decode is done
-                sL.wait_event(ev_dec[ti])
+                wait(sL, ev_dec[ti])
             e = rec("codebook", sL)
             tc = time.perf_counter()
             status[s] = shard.shard_encode_tables(c, comm, codes[s], tabs[ti], counts[s],
@@ -582,7 +598,7 @@ def main():
         sF = cF.stream
         with torch.cuda.stream(sF):
             if used[s]:              # the slot's previous batch: encoded (codes[s] free) ...
-                sF.wait_event(ev_enc[s])
+                wait(sF, ev_enc[s])
             e = rec("assign", sF)
             if pm:
                 apq[i % na].assign_parts(x, codes[s], ctx=cF)
@@ -633,8 +649,8 @@ def main():
         if pair and i % 2 == 1:
             with torch.cuda.stream(sL):
                 s0, t0i, ti = (i - 1) % slots, tab_index(i - 1), tab_index(i)
-                sL.wait_event(ev_dec[t0i])
-                sL.wait_event(ev_dec[ti])
+                wait(sL, ev_dec[t0i])
+                wait(sL, ev_dec[ti])
                 e = rec("codebook", sL)
                 if i == state["nsteps"] - 1 and args.drain_trees != "default":
                     tabs[t0i].build(counts[s0], c, trees=args.drain_trees)   # the drain
@@ -648,7 +664,7 @@ def main():
         with torch.cuda.stream(sL):
             ti = tab_index(i)
             if elanes is not lanes:              # tabs[ti] free: its last decode is done
-                sL.wait_event(ev_dec[ti])
+                wait(sL, ev_dec[ti])
             e = rec("codebook", sL)
             # GPU trees + lookup tables, no host trip.  --drain-trees / --fill-trees pick
             # another builder for the run's last batch (built after the assignment stream is
@@ -753,6 +769,7 @@ def main():
         state["issue_t"] = []
         for i in range(steps):
             state["issue_t"].append(time.perf_counter())
+            state["step"] = i
             front(i)
             if i >= lag:
                 back(i - lag)
