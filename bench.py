@@ -163,6 +163,12 @@ def parse():
                          "untimed steps after the timed region).  An event record is a packet "
                          "on stream A: every step 2,531-2,550 Mvec/s, every 4th 2,575-2,604, "
                          "none 2,599-2,613 (200 steps)")
+    ap.add_argument("--assign-wgs-per-cu", type=float, default=2.5,
+                    help="workgroups per CU of the persistent K = 256 assignment grid "
+                         "(PQH_ASSIGN_WGS_PER_CU; the occupancy limit is 3): with three 166-VGPR "
+                         "waves on a SIMD no wave of the kernels beside the grid fits, so a "
+                         "lighter grid lets them co-run.  Measured at 200 steps: 3 -> 2,614-2,642, "
+                         "2.5 -> 2,676, 2 -> 2,669-2,688 Mvec/s; --sort --lanes 3: 1,969 -> 2,043")
     ap.add_argument("--tbufs", type=int, default=2,
                     help="code-table sets per table lane when --elanes > 0")
     ap.add_argument("--a-priority", action="store_true",
@@ -341,6 +347,8 @@ def pcie_ms(torch, x, codes, stream_bytes):
 
 def main():
     args = parse()
+    if args.assign_wgs_per_cu > 0:   # read by the library at each assignment launch
+        os.environ["PQH_ASSIGN_WGS_PER_CU"] = str(args.assign_wgs_per_cu)
     if int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.hist_on == "own":
         # 4 library/torch streams + RCCL's own: give each a hardware queue (HIP reads this at
         # initialisation; measured neutral at one rank, 2,150 vs 2,153 Mvec/s)
@@ -390,7 +398,9 @@ def main():
            if args.a_priority else codec.Context(local))
     sA = ctx.stream
     if args.lanes is None:   # 1 + lanes + elanes <= 4 streams: one hardware queue each
-        args.lanes = 3 if args.config == "k4096" else 2
+        # (k4096: the tree builds are the long stage; --sort: the sort and the histogram ride
+        # on the lanes -- 1,969 vs 1,877 Mvec/s)
+        args.lanes = 3 if args.config == "k4096" or args.sort else 2
     if args.elanes is None:
         args.elanes = 0 if args.config == "k4096" else 1
     nl = 1 if serial else max(1, args.lanes)
