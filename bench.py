@@ -169,6 +169,9 @@ def parse():
                          "waves on a SIMD no wave of the kernels beside the grid fits, so a "
                          "lighter grid lets them co-run.  Measured at 200 steps: 3 -> 2,614-2,642, "
                          "2.5 -> 2,676, 2 -> 2,669-2,688 Mvec/s; --sort --lanes 3: 1,969 -> 2,043")
+    ap.add_argument("--split-cus", type=int, default=0,
+                    help="> 0: the code-table, encode and decode streams on this many compute "
+                         "units, the assignment stream on the others (disjoint CU masks)")
     ap.add_argument("--tbufs", type=int, default=2,
                     help="code-table sets per table lane when --elanes > 0")
     ap.add_argument("--a-priority", action="store_true",
@@ -394,8 +397,15 @@ def main():
     # Serial: everything on A, in order.
     serial = args.sched == "serial" or args.no_overlap
     # stream A: torch's default stream, or (--a-priority) a high-priority stream of its own
-    ctx = (codec.Context(local, stream=torch.cuda.Stream(device=dev, priority=-1))
-           if args.a_priority else codec.Context(local))
+    # --split-cus N: the table / encode / decode streams on N compute units (spread over the
+    # XCDs), stream A -- the persistent assignment grid and the histogram -- on all the others
+    split = args.split_cus if 0 < args.split_cus < torch.cuda.get_device_properties(dev).multi_processor_count else 0
+    if split:
+        torch.cuda.synchronize()   # (A gets a stream of its own: the setup's work is done)
+        ctx = codec.Context(local, cus=split, complement=True)
+    else:
+        ctx = (codec.Context(local, stream=torch.cuda.Stream(device=dev, priority=-1))
+               if args.a_priority else codec.Context(local))
     sA = ctx.stream
     if args.lanes is None:   # 1 + lanes + elanes <= 4 streams: one hardware queue each
         # (k4096: the tree builds are the long stage; --sort: the sort and the histogram ride
@@ -408,12 +418,12 @@ def main():
     # count: no CU mask).  (torch.cuda.Stream lanes measured 1,107 vs 2,250 Mvec/s: torch's
     # stream pool maps them onto the hardware queues of its other streams.)  Tensors used on
     # them are released before the contexts destroy them (teardown below).
-    lanes = [ctx] if serial else [codec.Context(local, cus=args.table_cus or 1 << 20)
+    lanes = [ctx] if serial else [codec.Context(local, cus=split or args.table_cus or 1 << 20)
                                   for _ in range(nl)]
     # encode + decode streams: the table lanes themselves, or --elanes streams of their own
     # (then batch i's tables are built on lane i % lanes while the encode/decode streams
     # work on earlier batches, and a table lane rebuilds only after the decode that read it)
-    elanes = lanes if serial or args.elanes <= 0 else [codec.Context(local, cus=1 << 20)
+    elanes = lanes if serial or args.elanes <= 0 else [codec.Context(local, cus=split or 1 << 20)
                                                        for _ in range(args.elanes)]
     ne = len(elanes)
     pq = codec.PQ(ctx, cent)
