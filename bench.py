@@ -811,16 +811,25 @@ def main():
     # / 2,560-2,640.  The assignment kernel alone runs on the batch for --device-warmup-ms;
     # its codes are recomputed by every timed step, nothing carries over.
     dw_ms = 0.0
+    alone = []   # HIP-event times of the warm-up's assignment launches (the kernel alone)
     if args.device_warmup_ms > 0:
         barrier()
         tw = time.perf_counter()
         while (time.perf_counter() - tw) * 1e3 < args.device_warmup_ms:
-            for _ in range(8):
+            evs = []
+            for u in range(8):
+                if u >= 4:   # (the back half of each burst: the clocks have ramped)
+                    evs.append((torch.cuda.Event(enable_timing=True),
+                                torch.cuda.Event(enable_timing=True)))
+                    evs[-1][0].record(sA)
                 if pm:
                     pq.assign_parts(x, codes[0], ctx=ctx)
                 else:
                     pq.assign(x, codes[0], ctx=ctx)
+                if u >= 4:
+                    evs[-1][1].record(sA)
             torch.cuda.synchronize()
+            alone = [a.elapsed_time(b) for a, b in evs]   # (the last burst's)
         dw_ms = (time.perf_counter() - tw) * 1e3
     run(args.warmup)
     ev_pool.extend((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -968,7 +977,13 @@ def main():
                          # begin -> end); avg_ms above is HIP events around the launch on its
                          # stream, which also count the wait for CUs held by the lanes
                          "profile_avg_ms": (round(prof_avg_us / 1e3, 4)
-                                            if prof_avg_us is not None else None)},
+                                            if prof_avg_us is not None else None),
+                         # the same kernel alone (the device warm-up's last launches, HIP
+                         # events): frac is the in-schedule figure, where it shares the GPU
+                         # with the lanes' kernels by design
+                         "alone_avg_ms": (round(sum(alone) / len(alone), 4) if alone else None),
+                         "alone_frac": (round((vec_read + vec_write) * n / (sum(alone) / len(alone) * 1e-3)
+                                              / 1e9 / HBM_PEAK_GBS, 4) if alone else None)},
             "stages_ms": {s: round(v / args.steps * 1e3, 4) for s, v in acc.items()
                           if (s != "sort" or args.sort) and (s != "lut" or lut_a)},
             "stages_note": ("per-stage HIP-event times on their own streams (the assignment's "

@@ -407,8 +407,13 @@ __device__ __forceinline__ f32x16 tile_scores_a(const bf16x8* a, const bf16x8* B
 
 // this lane's 16 rows of ||c||^2 for tile t (LDS image [tile][half][16]: every lane of a
 // half-wave reads the same 64 bytes, a broadcast)
+// (four 16-byte reads: with one 64-byte vector read the compiler loses track of which LDS
+// array it reads and waits for the in-flight LDS DMA of the next chunk's x before every tile)
 __device__ __forceinline__ f32x16 tile_norms(const float* Cn, int t, int h) {
-    return *reinterpret_cast<const f32x16*>(Cn + (t * 2 + h) * 16);
+    const f32x4* p = reinterpret_cast<const f32x4*>(Cn + (t * 2 + h) * 16);
+    const f32x4 a = p[0], b = p[1], c = p[2], d = p[3];
+    return f32x16{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3],
+                  c[0], c[1], c[2], c[3], d[0], d[1], d[2], d[3]};
 }
 
 // A fragment p of tile t, [PA][KT][64 lanes] per subspace: from the workgroup's LDS copy
@@ -463,6 +468,14 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     // each wave's re-rank queue (the LDS budget stays at 32 KB, so a workgroup still fits on
     // a CU beside a code-table build's 112 KB)
     __shared__ uint2 rqs[kWavesPerWG][kRqLds];
+#ifndef PQH_ASSIGN_XLDS
+#define PQH_ASSIGN_XLDS 1
+#endif
+    // the next chunk's x slices, prefetched by LDS DMA instead of into registers (16 fewer
+    // VGPRs live across the step at D = 16): [wave][block][16-byte piece][64 lanes x 4]
+    constexpr bool kXLds = PQH_ASSIGN_XLDS && KT <= 8 && Slice<D>::XD % 4 == 0;
+    __shared__ __attribute__((aligned(16))) float xst[kXLds ? kWavesPerWG : 1][kXLds ? kNB : 1]
+                                                     [kXLds ? Slice<D>::XD / 4 : 1][kXLds ? 256 : 1];
     // (PQH_ASSIGN_CLDS, K = 256) the fp32 centroids for the exact re-rank's candidate rows
     __shared__ __attribute__((aligned(16))) float Cf[kLdsA && kCentLds ? K * D : 1];
 
@@ -581,6 +594,35 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         } else {
 #pragma unroll
             for (int j = 0; j < XD; ++j) dst[j] = xp[j];
+        }
+    };
+    // the same slices into xst[wave][slot] by LDS DMA (16 bytes per lane and piece)
+    auto load_x_lds = [&](int b, int slot) {
+        long long row0 = (long long)b * 32;
+        unsigned off = xlane_off;
+        if (b >= nfull) {
+            row0 = row0 < n - 1 ? row0 : n - 1;
+            const long long left = n - 1 - row0;
+            const unsigned last = (unsigned)(left < 31 ? left : 31);
+            off = __umul24(min((unsigned)r, last), ldx4) + xh_off;
+        }
+        const float* xp = reinterpret_cast<const float*>(xm + row0 * (long long)ldx4 + off);
+#pragma unroll
+        for (int j = 0; j < XD; j += 4) {
+#if defined(__HIP_DEVICE_COMPILE__)   // (the host pass rejects the 16-byte form)
+            __builtin_amdgcn_global_load_lds(
+                xp + (HALF ? 16 * (j >> 3) + (j & 7) : j),
+                (__attribute__((address_space(3))) void*)(&xst[wave][slot][j / 4][0]), 16, 0, 0);
+#else
+            (void)xp;
+#endif
+        }
+    };
+    auto read_x_lds = [&](int slot, float* dst) {
+#pragma unroll
+        for (int j = 0; j < XD; j += 4) {
+            const f32x4 q = *reinterpret_cast<const f32x4*>(&xst[wave][slot][j / 4][lane * 4]);
+            dst[j] = q.x; dst[j + 1] = q.y; dst[j + 2] = q.z; dst[j + 3] = q.w;
         }
     };
     // Deferred re-rank: a vector whose screening gap is too small is appended to this wave's
@@ -1106,15 +1148,28 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
 #endif
     };
     int ch = wave_id;
-    float xn[kNB][XD];
+    float xn[kXLds ? 1 : kNB][XD];
 #pragma unroll
-    for (int b = 0; b < kNB; ++b) load_x(ch * kNB + b, xn[b]);
+    for (int b = 0; b < kNB; ++b) {
+        if constexpr (kXLds)
+            load_x_lds(ch * kNB + b, b);
+        else
+            load_x(ch * kNB + b, xn[b]);
+    }
     while (ch < nchunk) {
         float xa[kNB][XD];
+        if constexpr (kXLds) {
 #pragma unroll
-        for (int b = 0; b < kNB; ++b)
+            for (int b = 0; b < kNB; ++b) read_x_lds(b, xa[b]);
+            // the slices are in registers before the next chunk's DMA overwrites them (a DMA
+            // write is not ordered with this wave's LDS reads)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        } else {
 #pragma unroll
-            for (int j = 0; j < XD; ++j) xa[b][j] = xn[b][j];
+            for (int b = 0; b < kNB; ++b)
+#pragma unroll
+                for (int j = 0; j < XD; ++j) xa[b][j] = xn[b][0 * j + j];
+        }
         int nc;
         if (!head) {
             nc = ch + waves_m;
@@ -1124,7 +1179,12 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         }
         const int pre = nc < nchunk ? nc : ch;   // branch-free: re-load at the end
 #pragma unroll
-        for (int b = 0; b < kNB; ++b) load_x(pre * kNB + b, xn[b]);
+        for (int b = 0; b < kNB; ++b) {
+            if constexpr (kXLds)
+                load_x_lds(pre * kNB + b, b);
+            else
+                load_x(pre * kNB + b, xn[b]);
+        }
         step((long long)ch * kNB, xa);
         while (qn >= 32u) {   // full batches of deferred vectors: done while the SIMD is busy
             rerank32(rqs[wave][qn - 32u + (unsigned)r], true);
