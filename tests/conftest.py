@@ -1,4 +1,5 @@
 import os
+import re
 import sys
 
 import numpy as np
@@ -24,3 +25,12 @@ def oracle():
     from oracle import oracle_ctypes
     oracle_ctypes.lib()
     return oracle_ctypes
+
+
+def run_fail_msg(r):
+    """a torchrun child's failure, readable: every rank's traceback lines first (torchrun
+    prefixes them with [rankN]:), then the tail of the output"""
+    out = (r.stdout or "") + (r.stderr or "")
+    lines = out.splitlines()
+    ranks = [ln for ln in lines if re.match(r"\s*\[rank\d+\]:", ln) or "Error" in ln]
+    return "\n".join(ranks[:200]) + "\n---- tail ----\n" + out[-3000:]

@@ -13,7 +13,7 @@ import sys
 import numpy as np
 import pytest
 
-from conftest import ROOT
+from conftest import ROOT, run_fail_msg
 
 pytestmark = pytest.mark.gpu
 
@@ -38,7 +38,7 @@ def test_two_rank_rehearsal_stitched_stream(oracle, tmp_path, mode, path):
            "--one-device", "--vectors", "30001", "--steps", "3", "--warmup", "1",
            "--mode", mode, "--no-cpu-baseline", "--dump", str(dump), "--shard-path", path]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.returncode == 0, run_fail_msg(r)
     d = np.load(dump, allow_pickle=False)
     codes = d["codes"]
     assert codes.shape == (60002, 8)

@@ -11,7 +11,7 @@ import sys
 import numpy as np
 import pytest
 
-from conftest import ROOT
+from conftest import ROOT, run_fail_msg
 
 pytestmark = pytest.mark.gpu
 
@@ -32,7 +32,7 @@ def test_two_rank_library_shard_encode(oracle, tmp_path, case, mode):
            "--out", str(dump)]
     r = subprocess.run(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1"), capture_output=True,
                        text=True, timeout=240)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.returncode == 0, run_fail_msg(r)
     d = np.load(dump, allow_pickle=False)
     rows = d["rows"]
     ctxm = mode == "ctx"
@@ -58,5 +58,5 @@ def test_two_rank_library_shard_encode_one_rank_fails(tmp_path):
            "--out", str(dump)]
     r = subprocess.run(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1"), capture_output=True,
                        text=True, timeout=240)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.returncode == 0, run_fail_msg(r)
     assert int(np.load(dump, allow_pickle=False)["failed"]) == 1
