@@ -58,7 +58,10 @@ namespace {
 #ifndef PQH_ASSIGN_DEFER
 #define PQH_ASSIGN_DEFER 1
 #endif
-constexpr int kRqLds = 128;      // deferred re-rank queue entries per wave (LDS)
+#ifndef PQH_ASSIGN_RQ
+#define PQH_ASSIGN_RQ 128
+#endif
+constexpr int kRqLds = PQH_ASSIGN_RQ;   // deferred re-rank queue entries per wave (LDS)
 constexpr int kWavesPerWG = PQH_ASSIGN_WPG;   // subspace waves per workgroup
 constexpr int kNB = PQH_ASSIGN_NB;            // 32-vector blocks screened together per step
 #ifndef PQH_ASSIGN_CLDS
@@ -459,7 +462,11 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     constexpr int PB = KT <= 8 ? 4 : 8;
     constexpr unsigned PMASK = (1u << PB) - 1;
     static_assert(2 * KT <= (1 << PB), "P-group index must fit the key's low bits");
-    __shared__ uint32_t hist[kWavesPerWG][kLdsA ? K : 1];
+    // the fused histogram's per-wave counters (non-context counts only): dynamic LDS that the
+    // launch allocates only when counts are requested, so the context path's workgroups
+    // leave those 4 KB to the kernels running beside the grid
+    extern __shared__ uint32_t hist_dyn[];
+    auto hist = [&](int w) -> uint32_t* { return hist_dyn + w * K; };
     // the subspace's A fragments, shared by the workgroup's waves (16 KB at D = 16): keeping
     // them out of VGPRs is what lets several waves share each SIMD
     __shared__ uint4 As[kLdsA ? P::PA * KT * 64 : 1];
@@ -512,7 +519,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         for (int i = threadIdx.x; i < KT * 2 * 16; i += blockDim.x)
             Cn[i] = cnorm[(long long)m * KT * 2 * 16 + i];
         if (kLdsA && counts)
-            for (int i = lane; i < K; i += 64) hist[wave][i] = 0;
+            for (int i = lane; i < K; i += 64) hist(wave)[i] = 0;
         if constexpr (kLdsA && kCentLds)
             for (int i = threadIdx.x; i < K * D; i += blockDim.x) Cf[i] = cent[(long long)m * K * D + i];
         __syncthreads();   // the only workgroup barrier
@@ -924,7 +931,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
             if (valid && own_lane && !(slow && deferred)) {
                 *reinterpret_cast<CodeT*>(reinterpret_cast<char*>(cbase + (blk0 + ba) * 32 * crs) +
                                           (pair ? code_pair_off : code_lane_off)) = (CodeT)code;
-                if (kLdsA && counts) atomicAdd(&hist[wave][code], 1u);
+                if (kLdsA && counts) atomicAdd(&hist(wave)[code], 1u);
             }
         }
     };
@@ -1140,7 +1147,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         if (valid && h == 0) {
             const int code = bidx == 0x7FFFFFFF ? 0 : bidx;
             cbase[v * crs] = (CodeT)code;
-            if (kLdsA && counts) atomicAdd(&hist[wave][code], 1u);
+            if (kLdsA && counts) atomicAdd(&hist(wave)[code], 1u);
         }
 #ifdef PQH_ASSIGN_STAMPS
         rr_ticks += __builtin_amdgcn_s_memrealtime() - rr0;
@@ -1234,7 +1241,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     if (kLdsA && counts) {
         __builtin_amdgcn_wave_barrier();
         for (int i = lane; i < K; i += 64) {
-            uint32_t c = hist[wave][i];
+            uint32_t c = hist(wave)[i];
             if (c) atomicAdd(&counts[(long long)m * K + i], c);
         }
     }
@@ -1439,15 +1446,16 @@ int launch_mfma(pqh_ctx* ctx, pqh_pq* pq, const float* x, long long n, long long
 #define PQH_CASE_KT(DD, KTT)                                                                \
     case DD: {                                                                              \
         int per_cu = 1;                                                                     \
+        const size_t dyn = KTT <= 8 && counts ? (size_t)kWavesPerWG * 256 * 4 : 0;         \
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(                                   \
-                &per_cu, (const void*)(pq_assign_mfma<DD, KTT, CodeT>), (int)block.x, 0) != \
+                &per_cu, (const void*)(pq_assign_mfma<DD, KTT, CodeT>), (int)block.x, dyn) != \
                 hipSuccess || per_cu < 1)                                                   \
             per_cu = 1;                                                                     \
         long long gx = (long long)((double)ctx->num_cus * assign_wgs_per_cu(per_cu) / groups); \
         gx = std::max(1ll, std::min(gx, ((nblk + kNB - 1) / kNB + kWavesPerWG - 1) / kWavesPerWG)); \
         if (gx >= 16) gx &= ~7ll;   /* CU-uniform subspace placement (see the kernel) */   \
         hipLaunchKernelGGL((pq_assign_mfma<DD, KTT, CodeT>), dim3((unsigned)(gx * groups)), block, \
-                           0, ctx->stream, x, n, ldx, pq->m, pq->d_afrag, pq->d_cn, pq->d_cent, \
+                           dyn, ctx->stream, x, n, ldx, pq->m, pq->d_afrag, pq->d_cn, pq->d_cent, \
                            pq->d_cmax, pq->d_sqc, codes, counts, rr, sched, (int)gx,         \
                            rr_next, sched ? ctx->d_sched + (1 - ring) * kSchedSet : nullptr, \
                            prio, ldc);                                                        \
