@@ -437,7 +437,9 @@ def main():
     # batch not yet encoded
     slots = nl + max(1, args.extra_slots)
     # part-major codes (--code-layout parts): codes[s] is (m, n), part i's codes in row i
-    pm = args.code_layout == "parts" and not args.sort and world == 1 and \
+    # (world > 1: through the library's part-major shard phases, the same pipeline as one rank)
+    pm = args.code_layout == "parts" and not args.sort and \
+        (world == 1 or lib_shard_req(args, world)) and \
         code_t == torch.uint8 and m in (8, 16) and not serial
     # (part rows padded to a multiple of 128 codes: the assignment's stores are then whole
     # 128-byte lines; with ld = n = 10^6 every odd part starts mid-line and each store
@@ -535,8 +537,10 @@ def main():
     ev_asg = [torch.cuda.Event() for _ in range(slots)]
     # the split histogram: partial counts per slot (the assignment stream writes slot s's while
     # a lane may still reduce another's)
+    # (world > 1, library path: the partials on stream A without the halo; phase 1 reduces
+    # them on the table lane and adds the shard-boundary pair -- pqh_shard_encode_tables_parts)
     hist_split = args.hist_split == "on" and ctxm and not serial and not hist_on_lane and \
-        not lib_shard and code_t == torch.uint8
+        (not lib_shard or pm) and code_t == torch.uint8
     hparts = [torch.empty(codec.histogram_partial_bytes(n, m, k), dtype=torch.uint8, device=dev)
               for _ in range(slots)] if hist_split else None
     parts = torch.arange(m, device=dev)
@@ -590,8 +594,13 @@ def main():
             if used[s]:              # the slot's previous batch: encoded (codes[s] free)
                 wait(sA, ev_enc[s])
             e = rec("assign", sA)
-            pq.assign(x, codes[s], ctx=ctx)
+            if pm:
+                pq.assign_parts(x, codes[s], ctx=ctx)
+            else:
+                pq.assign(x, codes[s], ctx=ctx)
             done(e, sA)
+            if hist_split:           # the partial pair counts, as at one rank (no halo yet)
+                hist(s, ctx, sA)
             ev_hist[s].record(sA)
         with torch.cuda.stream(sL):
             sL.wait_event(ev_hist[s])
@@ -601,7 +610,9 @@ def main():
             e = rec("codebook", sL)
             tc = time.perf_counter()
             status[s] = shard.shard_encode_tables(c, comm, codes[s], tabs[ti], counts[s],
-                                                  scratch[s], first_row=rank * n)
+                                                  scratch[s], first_row=rank * n,
+                                                  parts_n=n if pm else None,
+                                                  partials=hparts[s] if hist_split else None)
             acc["collectives"] += time.perf_counter() - tc if state["timed"] else 0.0
             done(e, sL)
             ev_tab[s].record(sL)
@@ -742,7 +753,7 @@ def main():
             if lib_shard:   # phase 2 of pqh_shard_encode: length, all-gather, offsets, write
                 shard.shard_encode_write(c, comm, codes[s], tj, out[j], args.chunk, coff[j],
                                          cprev[j], offs[j], scratch[s], status[s],
-                                         first_row=rank * n)
+                                         first_row=rank * n, parts_n=n if pm else None)
                 tot_dev[j].copy_(shard.scratch_shard_bits(scratch[s], world, m))
                 torch.minimum(shard_min[j], offs[j][1:], out=shard_min[j])
                 state["goff"] = offs[j][:1]
@@ -773,6 +784,7 @@ def main():
             done(e, sL)
             ev_dec[jt].record(sL)
         state["last"] = (s, j)
+        state["last_tab"] = jt
 
     # Every dependency is an event, so batches are issued in order.  With world > 1 the
     # collectives of all streams run in issue order on the process group's one stream: batch
@@ -877,6 +889,27 @@ def main():
         codec.encode_status(c)
     rows_last = codec.transpose_codes(ctx, codes[s_last], n) if pm else codes[s_last]
     assert torch.equal(dec[j_last], rows_last), "round trip mismatch"
+    if world == 1 and not serial:
+        # the last batch's stream, re-encoded from its rows by the row-major encoder
+        # (pqh_encode_write, the path tests/test_gpu_fullsize.py pins to the oracle on all 1M
+        # rows) with the same tables: every stream byte, the bit count and the chunk index
+        # must agree, so a wrong but self-consistent timed stream cannot pass
+        tl = tabs[state["last_tab"]]
+        ref_out = torch.empty_like(out[j_last])
+        ref_coff = torch.empty_like(coff[j_last])
+        ref_prev = torch.empty_like(cprev[j_last]) if ctxm else None
+        ref_tot = torch.zeros(1, dtype=torch.int64, device=dev)
+        codec.encode_write(ctx, tl, rows_last, ref_out, 0, raw_first, None, args.chunk, ref_coff,
+                           ref_prev, total=ref_tot)
+        codec.encode_status(ctx)
+        nbits = int(ref_tot.item())
+        assert int(tot_dev[j_last].item()) == nbits, "stream length != row-path re-encode"
+        assert torch.equal(out[j_last][:(nbits + 7) // 8], ref_out[:(nbits + 7) // 8]), \
+            "stream bytes != row-path re-encode"
+        assert torch.equal(coff[j_last], ref_coff), "chunk index != row-path re-encode"
+        if ctxm:
+            assert torch.equal(cprev[j_last], ref_prev), "chunk context rows != row-path re-encode"
+        del ref_out, ref_coff, ref_prev, ref_tot
     if lib_shard:   # every rank's pqh_shard_encode_write succeeded (no sentinel length)
         shard.status(elanes[j_last], offs[j_last])
         for j, sm in enumerate(shard_min):   # ... for every batch, not only the last
@@ -943,6 +976,11 @@ def main():
                                       "mode)" if args.sort else "no sort"),
                        "sort": bool(args.sort),
                        "code_layout": "parts" if pm else "rows",
+                       # the K = 256 assignment grid's workgroups per CU that this process set
+                       # (PQH_ASSIGN_WGS_PER_CU; a library caller that sets nothing gets the
+                       # occupancy limit, 3)
+                       "assign_wgs_per_cu": (os.environ.get("PQH_ASSIGN_WGS_PER_CU")
+                                             or "library default"),
                        "vectors_per_gpu": n, "d": d, "m": m, "k": k,
                        "mode": "ctx" if ctxm else "noctx",
                        "chunk_vectors": args.chunk, "parallelism": f"dp{world} row shards",

@@ -346,6 +346,25 @@ int pqh_shard_encode_write(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm, const b
                            unsigned long long* d_chunk_offsets, void* d_chunk_prev,
                            unsigned long long* d_offsets, void* d_scratch, int status,
                            int* raw_first);
+/* The two phases for PART-MAJOR codes (pqh_pq_assign_parts: part i's codes at
+ * d_codes[i * ld_codes + v], ld_codes >= the shard's rows), so a multi-rank pipeline runs the
+ * single-rank one (bench.py): phase 2 takes m = 8 or 16 (the row encoder reading part runs).
+ * d_partials (phase 1, optional, context mode): the shard's partial pair counts taken by
+ * pqh_histogram_partial_parts(d_codes, ld_codes, n, m, k, NULL, d_partials) -- e.g. on the
+ * assignment stream, ordered before this call by the caller; phase 1 then reduces them and
+ * adds the shard-boundary pair itself instead of running the histogram.  NULL: phase 1 runs
+ * the part-major histogram (with the halo pair).  Same errors and outputs as above. */
+int pqh_shard_encode_tables_parts(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm,
+                                  const block_t* shard, const void* d_codes, long long ld_codes,
+                                  int m, int k, int context, pqh_tables_t* tables,
+                                  uint32_t* d_counts, void* d_scratch, const void* d_partials);
+int pqh_shard_encode_write_parts(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm,
+                                 const block_t* shard, const void* d_codes, long long ld_codes,
+                                 int m, int k, int context, pqh_tables_t* tables,
+                                 unsigned char* d_out, unsigned long long out_bytes,
+                                 int chunk_vectors, unsigned long long* d_chunk_offsets,
+                                 void* d_chunk_prev, unsigned long long* d_offsets, void* d_scratch,
+                                 int status, int* raw_first);
 /* Synchronises; PQH_ERR_REMOTE if some rank's pqh_shard_encode behind d_offsets failed. */
 int pqh_shard_status(pqh_ctx_t* ctx, const unsigned long long* d_offsets);
 

@@ -157,9 +157,12 @@ SIGNATURES = [
     ("pqh_shard_status", I, [P, P]),
     ("pqh_shard_encode_tables", I, [P, P, P, P, I, I, I, P, P, P]),
     ("pqh_shard_encode_write", I, [P, P, P, P, I, I, I, P, P, ULL, I, P, P, P, P, I, P]),
+    ("pqh_shard_encode_tables_parts", I, [P, P, P, P, LL, I, I, I, P, P, P, P]),
+    ("pqh_shard_encode_write_parts", I, [P, P, P, P, LL, I, I, I, P, P, ULL, I, P, P, P, P, I, P]),
     ("pqh_shard_offsets", I, [P, I, I, P, P]),
     ("pqh_shard_stitch", I, [I, P, P, P, P, ULL]),
     ("pqh_shard_halo_source", I, [P, I, I, P, P]),
+    ("pqh_debug_poison_lds", I, [P, ctypes.c_uint]),
     ("pqh_tree_order", I, [LL, LL, P, P, P, P, P]),
     ("pqh_tree_order_device", I, [P, LL, LL, P, P, P, P, P, P]),
     ("pqh_tree_ext_index_device", LL, [P, LL, P, I, I, P, P, P]),

@@ -39,12 +39,11 @@ static_assert(kHistCarry == 4095u, "the flush test reads the top nibble of each 
 
 __device__ __forceinline__ void hist_flush_carry(uint32_t* pairs, int words, unsigned base_bin,
                                                  int k, uint32_t* __restrict__ acc) {
-    // The chunk's counts are in.  The explicit wait matters: in the part-major instance of
-    // hist_ctx_w the compiler put no lgkmcnt wait before this barrier, so another wave's
-    // last LDS atomics could land after this flush read the counter and be overwritten by
-    // `keep` (64 or 128 counts of a hot pair lost, on some runs only; a GPU test caught it).
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __syncthreads();
+    // The chunk's counts are in.  (lds_barrier's explicit wait matters: in the part-major
+    // instance of hist_ctx_w the compiler put no lgkmcnt wait before a bare barrier here, so
+    // another wave's last LDS atomics could land after this flush read the counter and be
+    // overwritten by `keep` -- 64 or 128 counts of a hot pair lost on some runs.)
+    lds_barrier();
     for (int w = threadIdx.x; w < words; w += blockDim.x) {
         const uint32_t x = pairs[w];
         if (!(x & 0xF000F000u)) continue;   // both halves <= 4095
@@ -60,7 +59,7 @@ __device__ __forceinline__ void hist_flush_carry(uint32_t* pairs, int words, uns
         }
         pairs[w] = keep;   // (this thread owns the word between the barriers)
     }
-    __syncthreads();
+    lds_barrier();
 }
 
 // Context histogram, pass 1: workgroup (chunk of kHistChunk vectors, part, prev-range z)
@@ -120,7 +119,7 @@ hist_ctx(const CodeT* __restrict__ codes, long long n, int m_total, int k,
     // that holds part m, kSub rows' dwords issued before their counter updates
     const bool dw = full && m_total != 8 && (m_total & 3) == 0 &&
                     (reinterpret_cast<uintptr_t>(codes) & 3) == 0;
-    __syncthreads();   // the counters are zeroed (one barrier on every path: `wide` varies)
+    lds_barrier();   // the counters are zeroed (one barrier on every path: `wide` varies)
     if (dw) {
         const int rw = m_total >> 2;   // dwords per row
         const uint32_t* rows = reinterpret_cast<const uint32_t*>(codes) + v0 * rw + (m >> 2);
@@ -165,7 +164,7 @@ hist_ctx(const CodeT* __restrict__ codes, long long n, int m_total, int k,
         }
     }
     }   // chunk
-    __syncthreads();
+    lds_barrier();
     uint32_t* out = partial + ((long long)m * groups + grp) * all_words + (long long)zs * words;
     if ((words & 3) == 0) {
         const uint4* src = reinterpret_cast<const uint4*>(pairs);
@@ -242,10 +241,7 @@ hist_ctx_w(const uint8_t* __restrict__ codes, long long n, int m_total, int k,
     unsigned carry = w0 > 0 ? (w0 - 1 < n ? (unsigned)(PM ? pm[w0 - 1] : codes[(w0 - 1) * m_total + m]) : ~0u)
                             : (prev_row ? (unsigned)prev_row[m] : ~0u);
     carry = (unsigned)__builtin_amdgcn_readfirstlane((int)carry);
-    if (first) {   // the counters are zeroed (explicit wait: see hist_flush_carry)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __syncthreads();
-    }
+    if (first) lds_barrier();   // the counters are zeroed
     first = false;
     if (PM && cnt == kR && !(reinterpret_cast<uintptr_t>(pm + w0) & 3)) {
         // part-major: lane l holds rows 4l .. 4l + 3 of a 256-row tile (one 4-byte load)
@@ -311,7 +307,7 @@ hist_ctx_w(const uint8_t* __restrict__ codes, long long n, int m_total, int k,
         }
     }
     }   // chunk
-    __syncthreads();
+    lds_barrier();
     uint32_t* out = partial + ((long long)m * groups + grp) * all_words + (long long)zs * words;
     if ((words & 3) == 0) {
         const uint4* src = reinterpret_cast<const uint4*>(pairs);
@@ -366,14 +362,14 @@ hist_plain(const CodeT* __restrict__ codes, long long n, int m_total, int k,
     extern __shared__ uint32_t bins[];
     const int m = blockIdx.y;
     for (int i = threadIdx.x; i < k; i += blockDim.x) bins[i] = 0;
-    __syncthreads();
+    lds_barrier();
     const long long per = (n + gridDim.x - 1) / gridDim.x;
     const long long v0 = (long long)blockIdx.x * per, v1 = min(n, v0 + per);
     for (long long v = v0 + threadIdx.x; v < v1; v += blockDim.x) {
         const unsigned c = ld_code(codes, ldc ? (long long)m * ldc + v : v * m_total + m);
         if (c < (unsigned)k) atomicAdd(&bins[c], 1u);
     }
-    __syncthreads();
+    lds_barrier();
     for (int i = threadIdx.x; i < k; i += blockDim.x)
         if (bins[i]) atomicAdd(&counts[(long long)m * k + i], bins[i]);
 }
@@ -445,7 +441,7 @@ enc_size(const CodeT* __restrict__ codes, long long n, int m_total, int k, int c
                                          enc, items, tree_prev) >> 56);
     for (int off = 32; off >= 1; off >>= 1) bits += __shfl_xor(bits, off);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = bits;
-    __syncthreads();
+    lds_barrier();
     if (threadIdx.x == 0) {
         uint32_t s = 0;
         for (int w = 0; w < kEncBlock / 64; ++w) s += red[w];
@@ -460,7 +456,7 @@ scan_blocks(const uint32_t* __restrict__ block_bits, long long nb,
     __shared__ unsigned long long wsum[16];
     __shared__ unsigned long long carry;
     if (threadIdx.x == 0) carry = 0;
-    __syncthreads();
+    lds_barrier();
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     for (long long base = 0; base < nb; base += blockDim.x) {
         const long long i = base + threadIdx.x;
@@ -471,13 +467,13 @@ scan_blocks(const uint32_t* __restrict__ block_bits, long long nb,
             if (lane >= off) incl += y;
         }
         if (lane == 63) wsum[wid] = incl;
-        __syncthreads();
+        lds_barrier();
         unsigned long long before = carry;
         for (int w = 0; w < wid; ++w) before += wsum[w];
         if (i < nb) block_off[i] = before + incl - x;
-        __syncthreads();
+        lds_barrier();
         if (threadIdx.x == blockDim.x - 1) carry = before + incl;
-        __syncthreads();
+        lds_barrier();
     }
     if (threadIdx.x == 0) *total = carry;
 }
@@ -634,7 +630,7 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
     // round trip); the shard's own buffer starts at its word, so only offset % 32 matters
     const unsigned long long bit_offset = d_bit_offset ? (*d_bit_offset & 31ull) : bit_offset_arg;
     if (tid == 0) s_id = (long long)(atomicAdd(ticket, 1ull) - ticket_base);
-    __syncthreads();
+    lds_barrier();
     const long long id = s_id;
     const long long v = id * BLK + tid;
     const bool stamp = id == nb / 2 && tid == 0;
@@ -697,7 +693,7 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
     }
     const uint32_t incl = wave_incl_scan(bits);
     if (lane == 63) wsum[wid] = incl;
-    __syncthreads();
+    lds_barrier();
     if (stamp) g_enc_stamps[1] = __builtin_amdgcn_s_memtime();
     uint32_t before = 0, block_bits = 0;
     for (int w = 0; w < BLK / 64; ++w) {
@@ -742,7 +738,7 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
         }
         if (lane == 0) s_excl = excl;
     }
-    __syncthreads();
+    lds_barrier();
     if (stamp) g_enc_stamps[2] = __builtin_amdgcn_s_memtime();
     const unsigned long long bs = bit_offset + s_excl, be = bs + block_bits;
     const long long wa = (long long)(bs >> 5);
@@ -752,7 +748,7 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
     const bool head_mem = (bs & 31) && bs == bit_offset;    // the caller's bits in word wa
     const bool overflow = nwords > 0 && wz >= cap_words;
     for (long long w = tid; w < nwords; w += BLK) img[w] = 0;
-    __syncthreads();
+    lds_barrier();
 
     unsigned long long pos = bs + before + incl - bits;
     if (v < n) {
@@ -825,7 +821,7 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
         if (nacc > 0) atomicOr(&img[w], (uint32_t)(acc << (32 - nacc)));
         pos += bits;
     }
-    __syncthreads();
+    lds_barrier();
     if (stamp) g_enc_stamps[3] = __builtin_amdgcn_s_memtime();
     // tail / head exchange with the neighbours (one lane)
     if (tid == 0) {
@@ -852,7 +848,7 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
         if (id == nb - 1) *total_out = be - bit_offset;
         if (overflow) atomicOr(err, 2ull);
     }
-    __syncthreads();
+    lds_barrier();
     if (stamp) g_enc_stamps[4] = __builtin_amdgcn_s_memtime();
     const bool last = id == nb - 1;
     if (!overflow) {
@@ -1276,6 +1272,25 @@ int pqh_histogram_set_dev(pqh_ctx_t* ctx, const void* d_codes, long long n, int 
     return histogram_impl(ctx, d_codes, n, m, k, 1, d_prev_row, d_counts, 1, d_rawf);
 }
 
+int pqh_histogram_set_dev_ld(pqh_ctx_t* ctx, const void* d_codes, long long ldc, long long n,
+                             int m, int k, const void* d_prev_row, const int* d_rawf,
+                             uint32_t* d_counts) {
+    return histogram_impl(ctx, d_codes, n, m, k, 1, d_prev_row, d_counts, 1, d_rawf, 0, nullptr,
+                          ldc);
+}
+
+int pqh_encode_write_at_dev_ld(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes,
+                               long long ldc, long long n, const void* d_prev_row,
+                               const int* d_rawf, const unsigned long long* d_global_bit_offset,
+                               unsigned char* d_out, unsigned long long out_bytes,
+                               int chunk_vectors, unsigned long long* d_chunk_offsets,
+                               void* d_chunk_prev) {
+    if (!d_global_bit_offset) return PQH_ERR_ARG;
+    return encode_write_impl(ctx, t, d_codes, n, 0, d_prev_row, 0, d_global_bit_offset, d_out,
+                             out_bytes, chunk_vectors, d_chunk_offsets, d_chunk_prev, nullptr,
+                             nullptr, d_rawf, ldc);
+}
+
 int pqh_encode_size_dev(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes, long long n,
                         const void* d_prev_row, const int* d_rawf,
                         unsigned long long* d_total_bits) {
@@ -1401,7 +1416,7 @@ hist_tree(const CodeT* __restrict__ rows, const uint16_t* __restrict__ tree_prev
     const int m = blockIdx.y;
     const int words = (k * k + 1) / 2;
     for (int w = threadIdx.x; w < words; w += blockDim.x) pairs[w] = 0;
-    __syncthreads();
+    lds_barrier();
     const long long p0 = (long long)blockIdx.x * kTreeChunk;
     const long long p1 = p0 + kTreeChunk < n ? p0 + kTreeChunk : n;
     for (long long p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
@@ -1411,7 +1426,7 @@ hist_tree(const CodeT* __restrict__ rows, const uint16_t* __restrict__ tree_prev
         const unsigned bin = prev * (unsigned)k + cur;
         atomicAdd(&pairs[bin >> 1], 1u << ((bin & 1u) * 16));
     }
-    __syncthreads();
+    lds_barrier();
     uint32_t* out = counts + (long long)m * k * k;
     for (int w = threadIdx.x; w < words; w += blockDim.x) {
         const uint32_t c = pairs[w];

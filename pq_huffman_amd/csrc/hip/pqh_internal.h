@@ -75,6 +75,16 @@ int pqh_pq_error_accum(pqh_ctx* ctx, const pqh_pq_t* pq, const float* d_x, long 
 extern "C" {
 int pqh_histogram_set_dev(pqh_ctx_t* ctx, const void* d_codes, long long n, int m, int k,
                           const void* d_prev_row, const int* d_rawf, uint32_t* d_counts);
+// the same with codes row-major (ldc = 0) or part-major (part i at d_codes + i * ldc)
+int pqh_histogram_set_dev_ld(pqh_ctx_t* ctx, const void* d_codes, long long ldc, long long n,
+                             int m, int k, const void* d_prev_row, const int* d_rawf,
+                             uint32_t* d_counts);
+int pqh_encode_write_at_dev_ld(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes,
+                               long long ldc, long long n, const void* d_prev_row,
+                               const int* d_rawf, const unsigned long long* d_global_bit_offset,
+                               unsigned char* d_out, unsigned long long out_bytes,
+                               int chunk_vectors, unsigned long long* d_chunk_offsets,
+                               void* d_chunk_prev);
 int pqh_encode_size_dev(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes, long long n,
                         const void* d_prev_row, const int* d_rawf,
                         unsigned long long* d_total_bits);
@@ -104,6 +114,15 @@ __device__ __forceinline__ void pqh_set_prio(int p) {
         case 3: __builtin_amdgcn_s_setprio(3); break;
         default: break;
     }
+}
+
+// A workgroup barrier that orders this wave's LDS accesses (atomics, stores, reads) before
+// every other wave's accesses after it.  The explicit lgkmcnt(0) matters: the compiler has
+// been seen to emit a bare s_barrier after LDS atomics whose results are unused (a histogram
+// lost counts that way), so every barrier that hands LDS data between waves uses this.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
 }
 
 // PQH_DEBUG_SYNC=1: synchronise and check after every launch, so an asynchronous fault is

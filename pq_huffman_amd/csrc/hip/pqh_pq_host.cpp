@@ -39,7 +39,8 @@ long long chunk_rows_for(int d, long long requested, long long n) {
 }
 
 // Two pinned host buffers and two device buffers of `chunk` rows (+ codes), events to
-// order them.  alloc() halves the chunk on an allocation failure before giving up.
+// order them.  alloc() halves the chunk (in multiples of 256 rows) on an allocation failure
+// before giving up with PQH_ERR_NOMEM.
 struct Pump {
     hipStream_t copy = nullptr;
     float* hin[2] = {nullptr, nullptr};
@@ -75,7 +76,10 @@ struct Pump {
             for (hipEvent_t* e : {&h2d[b], &asg[b], &d2h[b]})
                 if (!*e && hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess)
                     return PQH_ERR_HIP;
-        for (chunk = rows; chunk >= 1; chunk = chunk > 256 ? ((chunk / 2 + 255) / 256) * 256 : chunk / 2) {
+        // (never below 256 rows, or below the whole input when it is shorter: the error
+        // pass's 256-row block partials must line up with the one-shot pass's -- pq.h)
+        const long long floor_rows = std::min<long long>(rows, 256);
+        for (chunk = rows; chunk >= floor_rows; chunk = ((chunk / 2 + 255) / 256) * 256) {
             const size_t xb = (size_t)chunk * d * sizeof(float), cb = (size_t)chunk * code_bytes;
             bool ok = true;
             for (int b = 0; b < 2 && ok; ++b) {
@@ -88,7 +92,7 @@ struct Pump {
             if (ok) return PQH_OK;
             release();
             (void)hipGetLastError();   // (clear the failed allocation's sticky error)
-            if (chunk == 1) break;
+            if (chunk <= floor_rows) break;
         }
         return PQH_ERR_NOMEM;
     }

@@ -75,6 +75,28 @@ shard_length(const uint32_t* __restrict__ local, const unsigned long long* __res
     if ((threadIdx.x & 63) == 0 && s) atomicAdd(out, s);
 }
 
+// this shard's last row into the halo record (byte kHaloData on), from row-major codes
+// (ldc = 0) or part-major ones (part i's codes at i * ldc)
+__global__ void shard_last_row(const unsigned char* __restrict__ codes, long long ldc, long long n,
+                               int m, unsigned char* __restrict__ rec) {
+    for (int i = threadIdx.x; i < m; i += blockDim.x)
+        rec[kHaloData + i] = ldc ? codes[(long long)i * ldc + n - 1] : codes[(n - 1) * m + i];
+}
+
+// the shard-boundary pair (halo row, first row) of every part, one count each, when this
+// shard does not hold global row 0 (*rawf == 0): what the histogram's prev_row adds, for
+// counts reduced from partials that were taken without the halo (pqh_histogram_partial_parts
+// on the assignment stream, before the halo exchange)
+__global__ void shard_halo_pair(uint32_t* __restrict__ counts, const unsigned char* __restrict__ halo,
+                                const int* __restrict__ rawf, const unsigned char* __restrict__ codes,
+                                long long ldc, int m, int k) {
+    if (*rawf) return;
+    for (int i = threadIdx.x; i < m; i += blockDim.x) {
+        const unsigned p = halo[i], c = ldc ? codes[(long long)i * ldc] : codes[i];
+        if (p < (unsigned)k && c < (unsigned)k) counts[(long long)i * k * k + p * (unsigned)k + c] += 1u;
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -194,13 +216,15 @@ bool shard_local_bad(const block_t* shard, const void* d_codes, const pqh_tables
 // local: the rank stays in the collective sequence (an empty halo record, a histogram
 // counting nothing), the error is returned and must be handed to phase 2 (status), which
 // then sends the sentinel length so every rank sees it (pqh_shard_status).
-int pqh_shard_encode_tables(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm, const block_t* shard,
-                            const void* d_codes, int m, int k, int context,
-                            pqh_tables_t* tables, uint32_t* d_counts, void* d_scratch) {
+static int shard_tables_impl(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm, const block_t* shard,
+                             const void* d_codes, long long ldc, int m, int k, int context,
+                             pqh_tables_t* tables, uint32_t* d_counts, void* d_scratch,
+                             const void* d_partials) {
     if (shard_fatal(ctx, comm, m, k, context, d_scratch) || !d_counts) return PQH_ERR_ARG;
     int rc = pqh_use_device(ctx);
     if (rc) return rc;
     int err = shard_local_bad(shard, d_codes, tables, m, k, context) ? PQH_ERR_ARG : PQH_OK;
+    if (!err && ldc && (ldc < shard->size || (d_partials && !context))) err = PQH_ERR_ARG;
     auto local = [&](int r) {   // the first local failure is kept
         if (r && !err) err = r;
     };
@@ -214,10 +238,9 @@ int pqh_shard_encode_tables(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm, const 
         local(hipMemsetAsync(sc.halo_send, 0, sc.recb, ctx->stream) == hipSuccess ? PQH_OK : PQH_ERR_HIP);
         if (n > 0 && !err) {
             local(hipMemsetAsync(sc.halo_send, 1, 1, ctx->stream) == hipSuccess ? PQH_OK : PQH_ERR_HIP);
-            local(hipMemcpyAsync(sc.halo_send + kHaloData,
-                                 static_cast<const unsigned char*>(d_codes) + (n - 1) * m, m,
-                                 hipMemcpyDeviceToDevice, ctx->stream) == hipSuccess
-                      ? PQH_OK : PQH_ERR_HIP);
+            hipLaunchKernelGGL(shard_last_row, dim3(1), dim3(64), 0, ctx->stream,
+                               static_cast<const unsigned char*>(d_codes), ldc, n, m, sc.halo_send);
+            local(hipGetLastError() == hipSuccess ? PQH_OK : PQH_ERR_HIP);
         }
         if (comm->all_gather(comm->user, sc.halo_send, sc.halo_recv, sc.recb, st))
             return pqh_set_error(ctx, PQH_ERR_COMM, "shard halo all-gather failed");
@@ -227,13 +250,25 @@ int pqh_shard_encode_tables(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm, const 
     }
     // the shard's histogram (+ the halo pair), summed over ranks -> identical tables
     const long long items = context ? (long long)k * k : k;
-    if (err)
+    if (err) {
         local(hipMemsetAsync(d_counts, 0, (size_t)m * items * 4, ctx->stream) == hipSuccess
                   ? PQH_OK : PQH_ERR_HIP);
-    else if (context)
-        local(pqh_histogram_set_dev(ctx, d_codes, n, m, k, sc.halo_row, sc.rawf, d_counts));
-    else
-        local(pqh_histogram_set(ctx, d_codes, n, m, k, 0, nullptr, d_counts));
+    } else if (d_partials) {
+        // the partial counts were taken on another stream, without the halo: reduce them,
+        // then add the boundary pair
+        local(pqh_histogram_reduce(ctx, d_partials, n, m, k, d_counts, 1));
+        if (n > 0 && !err) {
+            hipLaunchKernelGGL(shard_halo_pair, dim3(1), dim3(64), 0, ctx->stream, d_counts,
+                               sc.halo_row, sc.rawf, static_cast<const unsigned char*>(d_codes),
+                               ldc, m, k);
+            local(hipGetLastError() == hipSuccess ? PQH_OK : PQH_ERR_HIP);
+        }
+    } else if (context) {
+        local(pqh_histogram_set_dev_ld(ctx, d_codes, ldc, n, m, k, sc.halo_row, sc.rawf, d_counts));
+    } else {
+        local(ldc ? pqh_histogram_parts(ctx, d_codes, ldc, n, m, k, 0, nullptr, d_counts, 1)
+                  : pqh_histogram_set(ctx, d_codes, n, m, k, 0, nullptr, d_counts));
+    }
     // (the local counts give phase 2 the shard's length without a pass over its codes)
     if (!err)
         local(hipMemcpyAsync(sc.local, d_counts, (size_t)m * items * 4, hipMemcpyDeviceToDevice,
@@ -244,20 +279,40 @@ int pqh_shard_encode_tables(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm, const 
     return err;
 }
 
+int pqh_shard_encode_tables(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm, const block_t* shard,
+                            const void* d_codes, int m, int k, int context,
+                            pqh_tables_t* tables, uint32_t* d_counts, void* d_scratch) {
+    return shard_tables_impl(ctx, comm, shard, d_codes, 0, m, k, context, tables, d_counts,
+                             d_scratch, nullptr);
+}
+
+int pqh_shard_encode_tables_parts(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm,
+                                  const block_t* shard, const void* d_codes, long long ld_codes,
+                                  int m, int k, int context, pqh_tables_t* tables,
+                                  uint32_t* d_counts, void* d_scratch, const void* d_partials) {
+    if (ld_codes <= 0) return PQH_ERR_ARG;
+    return shard_tables_impl(ctx, comm, shard, d_codes, ld_codes, m, k, context, tables, d_counts,
+                             d_scratch, d_partials);
+}
+
 // Phase 2: the shard's exact length, everyone's (all-gather; the sentinel ~0 when status,
 // the rank's phase-1 result, or this phase fails locally), the exclusive scan on the device,
 // and the write.
-int pqh_shard_encode_write(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm, const block_t* shard,
-                           const void* d_codes, int m, int k, int context, pqh_tables_t* tables,
-                           unsigned char* d_out, unsigned long long out_bytes, int chunk_vectors,
-                           unsigned long long* d_chunk_offsets, void* d_chunk_prev,
-                           unsigned long long* d_offsets, void* d_scratch, int status,
-                           int* raw_first_out) {
+static int shard_write_impl(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm, const block_t* shard,
+                            const void* d_codes, long long ldc, int m, int k, int context,
+                            pqh_tables_t* tables, unsigned char* d_out, unsigned long long out_bytes,
+                            int chunk_vectors, unsigned long long* d_chunk_offsets,
+                            void* d_chunk_prev, unsigned long long* d_offsets, void* d_scratch,
+                            int status, int* raw_first_out) {
     if (shard_fatal(ctx, comm, m, k, context, d_scratch) || !d_offsets) return PQH_ERR_ARG;
     int rc = pqh_use_device(ctx);
     if (rc) return rc;
     int err = status;
     if (!err && (shard_local_bad(shard, d_codes, tables, m, k, context) || !d_out || out_bytes < 4))
+        err = PQH_ERR_ARG;
+    // (part-major codes: the 8-byte-row encoder's shapes, m = 8 or 16 u8 codes)
+    if (!err && ldc && (ldc < shard->size || (m != 8 && m != 16) ||
+                        (reinterpret_cast<uintptr_t>(d_chunk_prev) & 7)))
         err = PQH_ERR_ARG;
     const long long n = err ? 0 : shard->size;
     const int world = comm->world, rank = comm->rank;
@@ -285,12 +340,12 @@ int pqh_shard_encode_write(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm, const b
     // word 0 of d_out = the global word offset / 32; the bits before the shard's offset in
     // that word belong to the previous shard and stay zero here
     PQH_HIP(ctx, hipMemsetAsync(d_out, 0, 4, ctx->stream));
-    rc = context ? pqh_encode_write_at_dev(ctx, tables, d_codes, n, sc.halo_row, sc.rawf, d_offsets,
-                                           d_out, out_bytes, chunk_vectors, d_chunk_offsets,
-                                           d_chunk_prev)
-                 : pqh_encode_write_at(ctx, tables, d_codes, n, 0, nullptr, d_offsets, d_out,
-                                       out_bytes, chunk_vectors, d_chunk_offsets, d_chunk_prev,
-                                       nullptr);
+    rc = context ? pqh_encode_write_at_dev_ld(ctx, tables, d_codes, ldc, n, sc.halo_row, sc.rawf,
+                                              d_offsets, d_out, out_bytes, chunk_vectors,
+                                              d_chunk_offsets, d_chunk_prev)
+                 : pqh_encode_write_at_dev_ld(ctx, tables, d_codes, ldc, n, nullptr, nullptr,
+                                              d_offsets, d_out, out_bytes, chunk_vectors,
+                                              d_chunk_offsets, d_chunk_prev);
     if (rc) return rc;
     if (raw_first_out) {   // (optional: the one host read, at the end)
         int rf = rank == 0 ? 1 : 0;
@@ -301,6 +356,30 @@ int pqh_shard_encode_write(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm, const b
         *raw_first_out = rf;
     }
     return PQH_OK;
+}
+
+int pqh_shard_encode_write(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm, const block_t* shard,
+                           const void* d_codes, int m, int k, int context, pqh_tables_t* tables,
+                           unsigned char* d_out, unsigned long long out_bytes, int chunk_vectors,
+                           unsigned long long* d_chunk_offsets, void* d_chunk_prev,
+                           unsigned long long* d_offsets, void* d_scratch, int status,
+                           int* raw_first_out) {
+    return shard_write_impl(ctx, comm, shard, d_codes, 0, m, k, context, tables, d_out, out_bytes,
+                            chunk_vectors, d_chunk_offsets, d_chunk_prev, d_offsets, d_scratch,
+                            status, raw_first_out);
+}
+
+int pqh_shard_encode_write_parts(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm,
+                                 const block_t* shard, const void* d_codes, long long ld_codes,
+                                 int m, int k, int context, pqh_tables_t* tables,
+                                 unsigned char* d_out, unsigned long long out_bytes,
+                                 int chunk_vectors, unsigned long long* d_chunk_offsets,
+                                 void* d_chunk_prev, unsigned long long* d_offsets, void* d_scratch,
+                                 int status, int* raw_first_out) {
+    if (ld_codes <= 0) return PQH_ERR_ARG;
+    return shard_write_impl(ctx, comm, shard, d_codes, ld_codes, m, k, context, tables, d_out,
+                            out_bytes, chunk_vectors, d_chunk_offsets, d_chunk_prev, d_offsets,
+                            d_scratch, status, raw_first_out);
 }
 
 int pqh_shard_encode(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm, const block_t* shard,

@@ -2073,6 +2073,18 @@ dec_rows(const uint32_t* __restrict__ words, long long nwords, long long n, int 
     if (!ok) atomicOr(err, 1ull);
 }
 
+// diagnostics only (pqh_debug_poison_lds): fills a whole CU's LDS (160 KB) with `value`, so a
+// kernel launched after it on any CU finds that pattern, not zeros or an earlier kernel's
+// data, in whatever LDS it reads before writing -- a test for stale-LDS reads
+__global__ void __launch_bounds__(1024)
+lds_poison(uint32_t value, int words, uint32_t* __restrict__ sink) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    volatile uint32_t* w = reinterpret_cast<volatile uint32_t*>(lds);
+    for (int i = threadIdx.x; i < words; i += blockDim.x) w[i] = value;
+    lds_barrier();
+    if (threadIdx.x == 0 && w[(blockIdx.x * 977u) % (unsigned)words] != value) sink[0] = 1u;
+}
+
 }  // namespace
 
 extern "C" {
@@ -2287,6 +2299,23 @@ int pqh_debug_tree_stamps(pqh_ctx_t* ctx, unsigned long long* out16) {
     if (!ctx || !out16) return PQH_ERR_ARG;
     PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
     PQH_HIP(ctx, hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_tree_stamps), 16 * sizeof(unsigned long long)));
+    return PQH_OK;
+}
+
+// diagnostics only: every CU's LDS filled with `value` (lds_poison), on ctx's stream; a
+// test runs it right before a kernel under test.  4 workgroups per CU, each holding all of
+// the CU's LDS, so every CU runs at least one.
+int pqh_debug_poison_lds(pqh_ctx_t* ctx, unsigned value) {
+    if (!ctx) return PQH_ERR_ARG;
+    int rc = pqh_use_device(ctx);
+    if (rc) return rc;
+    const int bytes = 160 * 1024;
+    PQH_HIP(ctx, hipFuncSetAttribute((const void*)lds_poison,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+    hipLaunchKernelGGL(lds_poison, dim3((unsigned)(4 * ctx->num_cus)), dim3(1024), bytes,
+                       ctx->stream, (uint32_t)value, bytes / 4,
+                       reinterpret_cast<uint32_t*>(ctx->d_diag + 5));
+    PQH_LAUNCH_CHECK(ctx);
     return PQH_OK;
 }
 

@@ -442,19 +442,29 @@ def _block(first_row, n):
     return b
 
 
-def shard_encode_tables(ctx, comm: TorchComm, codes, tables, counts, scratch, first_row=0) -> int:
+def shard_encode_tables(ctx, comm: TorchComm, codes, tables, counts, scratch, first_row=0,
+                        parts_n=None, partials=None) -> int:
     """Phase 1 on ctx's stream: halo, histogram, all-reduce, code tables.  Returns the
-    rank's status (0 or a negative pqh status), to be handed to shard_encode_write."""
-    n, m = codes.shape
+    rank's status (0 or a negative pqh status), to be handed to shard_encode_write.
+    parts_n: codes are PART-MAJOR (m, >= parts_n) (pqh_shard_encode_tables_parts);
+    partials: their partial pair counts, already taken (pqh_histogram_partial_parts)."""
     ptr = (lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None)
     comm.error = None
     comm.register(counts, scratch)
     try:
-        rc = _lib().pqh_shard_encode_tables(ctx.ptr, ctypes.byref(comm.struct),
-                                            ctypes.byref(_block(first_row, n)),
-                                            ptr(codes) if n else None, m, tables.k,
-                                            int(tables.context), tables.ptr, ptr(counts),
-                                            ptr(scratch))
+        if parts_n is not None:
+            m, n = codes.shape[0], parts_n
+            rc = _lib().pqh_shard_encode_tables_parts(
+                ctx.ptr, ctypes.byref(comm.struct), ctypes.byref(_block(first_row, n)),
+                ptr(codes) if n else None, codes.stride(0), m, tables.k, int(tables.context),
+                tables.ptr, ptr(counts), ptr(scratch), ptr(partials))
+        else:
+            n, m = codes.shape
+            rc = _lib().pqh_shard_encode_tables(ctx.ptr, ctypes.byref(comm.struct),
+                                                ctypes.byref(_block(first_row, n)),
+                                                ptr(codes) if n else None, m, tables.k,
+                                                int(tables.context), tables.ptr, ptr(counts),
+                                                ptr(scratch))
     finally:
         comm.clear()
     if comm.error is not None:
@@ -463,22 +473,31 @@ def shard_encode_tables(ctx, comm: TorchComm, codes, tables, counts, scratch, fi
 
 
 def shard_encode_write(ctx, comm: TorchComm, codes, tables, out, chunk_vectors, chunk_offsets,
-                       chunk_prev, offsets, scratch, status=0, first_row=0):
+                       chunk_prev, offsets, scratch, status=0, first_row=0, parts_n=None):
     """Phase 2 on ctx's stream: length, all-gather, device offsets (into `offsets`, a (2,)
     int64 tensor), the write.  Raises on this rank's failure; another rank's shows in
-    offsets[1] == -1 (status())."""
+    offsets[1] == -1 (status()).  parts_n: part-major codes (pqh_shard_encode_write_parts)."""
     from .capi import check
-    n, m = codes.shape
     ptr = (lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None)
     comm.error = None
     comm.register(scratch)
     try:
-        rc = _lib().pqh_shard_encode_write(ctx.ptr, ctypes.byref(comm.struct),
-                                           ctypes.byref(_block(first_row, n)),
-                                           ptr(codes) if n else None, m, tables.k,
-                                           int(tables.context), tables.ptr, ptr(out), out.numel(),
-                                           chunk_vectors, ptr(chunk_offsets), ptr(chunk_prev),
-                                           ptr(offsets), ptr(scratch), int(status), None)
+        if parts_n is not None:
+            m, n = codes.shape[0], parts_n
+            rc = _lib().pqh_shard_encode_write_parts(
+                ctx.ptr, ctypes.byref(comm.struct), ctypes.byref(_block(first_row, n)),
+                ptr(codes) if n else None, codes.stride(0), m, tables.k, int(tables.context),
+                tables.ptr, ptr(out), out.numel(), chunk_vectors, ptr(chunk_offsets),
+                ptr(chunk_prev), ptr(offsets), ptr(scratch), int(status), None)
+        else:
+            n, m = codes.shape
+            rc = _lib().pqh_shard_encode_write(ctx.ptr, ctypes.byref(comm.struct),
+                                               ctypes.byref(_block(first_row, n)),
+                                               ptr(codes) if n else None, m, tables.k,
+                                               int(tables.context), tables.ptr, ptr(out),
+                                               out.numel(), chunk_vectors, ptr(chunk_offsets),
+                                               ptr(chunk_prev), ptr(offsets), ptr(scratch),
+                                               int(status), None)
     finally:
         comm.clear()
     if comm.error is not None:

@@ -4,13 +4,15 @@ rank on cuda:0 (a fresh process per rank).  Writes rank 0's result to --out (.np
 the stitched stream (pqh_shard_stitch of every rank's buffer), the global histogram, and
 the rows the ranks encoded, for the test to compare with the oracle's one-shot results.
 
-  --case even|ragged|sort|fail   --mode ctx|noctx
+  --case even|ragged|sort|fail|parts|parts_ragged   --mode ctx|noctx
 even: contiguous shards; ragged: rank 1 holds no rows; fail: rank 1's call fails locally
 (an output buffer too small) -- both ranks must return, rank 1 with its error and rank 0
 through pqh_shard_status; sort: the distributed sample sort
 (shard.sort_rows_distributed with the library's stable radix sort) then the sorted slices,
 whose halo also goes through shard.halo_ragged into codec.histogram / encode_size (the
-library's halo must agree)."""
+library's halo must agree); parts / parts_ragged: the two-phase calls on part-major codes
+(pqh_shard_encode_tables_parts with the partial pair counts, pqh_shard_encode_write_parts),
+and each shard decoded through its own chunk index."""
 import argparse
 import os
 import sys
@@ -43,7 +45,7 @@ def main():
     if a.case == "sort":
         allc[np.random.default_rng(3).random(allc.shape) < 0.2] = 0   # strncmp-key ties
     ctx = codec.Context(0)
-    if a.case == "ragged":
+    if a.case in ("ragged", "parts_ragged"):
         b, e = (0, a.n) if rank == 0 else (a.n, a.n)
     else:
         b, e = shard.row_range(a.n, world, rank)
@@ -77,7 +79,40 @@ def main():
         ctx.close()
         dist.destroy_process_group()
         return
-    offsets, raw = shard.shard_encode(ctx, comm, mine, tabs, counts, out, first_row=b, check=True)
+    if a.case.startswith("parts"):
+        # the two phases on PART-MAJOR codes (bench.py's multi-rank pipeline): context mode
+        # hands phase 1 the partial pair counts taken without the halo (as the assignment
+        # stream does), non-context lets phase 1 run the part-major histogram itself
+        ld = (n + 127) // 128 * 128 + 64
+        pm = torch.full((m, max(ld, 1)), 0xA5, dtype=torch.uint8, device="cuda")
+        pm[:, :n] = mine.t()
+        pm = pm[:, :n]
+        hp = None
+        if ctxm:
+            hp = torch.empty(max(codec.histogram_partial_bytes(n, m, k), 4), dtype=torch.uint8,
+                             device="cuda")
+            if n:
+                codec.histogram_partial_parts(ctx, pm, n, k, hp)
+        scratch = shard.scratch_for(comm, m, torch.device("cuda", 0))
+        st = shard.shard_encode_tables(ctx, comm, pm, tabs, counts, scratch, first_row=b,
+                                       parts_n=n, partials=hp)
+        assert st == 0, st
+        chunks = (n + 7) // 8
+        coff = torch.empty(max(chunks, 1), dtype=torch.int64, device="cuda")
+        cprev = torch.empty((max(chunks, 1), m), dtype=torch.uint8, device="cuda") if ctxm else None
+        offsets = torch.zeros(2, dtype=torch.int64, device="cuda")
+        shard.shard_encode_write(ctx, comm, pm, tabs, out, 8, coff, cprev, offsets, scratch,
+                                 status=st, first_row=b, parts_n=n)
+        shard.status(ctx, offsets)
+        raw = 1 if b == 0 else 0
+        if n:   # the shard's own decode through its chunk index (halo row as chunk 0's context)
+            enc = codec.Encoded(out, -1, 8, coff, cprev, n, raw)
+            dec = codec.decode(ctx, tabs, enc)
+            codec.decode_status(ctx)
+            assert torch.equal(dec, mine), "part-major shard does not decode to its rows"
+    else:
+        offsets, raw = shard.shard_encode(ctx, comm, mine, tabs, counts, out, first_row=b,
+                                          check=True)
     torch.cuda.synchronize()
     goff, total = (int(v) for v in offsets.cpu().tolist())
     # every rank's length, for the stitch on rank 0

@@ -60,6 +60,57 @@ def _bench_path(gpu, x, cent, chunk=8, ctxm=True, sort=False):
     return pq, codes, counts, tabs, enc, dec
 
 
+def _bench_path_parts(gpu, x, cent, chunk=8):
+    """bench.py's DEFAULT per-batch calls at one rank (--code-layout parts, --hist-split on),
+    issued exactly as front()/back() issue them: pqh_pq_assign_parts into a 128-padded
+    [m][ld] buffer -> pqh_histogram_partial_parts + pqh_histogram_reduce -> code trees + decode
+    tables -> pqh_encode_write_parts (the part-major row encoder) -> pqh_decode.  Returns the
+    codes as rows (pqh_transpose_codes: the pq_indices.bvecsl layout) and the part buffer."""
+    torch, codec, ctx = gpu
+    n = x.shape[0]
+    m, k, _ = cent.shape
+    pq = codec.PQ(ctx, cent)
+    ldp = (n + 127) // 128 * 128
+    parts = torch.empty((m, ldp), dtype=torch.uint8, device=x.device)[:, :n]
+    pq.assign_parts(x, parts)
+    hp = torch.empty(codec.histogram_partial_bytes(n, m, k), dtype=torch.uint8, device=x.device)
+    codec.histogram_partial_parts(ctx, parts, n, k, hp)
+    counts = torch.empty((m, k * k), dtype=torch.int32, device=x.device)
+    codec.histogram_reduce(ctx, hp, n, m, k, counts)
+    tabs = codec.Tables(ctx, m, k, True)
+    tabs.build_trees(counts)
+    tabs.build_luts()
+    chunks = (n + chunk - 1) // chunk
+    out = torch.empty(n * m * 56 // 8 + 64, dtype=torch.uint8, device=x.device)
+    coff = torch.empty(chunks, dtype=torch.int64, device=x.device)
+    cprev = torch.empty((chunks, m), dtype=torch.uint8, device=x.device)
+    tot = torch.zeros(1, dtype=torch.int64, device=x.device)
+    codec.encode_write_parts(ctx, tabs, parts, n, out, 0, 1, None, chunk, coff, cprev, total=tot)
+    codec.encode_status(ctx)
+    enc = codec.Encoded(out, int(tot.item()), chunk, coff, cprev, n, 1)
+    dec = codec.decode(ctx, tabs, enc)
+    codec.decode_status(ctx)
+    tabs.status()
+    rows = codec.transpose_codes(ctx, parts, n)
+    return pq, rows, parts, counts, tabs, enc, dec
+
+
+def _check_chunk_index(torch, oracle, rows_h, ocb, enc, chunk):
+    """every chunk offset is the oracle's bit position of its first row (the cumulative
+    code lengths of the rows before it; row 0 raw), every chunk context row its predecessor"""
+    n, m = rows_h.shape
+    r = rows_h.astype(np.int64)
+    lens = np.empty(n, np.int64)
+    lens[0] = 8 * m                                    # row 0 raw (huffman_encoder.c:234)
+    idx = r[:-1] * ocb.k + r[1:]                       # (prev << 8) + cur per part
+    lens[1:] = ocb.lens[np.arange(m)[None, :], idx].sum(axis=1)
+    starts = np.concatenate([[0], np.cumsum(lens)])
+    want = starts[0:len(rows_h):chunk]
+    assert np.array_equal(enc.chunk_offsets.cpu().numpy(), want)
+    cp = enc.chunk_prev.cpu().numpy()
+    assert np.array_equal(cp[1:], rows_h[chunk - 1:len(rows_h) - 1:chunk][:len(cp) - 1])
+
+
 def _check_against_oracle(gpu, oracle, xh, cent, codes, tabs, enc, dec, ctxm=True, sort=False):
     torch, codec, ctx = gpu
     assert torch.equal(dec, codes)
@@ -89,6 +140,55 @@ def test_bench_path_sift1m_all_rows(gpu, oracle):
     pq, codes, counts, tabs, enc, dec = _bench_path(gpu, x, cent)
     assert pq.rerank_count() > 0
     _check_against_oracle(gpu, oracle, x.cpu().numpy(), cent, codes, tabs, enc, dec)
+
+
+def _check_parts_against_oracle(gpu, oracle, xh, cent, rows, counts, tabs, enc, dec, chunk):
+    """the part-major pipeline's every output against the oracle: codes, pair counts,
+    codebook file, stream bytes and bit count, chunk index, decode"""
+    torch, codec, ctx = gpu
+    k = cent.shape[1]
+    want, _ = oracle.pq_assign(xh, cent, threads=0)
+    got = rows.cpu().numpy()
+    bad = int((got != want).sum())
+    assert bad == 0, f"{bad} part-major PQ codes differ from the oracle"
+    assert np.array_equal(codec.counts_to_host(counts), oracle.histogram(want, k, True))
+    ocb = oracle.build_codebooks(want, k, True)
+    assert tabs.codebooks().file_bytes() == oracle.codebooks_file(ocb)
+    stream, bits = oracle.encode(want, ocb)
+    assert enc.bits == bits
+    assert enc.stream[:len(stream)].cpu().numpy().tobytes() == stream
+    _check_chunk_index(torch, oracle, want, ocb, enc, chunk)
+    assert torch.equal(dec, rows)
+
+
+def test_bench_parts_path_sift1m_all_rows(gpu, oracle):
+    """the pipeline bench.py TIMES at one rank (part-major codes, split histogram), on the
+    bench's own data and centroids, against the oracle on all 1,000,000 rows
+    (src/pq_encoder.c:192-213, src/huffman_encoder.c:166-238,398-428)."""
+    import bench
+    torch, codec, ctx = gpu
+    dev = torch.device("cuda", 0)
+    x = bench.make_data(torch, 1_000_000, 128, 0x5EED, 0, dev)
+    cent = bench.train_centroids(torch, bench.make_data(torch, 200_000, 128, 0x5EED, 0, dev),
+                                 8, 256)
+    pq, rows, parts, counts, tabs, enc, dec = _bench_path_parts(gpu, x, cent)
+    assert pq.rerank_count() > 0
+    _check_parts_against_oracle(gpu, oracle, x.cpu().numpy(), cent, rows, counts, tabs, enc,
+                                dec, 8)
+
+
+def test_bench_parts_path_deep1m_all_rows(gpu, oracle):
+    """`bench.py --config deep` as timed: 16 part-major runs, each vector encoded as two
+    8-part rows gathered from them (the lo pass active: unit-norm floats)."""
+    import bench
+    torch, codec, ctx = gpu
+    dev = torch.device("cuda", 0)
+    x = bench.make_deep(torch, 1_000_000, 96, 0x5EED, 0, dev)
+    cent = bench.train_centroids(torch, bench.make_deep(torch, 200_000, 96, 0x5EED, 0, dev),
+                                 16, 256)
+    pq, rows, parts, counts, tabs, enc, dec = _bench_path_parts(gpu, x, cent)
+    _check_parts_against_oracle(gpu, oracle, x.cpu().numpy(), cent, rows, counts, tabs, enc,
+                                dec, 8)
 
 
 def test_bench_path_deep1m_all_rows(gpu, oracle):
@@ -179,3 +279,19 @@ def test_configs2_shard_125m_rows(gpu, oracle):
     gbytes = enc.stream[start // 8:(stop + 7) // 8 + 1].cpu().numpy()
     gbits = np.unpackbits(gbytes)[start % 8:start % 8 + (stop - start)]
     assert np.array_equal(gbits, np.unpackbits(np.frombuffer(ostream, np.uint8))[64:obits])
+
+    # The pipeline bench.py times on this shard (part-major codes, multi-round split
+    # histogram, part-major row encoder), on the same rows: every code, the pair counts, every
+    # stream byte and every chunk offset equal the row path's just checked above.
+    row_stream = enc.stream[:(enc.bits + 7) // 8]
+    row_coff = enc.chunk_offsets
+    del dec, pq
+    torch.cuda.empty_cache()
+    pq2, rows2, parts2, counts2, tabs2, enc2, dec2 = _bench_path_parts(gpu, x, cent, chunk=64)
+    assert torch.equal(rows2, codes)
+    assert torch.equal(counts2, counts)
+    assert tabs2.codebooks().file_bytes() == oracle.codebooks_file(ocb)
+    assert enc2.bits == enc.bits
+    assert torch.equal(enc2.stream[:(enc2.bits + 7) // 8], row_stream)
+    assert torch.equal(enc2.chunk_offsets, row_coff)
+    assert torch.equal(dec2, codes)

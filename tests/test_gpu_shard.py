@@ -23,7 +23,8 @@ def _free_port():
 
 
 @pytest.mark.parametrize("case,mode", [("even", "ctx"), ("even", "noctx"), ("ragged", "ctx"),
-                                       ("sort", "ctx")])
+                                       ("sort", "ctx"), ("parts", "ctx"), ("parts", "noctx"),
+                                       ("parts_ragged", "ctx")])
 def test_two_rank_library_shard_encode(oracle, tmp_path, case, mode):
     dump = tmp_path / "shard.npz"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
