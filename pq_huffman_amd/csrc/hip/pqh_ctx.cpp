@@ -63,6 +63,23 @@ int pqh_ensure_ws(pqh_ctx* ctx, size_t bytes) {
     return pqh_set_error(ctx, PQH_ERR_NOMEM, "workspace: cannot allocate %zu bytes", bytes);
 }
 
+int pqh_ensure_enc_scratch(pqh_ctx* ctx, size_t bytes) {
+    if (bytes <= ctx->enc_scr_bytes) return PQH_OK;
+    if (ctx->enc_scr) {
+        PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        ctx->enc_scr_bytes = 0;
+        PQH_HIP(ctx, hipFree(ctx->enc_scr));
+        ctx->enc_scr = nullptr;
+    }
+    if (hipMalloc(&ctx->enc_scr, bytes) != hipSuccess) {
+        ctx->enc_scr = nullptr;
+        (void)hipGetLastError();
+        return pqh_set_error(ctx, PQH_ERR_NOMEM, "encode scratch: cannot allocate %zu bytes", bytes);
+    }
+    ctx->enc_scr_bytes = bytes;
+    return PQH_OK;
+}
+
 extern "C" {
 
 int pqh_device_count(int* count) {
@@ -148,6 +165,7 @@ int pqh_ctx_destroy(pqh_ctx_t* ctx) {
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->d_diag) (void)hipFree(ctx->d_diag);
     if (ctx->lb_state) (void)hipFree(ctx->lb_state);
+    if (ctx->enc_scr) (void)hipFree(ctx->enc_scr);
     if (ctx->sort_state) (void)hipFree(ctx->sort_state);
     if (ctx->d_sched) (void)hipFree(ctx->d_sched);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);

@@ -589,7 +589,15 @@ __device__ __forceinline__ void gather_entries(const CodeT* __restrict__ codes, 
 // stamps of the mid-grid workgroup, read by pqh_debug_enc_stamps.)
 __device__ unsigned long long g_enc_stamps[8];
 
-template <typename CodeT, int MAXM, int BLK, bool ROW8 = false, int CS = 1, bool PM = false>
+//
+// TILE = true (the default encoder, see encode_write_impl): the same kernel without any
+// inter-workgroup waiting.  Workgroup `id` = blockIdx.x codes tile id of the input into its
+// LDS image starting at bit 0, stores the image's words whole into its slot of the scratch
+// (out_words + id * cap_words, cap_words = the slot's words, a tile's worst case), its bit
+// count into tile_bits[id] (`state` as u32) and its chunk offsets relative to the tile; a
+// scan of the tile counts and enc_place then put every tile at its offset.
+template <typename CodeT, int MAXM, int BLK, bool ROW8 = false, int CS = 1, bool PM = false,
+          bool TILE = false>
 __global__ void __launch_bounds__(BLK)
 enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, int context,
             int raw_first, const CodeT* __restrict__ prev_row, const int* __restrict__ d_rawf,
@@ -628,10 +636,13 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
     if (d_rawf) raw_first = *d_rawf;   // decided on the device (pqh_shard_encode)
     // d_bit_offset: the shard's GLOBAL bit offset, produced on the device (multi-GPU, no host
     // round trip); the shard's own buffer starts at its word, so only offset % 32 matters
-    const unsigned long long bit_offset = d_bit_offset ? (*d_bit_offset & 31ull) : bit_offset_arg;
-    if (tid == 0) s_id = (long long)(atomicAdd(ticket, 1ull) - ticket_base);
-    lds_barrier();
-    const long long id = s_id;
+    const unsigned long long bit_offset =
+        TILE ? 0ull : d_bit_offset ? (*d_bit_offset & 31ull) : bit_offset_arg;
+    if constexpr (!TILE) {
+        if (tid == 0) s_id = (long long)(atomicAdd(ticket, 1ull) - ticket_base);
+        lds_barrier();
+    }
+    const long long id = TILE ? (long long)blockIdx.x : s_id;
     const long long v = id * BLK + tid;
     const bool stamp = id == nb / 2 && tid == 0;
     if (stamp) g_enc_stamps[0] = __builtin_amdgcn_s_memtime();
@@ -702,7 +713,13 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
     }
     // decoupled look-back, one wave wide: lane l inspects predecessor p - l; the walk stops
     // at the nearest published inclusive prefix, adding the aggregates in front of it
-    if (wid == 0) {
+    // (TILE: none -- the tile starts at its own bit 0)
+    if (TILE) {
+        if (tid == 0) {
+            s_excl = 0;
+            reinterpret_cast<uint32_t*>(state)[id] = block_bits;
+        }
+    } else if (wid == 0) {
         unsigned long long excl = 0;
         if (id == 0) {
             if (lane == 0) lb_store(state, lb_pack(epoch, kLbPrefix, block_bits));
@@ -823,6 +840,11 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
     }
     lds_barrier();
     if (stamp) g_enc_stamps[3] = __builtin_amdgcn_s_memtime();
+    if constexpr (TILE) {   // the whole image into the tile's scratch slot
+        uint32_t* slot = out_words + id * cap_words;
+        for (long long w = tid; w < nwords; w += BLK) slot[w] = img[w];
+        return;
+    }
     // tail / head exchange with the neighbours (one lane)
     if (tid == 0) {
         const bool tail_open = (be & 31) != 0;   // last word not complete: successor's head
@@ -860,6 +882,90 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
             out_words[wa] = bswap32(s_head);
     }
     if (stamp) g_enc_stamps[5] = __builtin_amdgcn_s_memtime();
+}
+
+// `take` (1..32) bits of a tile's MSB-first image starting at bit r, right-aligned (the slot
+// has one readable word past its last: masked off)
+__device__ __forceinline__ uint32_t slot_bits(const uint32_t* __restrict__ src, unsigned long long r,
+                                              int take) {
+    const long long w = (long long)(r >> 5);
+    const int sh = (int)(r & 31);
+    const uint32_t x = sh ? (src[w] << sh) | (src[w + 1] >> (32 - sh)) : src[w];
+    return x >> (32 - take);
+}
+
+// Places every tile's image (enc_onepass<..., TILE = true>) at its offset in the stream:
+// workgroup t writes the stream words whose first bit lies in tile t -- a word that runs past
+// the tile's end takes the next tiles' first bits from their slots -- so every word has one
+// writer and no workgroup waits for another.  The stream's first word, when bit_offset is
+// not word-aligned, is merged with its memory content (shards composed into one buffer).
+// Also adds the tile's offset to its chunks' tile-relative bit offsets.
+__global__ void __launch_bounds__(256)
+enc_place(const uint32_t* __restrict__ scratch, long long slot_words,
+          const uint32_t* __restrict__ tile_bits, const unsigned long long* __restrict__ tile_off,
+          long long nb, unsigned long long bit_offset_arg,
+          const unsigned long long* __restrict__ d_bit_offset, uint32_t* __restrict__ out_words,
+          long long cap_words, long long rows_per_tile, long long rows_per_chunk,
+          long long chunks, unsigned long long* __restrict__ chunk_off,
+          unsigned long long* __restrict__ err, const unsigned long long* __restrict__ total) {
+    const long long t = blockIdx.x;
+    const unsigned long long bo = d_bit_offset ? (*d_bit_offset & 31ull) : bit_offset_arg;
+    const unsigned long long gs = bo + tile_off[t];          // the tile's first stream bit
+    const unsigned long long nbits = tile_bits[t];
+    const unsigned long long ge = gs + nbits;
+    if (t == 0 && threadIdx.x == 0 && ((bo + *total + 31) >> 5) > (unsigned long long)cap_words)
+        atomicOr(err, 2ull);
+    // (the stream must fit: checked from the total by every workgroup, nothing written if not)
+    if (((bo + *total + 31) >> 5) > (unsigned long long)cap_words) return;
+    if (chunk_off && rows_per_chunk > 0) {
+        const long long r0 = t * rows_per_tile, r1 = r0 + rows_per_tile;
+        const long long j0 = (r0 + rows_per_chunk - 1) / rows_per_chunk;
+        const long long j1 = min(chunks, (r1 + rows_per_chunk - 1) / rows_per_chunk);
+        for (long long j = j0 + threadIdx.x; j < j1; j += blockDim.x) chunk_off[j] += gs;
+    }
+    if (!nbits) return;
+    const uint32_t* src = scratch + t * slot_words;
+    // the word holding the stream's first bit, when that is not word-aligned: memory bits + ours
+    if (gs == bo && (bo & 31) && threadIdx.x == 0) {
+        const int room = 32 - (int)(bo & 31);
+        const int take = nbits < (unsigned long long)room ? (int)nbits : room;
+        const uint32_t mine = slot_bits(src, 0, take) << (room - take);
+        const long long w = (long long)(bo >> 5);
+        out_words[w] = __builtin_bswap32(__builtin_bswap32(out_words[w]) | mine);
+        // (a tile shorter than the rest of that word: the next tiles' bits are placed by
+        // the general loop below only for words they own, so merge them here too)
+        unsigned long long filled = (unsigned long long)take;
+        long long tt = t + 1;
+        uint32_t more = 0;
+        while (filled < (unsigned long long)room && tt < nb) {
+            const unsigned long long b2 = tile_bits[tt];
+            const int tk = (int)min<unsigned long long>(b2, (unsigned long long)room - filled);
+            if (tk > 0)
+                more |= slot_bits(scratch + tt * slot_words, 0, tk) << (room - (int)filled - tk);
+            filled += (unsigned long long)tk;
+            ++tt;
+        }
+        if (more) out_words[w] = __builtin_bswap32(__builtin_bswap32(out_words[w]) | more);
+    }
+    const long long wa = (long long)((gs + 31) >> 5), wz = (long long)((ge + 31) >> 5);   // [wa, wz)
+    for (long long w = wa + threadIdx.x; w < wz; w += blockDim.x) {
+        const unsigned long long r = ((unsigned long long)w << 5) - gs;   // < nbits
+        uint32_t word;
+        if (r + 32 <= nbits) {
+            word = slot_bits(src, r, 32);
+        } else {   // the tile's last word: its bits, then the next tiles' first bits
+            const int have = (int)(nbits - r);
+            word = slot_bits(src, r, have) << (32 - have);
+            int filled = have;
+            for (long long tt = t + 1; filled < 32 && tt < nb; ++tt) {
+                const unsigned long long b2 = tile_bits[tt];
+                const int tk = (int)min<unsigned long long>(b2, (unsigned long long)(32 - filled));
+                if (tk > 0) word |= slot_bits(scratch + tt * slot_words, 0, tk) << (32 - filled - tk);
+                filled += tk;
+            }
+        }
+        __builtin_nontemporal_store(__builtin_bswap32(word), out_words + w);
+    }
 }
 
 }  // namespace
@@ -1146,6 +1252,70 @@ static int encode_write_impl(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* 
     const long long nb = (rows + blk - 1) / blk;
     const size_t lds = ((size_t)blk * (row8 ? 8 : t->m) * kMaxCodeLen / 32 + 4) * 4;
     if (lds > 160 * 1024) return PQH_ERR_UNSUPPORTED;
+    unsigned long long* total = d_total_bits ? d_total_bits : ctx->d_diag + 3;
+    uint32_t* words = reinterpret_cast<uint32_t*>(d_out);
+    const int enc_prio = pqh_prio("ENCODE", 0);
+    // The tiled encoder (default): tiles coded into scratch slots with no inter-workgroup
+    // waiting, a scan of their bit counts, then enc_place.  PQH_ENC_IMPL=onepass: the
+    // single-kernel decoupled look-back form.
+    static const bool onepass = [] {
+        const char* e = std::getenv("PQH_ENC_IMPL");
+        return e && !std::strcmp(e, "onepass");
+    }();
+    if (!onepass) {
+        const long long slot = (long long)(lds / 4);   // a tile's worst-case image, + 4 words
+        int rc2 = pqh_ensure_enc_scratch(ctx, ((size_t)nb * slot + 64) * 4);
+        if (rc2) return rc2;
+        const size_t a = ((size_t)nb * 4 + 255) & ~(size_t)255;
+        rc2 = pqh_ensure_ws(ctx, a + (size_t)nb * 8 + 256);
+        if (rc2) return rc2;
+        uint32_t* tile_bits = static_cast<uint32_t*>(ctx->ws);
+        unsigned long long* tile_off =
+            reinterpret_cast<unsigned long long*>(static_cast<char*>(ctx->ws) + a);
+        uint32_t* scr = static_cast<uint32_t*>(ctx->enc_scr);
+        unsigned long long* tb = reinterpret_cast<unsigned long long*>(tile_bits);
+#define PQH_ENC_T(T, MAXM, R8, CS, PMV)                                                          \
+    do {                                                                                         \
+        constexpr int B = MAXM > 0 && MAXM <= 8 ? 256 : kEncBlock;                               \
+        auto kf = enc_onepass<T, MAXM, B, R8, CS, PMV, true>;                                    \
+        if (lds > 64 * 1024)                                                                     \
+            PQH_HIP(ctx, hipFuncSetAttribute((const void*)kf,                                    \
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+        hipLaunchKernelGGL(kf, dim3((unsigned)nb), dim3(B), lds, ctx->stream,                   \
+                           static_cast<const T*>(d_codes), R8 ? rows : n, t->m, t->k, t->context, \
+                           raw_first, static_cast<const T*>(d_prev_row), d_rawf, t->d_enc,       \
+                           t->d_enc32, t->items, 0ull, nullptr, scr, slot, chunk_vectors,        \
+                           d_chunk_offsets, static_cast<T*>(d_chunk_prev), ctx->d_diag + 2, tb,  \
+                           nullptr, nullptr, 0ull, 0u, nb, nullptr, tree_prev, enc_prio, ldc);   \
+    } while (0)
+        if (ldc) {
+            if (cs == 2) PQH_ENC_T(uint8_t, 8, true, 2, true);
+            else PQH_ENC_T(uint8_t, 8, true, 1, true);
+        } else if (t->k <= 256) {
+            if (row8 && cs == 2) PQH_ENC_T(uint8_t, 8, true, 2, false);
+            else if (row8) PQH_ENC_T(uint8_t, 8, true, 1, false);
+            else if (t->m <= 8) PQH_ENC_T(uint8_t, 8, false, 1, false);
+            else if (t->m <= 16) PQH_ENC_T(uint8_t, 16, false, 1, false);
+            else PQH_ENC_T(uint8_t, 0, false, 1, false);
+        } else {
+            if (t->m <= 8) PQH_ENC_T(uint16_t, 8, false, 1, false);
+            else if (t->m <= 16) PQH_ENC_T(uint16_t, 16, false, 1, false);
+            else PQH_ENC_T(uint16_t, 0, false, 1, false);
+        }
+#undef PQH_ENC_T
+        PQH_LAUNCH_CHECK(ctx);
+        hipLaunchKernelGGL(scan_blocks, dim3(1), dim3(1024), 0, ctx->stream, tile_bits, nb,
+                           tile_off, total);
+        PQH_LAUNCH_CHECK(ctx);
+        const long long chunks = chunk_vectors > 0 ? (n + chunk_vectors - 1) / chunk_vectors : 0;
+        hipLaunchKernelGGL(enc_place, dim3((unsigned)nb), dim3(256), 0, ctx->stream, scr, slot,
+                           tile_bits, tile_off, nb, bit_offset, d_bit_offset, words,
+                           (long long)(out_bytes / 4), (long long)blk,
+                           chunk_vectors > 0 ? (long long)chunk_vectors * cs : 0ll, chunks,
+                           d_chunk_offsets, ctx->d_diag + 2, total);
+        PQH_LAUNCH_CHECK(ctx);
+        return PQH_OK;
+    }
     // look-back state: grow-only, epoch-tagged so it never needs clearing between calls
     if (nb > ctx->lb_cap) {
         PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));   // no launch may still use it
@@ -1165,9 +1335,6 @@ static int encode_write_impl(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* 
     unsigned long long* st = ctx->lb_state;
     unsigned long long* tails = st + ctx->lb_cap;
     unsigned long long* ticket = st + 2 * ctx->lb_cap;
-    unsigned long long* total = d_total_bits ? d_total_bits : ctx->d_diag + 3;
-    uint32_t* words = reinterpret_cast<uint32_t*>(d_out);
-    const int enc_prio = pqh_prio("ENCODE", 0);
 #define PQH_ENC(T, MAXM, R8, CS) PQH_ENC_PM(T, MAXM, R8, CS, false)
 #define PQH_ENC_PM(T, MAXM, R8, CS, PMV)                                                          \
     do {                                                                                          \

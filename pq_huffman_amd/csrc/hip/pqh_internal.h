@@ -48,6 +48,9 @@ struct pqh_ctx {
     unsigned sort_epoch = 0;
     unsigned long long sort_ticket_base = 0;
     int rerank_slot = 0;              // d_diag slot of the last assignment's re-rank count
+    // the tiled encoder's scratch: one worst-case slot per tile (grow-only)
+    void* enc_scr = nullptr;
+    size_t enc_scr_bytes = 0;
 };
 constexpr int kSchedMax = 64;      // subspaces with a work queue (more: static schedule)
 constexpr int kXcds = 8;
@@ -56,6 +59,7 @@ constexpr long long kSchedSet = (long long)kSchedMax * kXcds * kSchedStride;   /
 
 int pqh_set_error(pqh_ctx* ctx, int code, const char* fmt, ...);
 int pqh_ensure_ws(pqh_ctx* ctx, size_t bytes);
+int pqh_ensure_enc_scratch(pqh_ctx* ctx, size_t bytes);
 int pqh_use_device(pqh_ctx* ctx);
 int pqh_kmeans_fixed_shift(float max_abs, long long n);
 // k-means iteration pieces (pqh_kmeans.hip), shared by the one-shot and the streamed trainers
