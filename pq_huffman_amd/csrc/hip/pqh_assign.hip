@@ -67,6 +67,13 @@ constexpr int kNB = PQH_ASSIGN_NB;            // 32-vector blocks screened toget
 #ifndef PQH_ASSIGN_CLDS
 #define PQH_ASSIGN_CLDS 0
 #endif
+#ifndef PQH_ASSIGN_SHAREA   // K = 4096: the workgroup's waves share one LDS ring of A tiles
+#define PQH_ASSIGN_SHAREA 0    // (measured slower: 3.55 vs 2.6-2.9 ms per 1M rows alone, EXPERIMENTS.md)
+#endif
+constexpr int kAG = 8;            // (SHAREA) A tiles per ring group: one barrier per group
+#ifndef PQH_ASSIGN_XAUX   // cache policy of the x slices' LDS DMA (2 = nt; experiment knob)
+#define PQH_ASSIGN_XAUX 0
+#endif
 constexpr bool kCentLds = PQH_ASSIGN_CLDS != 0;
 
 template <int D>
@@ -485,6 +492,15 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
                                                      [kXLds ? Slice<D>::XD / 4 : 1][kXLds ? 256 : 1];
     // (PQH_ASSIGN_CLDS, K = 256) the fp32 centroids for the exact re-rank's candidate rows
     __shared__ __attribute__((aligned(16))) float Cf[kLdsA && kCentLds ? K * D : 1];
+    // K = 4096 (SHAREA): the A fragments stream through an LDS ring of 2 kAG tiles that the
+    // workgroup's waves fill together by LDS DMA and all read -- one L2 fetch of a tile per
+    // workgroup instead of one per wave (the streamed kernel was bound by those L2 reads:
+    // 256 KB per 64 vectors, 32 GB per 1M-row launch).  Tile t sits in slot t % (2 kAG):
+    // Ar[(slot * PA + p) * 64 + lane].  The waves then run their chunks in lockstep (one
+    // barrier per group), on a static workgroup schedule.
+    constexpr bool kShareA = !kLdsA && PQH_ASSIGN_SHAREA != 0;
+    constexpr int kAR = 2 * kAG;
+    __shared__ __attribute__((aligned(16))) uint4 Ar[kShareA ? kAR * P::PA * 64 : 1];
 
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // (uniform: SGPR math)
@@ -619,7 +635,8 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
 #if defined(__HIP_DEVICE_COMPILE__)   // (the host pass rejects the 16-byte form)
             __builtin_amdgcn_global_load_lds(
                 xp + (HALF ? 16 * (j >> 3) + (j & 7) : j),
-                (__attribute__((address_space(3))) void*)(&xst[wave][slot][j / 4][0]), 16, 0, 0);
+                (__attribute__((address_space(3))) void*)(&xst[wave][slot][j / 4][0]), 16, 0,
+                PQH_ASSIGN_XAUX);
 #else
             (void)xp;
 #endif
@@ -630,6 +647,32 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         for (int j = 0; j < XD; j += 4) {
             const f32x4 q = *reinterpret_cast<const f32x4*>(&xst[wave][slot][j / 4][lane * 4]);
             dst[j] = q.x; dst[j + 1] = q.y; dst[j + 2] = q.z; dst[j + 3] = q.w;
+        }
+    };
+    // (SHAREA) tile t's A fragments from the LDS ring, and one group's DMA into it: the group's
+    // kAG * PA pieces of 1 KB (64 lanes x 16 B) spread over the workgroup's waves
+    auto read_ring = [&](int t, bf16x8* a) {
+#pragma unroll
+        for (int p = 0; p < P::PA; ++p)
+            a[p] = *reinterpret_cast<const bf16x8*>(&Ar[((t % kAR) * P::PA + p) * 64 + lane]);
+    };
+    auto dma_group = [&](int g) {
+        if constexpr (kShareA) {
+            const uint4* src = reinterpret_cast<const uint4*>(afrag) + (long long)m * P::PA * KT * 64;
+            static_assert((kAG * P::PA) % kWavesPerWG == 0, "whole pieces per wave");
+#pragma unroll
+            for (int i = 0; i < (kAG * P::PA) / kWavesPerWG; ++i) {
+                const int q = wave + i * kWavesPerWG;
+                const int t = g * kAG + q / P::PA, p = q % P::PA;
+#if defined(__HIP_DEVICE_COMPILE__)
+                __builtin_amdgcn_global_load_lds(
+                    src + (p * KT + t) * 64 + lane,
+                    (__attribute__((address_space(3))) void*)(&Ar[((t % kAR) * P::PA + p) * 64]),
+                    16, 0, 0);
+#else
+                (void)src; (void)t; (void)p;
+#endif
+            }
         }
     };
     // Deferred re-rank: a vector whose screening gap is too small is appended to this wave's
@@ -771,6 +814,44 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
                     reduce(acc[b], t, b, t == 0);
                     if (t + 1 < KT) acc[b] = tile_scores_a<D>(a, Bm[b], Bl[b], LO, cn);
                     __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        } else if constexpr (kShareA) {
+            // the LDS ring: group g + 1 was requested a group ago; at the last tile of group g
+            // every wave has issued the MFMAs that read group g, so after the barrier group
+            // g's slots take group g + 2 (past the last group: the next chunk's 0 and 1)
+            constexpr int NG = KT / kAG;
+#pragma unroll
+            for (int b = 0; b < kNB; ++b) {
+                pm1[b] = pm2[b] = 0x7F800000u;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) qg[b][j] = qh[b][j] = 0x7F800000u;
+            }
+            bf16x8 a[P::PA];
+            read_ring(0, a);
+            f32x16 cn = tile_norms(Cn, 0, h);
+#pragma unroll
+            for (int b = 0; b < kNB; ++b) acc[b] = tile_scores_a<D>(a, Bm[b], Bl[b], LO, cn);
+#pragma unroll 1
+            for (int g = 0; g < NG; ++g) {
+#pragma unroll
+                for (int u = 0; u < kAG; ++u) {
+                    const int t = g * kAG + u;
+                    if (u == kAG - 1) {
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs
+                        lds_barrier();                                      // everyone's
+                        dma_group(g + 2 < NG ? g + 2 : g + 2 - NG);
+                    }
+                    // (past the last tile: the next chunk's tile 0, whose scores are never
+                    // reduced -- an unconditional MFMA keeps the accumulators in place)
+                    read_ring((t + 1) & (KT - 1), a);
+                    cn = tile_norms(Cn, (t + 1) & (KT - 1), h);
+#pragma unroll
+                    for (int b = 0; b < kNB; ++b) {
+                        reduce_pair(acc[b], t, b, u & 1);
+                        acc[b] = tile_scores_a<D>(a, Bm[b], Bl[b], LO, cn);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
                 }
             }
         } else {
@@ -994,7 +1075,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     const int waves_m = gx * kWavesPerWG;
     const int nchunk = (nblk + kNB - 1) / kNB;
     const int R = nchunk > waves_m ? (nchunk - waves_m + kXcds - 1) / kXcds : 0;
-    uint32_t* head = sched ? sched + (long long)m * kXcds * kSchedStride : nullptr;
+    uint32_t* head = sched && !kShareA ? sched + (long long)m * kXcds * kSchedStride : nullptr;
     int xr = head ? (int)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & (kXcds - 1)) : 0;
     int tries = head && R > 0 ? 0 : kXcds;
     auto ticket = [&]() -> unsigned {
@@ -1154,7 +1235,43 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         ++rr_batches;
 #endif
     };
-    int ch = wave_id;
+    if constexpr (kShareA) {
+        // lockstep waves: workgroup bx takes super-chunks sc = bx, bx + gx, ... of kWavesPerWG
+        // chunks, wave w chunk kWavesPerWG sc + w (past nchunk: clamped rows, nothing stored)
+        const int nsuper = (nchunk + kWavesPerWG - 1) / kWavesPerWG;
+        int sc = bx;
+        dma_group(0);
+        dma_group(1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_barrier();
+        int chs = sc * kWavesPerWG + wave;
+        float xq[kNB][XD];
+#pragma unroll
+        for (int b = 0; b < kNB; ++b) load_x(chs * kNB + b, xq[b]);
+        while (sc < nsuper) {   // (uniform in the workgroup)
+            float xa[kNB][XD];
+#pragma unroll
+            for (int b = 0; b < kNB; ++b)
+#pragma unroll
+                for (int j = 0; j < XD; ++j) xa[b][j] = xq[b][0 * j + j];
+            const int nsc = sc + gx;
+            const int nch = nsc * kWavesPerWG + wave;
+            const int pre = nsc < nsuper ? nch : chs;   // branch-free: re-load at the end
+#pragma unroll
+            for (int b = 0; b < kNB; ++b) load_x(pre * kNB + b, xq[b]);
+            step((long long)chs * kNB, xa);
+            while (qn >= 32u) {
+                rerank32(rqs[wave][qn - 32u + (unsigned)r], true);
+                qn -= 32u;
+            }
+            sc = nsc;
+            chs = nch;
+        }
+        // (the last group barrier requested the next chunk's first tiles: let them land
+        // before the workgroup's LDS is released)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    int ch = kShareA ? nchunk : wave_id;
     float xn[kXLds ? 1 : kNB][XD];
 #pragma unroll
     for (int b = 0; b < kNB; ++b) {

@@ -374,6 +374,55 @@ hist_plain(const CodeT* __restrict__ codes, long long n, int m_total, int k,
         if (bins[i]) atomicAdd(&counts[(long long)m * k + i], bins[i]);
 }
 
+// Non-context histogram of 8-part u16 rows (K > 256, configs[4]): a workgroup counts `rows`
+// consecutive rows -- one 16-byte load per row, coalesced across the workgroup -- into u16
+// pair counters for all 8 parts in LDS (8 x K/2 words: 64 KB at K = 4,096; a workgroup's
+// rows stay below 65,536, so no counter overflows) and stores the image as its slice of the
+// partials [part][group][K/2 words]; hist_ctx_reduce sums them.  (hist_plain flushed every
+// non-zero bin of every workgroup by a global atomic: ~32 MB of atomic traffic per 1M rows
+// for 128 KB of counts.)
+__global__ void __launch_bounds__(256)
+hist_plain_rows16(const uint16_t* __restrict__ codes, long long n, int k, long long rows,
+                  uint32_t* __restrict__ partial, int groups) {
+    extern __shared__ uint32_t bins[];   // [8][k / 2]
+    const int words = k / 2;
+    for (int w = threadIdx.x; w < 8 * words; w += blockDim.x) bins[w] = 0;
+    lds_barrier();
+    const long long r0 = (long long)blockIdx.x * rows, r1 = min(n, r0 + rows);
+    const uint4* rp = reinterpret_cast<const uint4*>(codes);
+    auto count = [&](uint32_t pair, int part) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const unsigned c = h ? pair >> 16 : pair & 0xFFFFu;
+            if (c < (unsigned)k) {
+                const unsigned bin = (unsigned)(part + h) * (unsigned)k + c;
+                atomicAdd(&bins[bin >> 1], 1u << ((bin & 1u) * 16));
+            }
+        }
+    };
+#pragma unroll 1
+    for (long long r = r0 + threadIdx.x; r < r1; r += 4 * (long long)blockDim.x) {
+        uint4 q[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {   // four rows' loads in flight before their counts
+            const long long rr = r + (long long)u * blockDim.x;
+            q[u] = rr < r1 ? rp[rr] : make_uint4(~0u, ~0u, ~0u, ~0u);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            count(q[u].x, 0);
+            count(q[u].y, 2);
+            count(q[u].z, 4);
+            count(q[u].w, 6);
+        }
+    }
+    lds_barrier();
+    for (int w = threadIdx.x; w < 8 * words; w += blockDim.x) {
+        const int part = w / words, ww = w - part * words;
+        partial[((long long)part * groups + blockIdx.x) * words + ww] = bins[w];
+    }
+}
+
 // part-major codes [m][ldc] -> rows [n][m] (one thread per row: coalesced loads of each part,
 // one 8- or 16-byte store per row where the row allows)
 template <typename CodeT>
@@ -982,10 +1031,10 @@ struct HistPlan {
 };
 
 static int hist_split(int k) {
-    static const int split_env = [] {   // PQH_HIST_SPLIT = 1, 2 or 4; default 2 for even k
+    static const int split_env = [] {   // PQH_HIST_SPLIT = 1, 2, 4 or 8; default 2 for even k
         const char* e = std::getenv("PQH_HIST_SPLIT");
         const int v = e ? std::atoi(e) : 2;
-        return v == 1 || v == 4 ? v : 2;
+        return v == 1 || v == 4 || v == 8 ? v : 2;
     }();
     return k % (2 * split_env) == 0 ? split_env : (k % 4 == 0 ? 2 : 1);
 }
@@ -1031,7 +1080,10 @@ static int histogram_impl(pqh_ctx_t* ctx, const void* d_codes, long long n, int 
     int rc = pqh_use_device(ctx);
     if (rc) return rc;
     const long long items = context ? (long long)k * k : k;
-    if (set && (n == 0 || !context) && phase != 1)   // the plain kernel and an empty input only add
+    // (8-part u16 rows, K > 256: per-workgroup partials + a reduce that overwrites)
+    const bool wide16 = !context && k > 256 && !ldc && m == 8 && k % 2 == 0 && k <= 4096 &&
+                        !(reinterpret_cast<uintptr_t>(d_codes) & 15);
+    if (set && (n == 0 || (!context && !wide16)) && phase != 1)   // the plain kernel and an empty input only add
         PQH_HIP(ctx, hipMemsetAsync(d_counts, 0, (size_t)m * items * 4, ctx->stream));
     if (n == 0) return PQH_OK;
     if (context) {
@@ -1114,6 +1166,23 @@ static int histogram_impl(pqh_ctx_t* ctx, const void* d_codes, long long n, int 
             hipLaunchKernelGGL(hist_ctx_reduce, dim3((unsigned)((words + 255) / 256), m), dim3(256),
                                0, ctx->stream, partial, hp.groups, words, (long long)k * k,
                                d_counts, set, acc);
+    } else if (wide16) {
+        // 8-part u16 rows: per-workgroup partial images + hist_ctx_reduce (no global atomics)
+        const long long rows = std::max<long long>(1, std::min<long long>(16384, (n + 63) / 64));
+        const int groups = (int)((n + rows - 1) / rows);
+        const int words = k / 2;
+        rc = pqh_ensure_ws(ctx, (size_t)8 * groups * words * 4);
+        if (rc) return rc;
+        uint32_t* partial = static_cast<uint32_t*>(ctx->ws);
+        const size_t lds = (size_t)8 * words * 4;
+        PQH_HIP(ctx, hipFuncSetAttribute((const void*)hist_plain_rows16,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL(hist_plain_rows16, dim3((unsigned)groups), dim3(256), lds, ctx->stream,
+                           static_cast<const uint16_t*>(d_codes), n, k, rows, partial, groups);
+        PQH_LAUNCH_CHECK(ctx);
+        hipLaunchKernelGGL(hist_ctx_reduce, dim3((unsigned)((words + 255) / 256), m), dim3(256), 0,
+                           ctx->stream, partial, groups, words, (long long)k, d_counts,
+                           set ? 1 : 0, nullptr);
     } else {
         const unsigned blocks = (unsigned)std::min<long long>((n + 4095) / 4096, 512);
         if (k <= 256)

@@ -142,7 +142,7 @@ bool pqh_debug_sync();
 //   enc [m][items] u64: (len << 56) | code (right-aligned, len <= 56; 0 = no code)
 //   enc32 [m][items] u32: the same entry as len << 26 | code when len <= 26, else ~0u
 //   Decode: two-level lookup per alphabet (tables = m * roots, roots = K in context mode)
-//   lut1 [tables][1 << kL1Max] u16, the first 2^l1_bits entries used (W1 = l1_bits for
+//   lut1 [tables][1 << l1_bits] u16 (rows packed at the table set's own W1 = l1_bits, for
 //        every alphabet): (len << 12) | sym for 1 <= len <= W1 (replicated);
 //        (15 << 12) | sub = a longer code, subtable `sub` of this alphabet; 0 = invalid
 //   meta [tables] u32: l2base << 9 | noL2 << 8 | w2 << 4 | W1 -- the alphabet's subtables

@@ -27,7 +27,7 @@ namespace {
 
 constexpr int kMaxCodeLen = 56;
 constexpr unsigned long long kCodeMask = (1ull << 56) - 1;
-constexpr int kL1Max = 11;                      // decode first level: 2^W1 entries, W1 <= 11
+constexpr int kL1Max = 13;                      // decode first level: 2^W1 entries, W1 <= 13
 constexpr long long kL2BaseMax = 1ll << 23;     // (meta holds l2base in 23 bits)
 
 // ------------------------------------------------------------------- tree building
@@ -1088,7 +1088,7 @@ __device__ __forceinline__ void grp_luts(const GrpLut& L, long long t, int k, in
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     }
     wave_sync_lds();
-    uint16_t* const L1 = L.lut1 + (t << kL1Max);
+    uint16_t* const L1 = L.lut1 + (t << L.w1);
 #pragma unroll 1
     for (int s = gl; s < k; s += 16) {
         const unsigned long long v = code[s];
@@ -1467,7 +1467,7 @@ lut_build(const unsigned long long* __restrict__ enc, uint32_t* __restrict__ enc
     __shared__ uint32_t part[256];
     const long long t = blockIdx.x;
     const unsigned long long* e = enc + t * k;
-    uint16_t* L1 = lut1 + (t << kL1Max);
+    uint16_t* L1 = lut1 + (t << w1);
     block_w2max(e, k, w1, l2_bits, w2max);
     // subtable ids in prefix order: per-thread chunk counts, then a block-wide exclusive
     // scan (wave scans + the four wave totals; 256 threads)
@@ -1642,7 +1642,7 @@ struct DecTables {
 __device__ __forceinline__ bool dec_symbol(BitReader& br, const DecTables& T, long long tab,
                                            unsigned& sym) {
     const int w1 = T.w1;
-    const uint16_t e = T.lut1[(tab << kL1Max) + br.peek(w1)];
+    const uint16_t e = T.lut1[(tab << w1) + br.peek(w1)];
     const uint32_t mt = T.meta[tab];
     const int len = e >> 12;
     sym = e & 0xFFFu;
@@ -1790,7 +1790,7 @@ dec_chunks(const uint32_t* __restrict__ words, long long nwords, long long n, in
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int m = MT ? MT : m_rt;
     const long long meta_b = (tables * 4 + 15) & ~15ll;
-    const long long l1_b = L1_IN_LDS ? (((tables << kL1Max) * 2 + 15) & ~15ll) : 0;
+    const long long l1_b = L1_IN_LDS ? (((tables << w1) * 2 + 15) & ~15ll) : 0;
     uint32_t* meta = reinterpret_cast<uint32_t*>(lds);
     uint16_t* l1s = reinterpret_cast<uint16_t*>(lds + meta_b);
     uint32_t* win = reinterpret_cast<uint32_t*>(lds + meta_b + l1_b);
@@ -1803,7 +1803,7 @@ dec_chunks(const uint32_t* __restrict__ words, long long nwords, long long n, in
     if (stamp) g_tree_stamps[8] = __builtin_amdgcn_s_memtime();
     for (long long t = lane; t < tables; t += 64) meta[t] = meta_g[t];
     if constexpr (L1_IN_LDS) {
-        const long long n16 = (tables << kL1Max) * 2 / 16;
+        const long long n16 = ((tables << w1) * 2 + 15) / 16;
         const uint4* src = reinterpret_cast<const uint4*>(lut1_g);
         uint4* dst = reinterpret_cast<uint4*>(l1s);
         for (long long i = lane; i < n16; i += 64) dst[i] = src[i];
@@ -1926,7 +1926,7 @@ struct Row8Tabs {
 template <bool LDS>
 __device__ __forceinline__ int dec_sym8(BitRd<LDS>& br, const Row8Tabs& T, unsigned tab) {
     const int w1 = T.w1;
-    const uint16_t e = T.lut1[(tab << kL1Max) + br.peek(w1)];
+    const uint16_t e = T.lut1[(tab << w1) + br.peek(w1)];
     const int len = e >> 12;
     unsigned sym = e & 0xFFFu;
     if (len >= 1 && len <= w1) {
@@ -2104,7 +2104,11 @@ int pqh_tables_alloc(pqh_ctx_t* ctx, int m, int k, int context, pqh_tables_t** o
     t->roots = context ? k : 1;
     t->items = (long long)t->roots * k;
     t->tables = (long long)m * t->roots;
-    t->l1_bits = context ? 9 : kL1Max;   // 1 KB first level per context alphabet
+    // first-level width W1 (the table set's lut1 rows are 2^W1 entries, packed): 9 in context
+    // mode (1 KB per alphabet, K * m alphabets), 11 for K <= 256, 13 for K = 4,096 (codes
+    // average ~12 bits there: with 11, most symbols took the second level, whose subtables
+    // -- up to 2^12 entries per long prefix -- made the K = 4,096 decode read ~27x its stream)
+    t->l1_bits = context ? 9 : (k > 256 ? 13 : 11);
     // Second-level width: 8 bits for K <= 256 (codes past W1 + 8 bits are rare); 12 bits
     // for larger alphabets, whose rarest symbols sit ~log2(N) bits deep -- with 8 bits
     // (19 covered) a K = 4096 stream spent its decode in the long-code list (133 ms per
@@ -2114,7 +2118,7 @@ int pqh_tables_alloc(pqh_ctx_t* ctx, int m, int k, int context, pqh_tables_t** o
                                       kL2BaseMax - 1);
     if (hipMalloc(&t->d_enc, (size_t)m * t->items * 8) != hipSuccess ||
         hipMalloc(&t->d_enc32, (size_t)m * t->items * 4) != hipSuccess ||
-        hipMalloc(&t->d_lut1, (size_t)(t->tables << kL1Max) * 2) != hipSuccess ||
+        hipMalloc(&t->d_lut1, (size_t)(t->tables << t->l1_bits) * 2 + 16) != hipSuccess ||
         hipMalloc(&t->d_lut2, (size_t)t->lut2_cap * 2) != hipSuccess ||
         hipMalloc(&t->d_meta, (size_t)t->tables * 4 + 16) != hipSuccess ||
         hipMalloc(&t->d_long, (size_t)t->tables * k * sizeof(pqh_long_code)) != hipSuccess ||
@@ -2417,7 +2421,7 @@ int pqh_decode(pqh_ctx_t* ctx, const pqh_tables_t* t, const unsigned char* d_str
     const long long nwords = (long long)(stream_bytes / 4);
     const unsigned blocks = (unsigned)((chunks + 63) / 64);
     if (reinterpret_cast<uintptr_t>(d_codes) & 3u) return PQH_ERR_ARG;
-    const size_t l1_bytes = (size_t)(t->tables << kL1Max) * 2;
+    const size_t l1_bytes = (size_t)(t->tables << t->l1_bits) * 2;
     const size_t meta_bytes = ((size_t)t->tables * 4 + 15) & ~(size_t)15;
     const bool lds_l1 = meta_bytes + l1_bytes <= 48 * 1024;
     const size_t esz = t->k <= 256 ? 1 : 2;
