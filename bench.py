@@ -174,6 +174,11 @@ def parse():
                          "waves on a SIMD no wave of the kernels beside the grid fits, so a "
                          "lighter grid lets them co-run.  Measured at 200 steps: 3 -> 2,614-2,642, "
                          "2.5 -> 2,676, 2 -> 2,669-2,688 Mvec/s; --sort --lanes 3: 1,969 -> 2,043")
+    ap.add_argument("--hist-tune", default="4x256",
+                    help="SPLITxTHREADS: the context histogram's launch shape when it runs off the "
+                         "assignment stream (--hist-on lanes/own): split of the previous-symbol "
+                         "range (LDS per workgroup 128 KB / split) x workgroup threads, so its "
+                         "workgroups fit beside the assignment grid (pqh_ctx_set_tuning)")
     ap.add_argument("--split-cus", type=int, default=0,
                     help="> 0: the code-table, encode and decode streams on this many compute "
                          "units, the assignment stream on the others (disjoint CU masks)")
@@ -355,8 +360,6 @@ def pcie_ms(torch, x, codes, stream_bytes):
 
 def main():
     args = parse()
-    if args.assign_wgs_per_cu > 0:   # read by the library at each assignment launch
-        os.environ["PQH_ASSIGN_WGS_PER_CU"] = str(args.assign_wgs_per_cu)
     if int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.hist_on == "own":
         # 4 library/torch streams + RCCL's own: give each a hardware queue (HIP reads this at
         # initialisation; measured neutral at one rank, 2,150 vs 2,153 Mvec/s)
@@ -436,6 +439,11 @@ def main():
     # (the assignment's work-queue state is per object, so launches may overlap)
     na = 1 if serial or lib_shard_req(args, world) else max(1, args.astreams)
     actx = [ctx] + [codec.Context(local, cus=1 << 20) for _ in range(na - 1)]
+    # the assignment grid's workgroups per CU, on the contexts that launch it (a library
+    # caller that sets nothing gets the occupancy limit; pqh_ctx_set_tuning)
+    if args.assign_wgs_per_cu > 0:
+        for c in actx:
+            c.set_tuning(assign_wgs_per_cu=args.assign_wgs_per_cu)
     apq = [pq] + [codec.PQ(c, cent) for c in actx[1:]]
     items = k * k if ctxm else k
     # codes / counts buffers: the assignment runs up to `slots` batches ahead of the oldest
@@ -539,6 +547,9 @@ def main():
     # --hist-on own: the histogram of batch i on a stream of its own, after batch i's
     # assignment, so stream A carries the assignments only
     hctx = codec.Context(local, cus=1 << 20) if args.hist_on == "own" and not serial else None
+    hsplit, hthreads = (int(v) for v in args.hist_tune.lower().split("x"))
+    for c in ([hctx] if hctx is not None else lanes if hist_on_lane else []):
+        c.set_tuning(hist_split=hsplit, hist_block=hthreads)
     ev_asg = [torch.cuda.Event() for _ in range(slots)]
     # the split histogram: partial counts per slot (the assignment stream writes slot s's while
     # a lane may still reduce another's)
@@ -981,11 +992,15 @@ def main():
                                       "mode)" if args.sort else "no sort"),
                        "sort": bool(args.sort),
                        "code_layout": "parts" if pm else "rows",
-                       # the K = 256 assignment grid's workgroups per CU that this process set
-                       # (PQH_ASSIGN_WGS_PER_CU; a library caller that sets nothing gets the
-                       # occupancy limit, 3)
-                       "assign_wgs_per_cu": (os.environ.get("PQH_ASSIGN_WGS_PER_CU")
-                                             or "library default"),
+                       # the K = 256 assignment grid's workgroups per CU set on the assignment
+                       # contexts (pqh_ctx_set_tuning; a library caller that sets nothing gets
+                       # the occupancy limit, 3)
+                       "assign_wgs_per_cu": (args.assign_wgs_per_cu if args.assign_wgs_per_cu > 0
+                                             else "library default"),
+                       "histogram_stream": "assignment" if not (hist_on_lane or hctx) else
+                                           ("table lanes" if hist_on_lane else "own"),
+                       "histogram_launch": (args.hist_tune if (hist_on_lane or hctx) else
+                                            "library default"),
                        "vectors_per_gpu": n, "d": d, "m": m, "k": k,
                        "mode": "ctx" if ctxm else "noctx",
                        "chunk_vectors": args.chunk, "parallelism": f"dp{world} row shards",

@@ -63,6 +63,20 @@ int pqh_ctx_destroy(pqh_ctx_t* ctx);
  * (legacy, synchronising) stream -- what torch's current stream usually is. */
 int pqh_ctx_set_stream(pqh_ctx_t* ctx, void* hip_stream);
 int pqh_ctx_sync(pqh_ctx_t* ctx);
+/* Per-context launch shapes of the kernels this context launches (results never change;
+ * 0 restores the library default, which the PQH_* environment variable of the same name
+ * can set process-wide):
+ *   PQH_TUNE_ASSIGN_WGS_PER_CU  workgroups per CU of the K = 256 assignment grid (<= its
+ *                               occupancy limit, 3): fewer leave SIMD room for kernels
+ *                               running beside it on other streams (PQH_ASSIGN_WGS_PER_CU);
+ *   PQH_TUNE_HIST_SPLIT         the context histogram's split of the previous-symbol range
+ *                               (1, 2, 4 or 8): LDS per workgroup = 128 KB / split at K = 256
+ *                               (PQH_HIST_SPLIT);
+ *   PQH_TUNE_HIST_BLOCK         its workgroup size, 256 or 1024 threads (PQH_HIST_BLOCK).
+ * A histogram that runs beside the assignment grid (on another stream) fits best at
+ * split 4, 256 threads. */
+enum { PQH_TUNE_ASSIGN_WGS_PER_CU = 1, PQH_TUNE_HIST_SPLIT = 2, PQH_TUNE_HIST_BLOCK = 3 };
+int pqh_ctx_set_tuning(pqh_ctx_t* ctx, int key, double value);
 const char* pqh_status_string(int status);
 const char* pqh_ctx_last_error(const pqh_ctx_t* ctx);
 int pqh_device_count(int* count);

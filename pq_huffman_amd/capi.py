@@ -163,6 +163,7 @@ SIGNATURES = [
     ("pqh_shard_stitch", I, [I, P, P, P, P, ULL]),
     ("pqh_shard_halo_source", I, [P, I, I, P, P]),
     ("pqh_debug_poison_lds", I, [P, ctypes.c_uint]),
+    ("pqh_ctx_set_tuning", I, [P, I, D]),
     ("pqh_tree_order", I, [LL, LL, P, P, P, P, P]),
     ("pqh_tree_order_device", I, [P, LL, LL, P, P, P, P, P, P]),
     ("pqh_tree_ext_index_device", LL, [P, LL, P, I, I, P, P, P]),

@@ -83,6 +83,16 @@ class Context:
         self.stream = stream
         check(lib().pqh_ctx_set_stream(self.ptr, ctypes.c_void_p(stream.cuda_stream)))
 
+    TUNE = {"assign_wgs_per_cu": 1, "hist_split": 2, "hist_block": 3}
+
+    def set_tuning(self, **kw) -> "Context":
+        """launch shapes of this context's kernels (pqh_ctx_set_tuning; results never
+        change): assign_wgs_per_cu, hist_split, hist_block -- 0 restores the default"""
+        for key, value in kw.items():
+            check(lib().pqh_ctx_set_tuning(self.ptr, self.TUNE[key], float(value)),
+                  f"pqh_ctx_set_tuning({key})")
+        return self
+
     def sync(self) -> None:
         check(lib().pqh_ctx_sync(self.ptr), "pqh_ctx_sync")
 

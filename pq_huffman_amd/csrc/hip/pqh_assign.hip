@@ -1533,9 +1533,12 @@ int plan_pa(int dsub) {
 // workgroups per CU of the persistent assignment grid: the occupancy limit, or fewer
 // (PQH_ASSIGN_WGS_PER_CU, a fraction allowed: an experiment knob -- with three waves of 166
 // VGPRs on every SIMD, no 32-VGPR wave of the kernels running beside the grid fits)
-double assign_wgs_per_cu(int occ) {
-    const char* e = getenv("PQH_ASSIGN_WGS_PER_CU");
-    const double v = e ? atof(e) : 0.0;
+double assign_wgs_per_cu(const pqh_ctx* ctx, int occ) {
+    double v = ctx->tune_wgs_per_cu;   // pqh_ctx_set_tuning, else the environment
+    if (!(v > 0.0)) {
+        const char* e = getenv("PQH_ASSIGN_WGS_PER_CU");
+        v = e ? atof(e) : 0.0;
+    }
     return v > 0.0 && v < occ ? v : (double)occ;
 }
 
@@ -1568,7 +1571,7 @@ int launch_mfma(pqh_ctx* ctx, pqh_pq* pq, const float* x, long long n, long long
                 &per_cu, (const void*)(pq_assign_mfma<DD, KTT, CodeT>), (int)block.x, dyn) != \
                 hipSuccess || per_cu < 1)                                                   \
             per_cu = 1;                                                                     \
-        long long gx = (long long)((double)ctx->num_cus * assign_wgs_per_cu(per_cu) / groups); \
+        long long gx = (long long)((double)ctx->num_cus * assign_wgs_per_cu(ctx, per_cu) / groups); \
         gx = std::max(1ll, std::min(gx, ((nblk + kNB - 1) / kNB + kWavesPerWG - 1) / kWavesPerWG)); \
         if (gx >= 16) gx &= ~7ll;   /* CU-uniform subspace placement (see the kernel) */   \
         hipLaunchKernelGGL((pq_assign_mfma<DD, KTT, CodeT>), dim3((unsigned)(gx * groups)), block, \

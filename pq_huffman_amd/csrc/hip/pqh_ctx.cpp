@@ -184,6 +184,29 @@ int pqh_ctx_set_stream(pqh_ctx_t* ctx, void* hip_stream) {
     return PQH_OK;
 }
 
+int pqh_ctx_set_tuning(pqh_ctx_t* ctx, int key, double value) {
+    if (!ctx || value < 0.0) return PQH_ERR_ARG;
+    switch (key) {
+        case PQH_TUNE_ASSIGN_WGS_PER_CU:
+            ctx->tune_wgs_per_cu = value;
+            return PQH_OK;
+        case PQH_TUNE_HIST_SPLIT: {
+            const int v = (int)value;
+            if (v != 0 && v != 1 && v != 2 && v != 4 && v != 8) return PQH_ERR_ARG;
+            ctx->tune_hist_split = v;
+            return PQH_OK;
+        }
+        case PQH_TUNE_HIST_BLOCK: {
+            const int v = (int)value;
+            if (v != 0 && v != 256 && v != 1024) return PQH_ERR_ARG;
+            ctx->tune_hist_block = v;
+            return PQH_OK;
+        }
+        default:
+            return PQH_ERR_ARG;
+    }
+}
+
 int pqh_ctx_sync(pqh_ctx_t* ctx) {
     if (!ctx) return PQH_ERR_ARG;
     PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));

@@ -1030,25 +1030,29 @@ struct HistPlan {
     size_t partial_bytes, acc_offset, total_bytes;
 };
 
-static int hist_split(int k) {
+static int hist_split(int k, int ctx_split) {
     static const int split_env = [] {   // PQH_HIST_SPLIT = 1, 2, 4 or 8; default 2 for even k
         const char* e = std::getenv("PQH_HIST_SPLIT");
         const int v = e ? std::atoi(e) : 2;
         return v == 1 || v == 4 || v == 8 ? v : 2;
     }();
-    return k % (2 * split_env) == 0 ? split_env : (k % 4 == 0 ? 2 : 1);
+    const int want = ctx_split > 0 ? ctx_split : split_env;   // pqh_ctx_set_tuning first
+    return k % (2 * want) == 0 ? want : (k % 4 == 0 ? 2 : 1);
 }
 
-static HistPlan hist_plan(long long n, int m, int k) {
+static HistPlan hist_plan(long long n, int m, int k, int ctx_split = 0) {
     HistPlan p{};
-    p.split = hist_split(k);
+    p.split = hist_split(k, ctx_split);
     p.chunks = (n + kHistChunk - 1) / kHistChunk;
     static const int target = [] {   // PQH_HIST_WGS: the multi-round grid's workgroups
         const char* e = std::getenv("PQH_HIST_WGS");
         const int v = e ? std::atoi(e) : 256;
         return v >= 8 ? v : 256;
     }();
-    const int gt = std::max(8, (target / (m * p.split)) / 8 * 8);   // groups per (part, split)
+    // groups per (part, split), independent of the split: the partials' layout (and the
+    // reduce that reads them, possibly on another context with another split) depends only on
+    // n, m and k
+    const int gt = std::max(8, (target / (m * 2)) / 8 * 8);
     if (p.chunks <= 4ll * gt) {
         p.rounds = 1;
         p.groups = (int)p.chunks;
@@ -1087,7 +1091,7 @@ static int histogram_impl(pqh_ctx_t* ctx, const void* d_codes, long long n, int 
         PQH_HIP(ctx, hipMemsetAsync(d_counts, 0, (size_t)m * items * 4, ctx->stream));
     if (n == 0) return PQH_OK;
     if (context) {
-        const HistPlan hp = hist_plan(n, m, k);
+        const HistPlan hp = hist_plan(n, m, k, ctx->tune_hist_split);
         const int words = (k * k + 1) / 2;
         const int split = hp.split;
         const size_t lds = (size_t)(split == 1 ? words : (k / split) * k / 2) * 4;
@@ -1114,7 +1118,8 @@ static int histogram_impl(pqh_ctx_t* ctx, const void* d_codes, long long n, int 
         // 1024-thread workgroups; PQH_HIST_BLOCK=256: 256 threads with <= 32 VGPRs, which fit
         // beside the assignment grid (measured: histogram 0.19 vs 0.075 ms in the bench -- a
         // quarter of the loads in flight -- and the bench 2,119 vs 2,534 Mvec/s)
-        const char* hb = std::getenv("PQH_HIST_BLOCK");
+        const char* hb_env = std::getenv("PQH_HIST_BLOCK");
+        const int hb_v = ctx->tune_hist_block ? ctx->tune_hist_block : (hb_env ? std::atoi(hb_env) : 0);
         // the wave-contiguous form for u8 codes with m % 4 == 0 (aligned rows; PQH_HIST_IMPL=
         // thread keeps the per-thread runs of hist_ctx)
         static const int form_env = [] {   // 1: thread, 2: wave (any m % 4 == 0), 0: default
@@ -1125,7 +1130,7 @@ static int histogram_impl(pqh_ctx_t* ctx, const void* d_codes, long long n, int 
         const uintptr_t al = reinterpret_cast<uintptr_t>(d_codes);
         // (measured alone, tools/bench_hist.py: 0.027 vs 0.035 ms per 1M rows at m = 8, 0.052
         // vs 0.108 at m = 16; the Deep bench 1,300 vs 1,218 Mvec/s)
-        const bool slim = hb && std::atoi(hb) == 256;
+        const bool slim = hb_v == 256;
         // (part-major codes: always the wave form, which reads each part's run directly)
         const bool wave_form = ldc || (!thread_form && m % 4 == 0 && (al & (m == 8 ? 15u : 3u)) == 0);
         if (wave_form && slim) {

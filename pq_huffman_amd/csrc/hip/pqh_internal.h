@@ -48,6 +48,10 @@ struct pqh_ctx {
     unsigned sort_epoch = 0;
     unsigned long long sort_ticket_base = 0;
     int rerank_slot = 0;              // d_diag slot of the last assignment's re-rank count
+    // pqh_ctx_set_tuning (0: the library / environment default)
+    double tune_wgs_per_cu = 0.0;
+    int tune_hist_split = 0;
+    int tune_hist_block = 0;
     // the tiled encoder's scratch: one worst-case slot per tile (grow-only)
     void* enc_scr = nullptr;
     size_t enc_scr_bytes = 0;
