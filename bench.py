@@ -158,10 +158,14 @@ def parse():
     ap.add_argument("--sort-on", choices=["assign", "lanes"], default="lanes",
                     help="--sort: the sort (and then the histogram) of batch i on its table lane "
                          "after its assignment (default), or on the assignment stream")
-    ap.add_argument("--hist-on", choices=["assign", "lanes", "own"], default="assign",
+    ap.add_argument("--hist-on", choices=["auto", "assign", "lanes", "own"], default="auto",
                     help="stream of the context histogram: the assignment's, the batch's "
-                         "lane (before its code tables), or a stream of its own (a fifth "
-                         "stream: the process then asks HIP for 8 hardware queues)"),
+                         "lane (before its code tables; --hist-tune shapes it to fit beside the "
+                         "assignment grid), or a stream of its own (a fifth stream: the process "
+                         "then asks HIP for 8 hardware queues); auto: lanes below 16M rows per "
+                         "batch, else the assignment's (measured: 1M rows 3,118-3,127 vs "
+                         "3,000-3,009 Mvec/s at 200 steps, Deep 1,554-1,569 vs 1,530-1,535; "
+                         "125M rows 3,633 vs 3,674)"),
     ap.add_argument("--assign-event-every", type=int, default=4,
                     help="record the assignment's start/end HIP events (the roofline's kernel "
                          "time) on every N-th timed step (0: none -- the roofline then uses the "
@@ -360,6 +364,8 @@ def pcie_ms(torch, x, codes, stream_bytes):
 
 def main():
     args = parse()
+    if args.hist_on == "auto":
+        args.hist_on = "lanes" if args.vectors < 16_000_000 else "assign"
     if int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.hist_on == "own":
         # 4 library/torch streams + RCCL's own: give each a hardware queue (HIP reads this at
         # initialisation; measured neutral at one rank, 2,150 vs 2,153 Mvec/s)
@@ -657,9 +663,12 @@ def main():
                 codec.sort_rows(cF, codes[s], sort_tmp)
                 done(e, sF)
             halo[s] = None
+            # (the run's last batch: its histogram on this stream, which the drain leaves
+            # idle, instead of on the lane in front of its tables)
+            lane_hist = hist_on_lane and (sort_on_lane or i != state["nsteps"] - 1)
             if hctx is not None:
                 ev_asg[s].record(sF)
-            elif not hist_on_lane:   # (the shard-boundary pair is added on the lane)
+            elif not lane_hist:   # (the shard-boundary pair is added on the lane)
                 hist(s, cF, sF)
                 ev_hist[s].record(sF)
             else:
@@ -683,7 +692,7 @@ def main():
                 e = rec("sort", sL)
                 codec.sort_rows(c, codes[s], sort_tmps[j])
                 done(e, sL)
-            if hist_on_lane:
+            if lane_hist:
                 hist(s, c, sL)
             elif halo[s] is not None:
                 cs = counts[s]
