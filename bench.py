@@ -212,6 +212,11 @@ def parse():
     ap.add_argument("--dump", default="",
                     help="write the last batch's stitched stream and all ranks' codes to this "
                          ".npz on rank 0 (parity tests)")
+    ap.add_argument("--diag-skip", default="",
+                    help="(diagnostic, never a result: the JSON line is marked) comma list of "
+                         "stages -- trees, luts, hist, encode, decode -- issued only for the first "
+                         "batches, so a run shows what each stage costs the schedule (every batch "
+                         "holds the same data, so later batches reuse valid tables / streams)")
     ap.add_argument("--table-cus", type=int, default=0,
                     help="limit each lane stream to this many CUs (0: no CU mask)")
     return ap.parse_args()
@@ -640,8 +645,14 @@ def main():
             ev_tab[s].record(sL)
         used[s] = True
 
+    diag = set(x for x in args.diag_skip.replace("+", ",").split(",") if x)
+
+    def skip(stage):   # (--diag-skip: the stage after the first batches)
+        return stage in diag and state.get("issued", 0) > 2 * slots
+
     def front(i):
         """batch i: assignment + histogram on A, then its code tables on its lane"""
+        state["issued"] = state.get("issued", 0) + 1
         if lib_shard:
             return front_lib(i)
         s, j = i % slots, lane_of(i)
@@ -668,6 +679,8 @@ def main():
             lane_hist = hist_on_lane and (sort_on_lane or i != state["nsteps"] - 1)
             if hctx is not None:
                 ev_asg[s].record(sF)
+            elif skip("hist"):
+                ev_hist[s].record(sF)
             elif not lane_hist:   # (the shard-boundary pair is added on the lane)
                 hist(s, cF, sF)
                 ev_hist[s].record(sF)
@@ -681,7 +694,8 @@ def main():
                 ev_hist[s].record(sH)
         with torch.cuda.stream(sL):
             sL.wait_event(ev_hist[s])
-            hist_reduce(s, c)
+            if not skip("hist"):
+                hist_reduce(s, c)
             # the one-row halo all-gather on the lane too, so the assignment stream never
             # waits for RCCL; the pair (previous shard's last row, first row) is one more
             # count per part, exactly what pqh_histogram's prev_row adds
@@ -692,7 +706,7 @@ def main():
                 e = rec("sort", sL)
                 codec.sort_rows(c, codes[s], sort_tmps[j])
                 done(e, sL)
-            if lane_hist:
+            if lane_hist and not skip("hist"):
                 hist(s, c, sL)
             elif halo[s] is not None:
                 cs = counts[s]
@@ -738,12 +752,14 @@ def main():
                 # trees, then the decode tables: with the group builder the encode tables
                 # are complete after the trees (encode_ready), so the encode stream waits
                 # for ev_trees only and runs beside the decode-table build
-                tabs[ti].build_trees(counts[s], c, trees=tr)
+                if not skip("trees"):
+                    tabs[ti].build_trees(counts[s], c, trees=tr)
                 # (the run's last batch always: its encode is on the drain's critical path)
                 early[s] = (args.encode_after == "trees" or i == state["nsteps"] - 1) and \
                     tabs[ti].encode_ready()
                 ev_trees[s].record(sL)
-                tabs[ti].build_luts(c)
+                if not skip("luts"):
+                    tabs[ti].build_luts(c)
                 done(e, sL)
                 ev_tab[s].record(sL)
         if lut_a and i >= dl:
@@ -792,6 +808,8 @@ def main():
                 acc["collectives"] += time.perf_counter() - tc if state["timed"] else 0.0
                 codec.encode_write_at(c, tj, codes[s], out[j], goff, raw_first, halo[s],
                                       args.chunk, coff[j], cprev[j], total=tot_dev[j])
+            elif skip("encode"):
+                pass
             elif pm:   # the row encoder gathering each row from the part runs
                 codec.encode_write_parts(c, tj, codes[s], n, out[j], 0, raw_first, halo[s],
                                          args.chunk, coff[j], cprev[j], total=tot_dev[j])
@@ -805,7 +823,8 @@ def main():
             if elanes is not lanes and early[s] and not lib_shard:
                 sL.wait_event(ev_tab[s])   # the decode tables
             e = rec("decode", sL)
-            codec.decode(c, tj, enc, out=dec[j])
+            if not skip("decode"):
+                codec.decode(c, tj, enc, out=dec[j])
             done(e, sL)
             ev_dec[jt].record(sL)
         state["last"] = (s, j)
@@ -980,8 +999,10 @@ def main():
             "k4096": "synthetic SIFT-like (integer-valued fp32 in [0,255], Gaussian mixture, "
                      "Zipf(1.1) weights), generated on device"}[args.config]
         res = {
-            "metric": METRIC if args.config == "sift" else
-            f"Mvec/s encode+decode round-trip, {d}-d fp32 M={m} K={k}; % HBM-read roofline",
+            "metric": (f"DIAGNOSTIC (stages skipped: {args.diag_skip}; not a result) "
+                       if args.diag_skip else "") +
+            (METRIC if args.config == "sift" else
+             f"Mvec/s encode+decode round-trip, {d}-d fp32 M={m} K={k}; % HBM-read roofline"),
             "value": round(world * n * args.steps / elapsed / 1e6, 2),
             "unit": "Mvec/s",
             "n_gpus": world,

@@ -498,33 +498,37 @@ enc_size(const CodeT* __restrict__ codes, long long n, int m_total, int k, int c
     }
 }
 
-// exclusive scan of nb block totals by one workgroup (nb ~ n/256)
-__global__ void __launch_bounds__(1024)
+// Exclusive scan of nb block totals by one 256-thread workgroup (nb ~ n/256: 3,907 tiles at
+// 1M rows, 488K at 125M).  Thread t owns the contiguous run [t*per, (t+1)*per): it sums its
+// run, the 256 run sums are scanned once, then it writes its run's offsets.  Two passes over
+// the totals and no per-element barriers; four waves fit beside the assignment grid, where a
+// 1,024-thread workgroup waited for a whole CU's wave slots.
+constexpr int kScanThreads = 256;
+__global__ void __launch_bounds__(kScanThreads)
 scan_blocks(const uint32_t* __restrict__ block_bits, long long nb,
             unsigned long long* __restrict__ block_off, unsigned long long* __restrict__ total) {
-    __shared__ unsigned long long wsum[16];
-    __shared__ unsigned long long carry;
-    if (threadIdx.x == 0) carry = 0;
-    lds_barrier();
+    __shared__ unsigned long long wsum[kScanThreads / 64];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (long long base = 0; base < nb; base += blockDim.x) {
-        const long long i = base + threadIdx.x;
-        unsigned long long x = i < nb ? block_bits[i] : 0;
-        unsigned long long incl = x;
-        for (int off = 1; off < 64; off <<= 1) {
-            unsigned long long y = __shfl_up(incl, off);
-            if (lane >= off) incl += y;
-        }
-        if (lane == 63) wsum[wid] = incl;
-        lds_barrier();
-        unsigned long long before = carry;
-        for (int w = 0; w < wid; ++w) before += wsum[w];
-        if (i < nb) block_off[i] = before + incl - x;
-        lds_barrier();
-        if (threadIdx.x == blockDim.x - 1) carry = before + incl;
-        lds_barrier();
+    const long long per = (nb + kScanThreads - 1) / kScanThreads;
+    const long long lo = min(nb, per * threadIdx.x), hi = min(nb, lo + per);
+    unsigned long long run = 0;
+#pragma unroll 8
+    for (long long i = lo; i < hi; ++i) run += block_bits[i];
+    unsigned long long incl = run;
+    for (int off = 1; off < 64; off <<= 1) {
+        const unsigned long long y = __shfl_up(incl, off);
+        if (lane >= off) incl += y;
     }
-    if (threadIdx.x == 0) *total = carry;
+    if (lane == 63) wsum[wid] = incl;
+    lds_barrier();
+    unsigned long long acc = incl - run;
+    for (int w = 0; w < wid; ++w) acc += wsum[w];
+    if (threadIdx.x == kScanThreads - 1) *total = acc + run;
+#pragma unroll 8
+    for (long long i = lo; i < hi; ++i) {
+        block_off[i] = acc;
+        acc += block_bits[i];
+    }
 }
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
@@ -1274,7 +1278,7 @@ static int run_size(pqh_ctx* ctx, const pqh_tables* t, const void* d_codes, long
                            raw_first, static_cast<const uint16_t*>(d_prev_row), d_rawf, t->d_enc,
                            t->items, bb, nullptr);
     PQH_LAUNCH_CHECK(ctx);
-    hipLaunchKernelGGL(scan_blocks, dim3(1), dim3(1024), 0, ctx->stream, bb, nb, bo, d_total);
+    hipLaunchKernelGGL(scan_blocks, dim3(1), dim3(kScanThreads), 0, ctx->stream, bb, nb, bo, d_total);
     PQH_LAUNCH_CHECK(ctx);
     return PQH_OK;
 }
@@ -1378,7 +1382,7 @@ static int encode_write_impl(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* 
         }
 #undef PQH_ENC_T
         PQH_LAUNCH_CHECK(ctx);
-        hipLaunchKernelGGL(scan_blocks, dim3(1), dim3(1024), 0, ctx->stream, tile_bits, nb,
+        hipLaunchKernelGGL(scan_blocks, dim3(1), dim3(kScanThreads), 0, ctx->stream, tile_bits, nb,
                            tile_off, total);
         PQH_LAUNCH_CHECK(ctx);
         const long long chunks = chunk_vectors > 0 ? (n + chunk_vectors - 1) / chunk_vectors : 0;
