@@ -1050,8 +1050,10 @@ def main():
                          # HBM read roofline); `measured_limiter`: what the PMC counters show
                          # limits the kernel
                          "bound": "hbm",
-                         "measured_limiter": "VALU issue (the top-2 key reduction, ~4 cycles "
-                                             "per wave64 instruction) -- not HBM",
+                         "measured_limiter": "dependency waits: each tile's VALU top-2 "
+                                             "reduction on its MFMA results at 2.5 waves per "
+                                             "SIMD (VALU + MFMA issue fill ~37 % of the SIMD "
+                                             "time) -- not HBM",
                          "mfma_tflops_algorithmic": round(tf, 1),
                          # of the dense bf16 peak (~2.5 PF/s); each fp32 product costs two or
                          # three bf16 MFMA passes (the hi/lo split), so issued MFMA work is 2-3x
