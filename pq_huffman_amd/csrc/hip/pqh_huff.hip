@@ -531,6 +531,100 @@ scan_blocks(const uint32_t* __restrict__ block_bits, long long nb,
     }
 }
 
+// Large inputs (more than kScanOneWg counts: past 4.2M rows of 256-row tiles) scan in two
+// launches of one workgroup per segment of kScanSeg counts, all loads coalesced:
+// scan_seg_sums writes each segment's sum; scan_seg_write adds up the sums before its
+// segment (at most a few thousand) and scans its own segment, 16 consecutive counts per
+// thread.  (One workgroup at 125M rows -- 488K counts, 1,907 per thread -- took 0.9 ms.)
+constexpr int kScanSeg = 16 * kScanThreads;
+constexpr long long kScanOneWg = 16384;
+__global__ void __launch_bounds__(kScanThreads)
+scan_seg_sums(const uint32_t* __restrict__ bits, long long nb,
+              unsigned long long* __restrict__ seg_sum) {
+    __shared__ unsigned long long wsum[kScanThreads / 64];
+    const long long base = (long long)blockIdx.x * kScanSeg;
+    unsigned long long v = 0;
+#pragma unroll 4
+    for (int i = threadIdx.x; i < kScanSeg; i += kScanThreads) {
+        const long long j = base + i;
+        v += j < nb ? bits[j] : 0u;
+    }
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = v;
+    lds_barrier();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int w = 0; w < kScanThreads / 64; ++w) t += wsum[w];
+        seg_sum[blockIdx.x] = t;
+    }
+}
+
+__global__ void __launch_bounds__(kScanThreads)
+scan_seg_write(const uint32_t* __restrict__ bits, long long nb,
+               const unsigned long long* __restrict__ seg_sum,
+               unsigned long long* __restrict__ block_off, unsigned long long* __restrict__ total) {
+    __shared__ unsigned long long wsum[kScanThreads / 64];
+    __shared__ unsigned long long s_base;
+    const int seg = (int)blockIdx.x;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    unsigned long long b = 0;   // the segments before this one
+    for (int i = threadIdx.x; i < seg; i += kScanThreads) b += seg_sum[i];
+    for (int o = 32; o >= 1; o >>= 1) b += __shfl_xor(b, o);
+    if (lane == 0) wsum[wid] = b;
+    lds_barrier();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int w = 0; w < kScanThreads / 64; ++w) t += wsum[w];
+        s_base = t;
+    }
+    lds_barrier();
+    const long long j0 = (long long)seg * kScanSeg + 16ll * threadIdx.x;
+    uint32_t v[16];
+    if (j0 + 16 <= nb) {   // (16-count runs are 64-byte aligned)
+        const uint4* p = reinterpret_cast<const uint4*>(bits + j0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint4 x = p[q];
+            v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = j0 + i < nb ? bits[j0 + i] : 0u;
+    }
+    unsigned long long run = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) run += v[i];
+    unsigned long long incl = run;
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[wid] = incl;
+    lds_barrier();
+    unsigned long long acc = s_base + incl - run;
+    for (int w = 0; w < wid; ++w) acc += wsum[w];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        if (j0 + i < nb) block_off[j0 + i] = acc;
+        acc += v[i];
+    }
+    if (seg == (int)gridDim.x - 1 && threadIdx.x == kScanThreads - 1) *total = acc;
+}
+
+// the exclusive scan of nb counts and their total; seg: ceil(nb / kScanSeg) u64 of scratch
+static void launch_scan(hipStream_t st, const uint32_t* bits, long long nb,
+                        unsigned long long* off, unsigned long long* total,
+                        unsigned long long* seg) {
+    if (nb <= kScanOneWg) {
+        hipLaunchKernelGGL(scan_blocks, dim3(1), dim3(kScanThreads), 0, st, bits, nb, off, total);
+        return;
+    }
+    const unsigned nseg = (unsigned)((nb + kScanSeg - 1) / kScanSeg);
+    hipLaunchKernelGGL(scan_seg_sums, dim3(nseg), dim3(kScanThreads), 0, st, bits, nb, seg);
+    hipLaunchKernelGGL(scan_seg_write, dim3(nseg), dim3(kScanThreads), 0, st, bits, nb, seg, off,
+                       total);
+}
+
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
 // Inclusive wave64 scan of u32 with DPP row shifts and row broadcasts (no LDS permutes, no
@@ -1248,11 +1342,12 @@ int pqh_histogram_partial_parts(pqh_ctx_t* ctx, const void* d_codes, long long l
                           static_cast<uint32_t*>(d_partials), ld_codes);
 }
 
-// workspace layout for encode: [block_bits u32 nb][pad][block_off u64 nb]
+// workspace layout for encode: [block_bits u32 nb][pad][block_off u64 nb][scan segments]
+static size_t scan_seg_bytes(long long nb) { return (size_t)((nb + kScanSeg - 1) / kScanSeg) * 8; }
 static int enc_ws(pqh_ctx* ctx, long long n, uint32_t** bb, unsigned long long** bo) {
     const long long nb = (n + kEncBlock - 1) / kEncBlock;
     const size_t a = ((size_t)nb * 4 + 255) & ~(size_t)255;
-    int rc = pqh_ensure_ws(ctx, a + (size_t)nb * 8 + 256);
+    int rc = pqh_ensure_ws(ctx, a + (size_t)nb * 8 + scan_seg_bytes(nb) + 256);
     if (rc) return rc;
     *bb = static_cast<uint32_t*>(ctx->ws);
     *bo = reinterpret_cast<unsigned long long*>(static_cast<char*>(ctx->ws) + a);
@@ -1278,7 +1373,7 @@ static int run_size(pqh_ctx* ctx, const pqh_tables* t, const void* d_codes, long
                            raw_first, static_cast<const uint16_t*>(d_prev_row), d_rawf, t->d_enc,
                            t->items, bb, nullptr);
     PQH_LAUNCH_CHECK(ctx);
-    hipLaunchKernelGGL(scan_blocks, dim3(1), dim3(kScanThreads), 0, ctx->stream, bb, nb, bo, d_total);
+    launch_scan(ctx->stream, bb, nb, bo, d_total, bo + nb);
     PQH_LAUNCH_CHECK(ctx);
     return PQH_OK;
 }
@@ -1345,7 +1440,7 @@ static int encode_write_impl(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* 
         int rc2 = pqh_ensure_enc_scratch(ctx, ((size_t)nb * slot + 64) * 4);
         if (rc2) return rc2;
         const size_t a = ((size_t)nb * 4 + 255) & ~(size_t)255;
-        rc2 = pqh_ensure_ws(ctx, a + (size_t)nb * 8 + 256);
+        rc2 = pqh_ensure_ws(ctx, a + (size_t)nb * 8 + scan_seg_bytes(nb) + 256);
         if (rc2) return rc2;
         uint32_t* tile_bits = static_cast<uint32_t*>(ctx->ws);
         unsigned long long* tile_off =
@@ -1382,8 +1477,7 @@ static int encode_write_impl(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* 
         }
 #undef PQH_ENC_T
         PQH_LAUNCH_CHECK(ctx);
-        hipLaunchKernelGGL(scan_blocks, dim3(1), dim3(kScanThreads), 0, ctx->stream, tile_bits, nb,
-                           tile_off, total);
+        launch_scan(ctx->stream, tile_bits, nb, tile_off, total, tile_off + nb);
         PQH_LAUNCH_CHECK(ctx);
         const long long chunks = chunk_vectors > 0 ? (n + chunk_vectors - 1) / chunk_vectors : 0;
         hipLaunchKernelGGL(enc_place, dim3((unsigned)nb), dim3(256), 0, ctx->stream, scr, slot,

@@ -295,3 +295,45 @@ def test_configs2_shard_125m_rows(gpu, oracle):
     assert torch.equal(enc2.stream[:(enc2.bits + 7) // 8], row_stream)
     assert torch.equal(enc2.chunk_offsets, row_coff)
     assert torch.equal(dec2, codes)
+
+
+def test_encode_segmented_scan_5m_rows(gpu, oracle):
+    """More than 16,384 encoder tiles (5M rows): the tiles' bit offsets come from the
+    two-launch segmented scan (scan_seg_sums + scan_seg_write) instead of the one-workgroup
+    scan.  For the row encoder and the part-major encoder alike: the bit count, every stream
+    byte and the chunk index equal the oracle's (huffman_encoder.c:207-238), and the decode is
+    exact."""
+    torch, codec, ctx = gpu
+    n, m, k, chunk = 5_000_003, 8, 256, 4
+    rng = np.random.default_rng(91)
+    base = np.minimum(rng.geometric(0.03, size=(n, m)) - 1, k - 1)
+    codes_h = np.empty((n, m), np.uint8)
+    for j in range(m):
+        codes_h[:, j] = rng.permutation(k)[base[:, j]].astype(np.uint8)
+    cd = torch.from_numpy(codes_h).cuda()
+    counts = codec.histogram(ctx, cd, k, True)
+    tabs = codec.Tables(ctx, m, k, True).build(counts)
+    ocb = oracle.build_codebooks(codes_h, k, True)
+    assert tabs.codebooks().file_bytes() == oracle.codebooks_file(ocb)
+    stream, bits = oracle.encode(codes_h, ocb)
+    enc = codec.encode(ctx, tabs, cd, chunk_vectors=chunk)
+    assert enc.bits == bits
+    assert enc.stream[:len(stream)].cpu().numpy().tobytes() == stream
+    _check_chunk_index(torch, oracle, codes_h, ocb, enc, chunk)
+    # the part-major encoder on the same rows
+    ld = (n + 127) // 128 * 128
+    parts = torch.empty((m, ld), dtype=torch.uint8, device=cd.device)
+    parts[:, :n] = cd.t()
+    out = torch.zeros_like(enc.stream)
+    coff = torch.empty_like(enc.chunk_offsets)
+    cprev = torch.empty_like(enc.chunk_prev)
+    tot = torch.zeros(1, dtype=torch.int64, device=cd.device)
+    codec.encode_write_parts(ctx, tabs, parts[:, :n], n, out, 0, 1, None, chunk, coff, cprev,
+                             total=tot)
+    codec.encode_status(ctx)
+    assert int(tot.item()) == bits
+    assert out[:len(stream)].cpu().numpy().tobytes() == stream
+    assert torch.equal(coff, enc.chunk_offsets) and torch.equal(cprev, enc.chunk_prev)
+    dec = codec.decode(ctx, tabs, enc)
+    codec.decode_status(ctx)
+    assert torch.equal(dec, cd)
