@@ -64,10 +64,12 @@ def pmc_traffic(kernel, tag):
     import re
     files = []
     for f in glob.glob(os.path.join(ROOT, "profiles", f"r*_{tag}_pmc_summary.json")):
-        mt = re.match(r"r(\d+)_" + re.escape(tag) + r"_pmc_summary\.json$", os.path.basename(f))
+        # r<N>_<tag> or r<N>_final_<tag> (a round's last profile of the configuration)
+        mt = re.match(r"r(\d+)_(final_)?" + re.escape(tag) + r"_pmc_summary\.json$",
+                      os.path.basename(f))
         if mt:
-            files.append((int(mt.group(1)), f))
-    for _, f in sorted(files, reverse=True):
+            files.append((int(mt.group(1)), 1 if mt.group(2) else 0, f))
+    for *_, f in sorted(files, reverse=True):
         try:
             e = json.load(open(f))["kernels"].get(kernel)
         except (OSError, ValueError, KeyError):
