@@ -1331,9 +1331,13 @@ huff_trees_par(const uint32_t* __restrict__ counts, int k, long long trees,
         err = err2;
     }
     using Key = ParHeap::Key;
+    // 104 KB at K = 4,096, so a build fits on a CU beside the K = 4,096 assignment grid's two
+    // workgroups (~40 KB): the heap and the node codes share one region -- the heap lives
+    // during the merges, the codes after them -- and the leaf counts are parked in it before
+    // the pushes (leaf j's count sits at slot j, read before push j can write there)
     extern __shared__ __attribute__((aligned(16))) char lds[];
-    Key* heap = reinterpret_cast<Key*>(lds);                              // [KMAX + 1]
-    unsigned long long* ncode = heap + (KMAX + 1);                       // [2 KMAX]
+    Key* heap = reinterpret_cast<Key*>(lds);                              // [KMAX + 1] |
+    unsigned long long* ncode = heap;                                    // [2 KMAX]
     uint32_t* kid = reinterpret_cast<uint32_t*>(ncode + 2 * KMAX);       // [KMAX]
     uint16_t* lsym = reinterpret_cast<uint16_t*>(kid + KMAX);            // [KMAX]
     uint16_t* par = lsym + KMAX;                                         // [2 KMAX]
@@ -1343,7 +1347,6 @@ huff_trees_par(const uint32_t* __restrict__ counts, int k, long long trees,
     unsigned long long* out = enc + tree * k;
     const bool stamp = tree == 0 && lane == 0;
     if (stamp) g_tree_stamps[0] = __builtin_amdgcn_s_memtime();
-    for (int s = lane; s <= KMAX; s += 64) heap[s] = ParHeap::kMaxKey;
     // nonzero symbols in symbol order (their counts parked in ncode); no code for the rest
     int nz = 0;
     for (int s0 = 0; s0 < k; s0 += 64) {
@@ -1366,6 +1369,11 @@ huff_trees_par(const uint32_t* __restrict__ counts, int k, long long trees,
     constexpr Key kNode = ParHeap::kTie - 1;
     if (stamp) g_tree_stamps[1] = __builtin_amdgcn_s_memtime();
     for (int j = 0; j < nz; ++j) hp.push((ncode[j] << 16) | (Key)j, lane);
+    // the slots past the heap become sentinels (they held the parked counts and older data)
+    __builtin_amdgcn_wave_barrier();
+    for (int q = nz + lane; q <= KMAX; q += 64) heap[q] = ParHeap::kMaxKey;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
     if (stamp) g_tree_stamps[2] = __builtin_amdgcn_s_memtime();
     int next = nz;
     if (hp.size == 1) {   // lone symbol: code "0" (huffman_encode.c:168-177)
@@ -2278,7 +2286,7 @@ static int build_trees(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts
         if (rc) return rc;
     } else if (!(impl && std::strcmp(impl, "lane") == 0)) {
         // K > 256: one wavefront per tree, sifts read in parallel (huff_trees_par)
-        const size_t lds = (size_t)(4096 + 1) * 8 + (size_t)4096 * (16 + 4 + 2 + 4);
+        const size_t lds = (size_t)2 * 4096 * 8 + (size_t)4096 * (4 + 2 + 4);   // 104 KB
         PQH_HIP(ctx, hipFuncSetAttribute((const void*)huff_trees_par<4096>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         const long long all = trees + (t2 ? t2->tables : 0);
