@@ -14,7 +14,7 @@
 // byte), so the first pass reads the codes and the last writes the sorted rows in place -- no
 // index permutation and no gather.  One kernel counts the digits
 // of the first pass's byte (`sort_digits`); each pass (`sort_pass`) is one kernel over
-// 8,192-row tiles taken in ticket order: a wave ranks its rows among equal digits with 8
+// 4,096-row tiles taken in ticket order: a wave ranks its rows among equal digits with 8
 // ballots per 64 rows (stable: rows are ranked in index order), counts the next pass's
 // digits, chains the workgroup's per-digit counts across tiles by a decoupled look-back (one
 // lane per digit, 16 tiles per round), and scatters every row to digit base + earlier tiles
@@ -82,8 +82,8 @@ gather_rows(const uint8_t* __restrict__ src, long long n, int m, const uint32_t*
 #ifndef PQH_SORT_THREADS
 #define PQH_SORT_THREADS 512
 #endif
-#ifndef PQH_SORT_ITEMS
-#define PQH_SORT_ITEMS 16
+#ifndef PQH_SORT_ITEMS   // (8: 100 VGPRs, so a pass's waves fit beside two assignment waves;
+#define PQH_SORT_ITEMS 8   //  16: 141 VGPRs -- the sort stage 0.40 vs 0.36 ms in the bench)
 #endif
 #ifndef PQH_SORT_WIN
 #define PQH_SORT_WIN 16
@@ -91,7 +91,7 @@ gather_rows(const uint8_t* __restrict__ src, long long n, int m, const uint32_t*
 constexpr int kSortThreads = PQH_SORT_THREADS;
 constexpr int kSortWaves = kSortThreads / 64;
 constexpr int kSortItems = PQH_SORT_ITEMS;                 // rows per lane
-constexpr int kSortTile = kSortThreads * kSortItems;       // rows per workgroup (8,192)
+constexpr int kSortTile = kSortThreads * kSortItems;       // rows per workgroup (4,096)
 constexpr int kLookWin = PQH_SORT_WIN;                     // tiles read per look-back round
 constexpr unsigned long long kStAgg = 1ull << 46, kStPre = 1ull << 47;
 constexpr unsigned long long kStVal = (1ull << 46) - 1;
