@@ -43,7 +43,14 @@ def main():
         L, out = stamps()
         L.pqh_debug_tree_stamps(ctx.ptr, out)
         st = list(out)
+        e2, e3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e2.record()
+        for _ in range(reps):   # the trees alone (build - trees = the decode tables)
+            tabs.build_trees(counts)
+        e3.record()
+        torch.cuda.synchronize()
         print(f"ctx={mode} build_ms={e0.elapsed_time(e1) / reps:.4f} "
+              f"trees_ms={e2.elapsed_time(e3) / reps:.4f} "
               f"tree0 cycles: scan={st[1]-st[0]} leaves={st[2]-st[1]} merges={st[3]-st[2]} "
               f"codes={st[4]-st[3]} nz={st[5]} nodes={st[6]}", flush=True)
 
