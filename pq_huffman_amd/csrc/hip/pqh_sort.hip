@@ -21,8 +21,11 @@
 // + earlier waves + its rank.  Measured (1M x 8, alone): 0.25 ms, as the rocPRIM path
 // (PQH_SORT_IMPL=rocprim); a pass is ~29 us, of which the look-back ~11 and the scatter ~8
 // (PQH_SORT_DIAG timing runs).
-// Other M (> 16): LSD over 8-byte key chunks, each a stable rocPRIM radix sort of (key, row
-// index) pairs, then a gather of the rows.
+// Other M (1, > 16): the same passes over (key chunk, row index) pairs -- LSD over 8-byte
+// chunks of the key, least significant chunk first: `sort_chunk_keys` gathers each row's chunk
+// (cleared past the row's first 0 byte) in the current order and counts its last byte, then
+// one pass per byte of the chunk carries the pair -- and a final gather of the rows.
+// (PQH_SORT_IMPL=rocprim: the same chunk order with rocPRIM pair sorts; a cross-check.)
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
@@ -190,6 +193,71 @@ sort_unpack(const unsigned long long* __restrict__ rows, long long n, int m, uin
     for (int q = 0; q < m; ++q) codes[v * m + q] = (uint8_t)(rows[v * W + (q >> 3)] >> (8 * (q & 7)));
 }
 
+// (pair passes) chunk c of row idx[v] as a little-endian word -- key byte q of the chunk at
+// bits 8q, cleared past the row's first 0 byte -- and the digit counts of the chunk's last
+// byte nb - 1 (counts[256], zeroed by the caller).  The first chunk (idx null) runs in row
+// order: it writes the identity into idx_out and each row's first-0 position into zpos, which
+// the later chunks' gathers use instead of rescanning the row.  W8: m % 8 == 0 and the codes
+// 8-byte aligned (the chunk is one u64 load).
+template <bool W8>
+__global__ void __launch_bounds__(256)
+sort_chunk_keys(const uint8_t* __restrict__ codes, long long n, int m, int c, int nb,
+                const uint32_t* __restrict__ idx, uint32_t* __restrict__ idx_out,
+                uint16_t* __restrict__ zpos, unsigned long long* __restrict__ keys,
+                uint32_t* __restrict__ counts) {
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long key = 0;
+    if (v < n) {
+        const long long r = idx ? (long long)idx[v] : v;
+        const uint8_t* row = codes + r * m;
+        int z;   // the row's first 0 byte (m if none)
+        if (!idx) {
+            idx_out[v] = (uint32_t)v;
+            z = m;
+            if (W8) {
+                for (int w = 0; w < m / 8; ++w) {
+                    const unsigned long long q = reinterpret_cast<const unsigned long long*>(row)[w];
+                    const unsigned long long zb = (q - 0x0101010101010101ull) & ~q & 0x8080808080808080ull;
+                    if (zb) {
+                        z = 8 * w + ((__ffsll((long long)zb) - 1) >> 3);
+                        break;
+                    }
+                }
+            } else {
+                for (int j = 0; j < m; ++j)
+                    if (row[j] == 0) {
+                        z = j;
+                        break;
+                    }
+            }
+            zpos[v] = (uint16_t)z;
+        } else {
+            z = zpos[r];
+        }
+        if (W8) {
+            key = reinterpret_cast<const unsigned long long*>(row)[c];
+        } else {
+            key = 0;
+            for (int q = 0; q < nb; ++q) key |= (unsigned long long)row[8 * c + q] << (8 * q);
+        }
+        // bytes 8c + q > z cleared
+        const int keep = z - 8 * c + 1;   // bytes of the chunk kept
+        if (keep <= 0) key = 0;
+        else if (keep < 8) key &= (1ull << (8 * keep)) - 1;
+        keys[v] = key;
+    }
+    // one LDS add per distinct digit of the wave (skewed codes share digits: a plain atomic
+    // per lane serialises on the popular bins)
+    const unsigned d = (unsigned)(key >> (8 * (nb - 1))) & 0xFFu;
+    const unsigned long long match = match_digit(d, v < n);
+    if (v < n && lanes_below(match) == 0) atomicAdd(&h[d], (uint32_t)__popcll(match));
+    __syncthreads();
+    if (h[threadIdx.x]) atomicAdd(counts + threadIdx.x, h[threadIdx.x]);
+}
+
 __device__ __forceinline__ void st_store(unsigned long long* p, unsigned long long v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -200,13 +268,17 @@ __device__ __forceinline__ unsigned long long st_load(const unsigned long long* 
 // one stable counting pass by byte position j (digit counts of j in `counts`, the next
 // pass's byte j - 1 counted into `counts_next`).  Elements are rows of W u64 words.  FIRST:
 // rows come from the codes; LAST: the rows go to the codes (never both in one launch: m >= 2)
-template <bool FIRST, bool LAST, int W>
+// IDX: elements are (key chunk, row index) pairs (W = 1, never FIRST): the chunk from rin /
+// iin to rout / iout
+template <bool FIRST, bool LAST, int W, bool IDX = false>
 __global__ void __launch_bounds__(kSortThreads)
 sort_pass(const uint8_t* __restrict__ codes_in, uint8_t* __restrict__ codes_out, long long n, int m,
           int j, const unsigned long long* __restrict__ rin, unsigned long long* __restrict__ rout,
           const uint32_t* __restrict__ counts, uint32_t* __restrict__ counts_next,
           unsigned long long* __restrict__ state, unsigned long long* __restrict__ ticket,
-          unsigned long long ticket_base, unsigned epoch, int diag) {
+          unsigned long long ticket_base, unsigned epoch, int diag,
+          const uint32_t* __restrict__ iin = nullptr, uint32_t* __restrict__ iout = nullptr) {
+    static_assert(!IDX || (W == 1 && !FIRST), "pairs carry one key word");
     __shared__ uint32_t wcnt[kSortWaves][256];   // per-wave digit counters, then bases
     __shared__ uint32_t hnext[LAST ? 1 : 2][256];   // the next pass's digit counts
     __shared__ uint32_t wsum[4];
@@ -221,6 +293,7 @@ sort_pass(const uint8_t* __restrict__ codes_in, uint8_t* __restrict__ codes_out,
     const long long base = tile * kSortTile + (long long)wave * 64 * kSortItems;
     unsigned long long row[kSortItems][W];
     uint32_t rank[kSortItems];
+    uint32_t id[IDX ? kSortItems : 1];   // (IDX) the pair's row index
     uint8_t dig[kSortItems];   // this pass's key byte of each row
     // every load first (the ranking below needs each key; issuing them all up front keeps
     // the tile's reads in flight together)
@@ -238,6 +311,7 @@ sort_pass(const uint8_t* __restrict__ codes_in, uint8_t* __restrict__ codes_out,
                 row[it][W - 1] = (unsigned long long)q.z | ((unsigned long long)q.w << 32);
             } else {
                 row[it][0] = rin[v];
+                if constexpr (IDX) id[it] = iin[v];
             }
         }
     }
@@ -336,8 +410,9 @@ sort_pass(const uint8_t* __restrict__ codes_in, uint8_t* __restrict__ codes_out,
         if (diag) dst = dst < n ? dst : n - 1;   // (diagnostic runs: bases are wrong, stay in range)
         // (the last pass writes 8- and 16-byte rows straight into the codes; other m go
         // through sort_unpack)
-        unsigned long long* dstp = LAST && m == 8 * W ? reinterpret_cast<unsigned long long*>(codes_out)
-                                                      : rout;
+        unsigned long long* dstp = !IDX && LAST && m == 8 * W
+                                       ? reinterpret_cast<unsigned long long*>(codes_out) : rout;
+        if constexpr (IDX) iout[dst] = id[it];
         if (W == 2) {
             reinterpret_cast<uint4*>(dstp)[dst] =
                 make_uint4((uint32_t)row[it][0], (uint32_t)(row[it][0] >> 32),
@@ -348,9 +423,8 @@ sort_pass(const uint8_t* __restrict__ codes_in, uint8_t* __restrict__ codes_out,
     }
 }
 
-template <int W>
-int sort_rows_radix(pqh_ctx_t* ctx, uint8_t* codes, long long n, int m) {
-    const long long tiles = (n + kSortTile - 1) / kSortTile;
+// the look-back's per-tile state for `tiles` tiles (grown on demand; tags are epochs)
+int sort_state_for(pqh_ctx_t* ctx, long long tiles) {
     if (tiles > ctx->sort_cap) {
         PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));   // no launch may still use it
         if (ctx->sort_state) (void)hipFree(ctx->sort_state);
@@ -367,9 +441,34 @@ int sort_rows_radix(pqh_ctx_t* ctx, uint8_t* codes, long long n, int m) {
         ctx->sort_epoch = 0;
         ctx->sort_ticket_base = 0;
     }
+    return PQH_OK;
+}
+
+// the next pass's epoch (wrap: clear the tags)
+int sort_next_epoch(pqh_ctx_t* ctx) {
+    if (++ctx->sort_epoch >= 0xFFFF) {
+        PQH_HIP(ctx, hipMemsetAsync(ctx->sort_state, 0, (size_t)ctx->sort_cap * 256 * 8, ctx->stream));
+        ctx->sort_epoch = 1;
+    }
+    return PQH_OK;
+}
+
+int sort_diag() {   // PQH_SORT_DIAG (timing diagnostics only: wrong results)
+    static const int diag = [] {
+        const char* e = std::getenv("PQH_SORT_DIAG");
+        return e ? std::atoi(e) : 0;
+    }();
+    return diag;
+}
+
+template <int W>
+int sort_rows_radix(pqh_ctx_t* ctx, uint8_t* codes, long long n, int m) {
+    const long long tiles = (n + kSortTile - 1) / kSortTile;
+    int rc = sort_state_for(ctx, tiles);
+    if (rc) return rc;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t eb = al((size_t)n * 8 * W);
-    int rc = pqh_ensure_ws(ctx, 2 * eb + al(16 * 256 * 4));
+    rc = pqh_ensure_ws(ctx, 2 * eb + al(16 * 256 * 4));
     if (rc) return rc;
     char* w = static_cast<char*>(ctx->ws);
     unsigned long long* r0 = reinterpret_cast<unsigned long long*>(w);
@@ -381,16 +480,11 @@ int sort_rows_radix(pqh_ctx_t* ctx, uint8_t* codes, long long n, int m) {
                        dcnt + (m - 1) * 256);
     PQH_LAUNCH_CHECK(ctx);
     unsigned long long* ticket = ctx->sort_state + ctx->sort_cap * 256;
-    static const int diag = [] {   // PQH_SORT_DIAG (timing diagnostics only: wrong results)
-        const char* e = std::getenv("PQH_SORT_DIAG");
-        return e ? std::atoi(e) : 0;
-    }();
+    const int diag = sort_diag();
     for (int p = 0; p < m; ++p) {   // byte m - 1 first
         const int j = m - 1 - p;
-        if (++ctx->sort_epoch >= 0xFFFF) {   // wrap: clear the tags
-            PQH_HIP(ctx, hipMemsetAsync(ctx->sort_state, 0, (size_t)ctx->sort_cap * 256 * 8, ctx->stream));
-            ctx->sort_epoch = 1;
-        }
+        rc = sort_next_epoch(ctx);
+        if (rc) return rc;
         const bool first = p == 0, last = p == m - 1;
         // (first: codes -> r0; middle: ping-pong; last: -> codes, or r0/r1 + unpack)
         const unsigned long long* rin = (p & 1) ? r0 : r1;
@@ -412,6 +506,62 @@ int sort_rows_radix(pqh_ctx_t* ctx, uint8_t* codes, long long n, int m) {
             PQH_LAUNCH_CHECK(ctx);
         }
     }
+    return PQH_OK;
+}
+
+// m = 1 or m > 16: (key chunk, index) pair passes, chunk by chunk from the last, then the rows
+// gathered through the final permutation (into d_tmp or the workspace) and copied back
+int sort_rows_pairs(pqh_ctx_t* ctx, uint8_t* codes, long long n, int m, void* d_tmp) {
+    const long long tiles = (n + kSortTile - 1) / kSortTile;
+    int rc = sort_state_for(ctx, tiles);
+    if (rc) return rc;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t kb = al((size_t)n * 8), ib = al((size_t)n * 4), zb = al((size_t)n * 2);
+    const size_t rb = d_tmp ? 0 : al((size_t)n * m);
+    rc = pqh_ensure_ws(ctx, 2 * kb + 2 * ib + zb + al(8 * 256 * 4) + rb);
+    if (rc) return rc;
+    char* w = static_cast<char*>(ctx->ws);
+    unsigned long long* kin = reinterpret_cast<unsigned long long*>(w);
+    unsigned long long* kout = reinterpret_cast<unsigned long long*>(w + kb);
+    uint32_t* iin = reinterpret_cast<uint32_t*>(w + 2 * kb);
+    uint32_t* iout = reinterpret_cast<uint32_t*>(w + 2 * kb + ib);
+    uint16_t* zpos = reinterpret_cast<uint16_t*>(w + 2 * kb + 2 * ib);
+    uint32_t* dcnt = reinterpret_cast<uint32_t*>(w + 2 * kb + 2 * ib + zb);
+    uint8_t* rows = d_tmp ? static_cast<uint8_t*>(d_tmp)
+                          : reinterpret_cast<uint8_t*>(w + 2 * kb + 2 * ib + zb + al(8 * 256 * 4));
+    const bool w8 = (m & 7) == 0 && (reinterpret_cast<uintptr_t>(codes) & 7) == 0;
+    unsigned long long* ticket = ctx->sort_state + ctx->sort_cap * 256;
+    const int diag = sort_diag();
+    const unsigned blocks = (unsigned)((n + 255) / 256);
+    const int chunks = (m + 7) / 8;
+    for (int c = chunks - 1; c >= 0; --c) {   // least significant chunk first
+        const int nb = std::min(8, m - 8 * c);
+        PQH_HIP(ctx, hipMemsetAsync(dcnt, 0, 8 * 256 * 4, ctx->stream));
+        // (first chunk: the identity order, written into iin)
+        hipLaunchKernelGGL(w8 ? sort_chunk_keys<true> : sort_chunk_keys<false>, dim3(blocks),
+                           dim3(256), 0, ctx->stream, codes, n, m, c, nb,
+                           c == chunks - 1 ? nullptr : iin, iin, zpos, kin, dcnt + (nb - 1) * 256);
+        PQH_LAUNCH_CHECK(ctx);
+        for (int j = nb - 1; j >= 0; --j) {   // the chunk's last byte first
+            rc = sort_next_epoch(ctx);
+            if (rc) return rc;
+#define PQH_SORT_PAIR_PASS(L)                                                                     \
+    hipLaunchKernelGGL((sort_pass<false, L, 1, true>), dim3((unsigned)tiles), dim3(kSortThreads),  \
+                       0, ctx->stream, codes, codes, n, m, j, kin, kout, dcnt + j * 256,           \
+                       dcnt + (j > 0 ? j - 1 : 0) * 256, ctx->sort_state, ticket,                  \
+                       ctx->sort_ticket_base, ctx->sort_epoch, diag, iin, iout)
+            if (j == 0) PQH_SORT_PAIR_PASS(true);
+            else PQH_SORT_PAIR_PASS(false);
+#undef PQH_SORT_PAIR_PASS
+            PQH_LAUNCH_CHECK(ctx);
+            ctx->sort_ticket_base += (unsigned long long)tiles;
+            std::swap(kin, kout);
+            std::swap(iin, iout);
+        }
+    }
+    hipLaunchKernelGGL(gather_rows, dim3(blocks), dim3(256), 0, ctx->stream, codes, n, m, iin, rows);
+    PQH_LAUNCH_CHECK(ctx);
+    PQH_HIP(ctx, hipMemcpyAsync(codes, rows, (size_t)n * m, hipMemcpyDeviceToDevice, ctx->stream));
     return PQH_OK;
 }
 }  // namespace
@@ -436,6 +586,9 @@ int pqh_sort_rows(pqh_ctx_t* ctx, void* d_codes, long long n, int m, void* d_tmp
         if (rc != PQH_ERR_NOMEM) return rc;
         // out of device memory for the in-tree sort's 16 (m <= 8) or 32 B/row: the rocPRIM
         // path below needs 24 B/row + its temp when the caller passes d_tmp
+    } else if (n < (1ll << 31) && m < 65535 && !force_lib) {
+        rc = sort_rows_pairs(ctx, static_cast<uint8_t*>(d_codes), n, m, d_tmp);
+        if (rc != PQH_ERR_NOMEM) return rc;
     }
     // workspace: keys in/out (u64), index in/out (u32), rocPRIM temp, row buffer if no d_tmp
     size_t temp = 0;

@@ -530,11 +530,13 @@ def _zero_heavy_rows(n, m, seed):
 @pytest.mark.parametrize("n,m", [(1, 8), (2, 8), (1000, 8), (1000, 16), (777, 3), (513, 12),
                                  (300, 1), (2000, 24), (2048, 8), (2049, 8), (4097, 2),
                                  (50_000, 8), (30_001, 7), (100_000, 4), (300_000, 8),
-                                 (8193, 16), (40_000, 9), (20_001, 15), (300_000, 16)])
+                                 (8193, 16), (40_000, 9), (20_001, 15), (300_000, 16),
+                                 (4097, 1), (300_000, 1), (4099, 17), (50_000, 32),
+                                 (300_000, 32), (20_001, 41), (30_000, 64)])
 def test_gpu_sort_rows_vs_oracle(gpu, oracle, n, m):
     """2 <= m <= 16 runs the hand-written radix passes (one or two words per row; tiles of
-    8,192 rows chained by the look-back: the sizes straddle tile edges), m = 1 and m > 16
-    the rocPRIM chunk sort."""
+    4,096 rows chained by the look-back: the sizes straddle tile edges), m = 1 and m > 16
+    the same passes over (key chunk, row index) pairs, chunk by chunk."""
     torch, codec, ctx = gpu
     for seed in (1, 2):
         a = _zero_heavy_rows(n, m, seed)
@@ -543,13 +545,15 @@ def test_gpu_sort_rows_vs_oracle(gpu, oracle, n, m):
         assert np.array_equal(d.cpu().numpy(), oracle.sort_rows(a))
 
 
-def test_gpu_sort_rows_radix_vs_rocprim(gpu):
+@pytest.mark.parametrize("m", [8, 32])
+def test_gpu_sort_rows_radix_vs_rocprim(gpu, m):
     """The radix passes and the rocPRIM path (PQH_SORT_IMPL=rocprim) give the same rows, on
-    skewed full-alphabet codes and on heavy ties spread over many tiles."""
+    skewed full-alphabet codes and on heavy ties spread over many tiles (m = 32: the pair
+    passes)."""
     import sys
     import tempfile
     torch, codec, ctx = gpu
-    a = datagen.skewed_codes(200_000, 8, 256, seed=11)
+    a = datagen.skewed_codes(200_000, m, 256, seed=11)
     a[::3] = a[0]                                  # one row repeated across every tile
     d = torch.from_numpy(a.copy()).cuda()
     codec.sort_rows(ctx, d)
@@ -566,7 +570,7 @@ def test_gpu_sort_rows_radix_vs_rocprim(gpu):
         np.testing.assert_array_equal(d.cpu().numpy(), np.load(f))
 
 
-@pytest.mark.parametrize("m", [8, 16])
+@pytest.mark.parametrize("m", [8, 16, 32])
 def test_gpu_sort_full_size_vs_oracle(gpu, oracle, m):
     torch, codec, ctx = gpu
     a = datagen.skewed_codes(1_000_000, m, 256, seed=5, stay=0)

@@ -1,5 +1,5 @@
 """Sort-mode timing (huffman_encoder's default strncmp-key stable sort, pqh_sort_rows) on
-1M x 8 skewed codes, alone on the GPU: ms per call by HIP events over 50 calls.
+M x N skewed codes (env M, N; default 1M x 8), alone on the GPU: ms per call by HIP events over 50 calls.
 PQH_SORT_IMPL=rocprim selects the library path."""
 import json
 import os
