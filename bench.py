@@ -79,9 +79,10 @@ def pmc_traffic(kernel, tag):
     return None, None, None
 
 
-def lib_shard_req(args, world):
-    """world > 1 through the C ABI's two-phase shard encode (bench's default there)"""
-    return world > 1 and args.shard_path == "library" and not args.sort and \
+def lib_shard_req(args, multi):
+    """world > 1 (or --dist-rehearse) through the C ABI's two-phase shard encode (bench's
+    default there)"""
+    return multi and args.shard_path == "library" and not args.sort and \
         not (args.sched == "serial" or args.no_overlap)
 
 
@@ -200,6 +201,19 @@ def parse():
     ap.add_argument("--shard-path", choices=["library", "python"], default="library",
                     help="world > 1: the library's two-phase pqh_shard_encode (C ABI, RCCL "
                          "hooks; default) or the Python composition of the same steps")
+    ap.add_argument("--dist-rehearse", action="store_true",
+                    help="run the multi-rank pipeline (process group, collectives, shard "
+                         "phases) even with one rank: a rehearsal of the RCCL route on a "
+                         "one-GPU box (launch through torch.distributed.run)")
+    ap.add_argument("--shard-groups", choices=["lanes", "one"], default="lanes",
+                    help="world > 1, library path: a process group (RCCL communicator, its own "
+                         "stream) per table lane for phase 1 and per encode stream for phase 2, "
+                         "so a collective waits only for its own lane's earlier work (default); "
+                         "'one': every collective on the default group, in issue order on one "
+                         "stream, phase 2 issued 'lanes x table sets - 1' batches late")
+    ap.add_argument("--nccl-priority", choices=["normal", "high"], default="normal",
+                    help="--shard-groups lanes over RCCL: the groups' internal streams at "
+                         "normal or high priority")
     ap.add_argument("--one-device", action="store_true",
                     help="every rank uses GPU 0 (schedule rehearsal on a one-GPU box)")
     ap.add_argument("--lut-on", choices=["lanes", "assign"], default="lanes",
@@ -373,10 +387,11 @@ def main():
     args = parse()
     if args.hist_on == "auto":
         args.hist_on = "lanes" if args.vectors < 16_000_000 else "assign"
-    if int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.hist_on == "own":
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.dist_rehearse or args.hist_on == "own":
         # 4 library/torch streams + RCCL's own: give each a hardware queue (HIP reads this at
         # initialisation; measured neutral at one rank, 2,150 vs 2,153 Mvec/s)
-        os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+        # (--shard-groups lanes: + one RCCL stream per lane; 16 so that no two share a queue)
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", "16" if args.shard_groups == "lanes" else "8")
     import torch
     import torch.distributed as dist
     from pq_huffman_amd import codec, shard
@@ -386,7 +401,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.one_device:
         local = 0
-    if world > 1:
+    multi = world > 1 or args.dist_rehearse   # the multi-rank pipeline (process group)
+    if multi:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
         if args.dist_backend == "nccl":
@@ -405,7 +421,7 @@ def main():
 
     x = gen(torch, n, d, 0x5EED, rank, dev)
     cent = train_centroids(torch, gen(torch, 200_000, d, 0x5EED, 0, dev), m, k)
-    if world > 1:   # one quantizer for the whole job: rank 0's centroids
+    if multi:   # one quantizer for the whole job: rank 0's centroids
         ct = torch.from_numpy(cent).to(dev)
         dist.broadcast(ct, 0)
         cent = ct.cpu().numpy()
@@ -450,7 +466,7 @@ def main():
     pq = codec.PQ(ctx, cent)
     # more assignment streams: each with its own context (histogram workspace) and PQ object
     # (the assignment's work-queue state is per object, so launches may overlap)
-    na = 1 if serial or lib_shard_req(args, world) else max(1, args.astreams)
+    na = 1 if serial or lib_shard_req(args, multi) else max(1, args.astreams)
     actx = [ctx] + [codec.Context(local, cus=1 << 20) for _ in range(na - 1)]
     # the assignment grid's workgroups per CU, on the contexts that launch it (a library
     # caller that sets nothing gets the occupancy limit; pqh_ctx_set_tuning)
@@ -465,7 +481,7 @@ def main():
     # part-major codes (--code-layout parts): codes[s] is (m, n), part i's codes in row i
     # (world > 1: through the library's part-major shard phases, the same pipeline as one rank)
     pm = args.code_layout == "parts" and not args.sort and \
-        (world == 1 or lib_shard_req(args, world)) and \
+        (not multi or lib_shard_req(args, multi)) and \
         code_t == torch.uint8 and m in (8, 16) and not serial
     # (part rows padded to a multiple of 128 codes: the assignment's stores are then whole
     # 128-byte lines; with ld = n = 10^6 every odd part starts mid-line and each store
@@ -512,17 +528,30 @@ def main():
     # world > 1 through the C ABI (pqh_shard_encode_tables on the table lane, then
     # pqh_shard_encode_write on the encode stream): the histogram moves off the assignment
     # stream into phase 1; each in-flight batch keeps its scratch (halo row, raw-first flag)
-    lib_shard = world > 1 and args.shard_path == "library" and not serial and not args.sort
+    lib_shard = multi and args.shard_path == "library" and not serial and not args.sort
     if lib_shard:
-        comm = shard.TorchComm(world, rank)
-        scratch = [shard.scratch_for(comm, m, dev) for _ in range(slots)]
+        # (--shard-groups lanes: every rank creates the groups in the same order)
+        if args.shard_groups == "lanes":
+            pgo = None
+            if args.dist_backend == "nccl" and args.nccl_priority == "high":
+                pgo = dist.ProcessGroupNCCL.Options()
+                pgo.is_high_priority_stream = True
+
+            def group():
+                return dist.new_group(list(range(world)), pg_options=pgo)
+            comm_t = [shard.TorchComm(world, rank, group=group()) for _ in range(nl)]
+            comm_e = [shard.TorchComm(world, rank, group=group()) for _ in range(ne)]
+        else:
+            comm_t = [shard.TorchComm(world, rank)] * nl
+            comm_e = comm_t[:1] * ne
+        scratch = [shard.scratch_for(comm_t[0], m, dev) for _ in range(slots)]
         status = [0] * slots
         offs = [torch.zeros(2, dtype=torch.int64, device=dev) for _ in elanes]
         # every batch's global length, folded by min on the encode streams: -1 (the sentinel
         # ~0) if any rank's phase 2 failed for any batch (checked after the timed region)
         shard_min = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in elanes]
     stages = ("assign", "sort", "hist", "codebook", "lut", "encode", "decode")
-    if args.sort and (k > 256 or world > 1):
+    if args.sort and (k > 256 or multi):
         raise SystemExit("--sort: one rank, K <= 256 (the distributed sort is shard.py's)")
     sort_tmp = torch.empty((n, m), dtype=torch.uint8, device=dev) if args.sort else None
     # sort mode: the sort of batch i runs on its table lane (after the assignment), so the
@@ -638,7 +667,7 @@ def main():
                 wait(sL, ev_dec[ti])
             e = rec("codebook", sL)
             tc = time.perf_counter()
-            status[s] = shard.shard_encode_tables(c, comm, codes[s], tabs[ti], counts[s],
+            status[s] = shard.shard_encode_tables(c, comm_t[j], codes[s], tabs[ti], counts[s],
                                                   scratch[s], first_row=rank * n,
                                                   parts_n=n if pm else None,
                                                   partials=hparts[s] if hist_split else None)
@@ -794,14 +823,14 @@ def main():
             e = rec("encode", sL)
             tc = time.perf_counter()
             if lib_shard:   # phase 2 of pqh_shard_encode: length, all-gather, offsets, write
-                shard.shard_encode_write(c, comm, codes[s], tj, out[j], args.chunk, coff[j],
+                shard.shard_encode_write(c, comm_e[j], codes[s], tj, out[j], args.chunk, coff[j],
                                          cprev[j], offs[j], scratch[s], status[s],
                                          first_row=rank * n, parts_n=n if pm else None)
                 tot_dev[j].copy_(shard.scratch_shard_bits(scratch[s], world, m))
                 torch.minimum(shard_min[j], offs[j][1:], out=shard_min[j])
                 state["goff"] = offs[j][:1]
                 acc["collectives"] += time.perf_counter() - tc if state["timed"] else 0.0
-            elif world > 1:   # place the shard in the global stream before writing it: sizes,
+            elif multi:   # place the shard in the global stream before writing it: sizes,
                 # all-gather + prefix sum on the device, offset read by the kernel (no host sync)
                 total = codec.encode_size(c, tj, codes[s], raw_first, halo[s])
                 goff, _ = shard.bit_offsets_device(total, world, rank)
@@ -837,7 +866,8 @@ def main():
     # i's bit-offset all-gather (which waits for its tables) is issued after the halo and
     # histogram collectives of batch i + lag, so those never queue behind a table build.
     # (back(i) must be issued before front(i + lanes * nbuf) waits for its decode)
-    lag = 0 if world == 1 or serial else nl * nbuf - 1
+    lag = 0 if not multi or serial or (lib_shard and args.shard_groups == "lanes") \
+        else nl * nbuf - 1
     lag = max(lag, dl)   # (back(i) is issued after lut(i))
     if pair:
         lag = max(lag, 1)    # (back(i) is issued after its pair's build)
@@ -858,7 +888,7 @@ def main():
 
     def barrier():
         torch.cuda.synchronize()
-        if world > 1:
+        if multi:
             dist.barrier()
             torch.cuda.synchronize()
 
@@ -921,7 +951,7 @@ def main():
         for i, (name, e0, e1) in enumerate(events):
             print(f"TL {i:3d} {name:9s} {f0.elapsed_time(e0):8.3f} {f0.elapsed_time(e1):8.3f}",
                   file=sys.stderr)
-    if world > 1:
+    if multi:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -965,7 +995,7 @@ def main():
 
     if args.dump:   # the last batch's shard stream + codes, gathered to rank 0 (tests)
         nb = (int(tot_dev[j_last].item()) + 7) // 8 + 8
-        goff = int(state["goff"].item()) if world > 1 else 0
+        goff = int(state["goff"].item()) if multi else 0
         mine = {"codes": rows_last.cpu().numpy(), "bits": int(tot_dev[j_last].item()),
                 "goff": goff, "buf": out[j_last][:nb].cpu().numpy()}
         allp = [None] * world
@@ -1035,7 +1065,9 @@ def main():
                                             "library default"),
                        "vectors_per_gpu": n, "d": d, "m": m, "k": k,
                        "mode": "ctx" if ctxm else "noctx",
-                       "chunk_vectors": args.chunk, "parallelism": f"dp{world} row shards",
+                       "chunk_vectors": args.chunk, "parallelism": f"dp{world} row shards"
+                       + (" (--dist-rehearse: the multi-rank pipeline and its collectives at "
+                          "one rank)" if args.dist_rehearse else ""),
                        "schedule": ("serial" if serial else
                                     "lanes: assignment + histogram " +
                                     ("partial counts " if hist_split else "") +
@@ -1128,7 +1160,7 @@ def main():
     for c in {id(c): c for c in list(lanes) + list(elanes) + list(actx) +
               ([hctx] if hctx is not None else [])}.values():
         c.close()
-    if world > 1:
+    if multi:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -1398,18 +1398,24 @@ static int encode_write_impl(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* 
                              unsigned long long* d_chunk_offsets, void* d_chunk_prev,
                              unsigned long long* d_total_bits,
                              const uint16_t* tree_prev = nullptr, const int* d_rawf = nullptr,
-                             long long ldc = 0) {
-    if (!ctx || !t || n < 0 || (n > 0 && (!d_codes || !d_out))) return PQH_ERR_ARG;
+                             long long ldc = 0, int phase = 0) {
+    // phase (tiled encoder only): 0 = the whole write; 1 = the tiles and the scan (the
+    // total in *d_total_bits; d_out and the offset unused); 2 = the placement of phase 1's
+    // tiles at the offset, with the same arguments and nothing else run on ctx between
+    // (pqh_shard_encode_write: the length all-gather runs between them)
+    if (!ctx || !t || n < 0 || (n > 0 && !d_codes) || (n > 0 && phase != 1 && !d_out))
+        return PQH_ERR_ARG;
+    if (phase && !d_total_bits) return PQH_ERR_ARG;
     if (ldc && (ldc < n || t->k > 256 || (t->m != 8 && t->m != 16) || tree_prev ||
                 (reinterpret_cast<uintptr_t>(d_chunk_prev) & 7)))
         return ldc < n ? PQH_ERR_ARG : PQH_ERR_UNSUPPORTED;   // part-major: the row encoder only
-    if ((reinterpret_cast<uintptr_t>(d_out) & 3u) || (out_bytes & 3u))
+    if (phase != 1 && ((reinterpret_cast<uintptr_t>(d_out) & 3u) || (out_bytes & 3u)))
         return pqh_set_error(ctx, PQH_ERR_ARG, "stream buffer must be 4-byte aligned and sized");
     if (chunk_vectors > 0 && !d_chunk_offsets) return PQH_ERR_ARG;
     int rc = pqh_use_device(ctx);
     if (rc) return rc;
     if (n == 0) {
-        if (d_total_bits) PQH_HIP(ctx, hipMemsetAsync(d_total_bits, 0, 8, ctx->stream));
+        if (d_total_bits && phase != 2) PQH_HIP(ctx, hipMemsetAsync(d_total_bits, 0, 8, ctx->stream));
         return PQH_OK;
     }
     // 8-byte rows: m = 8 (one row per vector) or m = 16 (two rows per vector), u8 codes,
@@ -1435,7 +1441,7 @@ static int encode_write_impl(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* 
         const char* e = std::getenv("PQH_ENC_IMPL");
         return e && !std::strcmp(e, "onepass");
     }();
-    if (!onepass) {
+    if (!onepass || phase) {
         const long long slot = (long long)(lds / 4);   // a tile's worst-case image, + 4 words
         int rc2 = pqh_ensure_enc_scratch(ctx, ((size_t)nb * slot + 64) * 4);
         if (rc2) return rc2;
@@ -1447,6 +1453,17 @@ static int encode_write_impl(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* 
             reinterpret_cast<unsigned long long*>(static_cast<char*>(ctx->ws) + a);
         uint32_t* scr = static_cast<uint32_t*>(ctx->enc_scr);
         unsigned long long* tb = reinterpret_cast<unsigned long long*>(tile_bits);
+        const long long chunks = chunk_vectors > 0 ? (n + chunk_vectors - 1) / chunk_vectors : 0;
+        auto place = [&]() -> int {
+            hipLaunchKernelGGL(enc_place, dim3((unsigned)nb), dim3(256), 0, ctx->stream, scr, slot,
+                               tile_bits, tile_off, nb, bit_offset, d_bit_offset, words,
+                               (long long)(out_bytes / 4), (long long)blk,
+                               chunk_vectors > 0 ? (long long)chunk_vectors * cs : 0ll, chunks,
+                               d_chunk_offsets, ctx->d_diag + 2, total);
+            PQH_LAUNCH_CHECK(ctx);
+            return PQH_OK;
+        };
+        if (phase == 2) return place();
 #define PQH_ENC_T(T, MAXM, R8, CS, PMV)                                                          \
     do {                                                                                         \
         constexpr int B = MAXM > 0 && MAXM <= 8 ? 256 : kEncBlock;                               \
@@ -1479,14 +1496,7 @@ static int encode_write_impl(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* 
         PQH_LAUNCH_CHECK(ctx);
         launch_scan(ctx->stream, tile_bits, nb, tile_off, total, tile_off + nb);
         PQH_LAUNCH_CHECK(ctx);
-        const long long chunks = chunk_vectors > 0 ? (n + chunk_vectors - 1) / chunk_vectors : 0;
-        hipLaunchKernelGGL(enc_place, dim3((unsigned)nb), dim3(256), 0, ctx->stream, scr, slot,
-                           tile_bits, tile_off, nb, bit_offset, d_bit_offset, words,
-                           (long long)(out_bytes / 4), (long long)blk,
-                           chunk_vectors > 0 ? (long long)chunk_vectors * cs : 0ll, chunks,
-                           d_chunk_offsets, ctx->d_diag + 2, total);
-        PQH_LAUNCH_CHECK(ctx);
-        return PQH_OK;
+        return phase == 1 ? PQH_OK : place();
     }
     // look-back state: grow-only, epoch-tagged so it never needs clearing between calls
     if (nb > ctx->lb_cap) {
@@ -1628,6 +1638,30 @@ int pqh_encode_write_at_dev_ld(pqh_ctx_t* ctx, const pqh_tables_t* t, const void
     return encode_write_impl(ctx, t, d_codes, n, 0, d_prev_row, 0, d_global_bit_offset, d_out,
                              out_bytes, chunk_vectors, d_chunk_offsets, d_chunk_prev, nullptr,
                              nullptr, d_rawf, ldc);
+}
+
+// pqh_shard_encode_write's two halves of pqh_encode_write_at_dev_ld: phase 1 codes the tiles
+// and leaves the shard's exact length in *d_total_bits (before any offset is known), phase 2
+// places them at *d_global_bit_offset -- the length all-gather runs between (no size pass)
+int pqh_encode_tiles_dev_ld(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes,
+                            long long ldc, long long n, const void* d_prev_row, const int* d_rawf,
+                            int chunk_vectors, unsigned long long* d_chunk_offsets,
+                            void* d_chunk_prev, unsigned long long* d_total_bits) {
+    return encode_write_impl(ctx, t, d_codes, n, 0, d_prev_row, 0, nullptr, nullptr, 0,
+                             chunk_vectors, d_chunk_offsets, d_chunk_prev, d_total_bits, nullptr,
+                             d_rawf, ldc, 1);
+}
+
+int pqh_encode_place_dev_ld(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes,
+                            long long ldc, long long n, const void* d_prev_row, const int* d_rawf,
+                            const unsigned long long* d_global_bit_offset, unsigned char* d_out,
+                            unsigned long long out_bytes, int chunk_vectors,
+                            unsigned long long* d_chunk_offsets, void* d_chunk_prev,
+                            unsigned long long* d_total_bits) {
+    if (!d_global_bit_offset) return PQH_ERR_ARG;
+    return encode_write_impl(ctx, t, d_codes, n, 0, d_prev_row, 0, d_global_bit_offset, d_out,
+                             out_bytes, chunk_vectors, d_chunk_offsets, d_chunk_prev, d_total_bits,
+                             nullptr, d_rawf, ldc, 2);
 }
 
 int pqh_encode_size_dev(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes, long long n,

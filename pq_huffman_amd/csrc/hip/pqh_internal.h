@@ -93,6 +93,18 @@ int pqh_encode_write_at_dev_ld(pqh_ctx_t* ctx, const pqh_tables_t* t, const void
                                unsigned char* d_out, unsigned long long out_bytes,
                                int chunk_vectors, unsigned long long* d_chunk_offsets,
                                void* d_chunk_prev);
+// its two halves (tiled encoder): the tiles and the exact length, then the placement at the
+// device offset (pqh_shard_encode_write runs the length all-gather between them)
+int pqh_encode_tiles_dev_ld(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes,
+                            long long ldc, long long n, const void* d_prev_row, const int* d_rawf,
+                            int chunk_vectors, unsigned long long* d_chunk_offsets,
+                            void* d_chunk_prev, unsigned long long* d_total_bits);
+int pqh_encode_place_dev_ld(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes,
+                            long long ldc, long long n, const void* d_prev_row, const int* d_rawf,
+                            const unsigned long long* d_global_bit_offset, unsigned char* d_out,
+                            unsigned long long out_bytes, int chunk_vectors,
+                            unsigned long long* d_chunk_offsets, void* d_chunk_prev,
+                            unsigned long long* d_total_bits);
 int pqh_encode_size_dev(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes, long long n,
                         const void* d_prev_row, const int* d_rawf,
                         unsigned long long* d_total_bits);

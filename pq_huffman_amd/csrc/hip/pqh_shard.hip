@@ -53,28 +53,6 @@ __global__ void shard_halo_pick(const unsigned char* __restrict__ recs, long lon
         row[i] = prev >= 0 ? recs[prev * recb + kHaloData + i] : (unsigned char)0;
 }
 
-// The shard's exact bit length from its LOCAL histogram (kept in the scratch before the
-// all-reduce) and the code lengths of the shared tables: sum over (part, item) of count x
-// len -- huffman_estimate_size's sum (huffman_encode.c:271-277) over this shard -- plus 8 bits
-// per part when the shard writes the raw first row (huffman_encoder.c:234).  The histogram
-// counts exactly the symbols the encoder codes (the halo pair when it is not raw-first, no
-// out-of-alphabet symbol), so this equals the size pass over the codes without reading them.
-// *out must be zero on entry.
-__global__ void __launch_bounds__(256)
-shard_length(const uint32_t* __restrict__ local, const unsigned long long* __restrict__ enc,
-             long long total, int m, const int* __restrict__ rawf, int nonempty,
-             unsigned long long* __restrict__ out) {
-    unsigned long long s = 0;
-    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-         i += (long long)gridDim.x * blockDim.x) {
-        const uint32_t c = local[i];
-        if (c) s += (unsigned long long)c * (enc[i] >> 56);
-    }
-    for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);
-    if (blockIdx.x == 0 && threadIdx.x == 0 && nonempty && rawf && *rawf) s += 8ull * m;
-    if ((threadIdx.x & 63) == 0 && s) atomicAdd(out, s);
-}
-
 // this shard's last row into the halo record (byte kHaloData on), from row-major codes
 // (ldc = 0) or part-major ones (part i's codes at i * ldc)
 __global__ void shard_last_row(const unsigned char* __restrict__ codes, long long ldc, long long n,
@@ -114,15 +92,12 @@ int pqh_shard_block(long long n_total, int world, int rank, block_t* block) {
 }
 
 // scratch: [send record][world records][halo row (a record's size)][send length]
-//          [world lengths][raw-first flag, 64 B][pad to 256 B][local histogram, m x K^2 u32
-//          at K = 256: the largest histogram a shard encode takes]
-static long long shard_local_offset(int world, int m) {
-    return ((halo_record_bytes(m) * (world + 2) + 8ll * (world + 1) + 64 + 255) / 256) * 256;
-}
-
+//          [world lengths][raw-first flag, 64 B][pad to 256 B]
+// (round 5: the shard's length comes from the encoder's tile pass, so the copy of the local
+// histogram that round 4 kept here for it is gone)
 long long pqh_shard_scratch_bytes(int world, int m) {
     if (world <= 0 || m <= 0) return PQH_ERR_ARG;
-    return shard_local_offset(world, m) + (long long)m * 65536 * 4;
+    return ((halo_record_bytes(m) * (world + 2) + 8ll * (world + 1) + 64 + 255) / 256) * 256;
 }
 
 int pqh_shard_offsets(const unsigned long long* lengths, int world, int rank,
@@ -181,7 +156,6 @@ struct ShardScratch {
     unsigned long long* len_send;
     unsigned long long* len_recv;
     int* rawf;
-    uint32_t* local;   // the shard's own histogram, kept for its length (phase 2)
     long long recb;
     ShardScratch(void* d, int world, int m) {
         unsigned char* p = static_cast<unsigned char*>(d);
@@ -192,7 +166,6 @@ struct ShardScratch {
         len_send = reinterpret_cast<unsigned long long*>(p + recb * (world + 2));
         len_recv = len_send + 1;
         rawf = reinterpret_cast<int*>(len_recv + world);
-        local = reinterpret_cast<uint32_t*>(p + shard_local_offset(world, m));
     }
 };
 
@@ -269,10 +242,6 @@ static int shard_tables_impl(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm, const
         local(ldc ? pqh_histogram_parts(ctx, d_codes, ldc, n, m, k, 0, nullptr, d_counts, 1)
                   : pqh_histogram_set(ctx, d_codes, n, m, k, 0, nullptr, d_counts));
     }
-    // (the local counts give phase 2 the shard's length without a pass over its codes)
-    if (!err)
-        local(hipMemcpyAsync(sc.local, d_counts, (size_t)m * items * 4, hipMemcpyDeviceToDevice,
-                             ctx->stream) == hipSuccess ? PQH_OK : PQH_ERR_HIP);
     if (comm->all_reduce_sum_u32(comm->user, d_counts, (long long)m * items, st))
         return pqh_set_error(ctx, PQH_ERR_COMM, "shard histogram all-reduce failed");
     if (!err) local(pqh_tables_build(ctx, tables, d_counts));
@@ -317,18 +286,16 @@ static int shard_write_impl(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm, const 
     const long long n = err ? 0 : shard->size;
     const int world = comm->world, rank = comm->rank;
     ShardScratch sc(d_scratch, world, m);
-    if (!err) {   // the exact length: local histogram x code lengths (no size pass)
-        const long long total = (long long)m * tables->items;
-        if (hipMemsetAsync(sc.len_send, 0, 8, ctx->stream) != hipSuccess) {
-            err = PQH_ERR_HIP;
-        } else {
-            const long long want = (total + 255) / 256;
-            const unsigned grid = (unsigned)(want < 1024 ? (want > 0 ? want : 1) : 1024);
-            hipLaunchKernelGGL(shard_length, dim3(grid), dim3(256), 0, ctx->stream, sc.local,
-                               tables->d_enc, total, m, context ? sc.rawf : nullptr,
-                               n > 0 ? 1 : 0, sc.len_send);
-            if (hipGetLastError() != hipSuccess) err = PQH_ERR_HIP;
-        }
+    // the shard's exact length from the tiled encoder's first half (its tiles coded into
+    // scratch, their bit counts scanned -- nothing depends on the offset yet), all-gathered;
+    // the sentinel ~0 when status, the rank's phase-1 result, or this phase fails locally
+    const void* prev = context ? sc.halo_row : nullptr;
+    const int* rawf = context ? sc.rawf : nullptr;
+    if (!err) {
+        const int r = pqh_encode_tiles_dev_ld(ctx, tables, d_codes, ldc, n, prev, rawf,
+                                              chunk_vectors, d_chunk_offsets, d_chunk_prev,
+                                              sc.len_send);
+        if (r) err = r;
     }
     if (err) (void)hipMemsetAsync(sc.len_send, 0xFF, 8, ctx->stream);   // the sentinel length
     if (comm->all_gather(comm->user, sc.len_send, sc.len_recv, 8, ctx->stream))
@@ -340,12 +307,9 @@ static int shard_write_impl(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm, const 
     // word 0 of d_out = the global word offset / 32; the bits before the shard's offset in
     // that word belong to the previous shard and stay zero here
     PQH_HIP(ctx, hipMemsetAsync(d_out, 0, 4, ctx->stream));
-    rc = context ? pqh_encode_write_at_dev_ld(ctx, tables, d_codes, ldc, n, sc.halo_row, sc.rawf,
-                                              d_offsets, d_out, out_bytes, chunk_vectors,
-                                              d_chunk_offsets, d_chunk_prev)
-                 : pqh_encode_write_at_dev_ld(ctx, tables, d_codes, ldc, n, nullptr, nullptr,
-                                              d_offsets, d_out, out_bytes, chunk_vectors,
-                                              d_chunk_offsets, d_chunk_prev);
+    rc = pqh_encode_place_dev_ld(ctx, tables, d_codes, ldc, n, prev, rawf, d_offsets, d_out,
+                                 out_bytes, chunk_vectors, d_chunk_offsets, d_chunk_prev,
+                                 sc.len_send);
     if (rc) return rc;
     if (raw_first_out) {   // (optional: the one host read, at the end)
         int rf = rank == 0 ? 1 : 0;
