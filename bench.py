@@ -205,12 +205,18 @@ def parse():
                     help="run the multi-rank pipeline (process group, collectives, shard "
                          "phases) even with one rank: a rehearsal of the RCCL route on a "
                          "one-GPU box (launch through torch.distributed.run)")
-    ap.add_argument("--shard-groups", choices=["lanes", "one"], default="lanes",
+    ap.add_argument("--shard-groups", choices=["lanes", "one"], default="one",
                     help="world > 1, library path: a process group (RCCL communicator, its own "
                          "stream) per table lane for phase 1 and per encode stream for phase 2, "
-                         "so a collective waits only for its own lane's earlier work (default); "
-                         "'one': every collective on the default group, in issue order on one "
-                         "stream, phase 2 issued 'lanes x table sets - 1' batches late")
+                         "so a collective waits only for its own lane's earlier work; 'one' "
+                         "(default): every collective on the default group, in issue order on "
+                         "one stream, phase 2 issued 'lanes x table sets - 1' batches late "
+                         "(2,563 vs 2,558 Mvec/s in the one-rank rehearsal, fewer communicators)")
+    ap.add_argument("--write-on", choices=["encode", "tables"], default="encode",
+                    help="world > 1, library path: phase 2 (length all-gather, offsets, write) "
+                         "on the encode stream, or on the batch's table lane right after its "
+                         "tables, the encode stream then only decoding (needs --shard-groups "
+                         "lanes; measured 2,452 vs 2,558 Mvec/s in the one-rank rehearsal)")
     ap.add_argument("--nccl-priority", choices=["normal", "high"], default="normal",
                     help="--shard-groups lanes over RCCL: the groups' internal streams at "
                          "normal or high priority")
@@ -387,11 +393,8 @@ def main():
     args = parse()
     if args.hist_on == "auto":
         args.hist_on = "lanes" if args.vectors < 16_000_000 else "assign"
-    if int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.dist_rehearse or args.hist_on == "own":
-        # 4 library/torch streams + RCCL's own: give each a hardware queue (HIP reads this at
-        # initialisation; measured neutral at one rank, 2,150 vs 2,153 Mvec/s)
-        # (--shard-groups lanes: + one RCCL stream per lane; 16 so that no two share a queue)
-        os.environ.setdefault("GPU_MAX_HW_QUEUES", "16" if args.shard_groups == "lanes" else "8")
+    # (GPU_MAX_HW_QUEUES is left to the environment, HIP's default 4: the multi-rank pipeline
+    # measured 1,654 Mvec/s at 8 queues against 2,534 at 4 in the one-rank RCCL rehearsal)
     import torch
     import torch.distributed as dist
     from pq_huffman_amd import codec, shard
@@ -447,7 +450,9 @@ def main():
     if args.lanes is None:   # 1 + lanes + elanes <= 4 streams: one hardware queue each
         # (k4096: the tree builds are the long stage; --sort: the sort and the histogram ride
         # on the lanes -- 1,969 vs 1,877 Mvec/s)
-        args.lanes = 3 if args.config == "k4096" or args.sort else 2
+        # (world > 1: phase 1's collectives lengthen each table build; 2,500-2,537 vs 2,340
+        # Mvec/s at 3 lanes in the one-rank RCCL rehearsal, 1,414 at 4)
+        args.lanes = 3 if args.config == "k4096" or args.sort or multi else 2
     if args.elanes is None:
         args.elanes = 0 if args.config == "k4096" else 1
     nl = 1 if serial else max(1, args.lanes)
@@ -517,18 +522,27 @@ def main():
         if pair:   # lane (i // 2) % nl, pair buffer (i // 2 // nl) % (nbuf / 2), member i % 2
             return lane_of(i) * nbuf + ((i // 2) // nl) % (nbuf // 2) * 2 + i % 2
         return (i % nl) * nbuf + (i // nl) % nbuf
-    dec = [torch.empty((n, m), dtype=code_t, device=dev) for _ in elanes]
-    coff = [torch.empty(chunks, dtype=torch.int64, device=dev) for _ in elanes]
-    cprev = [torch.empty((chunks, m), dtype=torch.uint8, device=dev) if ctxm else None
-             for _ in elanes]
-    out = [torch.zeros(n * m * 56 // 8 + 64, dtype=torch.uint8, device=dev)  # worst case
-           for _ in elanes]
-    tot_dev = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in elanes]
-    raw_first = shard.raw_first(rank)
     # world > 1 through the C ABI (pqh_shard_encode_tables on the table lane, then
-    # pqh_shard_encode_write on the encode stream): the histogram moves off the assignment
-    # stream into phase 1; each in-flight batch keeps its scratch (halo row, raw-first flag)
+    # pqh_shard_encode_write on the encode stream, or on the table lane after the tables --
+    # --write-on tables): the histogram moves off the assignment stream into phase 1; each
+    # in-flight batch keeps its scratch (halo row, raw-first flag)
     lib_shard = multi and args.shard_path == "library" and not serial and not args.sort
+    wt = lib_shard and elanes is not lanes and args.shard_groups == "lanes" and \
+        args.write_on == "tables"
+    if args.write_on == "tables" and not wt:
+        raise SystemExit("--write-on tables: world > 1 (or --dist-rehearse), library path, "
+                         "--shard-groups lanes, encode streams of their own")
+    # the streams' buffers: one per encode stream, or (wt) one per table set, guarded by
+    # that set's ev_dec like the tables themselves
+    nw = len(tabs) if wt else ne
+    dec = [torch.empty((n, m), dtype=code_t, device=dev) for _ in elanes]
+    coff = [torch.empty(chunks, dtype=torch.int64, device=dev) for _ in range(nw)]
+    cprev = [torch.empty((chunks, m), dtype=torch.uint8, device=dev) if ctxm else None
+             for _ in range(nw)]
+    out = [torch.zeros(n * m * 56 // 8 + 64, dtype=torch.uint8, device=dev)  # worst case
+           for _ in range(nw)]
+    tot_dev = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(nw)]
+    raw_first = shard.raw_first(rank)
     if lib_shard:
         # (--shard-groups lanes: every rank creates the groups in the same order)
         if args.shard_groups == "lanes":
@@ -546,10 +560,10 @@ def main():
             comm_e = comm_t[:1] * ne
         scratch = [shard.scratch_for(comm_t[0], m, dev) for _ in range(slots)]
         status = [0] * slots
-        offs = [torch.zeros(2, dtype=torch.int64, device=dev) for _ in elanes]
-        # every batch's global length, folded by min on the encode streams: -1 (the sentinel
+        offs = [torch.zeros(2, dtype=torch.int64, device=dev) for _ in range(nw)]
+        # every batch's global length, folded by min on the writing streams: -1 (the sentinel
         # ~0) if any rank's phase 2 failed for any batch (checked after the timed region)
-        shard_min = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in elanes]
+        shard_min = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(nw)]
     stages = ("assign", "sort", "hist", "codebook", "lut", "encode", "decode")
     if args.sort and (k > 256 or multi):
         raise SystemExit("--sort: one rank, K <= 256 (the distributed sort is shard.py's)")
@@ -673,8 +687,25 @@ def main():
                                                   partials=hparts[s] if hist_split else None)
             acc["collectives"] += time.perf_counter() - tc if state["timed"] else 0.0
             done(e, sL)
+            if wt:   # phase 2 here, after the tables, on the lane's own process group
+                e = rec("encode", sL)
+                tc = time.perf_counter()
+                write_lib(i, c, comm_t[j], ti)
+                acc["collectives"] += time.perf_counter() - tc if state["timed"] else 0.0
+                done(e, sL)
+                ev_enc[s].record(sL)
             ev_tab[s].record(sL)
         used[s] = True
+
+    def write_lib(i, c, comm, w):
+        """phase 2 of pqh_shard_encode for batch i on c's stream, into write buffer w"""
+        s = i % slots
+        shard.shard_encode_write(c, comm, codes[s], tabs[tab_index(i)], out[w], args.chunk,
+                                 coff[w], cprev[w], offs[w], scratch[s], status[s],
+                                 first_row=rank * n, parts_n=n if pm else None)
+        tot_dev[w].copy_(shard.scratch_shard_bits(scratch[s], world, m))
+        torch.minimum(shard_min[w], offs[w][1:], out=shard_min[w])
+        state["goff"] = offs[w][:1]
 
     diag = set(x for x in args.diag_skip.replace("+", ",").split(",") if x)
 
@@ -812,6 +843,7 @@ def main():
         encode/decode stream (after an event wait for its tables)"""
         s, jt = i % slots, tab_index(i)
         j = i % ne
+        w = jt if wt else j   # the stream's write buffer
         c = elanes[j]
         sL = c.stream
         tj = tabs[jt]
@@ -820,15 +852,12 @@ def main():
                 sL.wait_event(ev_trees[s] if early[s] and not lib_shard else ev_tab[s])
             if halo[s] is not None:   # made on the table lane: keep it until this stream's use
                 halo[s].record_stream(sL)
-            e = rec("encode", sL)
+            e = rec("encode", sL) if not wt else None
             tc = time.perf_counter()
-            if lib_shard:   # phase 2 of pqh_shard_encode: length, all-gather, offsets, write
-                shard.shard_encode_write(c, comm_e[j], codes[s], tj, out[j], args.chunk, coff[j],
-                                         cprev[j], offs[j], scratch[s], status[s],
-                                         first_row=rank * n, parts_n=n if pm else None)
-                tot_dev[j].copy_(shard.scratch_shard_bits(scratch[s], world, m))
-                torch.minimum(shard_min[j], offs[j][1:], out=shard_min[j])
-                state["goff"] = offs[j][:1]
+            if wt:   # (written on the table lane after the tables)
+                pass
+            elif lib_shard:   # phase 2 of pqh_shard_encode: length, all-gather, offsets, write
+                write_lib(i, c, comm_e[j], w)
                 acc["collectives"] += time.perf_counter() - tc if state["timed"] else 0.0
             elif multi:   # place the shard in the global stream before writing it: sizes,
                 # all-gather + prefix sum on the device, offset read by the kernel (no host sync)
@@ -849,8 +878,9 @@ def main():
                 codec.encode_write(c, tj, codes[s], out[j], 0, raw_first, halo[s],
                                    args.chunk, coff[j], cprev[j], total=tot_dev[j])
             done(e, sL)
-            ev_enc[s].record(sL)
-            enc = codec.Encoded(out[j], -1, args.chunk, coff[j], cprev[j], n, raw_first)
+            if not wt:
+                ev_enc[s].record(sL)
+            enc = codec.Encoded(out[w], -1, args.chunk, coff[w], cprev[w], n, raw_first)
             if elanes is not lanes and early[s] and not lib_shard:
                 sL.wait_event(ev_tab[s])   # the decode tables
             e = rec("decode", sL)
@@ -859,6 +889,7 @@ def main():
             done(e, sL)
             ev_dec[jt].record(sL)
         state["last"] = (s, j)
+        state["last_w"] = w
         state["last_tab"] = jt
 
     # Every dependency is an event, so batches are issued in order.  With world > 1 the
@@ -956,6 +987,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     s_last, j_last = state["last"]
+    w_last = state["last_w"]
 
     # correctness after timing (not timed): exact round trip of the last batch, status words
     for t in tabs:
@@ -971,33 +1003,33 @@ def main():
         # rows) with the same tables: every stream byte, the bit count and the chunk index
         # must agree, so a wrong but self-consistent timed stream cannot pass
         tl = tabs[state["last_tab"]]
-        ref_out = torch.empty_like(out[j_last])
-        ref_coff = torch.empty_like(coff[j_last])
-        ref_prev = torch.empty_like(cprev[j_last]) if ctxm else None
+        ref_out = torch.empty_like(out[w_last])
+        ref_coff = torch.empty_like(coff[w_last])
+        ref_prev = torch.empty_like(cprev[w_last]) if ctxm else None
         ref_tot = torch.zeros(1, dtype=torch.int64, device=dev)
         codec.encode_write(ctx, tl, rows_last, ref_out, 0, raw_first, None, args.chunk, ref_coff,
                            ref_prev, total=ref_tot)
         codec.encode_status(ctx)
         nbits = int(ref_tot.item())
-        assert int(tot_dev[j_last].item()) == nbits, "stream length != row-path re-encode"
-        assert torch.equal(out[j_last][:(nbits + 7) // 8], ref_out[:(nbits + 7) // 8]), \
+        assert int(tot_dev[w_last].item()) == nbits, "stream length != row-path re-encode"
+        assert torch.equal(out[w_last][:(nbits + 7) // 8], ref_out[:(nbits + 7) // 8]), \
             "stream bytes != row-path re-encode"
-        assert torch.equal(coff[j_last], ref_coff), "chunk index != row-path re-encode"
+        assert torch.equal(coff[w_last], ref_coff), "chunk index != row-path re-encode"
         if ctxm:
-            assert torch.equal(cprev[j_last], ref_prev), "chunk context rows != row-path re-encode"
+            assert torch.equal(cprev[w_last], ref_prev), "chunk context rows != row-path re-encode"
         del ref_out, ref_coff, ref_prev, ref_tot
     if lib_shard:   # every rank's pqh_shard_encode_write succeeded (no sentinel length)
-        shard.status(elanes[j_last], offs[j_last])
+        shard.status(elanes[j_last], offs[w_last])
         for j, sm in enumerate(shard_min):   # ... for every batch, not only the last
             assert int(sm.item()) >= 0, f"a rank's shard encode failed (encode stream {j})"
     rerank = pq.rerank_count(ctx)
-    bits_per_vec = int(tot_dev[j_last].item()) / n
+    bits_per_vec = int(tot_dev[w_last].item()) / n
 
     if args.dump:   # the last batch's shard stream + codes, gathered to rank 0 (tests)
-        nb = (int(tot_dev[j_last].item()) + 7) // 8 + 8
+        nb = (int(tot_dev[w_last].item()) + 7) // 8 + 8
         goff = int(state["goff"].item()) if multi else 0
-        mine = {"codes": rows_last.cpu().numpy(), "bits": int(tot_dev[j_last].item()),
-                "goff": goff, "buf": out[j_last][:nb].cpu().numpy()}
+        mine = {"codes": rows_last.cpu().numpy(), "bits": int(tot_dev[w_last].item()),
+                "goff": goff, "buf": out[w_last][:nb].cpu().numpy()}
         allp = [None] * world
         if world > 1:
             dist.all_gather_object(allp, mine)

@@ -317,6 +317,7 @@ class TorchComm:
         from .capi import ALL_GATHER, ALL_REDUCE_U32, ShardComm
         self.world, self.rank, self.group = world, rank, group
         self._tensors = []
+        self._streams = {}   # the library streams' ExternalStream objects, made once each
         self._reduce = ALL_REDUCE_U32(self._all_reduce)
         self._gather = ALL_GATHER(self._all_gather)
         self.struct = ShardComm(None, world, rank, self._reduce, self._gather)
@@ -346,7 +347,11 @@ class TorchComm:
     def _on_stream(self, stream, fn):
         import torch
         try:
-            with torch.cuda.stream(torch.cuda.ExternalStream(stream)) if stream else _null():
+            if stream:
+                es = self._streams.get(stream)
+                if es is None:
+                    es = self._streams[stream] = torch.cuda.ExternalStream(stream)
+            with torch.cuda.stream(es) if stream else _null():
                 fn()
             return 0
         except Exception as e:  # the C caller gets a status; keep the reason
