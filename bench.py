@@ -217,6 +217,11 @@ def parse():
                          "on the encode stream, or on the batch's table lane right after its "
                          "tables, the encode stream then only decoding (needs --shard-groups "
                          "lanes; measured 2,452 vs 2,558 Mvec/s in the one-rank rehearsal)")
+    ap.add_argument("--a-queue", choices=["auto", "pool", "own"], default="auto",
+                    help="stream A on torch's default stream (from HIP's pool of hardware "
+                         "queues, which more than 4 streams share) or on an all-CU CU-masked "
+                         "stream with a hardware queue of its own (auto: own with world > 1, "
+                         "where RCCL's stream is a fifth)")
     ap.add_argument("--nccl-priority", choices=["normal", "high"], default="normal",
                     help="--shard-groups lanes over RCCL: the groups' internal streams at "
                          "normal or high priority")
@@ -443,6 +448,9 @@ def main():
     if split:
         torch.cuda.synchronize()   # (A gets a stream of its own: the setup's work is done)
         ctx = codec.Context(local, cus=split, complement=True)
+    elif args.a_queue == "own" or (args.a_queue == "auto" and multi and not args.a_priority):
+        torch.cuda.synchronize()   # (A gets a stream of its own: the setup's work is done)
+        ctx = codec.Context(local, cus=-1)
     else:
         ctx = (codec.Context(local, stream=torch.cuda.Stream(device=dev, priority=-1))
                if args.a_priority else codec.Context(local))
@@ -450,9 +458,10 @@ def main():
     if args.lanes is None:   # 1 + lanes + elanes <= 4 streams: one hardware queue each
         # (k4096: the tree builds are the long stage; --sort: the sort and the histogram ride
         # on the lanes -- 1,969 vs 1,877 Mvec/s)
-        # (world > 1: phase 1's collectives lengthen each table build; 2,500-2,537 vs 2,340
-        # Mvec/s at 3 lanes in the one-rank RCCL rehearsal, 1,414 at 4)
-        args.lanes = 3 if args.config == "k4096" or args.sort or multi else 2
+        # (world > 1: stream A on a hardware queue of its own, the 2 lanes, the encode stream
+        # and RCCL's stream on HIP's 4 pooled queues, none shared: 2,793 Mvec/s in the one-rank
+        # RCCL rehearsal; 3 lanes 1,604 with A's own queue, 2,500-2,563 without)
+        args.lanes = 3 if args.config == "k4096" or args.sort else 2
     if args.elanes is None:
         args.elanes = 0 if args.config == "k4096" else 1
     nl = 1 if serial else max(1, args.lanes)

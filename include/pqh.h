@@ -54,7 +54,9 @@ int pqh_ctx_create(pqh_ctx_t** ctx, int device);
  * latency-bound code-table build beside the next batch's assignment. */
 int pqh_ctx_create_cu_limited(pqh_ctx_t** ctx, int device, int cus);
 /* As pqh_ctx_create_cu_limited; complement != 0 takes every compute unit the cus-subset does
- * NOT use, so two contexts (cus, 0) and (cus, 1) run side by side on disjoint CUs. */
+ * NOT use, so two contexts (cus, 0) and (cus, 1) run side by side on disjoint CUs.
+ * cus < 0: every compute unit on a CU-masked stream, which HIP gives a hardware queue of its
+ * own (streams without a mask share GPU_MAX_HW_QUEUES queues). */
 int pqh_ctx_create_cu_split(pqh_ctx_t** ctx, int device, int cus, int complement);
 /* the context's current HIP stream (e.g. for torch.cuda.ExternalStream) */
 void* pqh_ctx_stream(const pqh_ctx_t* ctx);

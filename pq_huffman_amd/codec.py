@@ -67,7 +67,7 @@ class Context:
         self.device = device
         torch.cuda.set_device(device)
         self.ptr = ctypes.c_void_p()
-        if cus > 0:
+        if cus != 0:   # (< 0: all CUs on a CU-masked stream, a hardware queue of its own)
             check(lib().pqh_ctx_create_cu_split(ctypes.byref(self.ptr), device, cus,
                                                 int(complement)), "pqh_ctx_create_cu_split")
             self.stream = torch.cuda.ExternalStream(lib().pqh_ctx_stream(self.ptr), device=device)

@@ -127,9 +127,15 @@ int pqh_ctx_create_cu_split(pqh_ctx_t** out, int device, int cus, int complement
     int rc = pqh_ctx_create(out, device);
     if (rc) return rc;
     pqh_ctx* ctx = *out;
-    if (cus <= 0 || cus >= ctx->num_cus) return PQH_OK;
+    if (cus == 0 || cus >= ctx->num_cus) return PQH_OK;
     // every (num_cus / cus)-th compute unit, so the subset spans all XCDs / shader engines;
-    // complement: every other compute unit (a disjoint partner stream)
+    // complement: every other compute unit (a disjoint partner stream).  cus < 0: every
+    // compute unit, as a CU-masked stream -- HIP gives such a stream a hardware queue of its
+    // own instead of one shared from its pool of GPU_MAX_HW_QUEUES
+    if (cus < 0) {
+        cus = ctx->num_cus;
+        complement = 0;
+    }
     std::vector<uint32_t> mask((ctx->num_cus + 31) / 32, 0u);
     const int stride = std::max(1, ctx->num_cus / cus);
     std::vector<char> pick(ctx->num_cus, 0);
