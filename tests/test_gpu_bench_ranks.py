@@ -46,3 +46,27 @@ def test_two_rank_rehearsal_stitched_stream(oracle, tmp_path, mode, path):
     want, bits = oracle.encode(codes, cbs)
     assert int(d["bits"]) == bits
     assert d["stream"].tobytes() == want
+
+
+@pytest.mark.parametrize("groups", ["one", "lanes"])
+def test_one_rank_rccl_rehearsal_stream(oracle, tmp_path, groups):
+    """bench.py --dist-rehearse: the world > 1 pipeline (process group over RCCL, the
+    TorchComm hooks, both pqh_shard_encode phases, stream A on its own hardware queue) with
+    one rank -- the nccl route on hardware; the rank's stream must equal the oracle's and
+    the bench's own checks (round trip, row-path re-encode, shard status) must pass."""
+    dump = tmp_path / "dump.npz"
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(ROOT, "bench.py"), "--dist-rehearse", "--shard-groups", groups,
+           "--vectors", "30001", "--steps", "4", "--warmup", "1", "--no-cpu-baseline",
+           "--dump", str(dump)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, run_fail_msg(r)
+    d = np.load(dump, allow_pickle=False)
+    codes = d["codes"]
+    assert codes.shape == (30001, 8)
+    cbs = oracle.build_codebooks(codes, 256, True)
+    want, bits = oracle.encode(codes, cbs)
+    assert int(d["bits"]) == bits
+    assert d["stream"].tobytes() == want
