@@ -220,8 +220,9 @@ def parse():
     ap.add_argument("--a-queue", choices=["auto", "pool", "own"], default="auto",
                     help="stream A on torch's default stream (from HIP's pool of hardware "
                          "queues, which more than 4 streams share) or on an all-CU CU-masked "
-                         "stream with a hardware queue of its own (auto: own with world > 1, "
-                         "where RCCL's stream is a fifth)")
+                         "stream with a hardware queue of its own (auto = own: one rank "
+                         "2,873-2,905 vs 2,859-2,880 Mvec/s at 20 steps; with world > 1 RCCL's "
+                         "stream is a fifth, and a lane sharing A's queue stalled it)")
     ap.add_argument("--nccl-priority", choices=["normal", "high"], default="normal",
                     help="--shard-groups lanes over RCCL: the groups' internal streams at "
                          "normal or high priority")
@@ -448,7 +449,7 @@ def main():
     if split:
         torch.cuda.synchronize()   # (A gets a stream of its own: the setup's work is done)
         ctx = codec.Context(local, cus=split, complement=True)
-    elif args.a_queue == "own" or (args.a_queue == "auto" and multi and not args.a_priority):
+    elif args.a_queue == "own" or (args.a_queue == "auto" and not args.a_priority):
         torch.cuda.synchronize()   # (A gets a stream of its own: the setup's work is done)
         ctx = codec.Context(local, cus=-1)
     else:
