@@ -86,7 +86,7 @@ def lib_shard_req(args, multi):
         not (args.sched == "serial" or args.no_overlap)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     # 200 steps = 200 M vectors, ~0.1 s: the lanes pipeline fills and drains inside the timed
@@ -247,7 +247,7 @@ def parse():
                          "holds the same data, so later batches reuse valid tables / streams)")
     ap.add_argument("--table-cus", type=int, default=0,
                     help="limit each lane stream to this many CUs (0: no CU mask)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 GEN_CHUNK = 4_000_000   # rows generated at a time (a 125M-row shard is 64 GB)
@@ -1039,7 +1039,7 @@ def main():
         nb = (int(tot_dev[w_last].item()) + 7) // 8 + 8
         goff = int(state["goff"].item()) if multi else 0
         mine = {"codes": rows_last.cpu().numpy(), "bits": int(tot_dev[w_last].item()),
-                "goff": goff, "buf": out[w_last][:nb].cpu().numpy()}
+                "goff": goff, "buf": out[w_last][:nb].cpu().numpy(), "x": x.cpu().numpy()}
         allp = [None] * world
         if world > 1:
             dist.all_gather_object(allp, mine)
@@ -1048,8 +1048,11 @@ def main():
         if rank == 0:
             total = sum(p["bits"] for p in allp)
             stitched = shard.stitch_np([(p["buf"], p["goff"], p["bits"]) for p in allp], total)
+            # (+ every rank's input rows and the job's centroids: the tests check the codes
+            # against the oracle's assignment too, not only the stream of these codes)
             np.savez(args.dump, stream=stitched, bits=np.int64(total),
-                     codes=np.concatenate([p["codes"] for p in allp]))
+                     codes=np.concatenate([p["codes"] for p in allp]),
+                     x=np.concatenate([p["x"] for p in allp]), cent=cent)
 
     if rank == 0:
         t_assign = acc["assign"] / args.steps

@@ -161,7 +161,7 @@ __global__ void __launch_bounds__(256)
 sort_digits(const uint8_t* __restrict__ codes, long long n, int m, int j, uint32_t* __restrict__ counts) {
     __shared__ uint32_t h[4][256];   // one histogram per wave
     for (int i = threadIdx.x; i < 4 * 256; i += blockDim.x) (&h[0][0])[i] = 0;
-    __syncthreads();
+    lds_barrier();
     const int wave = threadIdx.x >> 6;
     constexpr int kPer = 8;   // rows per thread, loaded together
     for (long long v0 = (long long)blockIdx.x * blockDim.x * kPer + threadIdx.x; v0 < n;
@@ -179,7 +179,7 @@ sort_digits(const uint8_t* __restrict__ codes, long long n, int m, int j, uint32
             if (v0 + (long long)i * blockDim.x < n)
                 atomicAdd(&h[wave][row_digit<W>(row[i], sort_first_zero<W>(row[i]), j)], 1u);
     }
-    __syncthreads();
+    lds_barrier();
     const uint32_t c = h[0][threadIdx.x] + h[1][threadIdx.x] + h[2][threadIdx.x] + h[3][threadIdx.x];
     if (c) atomicAdd(counts + threadIdx.x, c);
 }
@@ -207,7 +207,7 @@ sort_chunk_keys(const uint8_t* __restrict__ codes, long long n, int m, int c, in
                 uint32_t* __restrict__ counts) {
     __shared__ uint32_t h[256];
     h[threadIdx.x] = 0;
-    __syncthreads();
+    lds_barrier();
     const long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     unsigned long long key = 0;
     if (v < n) {
@@ -254,7 +254,7 @@ sort_chunk_keys(const uint8_t* __restrict__ codes, long long n, int m, int c, in
     const unsigned d = (unsigned)(key >> (8 * (nb - 1))) & 0xFFu;
     const unsigned long long match = match_digit(d, v < n);
     if (v < n && lanes_below(match) == 0) atomicAdd(&h[d], (uint32_t)__popcll(match));
-    __syncthreads();
+    lds_barrier();
     if (h[threadIdx.x]) atomicAdd(counts + threadIdx.x, h[threadIdx.x]);
 }
 
@@ -288,7 +288,7 @@ sort_pass(const uint8_t* __restrict__ codes_in, uint8_t* __restrict__ codes_out,
     for (int i = tid; i < kSortWaves * 256; i += kSortThreads) (&wcnt[0][0])[i] = 0;
     if (!LAST)
         for (int i = tid; i < 2 * 256; i += kSortThreads) (&hnext[0][0])[i] = 0;
-    __syncthreads();
+    lds_barrier();
     const long long tile = s_tile;
     const long long base = tile * kSortTile + (long long)wave * 64 * kSortItems;
     unsigned long long row[kSortItems][W];
@@ -331,7 +331,7 @@ sort_pass(const uint8_t* __restrict__ codes_in, uint8_t* __restrict__ codes_out,
         if (valid && below == 0) wcnt[wave][d] = old + (uint32_t)__popcll(match);
         rank[it] = old + below;
     }
-    __syncthreads();
+    lds_barrier();
     // one lane per digit (the first 4 waves): wave prefixes, the tile's count, the look-back
     // over earlier tiles (kLookWin of them per round), the digit base
     const unsigned dg = (unsigned)tid & 255u;
@@ -386,7 +386,7 @@ sort_pass(const uint8_t* __restrict__ codes_in, uint8_t* __restrict__ codes_out,
         }
         if (lane == 63) wsum[wave] = x;
     }
-    __syncthreads();   // (also: every wave has read its counters)
+    lds_barrier();   // (also: every wave has read its counters)
     if (tid < 256) {
         uint32_t gb = x - counts[dg];
         for (int w = 0; w < wave; ++w) gb += wsum[w];
@@ -397,7 +397,7 @@ sort_pass(const uint8_t* __restrict__ codes_in, uint8_t* __restrict__ codes_out,
             run += c[w];
         }
     }
-    __syncthreads();
+    lds_barrier();
     if (diag & 2) {   // (diagnostic: no scatter)
         if (rank[0] == 0xFFFFFFFFu) rout[0] = row[0][0] + row[kSortItems - 1][W - 1];
         return;

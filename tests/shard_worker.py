@@ -1,5 +1,5 @@
 """One rank of the library's sharded encode (pqh_shard_encode through shard.shard_encode),
-run by tests/test_gpu_shard.py under torch.distributed.run with the gloo backend and every
+run by tests/test_gpu_zz_shard.py under torch.distributed.run with the gloo backend and every
 rank on cuda:0 (a fresh process per rank).  Writes rank 0's result to --out (.npz):
 the stitched stream (pqh_shard_stitch of every rank's buffer), the global histogram, and
 the rows the ranks encoded, for the test to compare with the oracle's one-shot results.

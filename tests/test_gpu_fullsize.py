@@ -23,6 +23,15 @@ import datagen
 pytestmark = pytest.mark.gpu
 
 
+def _bench_default_chunk():
+    """bench.py's --chunk default: the decode-chunk size the timed bench line runs at"""
+    import bench
+    return bench.parse([]).chunk
+
+
+BENCH_CHUNK = _bench_default_chunk()
+
+
 @pytest.fixture(scope="module")
 def gpu():
     import torch
@@ -171,10 +180,10 @@ def test_bench_parts_path_sift1m_all_rows(gpu, oracle):
     x = bench.make_data(torch, 1_000_000, 128, 0x5EED, 0, dev)
     cent = bench.train_centroids(torch, bench.make_data(torch, 200_000, 128, 0x5EED, 0, dev),
                                  8, 256)
-    pq, rows, parts, counts, tabs, enc, dec = _bench_path_parts(gpu, x, cent)
+    pq, rows, parts, counts, tabs, enc, dec = _bench_path_parts(gpu, x, cent, chunk=BENCH_CHUNK)
     assert pq.rerank_count() > 0
     _check_parts_against_oracle(gpu, oracle, x.cpu().numpy(), cent, rows, counts, tabs, enc,
-                                dec, 8)
+                                dec, BENCH_CHUNK)
 
 
 def test_bench_parts_path_deep1m_all_rows(gpu, oracle):
@@ -186,9 +195,9 @@ def test_bench_parts_path_deep1m_all_rows(gpu, oracle):
     x = bench.make_deep(torch, 1_000_000, 96, 0x5EED, 0, dev)
     cent = bench.train_centroids(torch, bench.make_deep(torch, 200_000, 96, 0x5EED, 0, dev),
                                  16, 256)
-    pq, rows, parts, counts, tabs, enc, dec = _bench_path_parts(gpu, x, cent)
+    pq, rows, parts, counts, tabs, enc, dec = _bench_path_parts(gpu, x, cent, chunk=BENCH_CHUNK)
     _check_parts_against_oracle(gpu, oracle, x.cpu().numpy(), cent, rows, counts, tabs, enc,
-                                dec, 8)
+                                dec, BENCH_CHUNK)
 
 
 def test_bench_path_deep1m_all_rows(gpu, oracle):

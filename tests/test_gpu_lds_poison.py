@@ -5,7 +5,7 @@ shows up as a wrong result instead of reading zeros or an earlier workgroup's id
 Covers the kernels whose workgroups hand data through LDS: the row decoders (dec_rows: the
 staged stream window with its zero pad, the staged rows), the any-shape decoder
 (dec_chunks), the context histograms (u16-pair counters, multi-round carries) and the
-one-pass encoder (the LDS bit image).  Each result must equal the unpoisoned run, which the
+one-pass encoder (the LDS bit image) and the row sort.  Each result must equal the unpoisoned run, which the
 other test files pin to the oracle (huffman_decode.c:137-191, huffman_encoder.c:166-238)."""
 import ctypes
 
@@ -108,3 +108,19 @@ def test_encode_after_lds_poison(gpu, m):
         assert got.bits == ref.bits
         assert torch.equal(got.stream[:nb], ref.stream[:nb]), hex(value)
         assert torch.equal(got.chunk_offsets, ref.chunk_offsets)
+
+
+@pytest.mark.parametrize("m,n", [(8, 1_000_000), (16, 600_001), (12, 300_007), (3, 200_003)])
+def test_sort_after_lds_poison(gpu, oracle, m, n):
+    """the stable strncmp-key row sort (pqh_sort.hip: the per-chunk key histograms, the
+    pass kernels' LDS digit counters and the next pass's counts) after every CU's LDS is
+    poisoned: the rows equal the oracle's sort (huffman_encoder.c:301-317)"""
+    torch, codec, ctx = gpu
+    codes = datagen.skewed_codes(n, m, seed=100 + m, stay=0)
+    codes[np.random.default_rng(m).random(codes.shape) < 0.25] = 0   # runs of equal keys
+    want = oracle.sort_rows(codes)
+    for value in POISON:
+        rows = torch.from_numpy(np.ascontiguousarray(codes)).cuda()
+        _poison(codec, ctx, value)
+        codec.sort_rows(ctx, rows, torch.empty_like(rows))
+        assert np.array_equal(rows.cpu().numpy(), want), hex(value)

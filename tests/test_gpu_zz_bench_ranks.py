@@ -6,7 +6,6 @@ rank 0 must equal the oracle's one-shot stream over all ranks' rows (huffman_enc
 :207-238 over the concatenated input), and both ranks must exit cleanly (status 0, no
 signal at teardown)."""
 import os
-import socket
 import subprocess
 import sys
 
@@ -18,10 +17,17 @@ from conftest import ROOT, run_fail_msg
 pytestmark = pytest.mark.gpu
 
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+# torchrun's own c10d store binds port 0 and the ranks reuse it (TORCHELASTIC_USE_AGENT_STORE):
+# no port is picked here and released before the launcher binds it.
+_LAUNCH = ["--standalone", "--local-addr=127.0.0.1"]
+
+
+def _check_assignment(oracle, d):
+    """the ranks' part-major assignment (pqh_pq_assign_parts, the bench's timed kernel) equals
+    the oracle's fp32 first-minimum assignment of the same rows (src/pq_encoder.c:270-272)"""
+    want, _ = oracle.pq_assign(d["x"], d["cent"], threads=0)
+    bad = int((d["codes"] != want).sum())
+    assert bad == 0, f"{bad} PQ codes differ from the oracle"
 
 
 @pytest.mark.parametrize("path", ["library", "python"])
@@ -33,7 +39,7 @@ def test_two_rank_rehearsal_stitched_stream(oracle, tmp_path, mode, path):
     dump = tmp_path / "dump.npz"
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           *_LAUNCH,
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
            "--one-device", "--vectors", "30001", "--steps", "3", "--warmup", "1",
            "--mode", mode, "--no-cpu-baseline", "--dump", str(dump), "--shard-path", path]
@@ -42,6 +48,7 @@ def test_two_rank_rehearsal_stitched_stream(oracle, tmp_path, mode, path):
     d = np.load(dump, allow_pickle=False)
     codes = d["codes"]
     assert codes.shape == (60002, 8)
+    _check_assignment(oracle, d)
     cbs = oracle.build_codebooks(codes, 256, mode == "ctx")
     want, bits = oracle.encode(codes, cbs)
     assert int(d["bits"]) == bits
@@ -57,7 +64,7 @@ def test_one_rank_rccl_rehearsal_stream(oracle, tmp_path, groups):
     dump = tmp_path / "dump.npz"
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           *_LAUNCH,
            os.path.join(ROOT, "bench.py"), "--dist-rehearse", "--shard-groups", groups,
            "--vectors", "30001", "--steps", "4", "--warmup", "1", "--no-cpu-baseline",
            "--dump", str(dump)]
@@ -66,6 +73,7 @@ def test_one_rank_rccl_rehearsal_stream(oracle, tmp_path, groups):
     d = np.load(dump, allow_pickle=False)
     codes = d["codes"]
     assert codes.shape == (30001, 8)
+    _check_assignment(oracle, d)
     cbs = oracle.build_codebooks(codes, 256, True)
     want, bits = oracle.encode(codes, cbs)
     assert int(d["bits"]) == bits

@@ -4,7 +4,6 @@ the global histogram must equal the oracle's one-shot results over all ranks' ro
 (huffman_encoder.c:139-238), for even shards, a shard with no rows, and the slices of the
 distributed sort (whose ragged halo also goes through shard.halo_ragged)."""
 import os
-import socket
 import subprocess
 import sys
 
@@ -16,10 +15,9 @@ from conftest import ROOT, run_fail_msg
 pytestmark = pytest.mark.gpu
 
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+# torchrun's own c10d store binds port 0 and the ranks reuse it (TORCHELASTIC_USE_AGENT_STORE):
+# no port is picked here and released before the launcher binds it.
+_LAUNCH = ["--standalone", "--local-addr=127.0.0.1"]
 
 
 @pytest.mark.parametrize("case,mode", [("even", "ctx"), ("even", "noctx"), ("ragged", "ctx"),
@@ -28,7 +26,7 @@ def _free_port():
 def test_two_rank_library_shard_encode(oracle, tmp_path, case, mode):
     dump = tmp_path / "shard.npz"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           *_LAUNCH,
            os.path.join(ROOT, "tests", "shard_worker.py"), "--case", case, "--mode", mode,
            "--out", str(dump)]
     r = subprocess.run(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1"), capture_output=True,
@@ -54,7 +52,7 @@ def test_two_rank_library_shard_encode_one_rank_fails(tmp_path):
     in a collective: rank 1 gets its error, rank 0 PQH_ERR_REMOTE from pqh_shard_status."""
     dump = tmp_path / "shard.npz"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           *_LAUNCH,
            os.path.join(ROOT, "tests", "shard_worker.py"), "--case", "fail", "--mode", "ctx",
            "--out", str(dump)]
     r = subprocess.run(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1"), capture_output=True,

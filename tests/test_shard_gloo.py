@@ -6,9 +6,8 @@ all-gathered bit offset (pqh_shard_offsets), and rank 0 stitches the shard buffe
 (pqh_shard_stitch).  The stitched stream and the reduced histogram must equal the oracle's
 single-process results bit for bit.  The library's host half of the protocol runs here;
 the per-shard bit packer is test code standing in for the GPU encoder, which needs a GPU
-(its two-rank run of the whole library protocol, pqh_shard_encode, is test_gpu_shard.py)."""
+(its two-rank run of the whole library protocol, pqh_shard_encode, is test_gpu_zz_shard.py)."""
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -21,10 +20,11 @@ from pq_huffman_amd import shard
 from tests.datagen import skewed_codes
 
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+def _init(rank, world, store_file):
+    """Rendezvous through a FileStore in the test's tmp_path: no TCP port is picked, released
+    and bound again later (the race a free-port probe leaves open)."""
+    dist.init_process_group("gloo", init_method=f"file://{store_file}", rank=rank,
+                            world_size=world)
 
 
 def _pack(codes, cbs, raw_first, prev_row, bit_off):
@@ -74,10 +74,8 @@ def _local_hist(codes, k, context, prev_row):
     return h
 
 
-def _worker(rank, world, port, n, m, k, context, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _worker(rank, world, store_file, n, m, k, context, q):
+    _init(rank, world, store_file)
     try:
         codes = skewed_codes(n, m, k, seed=11)
         b, e = shard.row_range(n, world, rank)
@@ -111,12 +109,12 @@ def _worker(rank, world, port, n, m, k, context, q):
 
 
 @pytest.mark.parametrize("world,context", [(2, True), (2, False), (3, True)])
-def test_sharded_encode_matches_single_process(world, context):
+def test_sharded_encode_matches_single_process(world, context, tmp_path):
     n, m, k = 301, 4, 256
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, m, k, context, q))
+    store_file = tmp_path / "store"
+    procs = [ctx.Process(target=_worker, args=(r, world, str(store_file), n, m, k, context, q))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -175,10 +173,8 @@ def _local_sort(t):
     return torch.from_numpy(orc.sort_rows(t.numpy())) if t.shape[0] else t
 
 
-def _sort_worker(rank, world, port, kind, n, m, k, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _sort_worker(rank, world, store_file, kind, n, m, k, q):
+    _init(rank, world, store_file)
     try:
         codes = _sort_codes(kind, n, m, k)
         b, e = shard.row_range(n, world, rank)
@@ -213,7 +209,7 @@ def _sort_worker(rank, world, port, kind, n, m, k, q):
 
 @pytest.mark.parametrize("world,kind,m", [(2, "skewed", 8), (3, "zeros", 8), (3, "zeros", 16),
                                           (2, "onekey", 4), (3, "skewed", 3)])
-def test_distributed_sort_mode_matches_single_process(world, kind, m):
+def test_distributed_sort_mode_matches_single_process(world, kind, m, tmp_path):
     """Sample sort across gloo ranks, then the sort+context encode on the sorted slices:
     the concatenated slices equal the oracle's stable strncmp-key sort of all rows, and the
     stitched stream equals the oracle's single-process sort+context stream
@@ -221,8 +217,8 @@ def test_distributed_sort_mode_matches_single_process(world, kind, m):
     n, k = 400, 256
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_sort_worker, args=(r, world, port, kind, n, m, k, q))
+    store_file = tmp_path / "store"
+    procs = [ctx.Process(target=_sort_worker, args=(r, world, str(store_file), kind, n, m, k, q))
              for r in range(world)]
     for p in procs:
         p.start()

@@ -1,7 +1,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/enc
-timeout -k 10 600 python -u -m pytest tests/test_gpu_huffman.py tests/test_gpu_parts.py tests/test_gpu_lds_poison.py tests/test_gpu_shard.py tests/test_gpu_configs.py tests/test_tree.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/enc/tests.log 2>&1 || { tail -40 gpurun_out/enc/tests.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_huffman.py tests/test_gpu_parts.py tests/test_gpu_lds_poison.py tests/test_gpu_zz_shard.py tests/test_gpu_configs.py tests/test_tree.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/enc/tests.log 2>&1 || { tail -40 gpurun_out/enc/tests.log; exit 1; }
 tail -2 gpurun_out/enc/tests.log
 for impl in tiled onepass; do
   for cfg in sift deep; do
