@@ -61,6 +61,11 @@ int pqh_ctx_create_cu_split(pqh_ctx_t** ctx, int device, int cus, int complement
 /* the context's current HIP stream (e.g. for torch.cuda.ExternalStream) */
 void* pqh_ctx_stream(const pqh_ctx_t* ctx);
 int pqh_ctx_destroy(pqh_ctx_t* ctx);
+/* Free the context's grow-only device scratch (workspace, the tiled encoder's tile images,
+ * the one-pass encoder's look-back state, the sort's state) after synchronising its stream;
+ * later calls allocate again as needed.  The largest is the encoder's: ~56 B per encoded
+ * row (one worst-case image per 256-row tile) for pqh_encode_write*. */
+int pqh_ctx_release_scratch(pqh_ctx_t* ctx);
 /* run all later calls on hip_stream, taken literally: NULL is the device's default
  * (legacy, synchronising) stream -- what torch's current stream usually is. */
 int pqh_ctx_set_stream(pqh_ctx_t* ctx, void* hip_stream);
@@ -74,10 +79,14 @@ int pqh_ctx_sync(pqh_ctx_t* ctx);
  *   PQH_TUNE_HIST_SPLIT         the context histogram's split of the previous-symbol range
  *                               (1, 2, 4 or 8): LDS per workgroup = 128 KB / split at K = 256
  *                               (PQH_HIST_SPLIT);
- *   PQH_TUNE_HIST_BLOCK         its workgroup size, 256 or 1024 threads (PQH_HIST_BLOCK).
+ *   PQH_TUNE_HIST_BLOCK         its workgroup size, 256 or 1024 threads (PQH_HIST_BLOCK);
+ *   PQH_TUNE_ENC_IMPL           the whole-stream encoder of pqh_encode_write*: 1 = tiled
+ *                               (tiles in context scratch, scan, placement), 2 = one pass
+ *                               with a decoupled look-back (PQH_ENC_IMPL=onepass).
  * A histogram that runs beside the assignment grid (on another stream) fits best at
  * split 4, 256 threads. */
-enum { PQH_TUNE_ASSIGN_WGS_PER_CU = 1, PQH_TUNE_HIST_SPLIT = 2, PQH_TUNE_HIST_BLOCK = 3 };
+enum { PQH_TUNE_ASSIGN_WGS_PER_CU = 1, PQH_TUNE_HIST_SPLIT = 2, PQH_TUNE_HIST_BLOCK = 3,
+       PQH_TUNE_ENC_IMPL = 4 };
 int pqh_ctx_set_tuning(pqh_ctx_t* ctx, int key, double value);
 const char* pqh_status_string(int status);
 const char* pqh_ctx_last_error(const pqh_ctx_t* ctx);
@@ -221,10 +230,12 @@ int pqh_codebooks_build(const double* counts, int m, int k, int context,
  * set for the shard holding global row 0; other shards pass d_prev_row instead. */
 int pqh_encode_size(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* d_codes, long long n,
                     int raw_first, const void* d_prev_row, unsigned long long* d_total_bits);
-/* Write the stream at bit offset `bit_offset` of d_out in ONE pass (no pqh_encode_size
- * needed): workgroups find their bit offsets by a decoupled look-back and store every word
- * of [bit_offset, bit_offset + bits) exactly once, zero padding the last word -- the buffer
- * needs no zeroing.  Bits of d_out before bit_offset in the first word are kept (they are
+/* Write the stream at bit offset `bit_offset` of d_out (no pqh_encode_size needed): every
+ * word of [bit_offset, bit_offset + bits) is stored exactly once, zero padding the last word
+ * -- the buffer needs no zeroing.  By default 256-row tiles are coded into context scratch
+ * (~56 B per row, grow-only; pqh_ctx_release_scratch frees it), scanned and placed; when that
+ * scratch cannot be allocated (or PQH_ENC_IMPL=onepass) one pass whose workgroups find their
+ * offsets by a decoupled look-back, with O(n / 256) state.  Bits of d_out before bit_offset in the first word are kept (they are
  * merged), so shards written at adjacent offsets into one buffer compose.
  * chunk_vectors > 0 also emits the chunk index: d_chunk_offsets[ceil(n/C)] (bit offsets
  * relative to d_out bit 0) and, in context mode, d_chunk_prev[ceil(n/C)][m] codes.

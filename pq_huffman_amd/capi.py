@@ -118,7 +118,7 @@ SIGNATURES = [
     # pqh.h
     ("pqh_ctx_create", I, [P, I]), ("pqh_ctx_destroy", I, [P]), ("pqh_ctx_set_stream", I, [P, P]),
     ("pqh_ctx_create_cu_limited", I, [P, I, I]), ("pqh_ctx_create_cu_split", I, [P, I, I, I]), ("pqh_ctx_stream", P, [P]),
-    ("pqh_ctx_sync", I, [P]), ("pqh_status_string", S, [I]), ("pqh_ctx_last_error", S, [P]),
+    ("pqh_ctx_sync", I, [P]), ("pqh_ctx_release_scratch", I, [P]), ("pqh_status_string", S, [I]), ("pqh_ctx_last_error", S, [P]),
     ("pqh_device_count", I, [P]),
     ("pqh_pq_create", I, [P, P, I, I, I, P]), ("pqh_pq_destroy", I, [P]),
     ("pqh_pq_assign", I, [P, P, P, LL, LL, P, P, I]),

@@ -83,11 +83,12 @@ class Context:
         self.stream = stream
         check(lib().pqh_ctx_set_stream(self.ptr, ctypes.c_void_p(stream.cuda_stream)))
 
-    TUNE = {"assign_wgs_per_cu": 1, "hist_split": 2, "hist_block": 3}
+    TUNE = {"assign_wgs_per_cu": 1, "hist_split": 2, "hist_block": 3, "enc_impl": 4}
 
     def set_tuning(self, **kw) -> "Context":
         """launch shapes of this context's kernels (pqh_ctx_set_tuning; results never
-        change): assign_wgs_per_cu, hist_split, hist_block -- 0 restores the default"""
+        change): assign_wgs_per_cu, hist_split, hist_block, enc_impl (1 tiled, 2 one-pass)
+        -- 0 restores the default"""
         for key, value in kw.items():
             check(lib().pqh_ctx_set_tuning(self.ptr, self.TUNE[key], float(value)),
                   f"pqh_ctx_set_tuning({key})")
@@ -95,6 +96,10 @@ class Context:
 
     def sync(self) -> None:
         check(lib().pqh_ctx_sync(self.ptr), "pqh_ctx_sync")
+
+    def release_scratch(self) -> None:
+        """free the context's grow-only device scratch (pqh_ctx_release_scratch)"""
+        check(lib().pqh_ctx_release_scratch(self.ptr), "pqh_ctx_release_scratch")
 
     def last_error(self) -> str:
         return (lib().pqh_ctx_last_error(self.ptr) or b"").decode()

@@ -90,8 +90,15 @@ struct Plan {
 // Scores and keys are fp32 values carried as their bit patterns (unsigned) and ordered as
 // floats: a key is a score with its low mantissa bits replaced by an index, which keeps the
 // order of scores whose truncations differ (truncation moves a positive value down and a
-// negative one up, monotonically) and makes every key distinct.  The min/med instructions
-// are written in asm so the compiler neither canonicalises nor reorders them.
+// negative one up, monotonically) and makes every key distinct.
+#ifndef PQH_ASSIGN_ASMMIN
+#define PQH_ASSIGN_ASMMIN 0
+#endif
+#if PQH_ASSIGN_ASMMIN
+// (PQH_ASSIGN_ASMMIN=1, the round-5 form) min/med written in asm so the compiler neither
+// canonicalises nor reorders them.  The compiler cannot tell what an asm VALU is, so it pads
+// the VALU that reads an asm result with an s_nop (a transcendental's forwarding hazard):
+// ~20 per 32-vector block.
 __device__ __forceinline__ unsigned med3u(unsigned a, unsigned b, unsigned c) {
     unsigned r;
     asm("v_med3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
@@ -126,6 +133,32 @@ __device__ __forceinline__ unsigned maxu(unsigned a, unsigned b) {
     asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
     return r;
 }
+#else
+// Compiler-generated gfx950 v_minimum3_f32 / v_maximum3_f32 (IEEE-754 2019 minimum /
+// maximum: NaN-propagating, so unlike fminf they need no canonicalising max before them --
+// checked in the ISA) and v_med3_f32, so the hazard recognizer sees every read: MFMA results
+// get exactly their wait states and no asm result costs an s_nop.  min and max of non-NaN
+// values are exact and order-free (-0 < +0 in both partitions alike), so the compiler's
+// freedom to re-associate them changes no result; a NaN score (non-finite input or
+// overflow) fails the gap test either way and is re-ranked.
+__device__ __forceinline__ unsigned med3u(unsigned a, unsigned b, unsigned c) {
+    return __float_as_uint(
+        __builtin_amdgcn_fmed3f(__uint_as_float(a), __uint_as_float(b), __uint_as_float(c)));
+}
+__device__ __forceinline__ unsigned min3u(unsigned a, unsigned b, unsigned c) {
+    return __float_as_uint(__builtin_elementwise_minimum(
+        __builtin_elementwise_minimum(__uint_as_float(a), __uint_as_float(b)), __uint_as_float(c)));
+}
+__device__ __forceinline__ unsigned min3d(unsigned a, unsigned b, unsigned c, unsigned) {
+    return min3u(a, b, c);
+}
+__device__ __forceinline__ unsigned minu(unsigned a, unsigned b) {
+    return __float_as_uint(__builtin_elementwise_minimum(__uint_as_float(a), __uint_as_float(b)));
+}
+__device__ __forceinline__ unsigned maxu(unsigned a, unsigned b) {
+    return __float_as_uint(__builtin_elementwise_maximum(__uint_as_float(a), __uint_as_float(b)));
+}
+#endif
 
 // min(a, b) of two accumulator values as a compiler-generated instruction (v_med3_f32
 // with -inf: the compiler inserts the MFMA wait states before it) -- the anchor of min3d.

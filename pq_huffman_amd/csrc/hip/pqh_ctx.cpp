@@ -179,6 +179,23 @@ int pqh_ctx_destroy(pqh_ctx_t* ctx) {
     return PQH_OK;
 }
 
+int pqh_ctx_release_scratch(pqh_ctx_t* ctx) {
+    if (!ctx) return PQH_ERR_ARG;
+    PQH_HIP(ctx, hipSetDevice(ctx->device));
+    PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));   // no launch may still use them
+    if (ctx->ws) (void)hipFree(ctx->ws);
+    if (ctx->enc_scr) (void)hipFree(ctx->enc_scr);
+    if (ctx->lb_state) (void)hipFree(ctx->lb_state);
+    if (ctx->sort_state) (void)hipFree(ctx->sort_state);
+    ctx->ws = ctx->enc_scr = nullptr;
+    ctx->ws_bytes = ctx->enc_scr_bytes = 0;
+    ctx->lb_state = nullptr;
+    ctx->lb_cap = 0;
+    ctx->sort_state = nullptr;
+    ctx->sort_cap = 0;
+    return PQH_OK;
+}
+
 int pqh_ctx_set_stream(pqh_ctx_t* ctx, void* hip_stream) {
     if (!ctx) return PQH_ERR_ARG;
     if (ctx->own_stream) {
@@ -206,6 +223,12 @@ int pqh_ctx_set_tuning(pqh_ctx_t* ctx, int key, double value) {
             const int v = (int)value;
             if (v != 0 && v != 256 && v != 1024) return PQH_ERR_ARG;
             ctx->tune_hist_block = v;
+            return PQH_OK;
+        }
+        case PQH_TUNE_ENC_IMPL: {
+            const int v = (int)value;
+            if (v != 0 && v != 1 && v != 2) return PQH_ERR_ARG;
+            ctx->tune_enc_impl = v;
             return PQH_OK;
         }
         default:

@@ -1437,12 +1437,23 @@ static int encode_write_impl(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* 
     // The tiled encoder (default): tiles coded into scratch slots with no inter-workgroup
     // waiting, a scan of their bit counts, then enc_place.  PQH_ENC_IMPL=onepass: the
     // single-kernel decoupled look-back form.
-    static const bool onepass = [] {
+    static const bool onepass_env = [] {
         const char* e = std::getenv("PQH_ENC_IMPL");
         return e && !std::strcmp(e, "onepass");
     }();
-    if (!onepass || phase) {
-        const long long slot = (long long)(lds / 4);   // a tile's worst-case image, + 4 words
+    const bool onepass = ctx->tune_enc_impl ? ctx->tune_enc_impl == 2 : onepass_env;
+    // The tiled encoder's scratch holds one worst-case tile image per 256 rows (56 B per
+    // row, 7 GB at 125M rows).  A whole write (phase 0) that cannot get it falls back to the
+    // one-pass encoder, which needs O(tiles) state; the two-phase shard write keeps its tiles
+    // between the phases, so it has no such fallback and reports PQH_ERR_NOMEM.
+    const long long slot = (long long)(lds / 4);   // a tile's worst-case image, + 4 words
+    bool tiled = !onepass || phase;
+    if (tiled && phase == 0 &&
+        pqh_ensure_enc_scratch(ctx, ((size_t)nb * slot + 64) * 4) == PQH_ERR_NOMEM) {
+        tiled = false;
+        pqh_set_error(ctx, PQH_OK, "");
+    }
+    if (tiled) {
         int rc2 = pqh_ensure_enc_scratch(ctx, ((size_t)nb * slot + 64) * 4);
         if (rc2) return rc2;
         const size_t a = ((size_t)nb * 4 + 255) & ~(size_t)255;

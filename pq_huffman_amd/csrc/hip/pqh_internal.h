@@ -52,6 +52,7 @@ struct pqh_ctx {
     double tune_wgs_per_cu = 0.0;
     int tune_hist_split = 0;
     int tune_hist_block = 0;
+    int tune_enc_impl = 0;   // 1 tiled, 2 one-pass (0: PQH_ENC_IMPL or tiled)
     // the tiled encoder's scratch: one worst-case slot per tile (grow-only)
     void* enc_scr = nullptr;
     size_t enc_scr_bytes = 0;

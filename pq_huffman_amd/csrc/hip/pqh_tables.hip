@@ -1446,7 +1446,7 @@ huff_trees_par(const uint32_t* __restrict__ counts, int k, long long trees,
 __device__ void block_w2max(const unsigned long long* e, int k, int w1, int l2_bits,
                             uint32_t* w2max /* LDS [1 << kL1Max] */) {
     for (int i = threadIdx.x; i < (1 << w1); i += blockDim.x) w2max[i] = 0;
-    __syncthreads();
+    lds_barrier();
     for (int s = threadIdx.x; s < k; s += blockDim.x) {
         const unsigned long long v = e[s];
         const int len = (int)(v >> 56);
@@ -1455,7 +1455,7 @@ __device__ void block_w2max(const unsigned long long* e, int k, int w1, int l2_b
             atomicMax(&w2max[p], (uint32_t)min(len - w1, l2_bits));
         }
     }
-    __syncthreads();
+    lds_barrier();   // (the atomics' results are unused: an explicit LDS wait before the barrier)
 }
 
 // One workgroup per alphabet: size its second level, take the pool range with one atomic
@@ -1468,8 +1468,12 @@ lut_build(const unsigned long long* __restrict__ enc, uint32_t* __restrict__ enc
           int l2_bits, uint32_t* __restrict__ meta, uint16_t* __restrict__ lut1,
           uint16_t* __restrict__ lut2, long long lut2_cap, pqh_long_code* __restrict__ longs,
           uint32_t* __restrict__ long_cnt, unsigned long long* __restrict__ pool_head) {
-    __shared__ uint32_t w2max[1 << kL1Max];
-    __shared__ uint32_t sub_id[1 << kL1Max];
+    // w2max[2^W1], sub_id[2^W1]: dynamic LDS sized by the set's W1 (8 KB at the K = 256
+    // W1 = 9 / 11, 64 KB only at K = 4096's W1 = 13), so a build beside the assignment grid
+    // takes only what its alphabet needs
+    extern __shared__ uint32_t lut_dyn[];
+    uint32_t* const w2max = lut_dyn;
+    uint32_t* const sub_id = lut_dyn + (1 << w1);
     __shared__ uint32_t nlong, nsub, w2s;
     __shared__ unsigned long long base_s;
     __shared__ uint32_t part[256];
@@ -1575,7 +1579,7 @@ lut_build(const unsigned long long* __restrict__ enc, uint32_t* __restrict__ enc
         const uint32_t idx = atomicAdd(&nlong, 1u);
         longs[t * k + idx] = {code, (uint32_t)len, (uint32_t)s};
     }
-    __syncthreads();
+    lds_barrier();
     if (threadIdx.x == 0) long_cnt[t] = nlong;
 }
 
@@ -2171,7 +2175,16 @@ static int launch_luts(pqh_ctx* ctx, pqh_tables* t) {
         return PQH_OK;
     }
     // (the pool head, d_err[2..3], was zeroed with the error word before the trees)
-    hipLaunchKernelGGL(lut_build, dim3((unsigned)t->tables), dim3(256), 0, ctx->stream, t->d_enc,
+    const size_t lds = (size_t)2 * 4 << t->l1_bits;   // w2max + sub_id
+    if (lds > 48 * 1024) {
+        static const bool big = [] {
+            return hipFuncSetAttribute((const void*)lut_build,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)((size_t)2 * 4 << kL1Max)) == hipSuccess;
+        }();
+        if (!big) return pqh_set_error(ctx, PQH_ERR_HIP, "lut_build: dynamic LDS attribute");
+    }
+    hipLaunchKernelGGL(lut_build, dim3((unsigned)t->tables), dim3(256), lds, ctx->stream, t->d_enc,
                        t->enc32_by_trees ? nullptr : t->d_enc32, t->k, t->l1_bits, t->l2_bits, t->d_meta, t->d_lut1, t->d_lut2,
                        t->lut2_cap, t->d_long, t->d_long_cnt,
                        reinterpret_cast<unsigned long long*>(t->d_err + 2));

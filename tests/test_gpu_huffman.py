@@ -652,3 +652,36 @@ def test_context_histogram_multi_round(gpu, oracle, m):
     codec.histogram_partial(ctx, cd[1:], 256, parts, prev_row=cd[0])
     codec.histogram_reduce(ctx, parts, n - 1, m, 256, junk, accumulate=True)
     assert np.array_equal(codec.counts_to_host(junk), 2 * want)
+
+
+@pytest.mark.parametrize("m,k,ctxm", [(8, 256, True), (16, 256, True), (8, 256, False),
+                                      (6, 256, True), (8, 4096, False)])
+def test_onepass_encoder_and_scratch_release(gpu, oracle, m, k, ctxm):
+    """The one-pass look-back encoder (the fallback when the tiled encoder's scratch cannot be
+    allocated; PQH_TUNE_ENC_IMPL = 2) writes the oracle's stream and chunk index, like the
+    tiled default; pqh_ctx_release_scratch frees the scratch and the next encode allocates
+    it again (huffman_encoder.c:207-238, bitstream.c:71-101)."""
+    torch, codec, _ = gpu
+    ctx = codec.Context(0)
+    n = 300_007
+    codes = datagen.skewed_codes(n, m, k=k, seed=140 + m, stay=0)
+    if k > 256:
+        cd = torch.from_numpy(codes.astype(np.uint16).view(np.int16)).cuda()
+    else:
+        cd = torch.from_numpy(np.ascontiguousarray(codes.astype(np.uint8))).cuda()
+    tabs = codec.Tables(ctx, m, k, ctxm).build(codec.histogram(ctx, cd, k, ctxm))
+    ocb = oracle.build_codebooks(codes, k, ctxm)
+    want, bits = oracle.encode(codes, ocb)
+    runs = {}
+    for impl in (2, 1, 2):
+        ctx.set_tuning(enc_impl=impl)
+        enc = codec.encode(ctx, tabs, cd, chunk_vectors=4)
+        assert enc.bits == bits, impl
+        assert enc.stream[:len(want)].cpu().numpy().tobytes() == want, impl
+        runs.setdefault(impl, enc.chunk_offsets.cpu().numpy())
+        assert np.array_equal(runs[impl], enc.chunk_offsets.cpu().numpy())
+        dec = codec.decode(ctx, tabs, enc)
+        codec.decode_status(ctx)
+        assert torch.equal(dec, cd), impl
+        ctx.release_scratch()
+    assert np.array_equal(runs[1], runs[2])
