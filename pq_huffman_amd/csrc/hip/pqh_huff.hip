@@ -749,7 +749,7 @@ __global__ void __launch_bounds__(BLK)
 enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, int context,
             int raw_first, const CodeT* __restrict__ prev_row, const int* __restrict__ d_rawf,
             const unsigned long long* __restrict__ enc, const uint32_t* __restrict__ enc32,
-            long long items,
+            const uint16_t* __restrict__ enc16, long long items,
             unsigned long long bit_offset_arg,
             const unsigned long long* __restrict__ d_bit_offset,
             uint32_t* __restrict__ out_words, long long cap_words,
@@ -825,7 +825,15 @@ enc_onepass(const CodeT* __restrict__ codes, long long n, int m_total, int k, in
                 const unsigned prv = (unsigned)(prow >> (8 * i)) & 0xFFu;
                 const bool ok = cur < (unsigned)k && (!context || prv < (unsigned)k);
                 const unsigned idx = ibase + (unsigned)i * (unsigned)items + (context ? prv * (unsigned)k + cur : cur);
-                ent[i] = raw ? ((8u << 26) | cur) : ok ? enc32[idx] : 0u;
+                // the u16 copy first (half the table bytes in L2), the u32 entry only for
+                // codes longer than 12 bits (escape 0xFFFF)
+                if (enc16) {
+                    const uint32_t h = ok ? (uint32_t)enc16[idx] : 0u;
+                    ent[i] = raw ? ((8u << 26) | cur)
+                                 : h != 0xFFFFu ? ((h >> 12) << 26) | (h & 0xFFFu) : enc32[idx];
+                } else {   // (PQH_ENC16=0: the u32 copy only)
+                    ent[i] = raw ? ((8u << 26) | cur) : ok ? enc32[idx] : 0u;
+                }
             }
 #pragma unroll
             for (int i = 0; i < 8; ++i)
@@ -1442,6 +1450,11 @@ static int encode_write_impl(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* 
         return e && !std::strcmp(e, "onepass");
     }();
     const bool onepass = ctx->tune_enc_impl ? ctx->tune_enc_impl == 2 : onepass_env;
+    static const bool no16 = [] {   // (diagnostic A/B: PQH_ENC16=0 gathers the u32 copy only)
+        const char* e = std::getenv("PQH_ENC16");
+        return e && !std::strcmp(e, "0");
+    }();
+    const uint16_t* const enc16 = no16 ? nullptr : t->d_enc16;
     // The tiled encoder's scratch holds one worst-case tile image per 256 rows (56 B per
     // row, 7 GB at 125M rows).  A whole write (phase 0) that cannot get it falls back to the
     // one-pass encoder, which needs O(tiles) state; the two-phase shard write keeps its tiles
@@ -1485,7 +1498,7 @@ static int encode_write_impl(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* 
         hipLaunchKernelGGL(kf, dim3((unsigned)nb), dim3(B), lds, ctx->stream,                   \
                            static_cast<const T*>(d_codes), R8 ? rows : n, t->m, t->k, t->context, \
                            raw_first, static_cast<const T*>(d_prev_row), d_rawf, t->d_enc,       \
-                           t->d_enc32, t->items, 0ull, nullptr, scr, slot, chunk_vectors,        \
+                           t->d_enc32, enc16, t->items, 0ull, nullptr, scr, slot, chunk_vectors,     \
                            d_chunk_offsets, static_cast<T*>(d_chunk_prev), ctx->d_diag + 2, tb,  \
                            nullptr, nullptr, 0ull, 0u, nb, nullptr, tree_prev, enc_prio, ldc);   \
     } while (0)
@@ -1540,7 +1553,7 @@ static int encode_write_impl(pqh_ctx_t* ctx, const pqh_tables_t* t, const void* 
                            ctx->stream, static_cast<const T*>(d_codes), R8 ? rows : n, t->m, t->k, \
                            t->context, raw_first, static_cast<const T*>(d_prev_row), d_rawf,     \
                            t->d_enc,                                                              \
-                           t->d_enc32, t->items, bit_offset, d_bit_offset, words,                 \
+                           t->d_enc32, enc16, t->items, bit_offset, d_bit_offset, words,           \
                            (long long)(out_bytes / 4),                                            \
                            chunk_vectors, d_chunk_offsets, static_cast<T*>(d_chunk_prev),         \
                            ctx->d_diag + 2, st, tails, ticket, ctx->lb_ticket_base,               \

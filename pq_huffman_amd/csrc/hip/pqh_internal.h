@@ -148,6 +148,13 @@ __device__ __forceinline__ void lds_barrier() {
 
 // PQH_DEBUG_SYNC=1: synchronise and check after every launch, so an asynchronous fault is
 // reported by the call that caused it (diagnostics only).
+// the u16 gather entry of a u64 code-table entry (enc16 above)
+__device__ __forceinline__ uint16_t pqh_enc16_of(unsigned long long e) {
+    const unsigned len = (unsigned)(e >> 56);
+    return len == 0 ? (uint16_t)0 : len <= 12 ? (uint16_t)((len << 12) | (unsigned)(e & 0xFFFu))
+                                              : (uint16_t)0xFFFFu;
+}
+
 bool pqh_debug_sync();
 #define PQH_LAUNCH_CHECK(ctx)                                                             \
     do {                                                                                  \
@@ -158,6 +165,7 @@ bool pqh_debug_sync();
 // Device-side code tables shared by the encode and decode kernels (pqh_tables.hip).
 //   enc [m][items] u64: (len << 56) | code (right-aligned, len <= 56; 0 = no code)
 //   enc32 [m][items] u32: the same entry as len << 26 | code when len <= 26, else ~0u
+//   enc16 [m][items] u16: len << 12 | code when 1 <= len <= 12, 0 (no code), else 0xFFFF
 //   Decode: two-level lookup per alphabet (tables = m * roots, roots = K in context mode)
 //   lut1 [tables][1 << l1_bits] u16 (rows packed at the table set's own W1 = l1_bits, for
 //        every alphabet): (len << 12) | sym for 1 <= len <= W1 (replicated);
@@ -179,6 +187,10 @@ struct pqh_tables {
     long long lut2_cap = 0;
     unsigned long long* d_enc = nullptr;
     uint32_t* d_enc32 = nullptr;     // [m][items] len << 26 | code (len <= 26), else ~0u
+    // [m][items] the encoder's first gather: len << 12 | code for 1 <= len <= 12, 0 = no code,
+    // 0xFFFF = longer (read d_enc32) -- half the bytes of d_enc32, so the context tables of
+    // a 16-part set (2 MB) stay in an XCD's 4 MB L2 beside the streams that pass through it
+    uint16_t* d_enc16 = nullptr;
     bool enc32_by_trees = false;     // the last tree build wrote d_enc32 (the LUT build skips it)
                                      // (escape: read d_enc) -- the encoder's gather table
     uint16_t* d_lut1 = nullptr;

@@ -848,6 +848,7 @@ __device__ __forceinline__ int grp_merge_heavy(unsigned long long* h, const unsi
 // Pointers of the decode tables lut_grp writes (the layout of lut_build, below).
 struct GrpLut {
     uint32_t* enc32;
+    uint16_t* enc16;   // (written with enc32)
     uint16_t* lut1;
     uint16_t* lut2;
     uint32_t* meta;
@@ -867,7 +868,8 @@ huff_trees_grp(const uint32_t* __restrict__ counts, int k, long long trees,
                unsigned long long* __restrict__ enc, uint32_t* __restrict__ err,
                long long trees2, const uint32_t* __restrict__ counts2,
                unsigned long long* __restrict__ enc2, uint32_t* __restrict__ err2, int prio,
-               uint32_t* __restrict__ e32, uint32_t* __restrict__ e32_2) {
+               uint32_t* __restrict__ e32, uint32_t* __restrict__ e32_2,
+               uint16_t* __restrict__ e16, uint16_t* __restrict__ e16_2) {
     // trees [0, trees) from counts -> enc (and the encoder's u32 gather copy e32); a paired
     // build adds [trees, trees + trees2)
     const long long blocks1 = (trees + kGrpTrees - 1) / kGrpTrees;
@@ -876,6 +878,7 @@ huff_trees_grp(const uint32_t* __restrict__ counts, int k, long long trees,
         counts = counts2 + b * kGrpTrees * k;
         enc = enc2 + b * kGrpTrees * k;
         e32 = e32_2 + b * kGrpTrees * k;
+        e16 = e16_2 + b * kGrpTrees * k;
         err = err2;
         trees = trees2 - b * kGrpTrees;
     } else {
@@ -883,6 +886,7 @@ huff_trees_grp(const uint32_t* __restrict__ counts, int k, long long trees,
         counts += (long long)blockIdx.x * kGrpTrees * k;
         enc += (long long)blockIdx.x * kGrpTrees * k;
         e32 += (long long)blockIdx.x * kGrpTrees * k;
+        e16 += (long long)blockIdx.x * kGrpTrees * k;
     }
     __shared__ __attribute__((aligned(16))) char lds[kGrpTrees * kGrpTreeBytes];
     const int lane = threadIdx.x, grp = lane >> 4, gl = lane & 15, gsh = grp * 16;
@@ -976,6 +980,7 @@ huff_trees_grp(const uint32_t* __restrict__ counts, int k, long long trees,
     asm volatile("" : "+v"(grp2));
     unsigned long long* out = enc + (long long)grp2 * k;
     uint32_t* out32 = e32 + (long long)grp2 * k;
+    uint16_t* out16 = e16 + (long long)grp2 * k;
     bool too_long = false;
     for (int s = gl; s < k; s += 16) {
         unsigned long long e = 0;
@@ -991,6 +996,7 @@ huff_trees_grp(const uint32_t* __restrict__ counts, int k, long long trees,
         // tables (lut_grp / lut_build then skip it)
         const unsigned len = (unsigned)(e >> 56);
         out32[s] = len <= 26 ? (uint32_t)((len << 26) | (uint32_t)(e & ((1ull << 26) - 1))) : ~0u;
+        out16[s] = pqh_enc16_of(e);
     }
     if (too_long) atomicOr(err, 1u);
     if (stamp) {
@@ -1093,8 +1099,10 @@ __device__ __forceinline__ void grp_luts(const GrpLut& L, long long t, int k, in
     for (int s = gl; s < k; s += 16) {
         const unsigned long long v = code[s];
         const int len = (int)(v >> 56);
-        if (L.enc32)   // (null: the tree build wrote it)
+        if (L.enc32) {   // (null: the tree build wrote them)
             L.enc32[t * k + s] = len <= 26 ? (uint32_t)(((unsigned long long)len << 26) | (v & kCodeMask)) : ~0u;
+            L.enc16[t * k + s] = pqh_enc16_of(v);
+        }
         if (!len) continue;
         const unsigned long long cbits = v & kCodeMask;
         if (len <= w1) {   // replicated over the 2^(W1 - len) patterns that start with it
@@ -1464,7 +1472,8 @@ __device__ void block_w2max(const unsigned long long* e, int k, int w1, int l2_b
 // subtables differently; the tables they describe are the same.  An alphabet whose range
 // would pass the pool's end keeps only L1: its long codes go to the long list.)
 __global__ void __launch_bounds__(256)
-lut_build(const unsigned long long* __restrict__ enc, uint32_t* __restrict__ enc32, int k, int w1,
+lut_build(const unsigned long long* __restrict__ enc, uint32_t* __restrict__ enc32,
+          uint16_t* __restrict__ enc16, int k, int w1,
           int l2_bits, uint32_t* __restrict__ meta, uint16_t* __restrict__ lut1,
           uint16_t* __restrict__ lut2, long long lut2_cap, pqh_long_code* __restrict__ longs,
           uint32_t* __restrict__ long_cnt, unsigned long long* __restrict__ pool_head) {
@@ -1547,9 +1556,11 @@ lut_build(const unsigned long long* __restrict__ enc, uint32_t* __restrict__ enc
     for (int s = threadIdx.x; s < k; s += blockDim.x) {
         const unsigned long long v = e[s];
         const int len = (int)(v >> 56);
-        if (enc32)   // (null: the tree build wrote it)
+        if (enc32) {   // (null: the tree build wrote them)
             enc32[t * k + s] = len <= 26 ? (uint32_t)(((unsigned long long)len << 26) | (v & kCodeMask))
                                          : ~0u;
+            enc16[t * k + s] = pqh_enc16_of(v);
+        }
         if (!len) continue;
         const unsigned long long code = v & kCodeMask;
         if (len <= w1) {
@@ -2130,6 +2141,7 @@ int pqh_tables_alloc(pqh_ctx_t* ctx, int m, int k, int context, pqh_tables_t** o
                                       kL2BaseMax - 1);
     if (hipMalloc(&t->d_enc, (size_t)m * t->items * 8) != hipSuccess ||
         hipMalloc(&t->d_enc32, (size_t)m * t->items * 4) != hipSuccess ||
+        hipMalloc(&t->d_enc16, (size_t)m * t->items * 2) != hipSuccess ||
         hipMalloc(&t->d_lut1, (size_t)(t->tables << t->l1_bits) * 2 + 16) != hipSuccess ||
         hipMalloc(&t->d_lut2, (size_t)t->lut2_cap * 2) != hipSuccess ||
         hipMalloc(&t->d_meta, (size_t)t->tables * 4 + 16) != hipSuccess ||
@@ -2149,7 +2161,7 @@ int pqh_tables_destroy(pqh_tables_t* t) {
         (void)hipSetDevice(t->ctx->device);
         (void)hipStreamSynchronize(t->ctx->stream);
     }
-    void* bufs[] = {t->d_enc, t->d_enc32, t->d_lut1, t->d_lut2, t->d_meta, t->d_long,
+    void* bufs[] = {t->d_enc, t->d_enc32, t->d_enc16, t->d_lut1, t->d_lut2, t->d_meta, t->d_long,
                     t->d_long_cnt, t->d_err};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -2158,7 +2170,7 @@ int pqh_tables_destroy(pqh_tables_t* t) {
 }
 
 static void launch_lut_grp(pqh_ctx* ctx, pqh_tables* t) {
-    const GrpLut lut{t->enc32_by_trees ? nullptr : t->d_enc32, t->d_lut1, t->d_lut2, t->d_meta, t->d_long, t->d_long_cnt,
+    const GrpLut lut{t->enc32_by_trees ? nullptr : t->d_enc32, t->d_enc16, t->d_lut1, t->d_lut2, t->d_meta, t->d_long, t->d_long_cnt,
                      reinterpret_cast<unsigned long long*>(t->d_err + 2), t->lut2_cap,
                      t->l1_bits, t->l2_bits, pqh_prio("LUTS", 3)};
     hipLaunchKernelGGL(lut_grp, dim3((unsigned)((t->tables + kGrpTrees - 1) / kGrpTrees)), dim3(64),
@@ -2185,7 +2197,7 @@ static int launch_luts(pqh_ctx* ctx, pqh_tables* t) {
         if (!big) return pqh_set_error(ctx, PQH_ERR_HIP, "lut_build: dynamic LDS attribute");
     }
     hipLaunchKernelGGL(lut_build, dim3((unsigned)t->tables), dim3(256), lds, ctx->stream, t->d_enc,
-                       t->enc32_by_trees ? nullptr : t->d_enc32, t->k, t->l1_bits, t->l2_bits, t->d_meta, t->d_lut1, t->d_lut2,
+                       t->enc32_by_trees ? nullptr : t->d_enc32, t->d_enc16, t->k, t->l1_bits, t->l2_bits, t->d_meta, t->d_lut1, t->d_lut2,
                        t->lut2_cap, t->d_long, t->d_long_cnt,
                        reinterpret_cast<unsigned long long*>(t->d_err + 2));
     PQH_LAUNCH_CHECK(ctx);
@@ -2265,7 +2277,7 @@ static int build_trees(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts
                            t->k, trees, t->d_enc, t->d_err, t2 ? t2->tables : 0ll,
                            t2 ? d_counts2 : d_counts, t2 ? t2->d_enc : t->d_enc,
                            t2 ? t2->d_err : t->d_err, pqh_prio("TREES", 3), t->d_enc32,
-                           t2 ? t2->d_enc32 : t->d_enc32);
+                           t2 ? t2->d_enc32 : t->d_enc32, t->d_enc16, t2 ? t2->d_enc16 : t->d_enc16);
         PQH_LAUNCH_CHECK(ctx);
         t->enc32_by_trees = true;
         if (t2) t2->enc32_by_trees = true;

@@ -33,7 +33,8 @@ def main():
     ap.add_argument("--config", default="sift")
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--chunk", type=int, default=8)
+    ap.add_argument("--chunk", type=int, default=4)
+    ap.add_argument("--enc-impl", type=int, default=0, help="PQH_TUNE_ENC_IMPL: 1 tiled, 2 one-pass")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     d, m = (128, 8) if a.config == "sift" else (96, 16)
@@ -42,6 +43,7 @@ def main():
     x = gen(torch, base, d, 0x5EED, 0, dev)
     cent = bench.train_centroids(torch, gen(torch, 200_000, d, 0x5EED, 0, dev), m, 256)
     ctx = codec.Context(0)
+    ctx.set_tuning(enc_impl=a.enc_impl)
     pq = codec.PQ(ctx, cent)
     rows1 = pq.assign(x)
     del x
@@ -71,7 +73,7 @@ def main():
     codec.decode_status(ctx)
     assert torch.equal(dec, rows)
     per = 1e6 / n
-    print(f"{a.config} rows={n} bits/row={bits / n:.2f}  encode_parts {t_pm * 1e3 * per:.1f} us/1M  "
+    print(f"{a.config} impl={a.enc_impl} C={C} rows={n} bits/row={bits / n:.2f}  encode_parts {t_pm * 1e3 * per:.1f} us/1M  "
           f"encode_rows {t_rw * 1e3 * per:.1f} us/1M  decode {t_dec * 1e3 * per:.1f} us/1M", flush=True)
 
 
