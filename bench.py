@@ -1108,7 +1108,11 @@ def main():
                                            ("table lanes" if hist_on_lane else "own"),
                        "histogram_launch": (args.hist_tune if (hist_on_lane or hctx) else
                                             "library default"),
-                       "vectors_per_gpu": n, "d": d, "m": m, "k": k,
+                       "vectors_per_gpu": n, "job_vectors_per_step": world * n,
+                       # which BASELINE.json configuration this line measures (weak scaling:
+                       # every rank encodes its own shard of vectors_per_gpu rows per step)
+                       "baseline_config": baseline_config(args.config, n, world),
+                       "d": d, "m": m, "k": k,
                        "mode": "ctx" if ctxm else "noctx",
                        "chunk_vectors": args.chunk, "parallelism": f"dp{world} row shards"
                        + (" (--dist-rehearse: the multi-rank pipeline and its collectives at "
@@ -1176,6 +1180,10 @@ def main():
             # here; huffman_indices.bin itself is unchanged): offset + context row per chunk
             "chunk_index_bytes_per_vector": round((8 + (m * code_bytes if ctxm else 0))
                                                   / args.chunk, 3),
+            # what a stored batch occupies with its decode index: the stream plus the chunk
+            # index (the index is the price of the short decode chains that --chunk buys)
+            "stream_plus_index_bytes_per_vector": round(
+                bits_per_vec / 8 + (8 + (m * code_bytes if ctxm else 0)) / args.chunk, 3),
             "rerank_fraction": round(rerank / (n * m), 6),
         }
         if world == 1:
@@ -1208,6 +1216,21 @@ def main():
     if multi:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def baseline_config(config, n, world):
+    """the BASELINE.json configuration a bench line measures"""
+    if config == "deep":
+        return "configs[3] (Deep-style 96-d, M=16)" + (f", {world} ranks" if world > 1 else "")
+    if config == "k4096":
+        return "configs[4] (K=4096)" + (f", {world} ranks" if world > 1 else "")
+    if n >= 125_000_000:
+        return (f"configs[2] per-rank shard (1B rows / 8 GPUs = 125M per rank); {world} rank(s) "
+                f"x {n:,} rows = {world * n:,} rows per step")
+    if world == 1:
+        return "configs[1] (SIFT1M: 1M x 128-d, M=8, K=256) -- the headline"
+    return (f"configs[1] weak-scaled: {world} ranks x {n:,} rows per step; configs[2]'s "
+            "1B-row job is this path at --vectors 125000000 per rank")
 
 
 def _cpu_name():
