@@ -1,0 +1,7 @@
+# The driver's round-end GPU checks, as it runs them: the whole -m gpu suite, then smoke()
+set -o pipefail
+cd $GRAFT_REPO_ROOT; O=gpurun_out/r6/final; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests/ -x -q -m gpu --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
