@@ -1111,7 +1111,8 @@ def main():
                        "vectors_per_gpu": n, "job_vectors_per_step": world * n,
                        # which BASELINE.json configuration this line measures (weak scaling:
                        # every rank encodes its own shard of vectors_per_gpu rows per step)
-                       "baseline_config": baseline_config(args.config, n, world),
+                       "baseline_config": baseline_config(args.config, n, world,
+                                                          args.dist_rehearse),
                        "d": d, "m": m, "k": k,
                        "mode": "ctx" if ctxm else "noctx",
                        "chunk_vectors": args.chunk, "parallelism": f"dp{world} row shards"
@@ -1218,8 +1219,11 @@ def main():
         dist.destroy_process_group()
 
 
-def baseline_config(config, n, world):
+def baseline_config(config, n, world, rehearse=False):
     """the BASELINE.json configuration a bench line measures"""
+    if rehearse and world == 1:
+        return ("the multi-rank pipeline rehearsed with one rank (--dist-rehearse) on "
+                + baseline_config(config, n, 8 if n < 125_000_000 else 1))
     if config == "deep":
         return "configs[3] (Deep-style 96-d, M=16)" + (f", {world} ranks" if world > 1 else "")
     if config == "k4096":
