@@ -1,5 +1,5 @@
 # Assignment-only timing of diagnostic builds (tools/build_assign_variant.sh) against the default:
-#   bash tools/gpu_r6_diag.sh <variant> ...
+#   bash tools/gpu_assign_variants.sh <variant> ...
 set -o pipefail
 cd $GRAFT_REPO_ROOT; O=gpurun_out/r6/diag; mkdir -p $O
 for r in 1 2; do

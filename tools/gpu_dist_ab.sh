@@ -1,5 +1,5 @@
 # One-rank RCCL rehearsal of the multi-rank pipeline against the one-rank pipeline:
-#   bash tools/gpu_r6_dist.sh [steps ...]
+#   bash tools/gpu_dist_ab.sh [steps ...]
 set -o pipefail
 cd $GRAFT_REPO_ROOT; O=gpurun_out/r6/dist; mkdir -p $O
 for r in 1 2; do

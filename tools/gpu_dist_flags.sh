@@ -1,5 +1,5 @@
 # One-rank RCCL rehearsal (bench.py --dist-rehearse) flag variants at 20 steps, two rounds:
-#   bash tools/gpu_r6_distflags.sh "label:flags" ...
+#   bash tools/gpu_dist_flags.sh "label:flags" ...
 set -o pipefail
 cd $GRAFT_REPO_ROOT; O=gpurun_out/r6/distflags; mkdir -p $O
 for r in 1 2; do

@@ -1,5 +1,5 @@
 # bench.py flag variants at the driver's 20 steps / 5 warmup, three rounds, interleaved:
-#   bash tools/gpu_r6_flags.sh "label:flags" ...     (NAME=VALUE words go to the environment)
+#   bash tools/gpu_flags.sh "label:flags" ...     (NAME=VALUE words go to the environment)
 set -o pipefail
 cd $GRAFT_REPO_ROOT; O=gpurun_out/r6/flags; mkdir -p $O
 for r in 1 2 3; do

@@ -1,4 +1,4 @@
-# Stage timeline of the 125M-row shard bench (configs[2] per rank): bash tools/gpu_r6_tl125.sh [steps]
+# Stage timeline of the 125M-row shard bench (configs[2] per rank): bash tools/gpu_timeline_125m.sh [steps]
 set -o pipefail
 cd $GRAFT_REPO_ROOT; O=gpurun_out/r6/tl125; mkdir -p $O
 S=${1:-3}
