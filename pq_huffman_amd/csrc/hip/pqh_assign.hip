@@ -203,6 +203,25 @@ __device__ __forceinline__ unsigned q_code_bits(int j) {
     return (unsigned)((j & 3) | ((j & 4) << 1));
 }
 
+// The running smallest (m1) and second smallest (m2 >= m1) keys after two more distinct keys
+// (3 VALU instead of two med3 + min folds): the new minimum is min3(m1, k0, k1); the new
+// second is the smaller of m2 and the second smallest of {m1, k0, k1} -- the minimum of the
+// four values lies in {m1, k0, k1}, and the rest's smallest is either that triple's second or
+// m2.
+#ifndef PQH_ASSIGN_FOLD4
+__device__ __forceinline__ void fold2(unsigned& m1, unsigned& m2, unsigned k0, unsigned k1) {
+    m2 = minu(med3u(m1, k0, k1), m2);
+    m1 = min3u(m1, k0, k1);
+}
+#else   // (the round-5 form, 4 VALU: A/B builds)
+__device__ __forceinline__ void fold2(unsigned& m1, unsigned& m2, unsigned k0, unsigned k1) {
+    m2 = med3u(m1, m2, k0);
+    m1 = minu(m1, k0);
+    m2 = med3u(m1, m2, k1);
+    m1 = minu(m1, k1);
+}
+#endif
+
 // Smallest and second smallest of 8 distinct keys (10 VALU): two triples and a pair give
 // their (min, second); every key but the overall minimum is >= one of the three seconds or
 // is the second smallest of the three minima, and each of those is a key other than the
@@ -783,10 +802,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
                 pm1[b] = minu(k0, k1);
                 pm2[b] = maxu(k0, k1);
             } else {
-                pm2[b] = med3u(pm1[b], pm2[b], k0);
-                pm1[b] = minu(pm1[b], k0);
-                pm2[b] = med3u(pm1[b], pm2[b], k1);
-                pm1[b] = minu(pm1[b], k1);
+                fold2(pm1[b], pm2[b], k0, k1);
             }
             // Q: running minima of the register pairs (j, j + 8)
 #pragma unroll
@@ -818,10 +834,7 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
                 // P index 2s + g = t - 1 + g (7 bits)
                 const unsigned k0 = (w0 & keymask) | opaque_s32(t - 1);
                 const unsigned k1 = (w1 & keymask) | opaque_s32(t);
-                pm2[b] = med3u(pm1[b], pm2[b], k0);
-                pm1[b] = minu(pm1[b], k0);
-                pm2[b] = med3u(pm1[b], pm2[b], k1);
-                pm1[b] = minu(pm1[b], k1);
+                fold2(pm1[b], pm2[b], k0, k1);
 #pragma unroll
                 for (int j = 0; j < 8; ++j) qh[b][j] = min3d(qh[b][j], a[j], a[j + 8], e1);
             }
