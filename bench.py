@@ -1134,10 +1134,13 @@ def main():
                          # HBM read roofline); `measured_limiter`: what the PMC counters show
                          # limits the kernel
                          "bound": "hbm",
-                         "measured_limiter": "dependency waits: each tile's VALU top-2 "
-                                             "reduction on its MFMA results at 2.5 waves per "
-                                             "SIMD (VALU + MFMA issue fill ~37 % of the SIMD "
-                                             "time) -- not HBM",
+                         "measured_limiter": "VALU issue: the exact top-2 reduction costs "
+                                             "~1 VALU per score (270 VALU per 32-vector block, "
+                                             "profiles/r6_assign_sq.txt); alone the kernel runs "
+                                             "at ~74 % of its VALU-issue bound, and in the "
+                                             "schedule it shares the SIMDs with the side "
+                                             "kernels -- not HBM (traffic 1.05x the "
+                                             "algorithmic bytes)",
                          "mfma_tflops_algorithmic": round(tf, 1),
                          # of the dense bf16 peak (~2.5 PF/s); each fp32 product costs two or
                          # three bf16 MFMA passes (the hi/lo split), so issued MFMA work is 2-3x
