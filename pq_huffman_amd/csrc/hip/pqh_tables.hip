@@ -1921,6 +1921,34 @@ struct BitRd {   // MSB-first reader over words [0, lim] (32-bit indices)
     }
 };
 
+// The LDS window's reader: the window holds the stream words already byte-swapped (MSB-first
+// as integers, done once when they are staged), and the reader keeps only the bit position, so
+// a peek is one two-word LDS read and a funnel shift and a skip one add (the 64-bit buffer of
+// BitRd costs ~17 VALU per skip: the refill's shifts and selects).  Words past `lim` read as
+// the last one (the window's zero pad).
+struct PosRd {
+    const uint32_t* w;
+    uint32_t lim;
+    uint32_t pos;
+    __device__ __forceinline__ uint32_t word(uint32_t i) const { return w[min(i, lim)]; }
+    __device__ __forceinline__ void init(unsigned long long p) { pos = (uint32_t)p; }
+    __device__ __forceinline__ uint32_t peek(int nb) const {   // 1 <= nb <= 32
+        // words i and i + 1 in one ds_read2 (i clamped so both are in [0, lim]: past the
+        // window's data both are its zero pad), then one 64-bit shift
+        const uint32_t i = min(pos >> 5, lim - 1);
+        const unsigned long long ab = ((unsigned long long)w[i] << 32) | w[i + 1];
+        return (uint32_t)((ab << (pos & 31u)) >> 32) >> (32 - nb);
+    }
+    __device__ __forceinline__ void skip(int nb) { pos += (uint32_t)nb; }
+    __device__ __forceinline__ unsigned long long peek56() const {   // the next 56 bits
+        const uint32_t i = pos >> 5;
+        const int o = (int)(pos & 31u);
+        const unsigned long long hi = ((unsigned long long)word(i) << 32) | word(i + 1);
+        const unsigned long long lo = word(i + 2);
+        return (o ? ((hi << o) | (lo >> (32 - o))) : hi) >> 8;
+    }
+};
+
 // codes beyond both table levels: linear search of the alphabet's long list against the
 // next 56 stream bits; returns len << 16 | sym, or 0 if none matches (inlined: a call would
 // cost the kernel its register budget)
@@ -1946,8 +1974,60 @@ struct Row8Tabs {
 };
 
 // one symbol of alphabet tab, or -1 (invalid)
-template <bool LDS>
-__device__ __forceinline__ int dec_sym8(BitRd<LDS>& br, const Row8Tabs& T, unsigned tab) {
+#ifndef PQH_DEC_SYM_OLD
+// A wave decodes 64 chains in lock step, so a branch taken by any lane costs every lane: with
+// W1 = 9 about 3 % of a SIFT batch's symbols are longer than the first level, so 87 % of the
+// wave's symbol steps run the second level.  This form keeps that path short: the alphabet's
+// meta word is loaded with the first-level entry (8 KB per table set: cache-resident), so the
+// second level is one dependent load, and every path but the long list ends in the same
+// single skip.  Same results as the round-5 form (PQH_DEC_SYM_OLD).
+template <typename Rd>
+__device__ __forceinline__ int dec_sym8(Rd& br, const Row8Tabs& T, unsigned tab) {
+    const int w1 = T.w1;
+    const uint32_t mt = T.meta[tab];
+    const uint32_t p32 = br.peek(32);   // (>= 33 bits are buffered; W1 + w2 <= 25)
+    const uint16_t e = T.lut1[(tab << w1) + (p32 >> (32 - w1))];
+    // (both loads complete here: without this the compiler sinks the meta load into the
+    // second-level branch, behind the first-level load's result)
+    asm volatile("" ::"v"(mt), "v"(e));
+    const int len = e >> 12;
+    unsigned sym = e & 0xFFFu;
+    int adv = -1;   // bits to skip; 0: the long list; -1: invalid
+    if (len >= 1 && len <= w1) {
+        adv = len;
+    } else if (len == 15) {
+        adv = 0;
+        if (sym != 0xFFFu) {   // second level
+            const int w2 = (int)((mt >> 4) & 15u);
+            const long long li = (long long)(mt >> 9) + ((long long)sym << w2) +
+                                 ((p32 >> (32 - w1 - w2)) & ((1u << w2) - 1u));
+            adv = -1;
+            if (w2 >= 1 && !(mt & 0x100u) && li < T.lut2_cap) {
+                const uint16_t e2 = T.lut2[li];
+                const int len2 = e2 >> 12;
+                if (len2 >= 1 && len2 <= w2) {
+                    adv = w1 + len2;
+                    sym = e2 & 0xFFFu;
+                } else if (len2 == 15) {
+                    adv = 0;
+                }
+            }
+        }
+    }
+    if (adv == 0) {   // codes beyond both levels: the alphabet's long list
+        const uint32_t f = dec_long(T.longs + (long long)tab * T.k, T.long_cnt[tab], br.peek56());
+        if (!f) return -1;
+        for (int nb = (int)(f >> 16); nb > 0; nb -= 32) br.skip(nb < 32 ? nb : 32);
+        sym = f & 0xFFFFu;
+        return sym < (unsigned)T.k ? (int)sym : -1;
+    }
+    if (adv < 0) return -1;
+    br.skip(adv);
+    return sym < (unsigned)T.k ? (int)sym : -1;
+}
+#else
+template <typename Rd>
+__device__ __forceinline__ int dec_sym8(Rd& br, const Row8Tabs& T, unsigned tab) {
     const int w1 = T.w1;
     const uint16_t e = T.lut1[(tab << w1) + br.peek(w1)];
     const int len = e >> 12;
@@ -1979,6 +2059,8 @@ __device__ __forceinline__ int dec_sym8(BitRd<LDS>& br, const Row8Tabs& T, unsig
     return sym < (unsigned)T.k ? (int)sym : -1;
 }
 
+#endif
+
 // One lane's chunk: rows of NW u64 words, SB-bit symbols packed little-end first (SB = 8:
 // u8 codes, 8 NW parts; SB = 16: u16 codes, 4 NW parts), so a row is decoded into NW
 // registers, staged in LDS and stored whole; the context row is those registers.
@@ -1990,7 +2072,11 @@ __device__ __forceinline__ bool dec_row_lane(const uint32_t* src, uint32_t lim,
                                              const Row8Tabs& T, unsigned long long* st) {
     constexpr int PW = 64 / SB;   // parts per word
     constexpr unsigned SMASK = (1u << SB) - 1u;
-    BitRd<LDS> br{src, lim, 0, 0, 0};
+    // (LDS: the window's words are byte-swapped when staged; global: BitRd swaps per load)
+    using Rd = typename std::conditional<LDS, PosRd, BitRd<false>>::type;
+    Rd br{};
+    br.w = src;
+    br.lim = lim;
     br.init(start);
     const long long v0 = j * chunk_vectors;
     const int cnt = (int)min((long long)chunk_vectors, n - v0);
@@ -2070,7 +2156,7 @@ dec_rows(const uint32_t* __restrict__ words, long long nwords, long long n, int 
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const long long w = w0 + u * 64 + lane;
-                if (w < nw) win[w] = r[u];
+                if (w < nw) win[w] = __builtin_bswap32(r[u]);   // (MSB-first: PosRd)
             }
         }
         if (lane < 4) win[nw + lane] = 0;   // zero pad read past the window
