@@ -420,6 +420,7 @@ __device__ __forceinline__ void build_b(const float* xh, const float* xl, int h,
 // (xh = bf16(x), xl = bf16(x - xh)), with packed conversions; xl only when LO.
 template <int D, bool LO>
 __device__ __forceinline__ void make_b(const float* xs, int h, bf16x8* Bm, bf16x8* Bl) {
+    using P = Plan<D>;
     if constexpr (Slice<D>::HALF) {
         typedef float f32x8 __attribute__((ext_vector_type(8)));
         constexpr int NP = Slice<D>::NP;
@@ -435,6 +436,55 @@ __device__ __forceinline__ void make_b(const float* xs, int h, bf16x8* Bm, bf16x
 #pragma unroll
                 for (int j = 0; j < 8; ++j) rem[j] = xs[8 * p + j] - (float)Bm[p][j];
                 Bl[p] = __builtin_convertvector(rem, bf16x8);
+            }
+        }
+    } else if constexpr (D % 2 == 0) {
+        // Even D without the half split (Deep's dsub 6): every B slot pair (2w, 2w + 1) of a
+        // pass holds a pair of consecutive dims (d, d + 1), d even, or zeros, so the lane
+        // converts its D/2 dim pairs once (packed v_cvt_pk_bf16_f32) and picks each word for its
+        // half-wave with one select: D/2 + 4 VALU per pass instead of a convert and a select
+        // per slot.  The same bf16 values as build_b (round to nearest even both ways).
+        typedef float f32x2 __attribute__((ext_vector_type(2)));
+        typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        constexpr int NQ = D / 2;
+        unsigned ph[NQ], pl[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const f32x2 v = {xs[2 * q], xs[2 * q + 1]};
+            const bf16x2 hb = __builtin_convertvector(v, bf16x2);
+            ph[q] = __builtin_bit_cast(unsigned, hb);
+            if constexpr (LO) {
+                const f32x2 r = {xs[2 * q] - (float)hb[0], xs[2 * q + 1] - (float)hb[1]};
+                pl[q] = __builtin_bit_cast(unsigned, __builtin_convertvector(r, bf16x2));
+            }
+        }
+        // main-layout word of slot s (even): dims s, s + 1 (s < D), again for the x . cl
+        // half (D <= s < 2D), else zero
+        auto mword = [&](int s) -> unsigned {
+            return s < D ? ph[s / 2] : s < 2 * D ? ph[(s - D) / 2] : 0u;
+        };
+#pragma unroll
+        for (int p = 0; p < P::PM; ++p) {
+            u32x4 wv;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const unsigned v0 = mword(16 * p + 2 * w), v1 = mword(16 * p + 8 + 2 * w);
+                wv[w] = h ? v1 : v0;
+            }
+            Bm[p] = __builtin_bit_cast(bf16x8, wv);
+        }
+        if constexpr (LO) {
+#pragma unroll
+            for (int p = 0; p < P::PL; ++p) {
+                u32x4 wv;
+#pragma unroll
+                for (int w = 0; w < 4; ++w) {
+                    const int s0 = 16 * p + 2 * w, s1 = 16 * p + 8 + 2 * w;
+                    const unsigned v0 = s0 < D ? pl[s0 / 2] : 0u, v1 = s1 < D ? pl[s1 / 2] : 0u;
+                    wv[w] = h ? v1 : v0;
+                }
+                Bl[p] = __builtin_bit_cast(bf16x8, wv);
             }
         }
     } else {
