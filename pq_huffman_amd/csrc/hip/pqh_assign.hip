@@ -723,6 +723,9 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
     };
     // the same slices into xst[wave][slot] by LDS DMA (16 bytes per lane and piece)
     auto load_x_lds = [&](int b, int slot) {
+#ifdef PQH_ASSIGN_NOMEM   // diagnostic: every chunk re-reads the first 64 blocks (cache hits)
+        b &= 63;
+#endif
         long long row0 = (long long)b * 32;
         unsigned off = xlane_off;
         if (b >= nfull) {
