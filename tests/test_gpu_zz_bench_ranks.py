@@ -1,10 +1,11 @@
-"""The multi-rank bench schedule on one GPU (gloo process group, every rank on cuda:0):
-two ranks run bench.py's real lane schedule -- the library's two-phase pqh_shard_encode, or
+"""bench.py itself, run as a child process, against the oracle: the multi-rank schedule on one
+GPU (gloo process group, every rank on cuda:0) -- the library's two-phase pqh_shard_encode, or
 the Python composition (halo all-gather, histogram all-reduce, device bit offsets,
-encode_write_at) -- as fresh child processes; the shards' streams stitched on
-rank 0 must equal the oracle's one-shot stream over all ranks' rows (huffman_encoder.c
-:207-238 over the concatenated input), and both ranks must exit cleanly (status 0, no
-signal at teardown)."""
+encode_write_at) -- whose shards' streams stitched on rank 0 must equal the oracle's one-shot
+stream over all ranks' rows (huffman_encoder.c:207-238 over the concatenated input); the
+multi-rank pipeline over RCCL with one rank; and the one-rank headline schedule itself.  Every
+run dumps its rows and centroids, so the codes are checked against the oracle's assignment
+too, and every rank must exit cleanly (status 0, no signal at teardown)."""
 import os
 import subprocess
 import sys
@@ -78,3 +79,27 @@ def test_one_rank_rccl_rehearsal_stream(oracle, tmp_path, groups):
     want, bits = oracle.encode(codes, cbs)
     assert int(d["bits"]) == bits
     assert d["stream"].tobytes() == want
+
+
+@pytest.mark.parametrize("config,mode", [("sift", "ctx"), ("deep", "ctx"), ("sift", "noctx")])
+def test_one_rank_bench_stream(oracle, tmp_path, config, mode):
+    """bench.py exactly as the headline runs it at one rank (no process group: stream A's
+    part-major assignment, the histogram and code tables on the table lanes, the part-major
+    encoder and the decoder on the encode stream, 4-vector chunks), on a small batch: its last
+    batch's codes equal the oracle's assignment and its stream the oracle's encoding of them
+    (src/pq_encoder.c:270-272, src/huffman_encoder.c:207-238)."""
+    dump = tmp_path / "dump.npz"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", config, "--mode", mode,
+           "--vectors", "30001", "--steps", "3", "--warmup", "1", "--no-cpu-baseline",
+           "--device-warmup-ms", "0", "--dump", str(dump)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, run_fail_msg(r)
+    d = np.load(dump, allow_pickle=False)
+    codes = d["codes"]
+    assert codes.shape == (30001, 16 if config == "deep" else 8)
+    _check_assignment(oracle, d)
+    cbs = oracle.build_codebooks(codes, 256, mode == "ctx")
+    want, bits = oracle.encode(codes, cbs)
+    assert int(d["bits"]) == bits
+    assert d["stream"].tobytes() == want
+
