@@ -381,5 +381,5 @@ def test_cli_pq_encoder_compute_error_streams(gpu, oracle, tmp_path):
     want_codes, _ = oracle.pq_assign(x, cent, threads=0)
     assert np.array_equal(codes, want_codes)
     one_err = codec.PQ(ctx, cent).error(torch.from_numpy(x).cuda(),
-                                        torch.from_numpy(np.ascontiguousarray(codes)).cuda())
+                                        torch.from_numpy(codes.copy()).cuda())
     assert (tmp_path / "pq_error").read_text() == "%f\n" % one_err
