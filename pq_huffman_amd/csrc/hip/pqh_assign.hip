@@ -896,6 +896,36 @@ pq_assign_mfma(const float* __restrict__ x, long long n, long long ldx, int m_to
         // right after its tile-t keys are reduced, so it runs while the other block's keys
         // are (the scheduling barriers keep the compiler from sinking the chain behind them).
         f32x16 acc[kNB];
+#ifdef PQH_ASSIGN_PF2
+        // experiment: A fragments and ||c||^2 read two tiles ahead (double-buffered operands)
+        if constexpr (kLdsA) {
+            bf16x8 a[2][P::PA];
+            f32x16 cn[2];
+            load_a(0, a[0]);
+            cn[0] = tile_norms(Cn, 0, h);
+            load_a(1, a[1]);
+            cn[1] = tile_norms(Cn, 1, h);
+#pragma unroll
+            for (int b = 0; b < kNB; ++b) acc[b] = tile_scores_a<D>(a[0], Bm[b], Bl[b], LO, cn[0]);
+#pragma unroll
+            for (int t = 0; t < KT; ++t) {
+                // buffer t & 1 (tile t) was consumed by MFMAs already issued: refill it with
+                // tile t + 2 while tile t + 1's MFMAs read the other buffer
+                if (t + 2 < KT) {
+                    load_a(t + 2, a[t & 1]);
+                    cn[t & 1] = tile_norms(Cn, t + 2, h);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int b = 0; b < kNB; ++b) {
+                    reduce(acc[b], t, b, t == 0);
+                    if (t + 1 < KT)
+                        acc[b] = tile_scores_a<D>(a[(t + 1) & 1], Bm[b], Bl[b], LO, cn[(t + 1) & 1]);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        } else
+#endif
         if constexpr (kLdsA) {
             bf16x8 a[P::PA];
             load_a(0, a);
