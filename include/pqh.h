@@ -211,7 +211,9 @@ int pqh_tables_upload(pqh_ctx_t* ctx, pqh_tables_t* tables, const huffman_codebo
 /* alloc + upload */
 int pqh_tables_create(pqh_ctx_t* ctx, const huffman_codebook_t* codebooks, int m,
                       pqh_tables_t** tables);
-/* Synchronises; PQH_ERR_CODE_TOO_LONG if the last build produced a code > 56 bits. */
+/* Synchronises; PQH_ERR_CODE_TOO_LONG if a GPU build of these tables since the last call
+ * produced a code > 56 bits (the error is sticky until read here: a build issues no
+ * zeroing dispatch of its own). */
 int pqh_tables_status(pqh_ctx_t* ctx, const pqh_tables_t* tables);
 /* Synchronises; fills m caller-provided structs with malloc'd host codebooks equal to the
  * tables (free with huffman_codebook_destroy) -- for huffman_codebook_save and stats. */
@@ -283,7 +285,8 @@ int pqh_decode(pqh_ctx_t* ctx, const pqh_tables_t* t, const unsigned char* d_str
                unsigned long long stream_bytes, long long n, int raw_first, int chunk_vectors,
                const unsigned long long* d_chunk_offsets, const void* d_chunk_prev,
                void* d_codes);
-/* Synchronises; PQH_ERR_CORRUPT if the last pqh_decode met an invalid code. */
+/* Synchronises; PQH_ERR_CORRUPT if a pqh_decode / pqh_decode_tree on this context since
+ * the last call met an invalid code (sticky until read here, like pqh_encode_status). */
 int pqh_decode_status(pqh_ctx_t* ctx);
 /* Build the chunk index of an existing stream (one produced without a sidecar, e.g. by
  * the reference encoder) with a sequential table walk on the HOST copy of the stream

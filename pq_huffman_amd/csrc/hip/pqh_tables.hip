@@ -405,6 +405,14 @@ __device__ __forceinline__ void wave_sync_lds() {
 // by pointer jumping over the tree (code(v) = code(anc) << len | bits) -- eight parallel
 // rounds instead of a serial walk from the root.
 constexpr int kTreeWaves = 4;
+// A tree build's first workgroup of each table set zeroes that set's LUT pool head
+// (d_err[2..3]), which the decode-table build that follows it allocates from: no memset
+// dispatch in front of the build.  The error word d_err[0] is sticky until
+// pqh_tables_status reads it.
+__device__ __forceinline__ void reset_pool_head(uint32_t* err) {
+    *reinterpret_cast<unsigned long long*>(err + 2) = 0ull;
+}
+
 __global__ void __launch_bounds__(64 * kTreeWaves)
 huff_trees_wave(const uint32_t* __restrict__ counts, int k, long long trees,
                 unsigned long long* __restrict__ enc, uint32_t* __restrict__ err) {
@@ -413,6 +421,7 @@ huff_trees_wave(const uint32_t* __restrict__ counts, int k, long long trees,
     __shared__ uint32_t s_al[kTreeWaves][512];                // anc | len << 16
     __shared__ unsigned long long s_code[kTreeWaves][512];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (blockIdx.x == 0 && threadIdx.x == 0) reset_pool_head(err);
     const long long tree = (long long)blockIdx.x * kTreeWaves + w;
     if (tree >= trees) return;   // no workgroup barriers below
     const uint32_t* cnt = counts + tree * k;
@@ -559,7 +568,9 @@ huff_trees_small(const uint32_t* __restrict__ counts, int k, long long trees,
         enc = enc2 + b * TPW * k;
         err = err2;
         trees = trees2 - b * TPW;
+        if (b == 0 && threadIdx.x == 0) reset_pool_head(err);
     } else {
+        if (blockIdx.x == 0 && threadIdx.x == 0) reset_pool_head(err);
         trees -= (long long)blockIdx.x * TPW;
         counts += (long long)blockIdx.x * TPW * k;
         enc += (long long)blockIdx.x * TPW * k;
@@ -873,6 +884,8 @@ huff_trees_grp(const uint32_t* __restrict__ counts, int k, long long trees,
     // trees [0, trees) from counts -> enc (and the encoder's u32 gather copy e32); a paired
     // build adds [trees, trees + trees2)
     const long long blocks1 = (trees + kGrpTrees - 1) / kGrpTrees;
+    if (((long long)blockIdx.x == 0 || (long long)blockIdx.x == blocks1) && threadIdx.x == 0)
+        reset_pool_head((long long)blockIdx.x == 0 ? err : err2);
     if ((long long)blockIdx.x >= blocks1) {
         const long long b = (long long)blockIdx.x - blocks1;
         counts = counts2 + b * kGrpTrees * k;
@@ -1148,6 +1161,7 @@ huff_trees(const uint32_t* __restrict__ counts, int k, long long trees,
     uint32_t* lcnt_all = kid_all + KMAX * TPW;
     uint16_t* lsym_all = reinterpret_cast<uint16_t*>(lcnt_all + KMAX * TPW);
     const int t = threadIdx.x;
+    if (blockIdx.x == 0 && t == 0) reset_pool_head(err);
     if (KMAX <= 256) {   // the whole workgroup fills the sentinel-heap slots (ncode region)
         uint4* z = reinterpret_cast<uint4*>(ncode_all);
         for (int q = t; q < 2 * KMAX * TPW / 2; q += blockDim.x)
@@ -1338,6 +1352,8 @@ huff_trees_par(const uint32_t* __restrict__ counts, int k, long long trees,
         enc = enc2 - trees * k;
         err = err2;
     }
+    if (((long long)blockIdx.x == 0 || (long long)blockIdx.x == trees) && threadIdx.x == 0)
+        reset_pool_head(err);
     using Key = ParHeap::Key;
     // 104 KB at K = 4,096, so a build fits on a CU beside the K = 4,096 assignment grid's two
     // workgroups (~40 KB): the heap and the node codes share one region -- the heap lives
@@ -2237,6 +2253,13 @@ int pqh_tables_alloc(pqh_ctx_t* ctx, int m, int k, int context, pqh_tables_t** o
         pqh_tables_destroy(t);
         return pqh_set_error(ctx, PQH_ERR_NOMEM, "hipMalloc tables");
     }
+    // the error word starts clear (builds leave it sticky; pqh_tables_status clears it);
+    // synchronised, as a build may run on another context's stream
+    if (hipMemsetAsync(t->d_err, 0, 16, ctx->stream) != hipSuccess ||
+        hipStreamSynchronize(ctx->stream) != hipSuccess) {
+        pqh_tables_destroy(t);
+        return pqh_set_error(ctx, PQH_ERR_HIP, "hipMemsetAsync tables");
+    }
     *out = t;
     return PQH_OK;
 }
@@ -2332,8 +2355,7 @@ static int build_trees(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts
     if (which < PQH_TREES_DEFAULT || which > PQH_TREES_GROUP) return PQH_ERR_ARG;
     int rc = pqh_use_device(ctx);
     if (rc) return rc;
-    PQH_HIP(ctx, hipMemsetAsync(t->d_err, 0, 16, ctx->stream));   // error word + LUT pool head
-    if (t2) PQH_HIP(ctx, hipMemsetAsync(t2->d_err, 0, 16, ctx->stream));
+    // (no memset: the tree kernel zeroes each set's LUT pool head; the error word is sticky)
     if (reinterpret_cast<uintptr_t>(d_counts) & 15u) return PQH_ERR_ARG;
     t->enc32_by_trees = false;   // (set below by the builds that write the gather copy)
     if (t2) t2->enc32_by_trees = false;
@@ -2487,6 +2509,7 @@ int pqh_tables_status(pqh_ctx_t* ctx, const pqh_tables_t* t) {
     uint32_t e = 0;
     PQH_HIP(ctx, hipMemcpyAsync(&e, t->d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
     PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (e) PQH_HIP(ctx, hipMemsetAsync(t->d_err, 0, 4, ctx->stream));   // (sticky until read)
     if (e & 2u) return pqh_set_error(ctx, PQH_ERR_UNSUPPORTED, "a k <= 256 tree builder ran with k > 256");
     return e ? pqh_set_error(ctx, PQH_ERR_CODE_TOO_LONG, "a Huffman code exceeds 56 bits") : PQH_OK;
 }
@@ -2535,7 +2558,7 @@ int pqh_decode(pqh_ctx_t* ctx, const pqh_tables_t* t, const unsigned char* d_str
     int rc = pqh_use_device(ctx);
     if (rc) return rc;
     if (n == 0) return PQH_OK;
-    PQH_HIP(ctx, hipMemsetAsync(ctx->d_diag + 1, 0, 8, ctx->stream));
+    // (no memset: d_diag[1] is sticky until pqh_decode_status reads it)
     const long long chunks = (n + chunk_vectors - 1) / chunk_vectors;
     const long long nwords = (long long)(stream_bytes / 4);
     const unsigned blocks = (unsigned)((chunks + 63) / 64);
@@ -2629,6 +2652,7 @@ int pqh_decode_status(pqh_ctx_t* ctx) {
     unsigned long long e = 0;
     PQH_HIP(ctx, hipMemcpyAsync(&e, ctx->d_diag + 1, 8, hipMemcpyDeviceToHost, ctx->stream));
     PQH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (e) PQH_HIP(ctx, hipMemsetAsync(ctx->d_diag + 1, 0, 8, ctx->stream));   // (sticky until read)
     return e ? pqh_set_error(ctx, PQH_ERR_CORRUPT, "invalid code in stream") : PQH_OK;
 }
 
@@ -2799,7 +2823,6 @@ int pqh_decode_tree(pqh_ctx_t* ctx, const pqh_tables_t* t, const unsigned char* 
     int rc = pqh_use_device(ctx);
     if (rc) return rc;
     if (n == 0) return PQH_OK;
-    PQH_HIP(ctx, hipMemsetAsync(ctx->d_diag + 1, 0, 8, ctx->stream));
     const long long chunks = (n + chunk_vectors - 1) / chunk_vectors;
     if (lds > 64 * 1024)
         PQH_HIP(ctx, hipFuncSetAttribute((const void*)dec_tree,
