@@ -198,5 +198,9 @@ struct pqh_tables {
     uint32_t* d_meta = nullptr;
     pqh_long_code* d_long = nullptr;
     uint32_t* d_long_cnt = nullptr;
-    uint32_t* d_err = nullptr;       // [0] code too long; [2..3] the LUT pool head (u64)
+    // [0] error word (sticky until pqh_tables_status); [2..3] / [4..5] two LUT pool heads
+    // (u64): a build allocates from slot pool_slot, a fused tree + LUT build zeroes the other
+    // slot for the next build (its own was zeroed by the build before it or at allocation)
+    uint32_t* d_err = nullptr;
+    int pool_slot = 0;
 };

@@ -405,12 +405,13 @@ __device__ __forceinline__ void wave_sync_lds() {
 // by pointer jumping over the tree (code(v) = code(anc) << len | bits) -- eight parallel
 // rounds instead of a serial walk from the root.
 constexpr int kTreeWaves = 4;
-// A tree build's first workgroup of each table set zeroes that set's LUT pool head
-// (d_err[2..3]), which the decode-table build that follows it allocates from: no memset
-// dispatch in front of the build.  The error word d_err[0] is sticky until
-// pqh_tables_status reads it.
+// A tree build's first workgroup of each table set zeroes that set's two LUT pool heads
+// (d_err[2..5]), which the decode-table build that follows it allocates from: no memset
+// dispatch in front of the build.  (A fused tree + LUT build zeroes only the slot it does
+// not use -- huff_trees_grp.)  The error word d_err[0] is sticky until pqh_tables_status.
 __device__ __forceinline__ void reset_pool_head(uint32_t* err) {
-    *reinterpret_cast<unsigned long long*>(err + 2) = 0ull;
+    reinterpret_cast<unsigned long long*>(err + 2)[0] = 0ull;
+    reinterpret_cast<unsigned long long*>(err + 2)[1] = 0ull;
 }
 
 __global__ void __launch_bounds__(64 * kTreeWaves)
@@ -871,8 +872,8 @@ struct GrpLut {
     int prio;   // wave issue priority (pqh_prio)
 };
 
-__device__ __forceinline__ void grp_luts(const GrpLut& L, long long t, int k, int gl, int gsh,
-                                         const unsigned long long* code, char* scratch);
+__device__ __forceinline__ void grp_luts(const GrpLut& L, long long t, int k, int lane, int gl,
+                                         int gsh, const unsigned long long* code, char* scratch);
 
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(32)))
 huff_trees_grp(const uint32_t* __restrict__ counts, int k, long long trees,
@@ -880,12 +881,18 @@ huff_trees_grp(const uint32_t* __restrict__ counts, int k, long long trees,
                long long trees2, const uint32_t* __restrict__ counts2,
                unsigned long long* __restrict__ enc2, uint32_t* __restrict__ err2, int prio,
                uint32_t* __restrict__ e32, uint32_t* __restrict__ e32_2,
-               uint16_t* __restrict__ e16, uint16_t* __restrict__ e16_2) {
+               uint16_t* __restrict__ e16, uint16_t* __restrict__ e16_2, GrpLut lut,
+               unsigned long long* __restrict__ pool_next) {
     // trees [0, trees) from counts -> enc (and the encoder's u32 gather copy e32); a paired
     // build adds [trees, trees + trees2)
     const long long blocks1 = (trees + kGrpTrees - 1) / kGrpTrees;
-    if (((long long)blockIdx.x == 0 || (long long)blockIdx.x == blocks1) && threadIdx.x == 0)
-        reset_pool_head((long long)blockIdx.x == 0 ? err : err2);
+    // lut.lut1 set: the decode tables too, each group right after its tree (unpaired builds);
+    // its pool slot was zeroed before this launch, the other one is zeroed here for the next
+    const bool fuse = lut.lut1 != nullptr;
+    if (((long long)blockIdx.x == 0 || (long long)blockIdx.x == blocks1) && threadIdx.x == 0) {
+        if (fuse) *pool_next = 0ull;
+        else reset_pool_head((long long)blockIdx.x == 0 ? err : err2);
+    }
     if ((long long)blockIdx.x >= blocks1) {
         const long long b = (long long)blockIdx.x - blocks1;
         counts = counts2 + b * kGrpTrees * k;
@@ -1005,6 +1012,7 @@ huff_trees_grp(const uint32_t* __restrict__ counts, int k, long long trees,
             }
         }
         out[s] = e;
+        if (fuse) code[s] = e;   // (the LUT build's input: 0 for absent and refused codes)
         // the encoder's gather copy here too, so an encode may start before the decode
         // tables (lut_grp / lut_build then skip it)
         const unsigned len = (unsigned)(e >> 56);
@@ -1016,6 +1024,18 @@ huff_trees_grp(const uint32_t* __restrict__ counts, int k, long long trees,
         g_tree_stamps[4] = __builtin_amdgcn_s_memtime();
         g_tree_stamps[5] = (unsigned long long)nz;
         g_tree_stamps[6] = (unsigned long long)(nz + nint);
+    }
+    if (fuse) {
+        // the codes of symbols 0..k-1 stay at base; the internal nodes' codes, kid and the
+        // parent links after them are dead, so lut_grp's 3 KB scratch goes at base + 2 KB
+        wave_sync_lds();
+        // (lane values made opaque here, so nothing of the LUT build is computed before
+        // the merges and held through them: the tree phase keeps its 32-VGPR budget)
+        char* b2 = base;
+        int ln2 = lane, gl2 = gl, gsh2 = gsh;
+        asm volatile("" : "+v"(b2), "+v"(ln2), "+v"(gl2), "+v"(gsh2));
+        grp_luts(lut, (long long)blockIdx.x * kGrpTrees + grp2, k, ln2, gl2, gsh2,
+                 reinterpret_cast<const unsigned long long*>(b2), b2 + 2048);
     }
 }
 
@@ -1035,15 +1055,21 @@ lut_grp(const unsigned long long* __restrict__ enc, int k, long long tables, Grp
 #pragma unroll 1
     for (int s = gl; s < k; s += 16) code[s] = e[s];
     wave_sync_lds();
-    grp_luts(lut, t, k, gl, gsh, code, base + 2048);
+    grp_luts(lut, t, k, lane, gl, gsh, code, base + 2048);
 }
 
 // lut_build's tables for alphabet t from its k code entries `code` (LDS), by the tree's 16
 // lanes; `scratch` = 3 KB of LDS (the L1 image u16 [2^w1 <= 512], the per-prefix widest
 // remainder / subtable id u32 [512]) + a counter word after them.  Same entries as
 // lut_build (whose comments give the format); only the pool ranges' placement may differ.
-__device__ __forceinline__ void grp_luts(const GrpLut& L, long long t, int k, int gl, int gsh,
-                                         const unsigned long long* code, char* scratch) {
+// shuffles within a lane's 16-lane group from an explicit lane id (so a caller can pass an
+// opaque copy: the fused tree build must not compute these addresses before its merges)
+__device__ __forceinline__ uint32_t g16_from(uint32_t v, int src_lane) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)v);
+}
+
+__device__ __forceinline__ void grp_luts(const GrpLut& L, long long t, int k, int lane, int gl,
+                                         int gsh, const unsigned long long* code, char* scratch) {
     const int w1 = L.w1, np = 1 << w1;                 // (w1 <= 9 here)
     uint16_t* img = reinterpret_cast<uint16_t*>(scratch);
     uint32_t* pre = reinterpret_cast<uint32_t*>(scratch + 1024);
@@ -1073,19 +1099,20 @@ __device__ __forceinline__ void grp_luts(const GrpLut& L, long long t, int k, in
     uint32_t incl = c_id;
 #pragma unroll
     for (int off = 1; off < 16; off <<= 1) {
-        const uint32_t y = __shfl_up(incl, off, 16);
+        const uint32_t y = g16_from(incl, gl >= off ? lane - off : lane);
         if (gl >= off) incl += y;
     }
 #pragma unroll
-    for (int off = 8; off >= 1; off >>= 1) w2 = max(w2, (uint32_t)__shfl_xor(w2, off, 16));
-    const uint32_t nsub = __shfl(incl, 15, 16);
+    for (int off = 8; off >= 1; off >>= 1) w2 = max(w2, g16_from(w2, lane ^ off));
+    const uint32_t nsub = g16_from(incl, lane | 15);
     uint32_t id = incl - c_id;
     // the pool range (sub ids must fit 12 bits; an alphabet without long codes takes none)
     unsigned long long l0 = 0;
     const bool ok = nsub < 4095;
     const unsigned long long size = ok ? (unsigned long long)nsub << w2 : 0ull;
     if (gl == 0 && size) l0 = atomicAdd(L.pool_head, size);
-    l0 = __shfl(l0, 0, 16);
+    l0 = ((unsigned long long)g16_from((uint32_t)(l0 >> 32), lane & ~15) << 32) |
+         g16_from((uint32_t)l0, lane & ~15);
     const bool fits = ok && l0 + size <= (unsigned long long)L.lut2_cap;
     if (gl == 0)
         L.meta[t] = fits ? (uint32_t)((l0 << 9) | (w2 << 4) | (uint32_t)w1)
@@ -2249,13 +2276,13 @@ int pqh_tables_alloc(pqh_ctx_t* ctx, int m, int k, int context, pqh_tables_t** o
         hipMalloc(&t->d_meta, (size_t)t->tables * 4 + 16) != hipSuccess ||
         hipMalloc(&t->d_long, (size_t)t->tables * k * sizeof(pqh_long_code)) != hipSuccess ||
         hipMalloc(&t->d_long_cnt, (size_t)t->tables * 4) != hipSuccess ||
-        hipMalloc(&t->d_err, 16) != hipSuccess) {
+        hipMalloc(&t->d_err, 32) != hipSuccess) {
         pqh_tables_destroy(t);
         return pqh_set_error(ctx, PQH_ERR_NOMEM, "hipMalloc tables");
     }
     // the error word starts clear (builds leave it sticky; pqh_tables_status clears it);
     // synchronised, as a build may run on another context's stream
-    if (hipMemsetAsync(t->d_err, 0, 16, ctx->stream) != hipSuccess ||
+    if (hipMemsetAsync(t->d_err, 0, 32, ctx->stream) != hipSuccess ||
         hipStreamSynchronize(ctx->stream) != hipSuccess) {
         pqh_tables_destroy(t);
         return pqh_set_error(ctx, PQH_ERR_HIP, "hipMemsetAsync tables");
@@ -2278,10 +2305,19 @@ int pqh_tables_destroy(pqh_tables_t* t) {
     return PQH_OK;
 }
 
+// the LUT pool head a build allocates from (slot pool_slot) and the other slot
+static unsigned long long* pool_slot_ptr(pqh_tables* t, int slot) {
+    return reinterpret_cast<unsigned long long*>(t->d_err + 2) + slot;
+}
+
+static GrpLut grp_lut_of(pqh_tables* t) {
+    return GrpLut{t->enc32_by_trees ? nullptr : t->d_enc32, t->d_enc16, t->d_lut1, t->d_lut2,
+                  t->d_meta, t->d_long, t->d_long_cnt, pool_slot_ptr(t, t->pool_slot),
+                  t->lut2_cap, t->l1_bits, t->l2_bits, pqh_prio("LUTS", 3)};
+}
+
 static void launch_lut_grp(pqh_ctx* ctx, pqh_tables* t) {
-    const GrpLut lut{t->enc32_by_trees ? nullptr : t->d_enc32, t->d_enc16, t->d_lut1, t->d_lut2, t->d_meta, t->d_long, t->d_long_cnt,
-                     reinterpret_cast<unsigned long long*>(t->d_err + 2), t->lut2_cap,
-                     t->l1_bits, t->l2_bits, pqh_prio("LUTS", 3)};
+    const GrpLut lut = grp_lut_of(t);
     hipLaunchKernelGGL(lut_grp, dim3((unsigned)((t->tables + kGrpTrees - 1) / kGrpTrees)), dim3(64),
                        0, ctx->stream, t->d_enc, t->k, t->tables, lut);
 }
@@ -2293,6 +2329,7 @@ static int launch_luts(pqh_ctx* ctx, pqh_tables* t) {
     if (!(impl && std::strcmp(impl, "block") == 0) && t->l1_bits <= 9 && t->k == 256) {
         launch_lut_grp(ctx, t);
         PQH_LAUNCH_CHECK(ctx);
+        t->pool_slot ^= 1;   // (the tree kernel before it zeroed both slots)
         return PQH_OK;
     }
     // (the pool head, d_err[2..3], was zeroed with the error word before the trees)
@@ -2307,9 +2344,9 @@ static int launch_luts(pqh_ctx* ctx, pqh_tables* t) {
     }
     hipLaunchKernelGGL(lut_build, dim3((unsigned)t->tables), dim3(256), lds, ctx->stream, t->d_enc,
                        t->enc32_by_trees ? nullptr : t->d_enc32, t->d_enc16, t->k, t->l1_bits, t->l2_bits, t->d_meta, t->d_lut1, t->d_lut2,
-                       t->lut2_cap, t->d_long, t->d_long_cnt,
-                       reinterpret_cast<unsigned long long*>(t->d_err + 2));
+                       t->lut2_cap, t->d_long, t->d_long_cnt, pool_slot_ptr(t, t->pool_slot));
     PQH_LAUNCH_CHECK(ctx);
+    t->pool_slot ^= 1;   // (the tree kernel before it zeroed both slots)
     return PQH_OK;
 }
 
@@ -2318,11 +2355,15 @@ int pqh_tables_build(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts) 
 }
 
 static int build_trees(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts, int which,
-                       pqh_tables_t* t2 = nullptr, const uint32_t* d_counts2 = nullptr);
+                       pqh_tables_t* t2 = nullptr, const uint32_t* d_counts2 = nullptr,
+                       bool* fused = nullptr);
 
 int pqh_tables_build_impl(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts, int which) {
-    const int rc = build_trees(ctx, t, d_counts, which);
-    return rc ? rc : launch_luts(ctx, t);
+    // trees and decode tables in one launch where the group builders serve both (context
+    // tables, K = 256; PQH_FUSE_LUTS=0: two launches); else the trees, then launch_luts
+    bool fused = false;
+    const int rc = build_trees(ctx, t, d_counts, which, nullptr, nullptr, &fused);
+    return rc ? rc : fused ? PQH_OK : launch_luts(ctx, t);
 }
 
 int pqh_tables_build_trees(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts, int which) {
@@ -2348,7 +2389,7 @@ int pqh_tables_build_luts(pqh_ctx_t* ctx, pqh_tables_t* t) {
 
 // the code tables' trees (d_enc) on ctx's stream; the decode tables follow (launch_luts)
 static int build_trees(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts, int which,
-                       pqh_tables_t* t2, const uint32_t* d_counts2) {
+                       pqh_tables_t* t2, const uint32_t* d_counts2, bool* fused) {
     // any context of the tables' device may run the build (on its own stream), so the
     // builds of consecutive batches can overlap on different streams
     if (!ctx || !t || !d_counts || !t->ctx || t->ctx->device != ctx->device) return PQH_ERR_ARG;
@@ -2381,14 +2422,31 @@ static int build_trees(pqh_ctx_t* ctx, pqh_tables_t* t, const uint32_t* d_counts
     if (t->k <= 256 && !(impl && std::strcmp(impl, "lane") == 0)) {
         const long long blocks = (trees + kGrpTrees - 1) / kGrpTrees +
                                  (t2 ? (t2->tables + kGrpTrees - 1) / kGrpTrees : 0);
+        static const bool fuse_env = [] {
+            const char* f = std::getenv("PQH_FUSE_LUTS");
+            const char* l = std::getenv("PQH_LUT_IMPL");
+            return !(f && std::strcmp(f, "0") == 0) && !(l && std::strcmp(l, "block") == 0);
+        }();
+        const bool fuse = fused && fuse_env && !t2 && t->k == 256 && t->l1_bits <= 9;
+        t->enc32_by_trees = true;   // (before grp_lut_of: the trees write the gather copies)
+        GrpLut lut{};
+        unsigned long long* next = nullptr;
+        if (fuse) {
+            lut = grp_lut_of(t);                      // slot pool_slot, zeroed beforehand
+            next = pool_slot_ptr(t, t->pool_slot ^ 1);   // zeroed by this launch
+        }
         hipLaunchKernelGGL(huff_trees_grp, dim3((unsigned)blocks), dim3(64), 0, ctx->stream, d_counts,
                            t->k, trees, t->d_enc, t->d_err, t2 ? t2->tables : 0ll,
                            t2 ? d_counts2 : d_counts, t2 ? t2->d_enc : t->d_enc,
                            t2 ? t2->d_err : t->d_err, pqh_prio("TREES", 3), t->d_enc32,
-                           t2 ? t2->d_enc32 : t->d_enc32, t->d_enc16, t2 ? t2->d_enc16 : t->d_enc16);
+                           t2 ? t2->d_enc32 : t->d_enc32, t->d_enc16, t2 ? t2->d_enc16 : t->d_enc16,
+                           lut, next);
         PQH_LAUNCH_CHECK(ctx);
-        t->enc32_by_trees = true;
         if (t2) t2->enc32_by_trees = true;
+        if (fuse) {
+            t->pool_slot ^= 1;
+            *fused = true;
+        }
         return PQH_OK;
     }
     // (every build writes every entry, 0 for symbols that never occur: no memset)
@@ -2483,7 +2541,7 @@ int pqh_tables_upload(pqh_ctx_t* ctx, pqh_tables_t* t, const huffman_codebook_t*
             for (int b = 0; b < c.bit_length; ++b) v = (v << 1) | ((c.code[b >> 3] >> (7 - (b & 7))) & 1u);
             h[(size_t)i * t->items + it] = ((unsigned long long)c.bit_length << 56) | v;
         }
-    PQH_HIP(ctx, hipMemsetAsync(t->d_err, 0, 16, ctx->stream));   // error word + LUT pool head
+    PQH_HIP(ctx, hipMemsetAsync(t->d_err, 0, 32, ctx->stream));   // error word + LUT pool heads
     PQH_HIP(ctx, hipMemcpyAsync(t->d_enc, h.data(), h.size() * 8, hipMemcpyHostToDevice, ctx->stream));
     t->enc32_by_trees = false;   // the LUT build writes the gather copy
     rc = launch_luts(ctx, t);

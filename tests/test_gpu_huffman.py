@@ -202,10 +202,15 @@ def test_corrupt_stream_is_reported(gpu):
     tabs = codec.Tables.from_codebooks(ctx, cbs)
     enc = codec.encode(ctx, tabs, cd, chunk_vectors=10)
     # part 1 has a single symbol: code "0"; a 1 bit there is invalid
+    good = enc.stream.clone()
     enc.stream[:] = 0xFF
     codec.decode(ctx, tabs, enc)
+    # the error is sticky: a good decode after it does not clear it, the status call does
+    enc.stream.copy_(good)
+    assert torch.equal(codec.decode(ctx, tabs, enc), cd)
     with pytest.raises(Exception):
         codec.decode_status(ctx)
+    codec.decode_status(ctx)
 
 
 @pytest.mark.parametrize("ctxm", [True, False])
@@ -685,3 +690,36 @@ def test_onepass_encoder_and_scratch_release(gpu, oracle, m, k, ctxm):
         assert torch.equal(dec, cd), impl
         ctx.release_scratch()
     assert np.array_equal(runs[1], runs[2])
+
+
+def test_fused_and_split_table_builds_alternate(gpu, oracle):
+    """One table set rebuilt by the fused tree + decode-table launch (pqh_tables_build) and by
+    the split pair (build_trees, build_luts) in turn, on two contexts: every build decodes the
+    oracle's stream exactly, and its code tables and codebook file equal the oracle's (the two
+    LUT pool heads alternate between builds; no memset dispatch in front of a build)
+    (huffman_encode.c:141-192, huffman_decode.c:137-191)."""
+    torch, codec, ctx = gpu
+    ctx2 = codec.Context(0)
+    m, k, n = 8, 256, 120_011
+    codes = datagen.skewed_codes(n, m, k=k, seed=991, stay=0)
+    cd = torch.from_numpy(np.ascontiguousarray(codes.astype(np.uint8))).cuda()
+    counts = codec.histogram(ctx, cd, k, True)
+    ocb = oracle.build_codebooks(codes, k, True)
+    want, bits = oracle.encode(codes, ocb)
+    tabs = codec.Tables(ctx, m, k, True)
+    for step, how in enumerate(["fused", "split", "split", "fused", "fused", "split"]):
+        c = ctx if step % 2 == 0 else ctx2
+        if how == "fused":
+            tabs.build(counts, c)
+        else:
+            tabs.build_trees(counts, c).build_luts(c)
+        torch.cuda.synchronize()
+        tabs.status()
+        enc = codec.encode(ctx, tabs, cd, chunk_vectors=4)
+        assert enc.bits == bits, (step, how)
+        assert enc.stream[:len(want)].cpu().numpy().tobytes() == want, (step, how)
+        dec = codec.decode(ctx, tabs, enc)
+        codec.decode_status(ctx)
+        assert torch.equal(dec, cd), (step, how)
+    assert tabs.codebooks(codec.counts_to_host(counts)).file_bytes() == oracle.codebooks_file(ocb)
+    ctx2.close()
