@@ -199,8 +199,9 @@ struct pqh_tables {
     pqh_long_code* d_long = nullptr;
     uint32_t* d_long_cnt = nullptr;
     // [0] error word (sticky until pqh_tables_status); [2..3] / [4..5] two LUT pool heads
-    // (u64): a build allocates from slot pool_slot, a fused tree + LUT build zeroes the other
-    // slot for the next build (its own was zeroed by the build before it or at allocation)
+    // (u64): a decode-table build allocates from slot pool_slot and zeroes the other slot for
+    // the next build (its own was zeroed by the build before it, by its tree kernel, or at
+    // allocation)
     uint32_t* d_err = nullptr;
     int pool_slot = 0;
 };

@@ -1043,10 +1043,12 @@ huff_trees_grp(const uint32_t* __restrict__ counts, int k, long long trees,
 // the same tables from <= 32 VGPRs and 20 KB of LDS, so -- like huff_trees_grp -- it runs
 // beside the assignment grid instead of waiting for its end (context mode, W1 <= 9).
 __global__ void __launch_bounds__(64)
-lut_grp(const unsigned long long* __restrict__ enc, int k, long long tables, GrpLut lut) {
+lut_grp(const unsigned long long* __restrict__ enc, int k, long long tables, GrpLut lut,
+        unsigned long long* __restrict__ pool_next) {
     __shared__ __attribute__((aligned(16))) char lds[kGrpTrees * (2048 + 3072 + 16)];
     const int lane = threadIdx.x, grp = lane >> 4, gl = lane & 15, gsh = grp * 16;
     const long long t = (long long)blockIdx.x * kGrpTrees + grp;
+    if (blockIdx.x == 0 && lane == 0) *pool_next = 0ull;   // (the next build's slot)
     if (t >= tables) return;   // no workgroup barriers below
     pqh_set_prio(lut.prio);
     char* base = lds + grp * (2048 + 3072 + 16);
@@ -1519,7 +1521,9 @@ lut_build(const unsigned long long* __restrict__ enc, uint32_t* __restrict__ enc
           uint16_t* __restrict__ enc16, int k, int w1,
           int l2_bits, uint32_t* __restrict__ meta, uint16_t* __restrict__ lut1,
           uint16_t* __restrict__ lut2, long long lut2_cap, pqh_long_code* __restrict__ longs,
-          uint32_t* __restrict__ long_cnt, unsigned long long* __restrict__ pool_head) {
+          uint32_t* __restrict__ long_cnt, unsigned long long* __restrict__ pool_head,
+          unsigned long long* __restrict__ pool_next) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *pool_next = 0ull;   // (the next build's slot)
     // w2max[2^W1], sub_id[2^W1]: dynamic LDS sized by the set's W1 (8 KB at the K = 256
     // W1 = 9 / 11, 64 KB only at K = 4096's W1 = 13), so a build beside the assignment grid
     // takes only what its alphabet needs
@@ -2319,7 +2323,8 @@ static GrpLut grp_lut_of(pqh_tables* t) {
 static void launch_lut_grp(pqh_ctx* ctx, pqh_tables* t) {
     const GrpLut lut = grp_lut_of(t);
     hipLaunchKernelGGL(lut_grp, dim3((unsigned)((t->tables + kGrpTrees - 1) / kGrpTrees)), dim3(64),
-                       0, ctx->stream, t->d_enc, t->k, t->tables, lut);
+                       0, ctx->stream, t->d_enc, t->k, t->tables, lut,
+                       pool_slot_ptr(t, t->pool_slot ^ 1));
 }
 
 static int launch_luts(pqh_ctx* ctx, pqh_tables* t) {
@@ -2329,7 +2334,7 @@ static int launch_luts(pqh_ctx* ctx, pqh_tables* t) {
     if (!(impl && std::strcmp(impl, "block") == 0) && t->l1_bits <= 9 && t->k == 256) {
         launch_lut_grp(ctx, t);
         PQH_LAUNCH_CHECK(ctx);
-        t->pool_slot ^= 1;   // (the tree kernel before it zeroed both slots)
+        t->pool_slot ^= 1;   // (the kernel zeroed the other slot for the next build)
         return PQH_OK;
     }
     // (the pool head, d_err[2..3], was zeroed with the error word before the trees)
@@ -2344,9 +2349,10 @@ static int launch_luts(pqh_ctx* ctx, pqh_tables* t) {
     }
     hipLaunchKernelGGL(lut_build, dim3((unsigned)t->tables), dim3(256), lds, ctx->stream, t->d_enc,
                        t->enc32_by_trees ? nullptr : t->d_enc32, t->d_enc16, t->k, t->l1_bits, t->l2_bits, t->d_meta, t->d_lut1, t->d_lut2,
-                       t->lut2_cap, t->d_long, t->d_long_cnt, pool_slot_ptr(t, t->pool_slot));
+                       t->lut2_cap, t->d_long, t->d_long_cnt, pool_slot_ptr(t, t->pool_slot),
+                       pool_slot_ptr(t, t->pool_slot ^ 1));
     PQH_LAUNCH_CHECK(ctx);
-    t->pool_slot ^= 1;   // (the tree kernel before it zeroed both slots)
+    t->pool_slot ^= 1;   // (the kernel zeroed the other slot for the next build)
     return PQH_OK;
 }
 

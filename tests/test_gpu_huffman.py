@@ -707,10 +707,14 @@ def test_fused_and_split_table_builds_alternate(gpu, oracle):
     ocb = oracle.build_codebooks(codes, k, True)
     want, bits = oracle.encode(codes, ocb)
     tabs = codec.Tables(ctx, m, k, True)
-    for step, how in enumerate(["fused", "split", "split", "fused", "fused", "split"]):
+    # ("luts": the decode tables rebuilt alone, after a fused build)
+    for step, how in enumerate(["fused", "split", "split", "fused", "luts", "fused", "fused",
+                                "luts", "split"]):
         c = ctx if step % 2 == 0 else ctx2
         if how == "fused":
             tabs.build(counts, c)
+        elif how == "luts":
+            tabs.build_luts(c)
         else:
             tabs.build_trees(counts, c).build_luts(c)
         torch.cuda.synchronize()
