@@ -21,8 +21,12 @@ namespace {
 // d_offsets = {sum of the lengths of the ranks before `rank`, sum of all lengths}; a rank
 // that failed locally sent the sentinel length ~0: then {0, ~0} (pqh_shard_status reports it)
 __global__ void shard_prefix(const unsigned long long* __restrict__ lengths, int world, int rank,
-                             unsigned long long* __restrict__ offsets) {
+                             unsigned long long* __restrict__ offsets,
+                             uint32_t* __restrict__ out_word0) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    // word 0 of the shard's output: the bits before its offset belong to the previous shard
+    // and stay zero here (the placement ORs its first bits into it) -- no memset dispatch
+    if (out_word0) *out_word0 = 0u;
     unsigned long long before = 0, all = 0;
     bool failed = false;
     for (int r = 0; r < world; ++r) {
@@ -53,12 +57,20 @@ __global__ void shard_halo_pick(const unsigned char* __restrict__ recs, long lon
         row[i] = prev >= 0 ? recs[prev * recb + kHaloData + i] : (unsigned char)0;
 }
 
-// this shard's last row into the halo record (byte kHaloData on), from row-major codes
-// (ldc = 0) or part-major ones (part i's codes at i * ldc)
+// this shard's halo record, all recb bytes written (no memset dispatch): the flag byte
+// (1 = the shard is non-empty), zero padding, and its last row at byte kHaloData, from
+// row-major codes (ldc = 0) or part-major ones (part i's codes at i * ldc); n = 0: all zero
 __global__ void shard_last_row(const unsigned char* __restrict__ codes, long long ldc, long long n,
-                               int m, unsigned char* __restrict__ rec) {
-    for (int i = threadIdx.x; i < m; i += blockDim.x)
-        rec[kHaloData + i] = ldc ? codes[(long long)i * ldc + n - 1] : codes[(n - 1) * m + i];
+                               int m, unsigned char* __restrict__ rec, long long recb) {
+    for (long long i = threadIdx.x; i < recb; i += blockDim.x) {
+        unsigned char v = 0;
+        if (i == 0) v = n > 0 ? 1 : 0;
+        else if (n > 0 && i >= kHaloData && i < kHaloData + m) {
+            const long long j = i - kHaloData;
+            v = ldc ? codes[j * ldc + n - 1] : codes[(n - 1) * m + j];
+        }
+        rec[i] = v;
+    }
 }
 
 // the shard-boundary pair (halo row, first row) of every part, one count each, when this
@@ -208,13 +220,11 @@ static int shard_tables_impl(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm, const
     // the halo (context mode): every rank's (non-empty flag, last row); the halo row and the
     // raw-first flag are picked on the device -- no host round trip
     if (context) {
-        local(hipMemsetAsync(sc.halo_send, 0, sc.recb, ctx->stream) == hipSuccess ? PQH_OK : PQH_ERR_HIP);
-        if (n > 0 && !err) {
-            local(hipMemsetAsync(sc.halo_send, 1, 1, ctx->stream) == hipSuccess ? PQH_OK : PQH_ERR_HIP);
-            hipLaunchKernelGGL(shard_last_row, dim3(1), dim3(64), 0, ctx->stream,
-                               static_cast<const unsigned char*>(d_codes), ldc, n, m, sc.halo_send);
-            local(hipGetLastError() == hipSuccess ? PQH_OK : PQH_ERR_HIP);
-        }
+        // (n = 0 -- an empty shard or a local failure: an all-zero record, "no rows")
+        hipLaunchKernelGGL(shard_last_row, dim3(1), dim3(64), 0, ctx->stream,
+                           static_cast<const unsigned char*>(d_codes), ldc, err ? 0ll : n, m,
+                           sc.halo_send, (long long)sc.recb);
+        local(hipGetLastError() == hipSuccess ? PQH_OK : PQH_ERR_HIP);
         if (comm->all_gather(comm->user, sc.halo_send, sc.halo_recv, sc.recb, st))
             return pqh_set_error(ctx, PQH_ERR_COMM, "shard halo all-gather failed");
         hipLaunchKernelGGL(shard_halo_pick, dim3(1), dim3(64), 0, ctx->stream, sc.halo_recv,
@@ -277,7 +287,8 @@ static int shard_write_impl(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm, const 
     int rc = pqh_use_device(ctx);
     if (rc) return rc;
     int err = status;
-    if (!err && (shard_local_bad(shard, d_codes, tables, m, k, context) || !d_out || out_bytes < 4))
+    if (!err && (shard_local_bad(shard, d_codes, tables, m, k, context) || !d_out || out_bytes < 4 ||
+                 (reinterpret_cast<uintptr_t>(d_out) & 3)))
         err = PQH_ERR_ARG;
     // (part-major codes: the 8-byte-row encoder's shapes, m = 8 or 16 u8 codes)
     if (!err && ldc && (ldc < shard->size || (m != 8 && m != 16) ||
@@ -300,13 +311,11 @@ static int shard_write_impl(pqh_ctx_t* ctx, const pqh_shard_comm_t* comm, const 
     if (err) (void)hipMemsetAsync(sc.len_send, 0xFF, 8, ctx->stream);   // the sentinel length
     if (comm->all_gather(comm->user, sc.len_send, sc.len_recv, 8, ctx->stream))
         return pqh_set_error(ctx, PQH_ERR_COMM, "shard length all-gather failed");
+    // (word 0 of d_out = the global word offset / 32: shard_prefix zeroes it)
     hipLaunchKernelGGL(shard_prefix, dim3(1), dim3(64), 0, ctx->stream, sc.len_recv, world, rank,
-                       d_offsets);
+                       d_offsets, err ? nullptr : reinterpret_cast<uint32_t*>(d_out));
     PQH_LAUNCH_CHECK(ctx);
     if (err) return err;
-    // word 0 of d_out = the global word offset / 32; the bits before the shard's offset in
-    // that word belong to the previous shard and stay zero here
-    PQH_HIP(ctx, hipMemsetAsync(d_out, 0, 4, ctx->stream));
     rc = pqh_encode_place_dev_ld(ctx, tables, d_codes, ldc, n, prev, rawf, d_offsets, d_out,
                                  out_bytes, chunk_vectors, d_chunk_offsets, d_chunk_prev,
                                  sc.len_send);
